@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""bench.py — batched LQR (Riccati backward + forward rollout) throughput on MI355X.
+
+Metric (BASELINE.json): LQR trajectories/sec, n=32 m=16 N=256 B=65536 fp64.
+A "step" = one lqrx_dp_solve launch over the rank's whole batch (inputs resident in HBM,
+outputs K/P/X/U written to HBM).  One process per GPU; for N>1 GPUs the batch is sharded
+(independent problems, no data-path collective): each rank solves its own `--batch`
+trajectories (weak scaling), generated from the same counter-based generator with a
+rank-offset trajectory index.
+
+Prints ONE JSON line on rank 0 (contract in the task description), with a `roofline`
+object for the Riccati kernel (fp64 compute roofline: algorithmic flops per launch ÷ the
+kernel's own HIP-event-timed duration on the launch stream) and a `cpu_baseline` object
+(the CPU oracle — a restatement of the reference path — timed on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "lqr.jl_amd"))
+sys.path.insert(0, ROOT)
+
+METRIC = "LQR trajectories/sec (Riccati bwd+fwd), n=32 m=16 N=256 B=65536; 1/2/4/8 GPU"
+PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 vector = FP64 matrix (spec); MI355X_MICROARCH.md
+PEAK_FP32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def dp_flops_per_traj(n, m, N):
+    """(N−1)[4n³+8n²m+4nm²+m³/3+2n²+2m²] + (N−1)(2n²+4nm)."""
+    return (N - 1) * (4 * n**3 + 8 * n**2 * m + 4 * n * m**2 + m**3 / 3 + 2 * n**2 + 2 * m**2) \
+        + (N - 1) * (2 * n**2 + 4 * n * m)
+
+
+def dp_bytes_per_traj(n, m, N, s=8):
+    """SURVEY.md §8(d), time-invariant: read (3n²+nm+m²+n)s, write ((N−1)mn+Nn+(N−1)m+n²)s."""
+    return (3 * n * n + n * m + m * m + n) * s + ((N - 1) * m * n + N * n + (N - 1) * m + n * n) * s
+
+
+def cpu_baseline(n, m, N, target_s=12.0, threads=None):
+    """Time the CPU oracle (C restatement of dynamic_programming.jl, OpenMP over the batch)
+    on a bounded sample of the same workload; returns traj/s and the sample description."""
+    import numpy as np
+    import lqrx
+    from oracle import oracle as orc
+
+    threads = threads or max(1, min(16, os.cpu_count() or 1))
+    orc.load()
+    probe = threads * 2
+    d = lqrx.random_batch(n, m, N, probe, seed=20260104)
+    t0 = time.perf_counter()
+    orc.dp_solve_abi(d, N, nthreads=threads)
+    dt = time.perf_counter() - t0
+    per = dt / probe
+    sample = int(max(probe, min(65536, target_s / max(per, 1e-9))))
+    sample = (sample // threads) * threads or threads
+    d = lqrx.random_batch(n, m, N, sample, seed=20260104)
+    t0 = time.perf_counter()
+    orc.dp_solve_abi(d, N, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return dict(value=sample / dt, unit="trajectories/s", cores=threads, kind="port",
+                sample=f"{sample} trajectories of n={n} m={m} N={N} fp64, oracle/lqr_oracle.c "
+                       f"(op-for-op C restatement of dynamic_programming.jl), OpenMP "
+                       f"{threads} threads, {dt:.1f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=32)
+    ap.add_argument("--m", type=int, default=16)
+    ap.add_argument("--N", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=65536, help="trajectories per GPU")
+    ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--seed", type=int, default=20260104)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import lqrx
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    lib = lqrx.load()
+    if lib.lqrx_device_available() != 1:
+        raise RuntimeError("liblqrx.so sees no gfx950 device")
+
+    n, m, N, bt = args.n, args.m, args.N, args.batch
+    f64 = args.dtype == "f64"
+    tdt = torch.float64 if f64 else torch.float32
+    host = lqrx.random_batch(n, m, N, bt, seed=args.seed, traj0=rank * bt,
+                             dtype=lqrx.F64 if f64 else lqrx.F32)
+    dev = torch.device("cuda", local)
+    t = {k: torch.from_numpy(host[k]).to(dev) for k in ("A", "B", "Q", "R", "Qf", "x0")}
+    t.update(n=n, m=m, batch=bt)
+    del host
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    out = lqrx.dp_solve_device(t, N, p_mode=0, stream=sh)   # allocates outputs once
+
+    def step():
+        lqrx.dp_solve_device(t, N, p_mode=0, stream=sh, out=out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps       # stream-timed launch duration
+    bad = int((out["info"] != 0).sum().item())
+
+    wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
+    wall = float(wall_t.item())
+    total = bt * world * args.steps
+    value = total / wall
+    ms_per_step = wall / args.steps * 1e3
+
+    if rank == 0:
+        flops = dp_flops_per_traj(n, m, N) * bt
+        achieved = flops / (kern_ms * 1e-3) / 1e12
+        peak = PEAK_FP64_TFLOPS if f64 else PEAK_FP32_TFLOPS
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            try:
+                tj = json.load(open(args.traffic_json))
+                key = f"n{n}_m{m}_N{N}_B{bt}_{args.dtype}"
+                traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(n, m, N, target_s=args.cpu_seconds)
+        line = {
+            "metric": METRIC, "value": value, "unit": "trajectories/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": args.dtype, "data": "synthetic (counter-based random dense LQR, "
+                                          "SURVEY.md §8(d) generator)",
+            "config": {"workload": "random dense time-invariant LQR, Riccati backward pass "
+                                   "+ forward rollout (BASELINE.json configs[3])",
+                       "n": n, "m": m, "N": N, "batch_per_gpu": bt, "global_batch": bt * world,
+                       "parallelism": f"batch-sharded x{world}"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak,
+                         "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
+                         "kernel": "dp_riccati_kernel", "kernel_ms": kern_ms,
+                         "flops_per_traj": dp_flops_per_traj(n, m, N),
+                         "alg_bytes_per_launch": dp_bytes_per_traj(n, m, N, 8 if f64 else 4) * bt},
+            "cpu_baseline": cpu,
+            "nonfinite_or_info": bad,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

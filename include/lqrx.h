@@ -1,0 +1,146 @@
+/*
+ * lqrx.h — C ABI of the MI355X-native batched LQR / block-tridiagonal-KKT solver.
+ *
+ * Drop-in boundary for the hot path of bjack205/LQR.jl.  The reference has no FFI: its
+ * only native boundary is Julia stdlib `ccall`s into LAPACK/BLAS, one call per knot-op
+ * (SURVEY.md §1, §2 "native arithmetic" table).  This ABI replaces those calls at batch
+ * grain — one call per batch of independent problems — and is what a Julia `ccall` shim
+ * binds (INTEGRATION.md shows the shim).
+ *
+ * Conventions (all entry points):
+ *   - plain C types only; `extern "C"`; no exceptions cross the boundary;
+ *   - the caller owns every buffer; the library never frees or retains caller pointers;
+ *   - layout 0 = Julia column-major with the batch index slowest, i.e. exactly the memory
+ *     of Array{T,3}(r,c,batch) / Array{T,4}(r,c,knots,batch) — no copy from Julia;
+ *   - return 0 on success; -i if argument i (1-based) is invalid (LAPACK convention);
+ *     1 if the call completed synchronously and at least one trajectory has info != 0;
+ *     LQRX_ERR_* (< -99) for runtime failures; lqrx_last_error() describes the last error
+ *     of the calling thread;
+ *   - `stream` is a hipStream_t: NULL = synchronous (like the reference's solve!), else the
+ *     work is enqueued and the call returns immediately (check info[] after syncing);
+ *   - reentrant; no mutable global state besides the thread-local error string.
+ */
+#ifndef LQRX_H
+#define LQRX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LQRX_ABI_VERSION 1
+
+#define LQRX_F64 0
+#define LQRX_F32 1
+
+#define LQRX_ERR_HIP (-100)         /* HIP runtime error (see lqrx_last_error)          */
+#define LQRX_ERR_UNSUPPORTED (-101) /* valid but not (yet) supported shape / option    */
+#define LQRX_ERR_NODEVICE (-102)    /* no gfx950 device / HIP runtime unavailable        */
+
+/* ------------------------------------------------------------------------------------
+ * DP path: Riccati backward pass + forward rollout.
+ * Replaces solve!(sol::LQRSolution, solver::DPSolver, prob::LQRProblem)
+ *   /root/reference/src/dynamic_programming.jl:54-72
+ * including compute_gain!/compute_ctg!/chol_solve! (:28-52) and the DPSolver scratch
+ * (:2-23: owned by the library, stream-ordered).  Problem data = LQRProblem fields
+ * (/root/reference/src/lqr_problem.jl:1-11): time-invariant A (n×n), B (n×m), Q (n×n),
+ * R (m×m), Qf (n×n), x0 (n), horizon N knots.
+ *
+ * Buffers (layout 0, element type per dtype):
+ *   A  n·n·batch     B  n·m·batch    Q  n·n·batch    R  m·m·batch    Qf n·n·batch
+ *   x0 n·batch
+ *   K  m·n·(N-1)·batch     sol.K[k], k = 1..N-1  (LQRSolution.K)
+ *   P  n·n·batch  (p_mode 0: P_1 = solver.P on return, :63)
+ *      n·n·N·batch (p_mode 1: P_k for k = 1..N, P_N = Qf)
+ *   X  n·N·batch           sol.X
+ *   U  m·(N-1)·batch       sol.U
+ *   info int32·batch : 0, or the knot k (1-based) of the first E = R + BᵀPB found not
+ *        positive definite in the backward sweep (the reference discards potrf's info,
+ *        dynamic_programming.jl:29; the solve still runs to completion, as there).
+ * ------------------------------------------------------------------------------------ */
+typedef struct lqrx_dp_desc {
+    int32_t n, m, N;        /* state dim, control dim, knots (N >= 2)                 */
+    int32_t dtype;          /* LQRX_F64 (reference precision) or LQRX_F32            */
+    int64_t batch;          /* number of independent problems                          */
+    int32_t layout;         /* 0 = column-major, batch slowest (only value supported)  */
+    int32_t p_mode;         /* 0 = P_1 only (reference-observable), 1 = all P_k        */
+    int64_t knot_stride_AB; /* 0 = time-invariant (reference LQRProblem); >0 reserved  */
+    int64_t knot_stride_QR; /* 0 = time-invariant; >0 reserved                         */
+} lqrx_dp_desc;
+
+/* device pointers (hipMalloc'd or torch CUDA/HIP tensors) */
+int lqrx_dp_solve(const lqrx_dp_desc *desc, const void *A, const void *B, const void *Q,
+                  const void *R, const void *Qf, const void *x0, void *K, void *P, void *X,
+                  void *U, int32_t *info, void *stream);
+
+/* host pointers: H2D, solve, D2H, synchronous (what the Julia shim calls by default) */
+int lqrx_dp_solve_host(const lqrx_dp_desc *desc, const void *A, const void *B, const void *Q,
+                       const void *R, const void *Qf, const void *x0, void *K, void *P,
+                       void *X, void *U, int32_t *info);
+
+/* ------------------------------------------------------------------------------------
+ * KKT path: one inner solve of CholeskySolver._solve!(solver)
+ *   /root/reference/src/cholesky_solver.jl:166-182
+ * = calculate_shur_factors! (jacobian_blocks.jl:220-286) → cholesky!(chol, shur)
+ *   (cholesky_solve.jl:206-226) → forward_/backward_substitution! (:252-302) →
+ *   calculate_primals! (cholesky_solver.jl:185-236); ginv = 0 gives the
+ *   second_order_correction! variant (cholesky_solver.jl:254-273): δẑ = −Dᵀ(DDᵀ)⁻¹d.
+ *
+ * Block structure (shared by the whole batch) = ConstraintBlocks (conblocks.jl:403-425):
+ * knot k (0-based here) has n1[k] previous-dynamics rows D2, p[k] stage rows C, n2[k]
+ * dynamics rows D1 and width w[k] (= n̄ + m for k < N-1, n̄ at the last knot).
+ * Packed per-trajectory inputs, each block column-major, concatenated over k:
+ *   Y  (n1+p+n2)×w   Y = [D2; C; D1]   (ConstraintBlock.Y)
+ *   y  p+n2          y = [c; d]        (ConstraintBlock.y)
+ *   H  h_mode 0/1: w×w cost Hessian (dense / block-diagonal Q,R; BlockCholesky modes,
+ *      block_cholesky.jl:55-77);  h_mode 2: the w diagonal entries (:82-91)
+ *   g  w             gradient [q; r]  (InvertedQuadratic gradient, block_cholesky.jl:126)
+ * Outputs:
+ *   dz  w per knot  (δZ, get_step ordering [x1;u1;…;xN])
+ *   lam p+n2 per knot  [μ_k; λ_k]  (get_multipliers ordering)
+ *   info int32·batch: 0 ok; k+1 if a Schur diagonal block at knot k was not SPD;
+ *        −(k+1) if H_k was not SPD.
+ * ------------------------------------------------------------------------------------ */
+typedef struct lqrx_kkt_desc {
+    int32_t N;          /* knots                                                  */
+    int32_t dtype;      /* LQRX_F64 only                                          */
+    int64_t batch;
+    const int32_t *n1;  /* [N] host arrays describing the block structure           */
+    const int32_t *p;   /* [N]                                                      */
+    const int32_t *n2;  /* [N]                                                      */
+    const int32_t *w;   /* [N]                                                      */
+    int32_t h_mode;     /* 0 dense, 1 block-diagonal, 2 diagonal                    */
+    int32_t ginv;       /* 1 = _solve!;  0 = second-order-correction variant        */
+    int32_t layout;     /* 0 = per-trajectory packed, batch slowest                 */
+    int32_t reserved;
+} lqrx_kkt_desc;
+
+int lqrx_kkt_solve(const lqrx_kkt_desc *desc, const void *Y, const void *y, const void *H,
+                   const void *g, void *dz, void *lam, int32_t *info, void *stream);
+int lqrx_kkt_solve_host(const lqrx_kkt_desc *desc, const void *Y, const void *y,
+                        const void *H, const void *g, void *dz, void *lam, int32_t *info);
+/* sizes (elements per trajectory) of the packed KKT buffers, for allocation */
+int lqrx_kkt_sizes(const lqrx_kkt_desc *desc, int64_t *nY, int64_t *ny, int64_t *nH,
+                   int64_t *ng, int64_t *nlam);
+
+/* ------------------------------------------------------------------------------------
+ * Utilities
+ * ------------------------------------------------------------------------------------ */
+int lqrx_abi_version(void);
+const char *lqrx_last_error(void);
+/* 1 if the HIP runtime sees a gfx950 device, else 0 (no compute; safe without a GPU) */
+int lqrx_device_available(void);
+
+/* Deterministic synthetic random-dense LQR batch: counter-based
+ * splitmix64 + Box–Muller keyed by (seed, trajectory, field, element); host memory,
+ * multi-threaded.  A = I + (0.1/√n)G, B = G/√n, Q = I + GᵀG/n, R = I + GᵀG/m, Qf = 10Q,
+ * x0 ~ N(0,1).  traj0 offsets the trajectory index (to generate one shard of a batch). */
+int lqrx_make_random_dp(int32_t n, int32_t m, int64_t batch, int64_t traj0, uint64_t seed,
+                        int32_t dtype, void *A, void *B, void *Q, void *R, void *Qf,
+                        void *x0);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LQRX_H */

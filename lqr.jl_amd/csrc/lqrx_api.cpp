@@ -1,0 +1,391 @@
+// lqrx_api.cpp — the C ABI (include/lqrx.h): argument validation, stream-ordered scratch,
+// host-pointer convenience wrappers, the synthetic-problem generator.
+#include "../../include/lqrx.h"
+#include "lqrx_internal.h"
+
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int set_err(int code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int hip_err(hipError_t e, const char *what)
+{
+    return set_err(LQRX_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+size_t dsize(int dtype) { return dtype == LQRX_F32 ? 4 : 8; }
+
+// ---- stream-ordered device buffers (for the *_host wrappers) ----
+struct DevBuf {
+    void *p = nullptr;
+    ~DevBuf()
+    {
+        if (p) (void)hipFree(p);
+    }
+};
+
+int dev_alloc(DevBuf &b, size_t bytes, const char *name)
+{
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e != hipSuccess) return hip_err(e, name);
+    return 0;
+}
+
+int validate_dp(const lqrx_dp_desc *d)
+{
+    if (!d) return set_err(-1, "desc is NULL");
+    if (d->n < 1) return set_err(-1, "desc.n must be >= 1 (got %d)", d->n);
+    if (d->m < 1) return set_err(-1, "desc.m must be >= 1 (got %d)", d->m);
+    if (d->N < 2) return set_err(-1, "desc.N must be >= 2 (got %d)", d->N);
+    if (d->dtype != LQRX_F64 && d->dtype != LQRX_F32)
+        return set_err(-1, "desc.dtype must be LQRX_F64 or LQRX_F32 (got %d)", d->dtype);
+    if (d->batch < 0) return set_err(-1, "desc.batch must be >= 0");
+    if (d->layout != 0) return set_err(LQRX_ERR_UNSUPPORTED, "desc.layout %d not supported", d->layout);
+    if (d->p_mode != 0 && d->p_mode != 1) return set_err(-1, "desc.p_mode must be 0 or 1");
+    if (d->knot_stride_AB != 0 || d->knot_stride_QR != 0)
+        return set_err(LQRX_ERR_UNSUPPORTED, "time-varying knot strides are not supported yet");
+    if (!lqrx::dp_supported(d->dtype, d->n, d->m))
+        return set_err(LQRX_ERR_UNSUPPORTED, "no kernel instantiated for n=%d m=%d", d->n, d->m);
+    return 0;
+}
+
+} // namespace
+
+extern "C" {
+
+int lqrx_abi_version(void) { return LQRX_ABI_VERSION; }
+
+const char *lqrx_last_error(void) { return g_err.c_str(); }
+
+int lqrx_device_available(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n < 1) return 0;
+    hipDeviceProp_t prop;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
+    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+}
+
+int lqrx_dp_solve(const lqrx_dp_desc *d, const void *A, const void *B, const void *Q,
+                  const void *R, const void *Qf, const void *x0, void *K, void *P, void *X,
+                  void *U, int32_t *info, void *stream)
+{
+    int st = validate_dp(d);
+    if (st) return st;
+    if (d->batch == 0) return 0;
+    const void *in[6] = {A, B, Q, R, Qf, x0};
+    for (int i = 0; i < 6; ++i)
+        if (!in[i]) return set_err(-(i + 2), "input pointer %d is NULL", i + 2);
+    void *out[4] = {K, P, X, U};
+    for (int i = 0; i < 4; ++i)
+        if (!out[i]) return set_err(-(i + 8), "output pointer %d is NULL", i + 8);
+
+    lqrx::DpArgs a{};
+    a.A = A; a.B = B; a.Q = Q; a.R = R; a.Qf = Qf; a.x0 = x0;
+    a.K = K; a.P = P; a.X = X; a.U = U; a.info = info;
+    a.n = d->n; a.m = d->m; a.N = d->N; a.dtype = d->dtype; a.p_all = d->p_mode;
+    a.batch = d->batch;
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = lqrx::dp_launch(a, s);
+    if (e == hipErrorNotSupported)
+        return set_err(LQRX_ERR_UNSUPPORTED, "no kernel for n=%d m=%d", d->n, d->m);
+    if (e != hipSuccess) return hip_err(e, "dp kernel launch");
+    if (stream == nullptr) {
+        e = hipStreamSynchronize(nullptr);
+        if (e != hipSuccess) return hip_err(e, "dp kernel");
+        if (info) {
+            std::vector<int32_t> h((size_t)d->batch);
+            e = hipMemcpy(h.data(), info, h.size() * 4, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) return hip_err(e, "info D2H");
+            for (int32_t v : h)
+                if (v) return 1;
+        }
+    }
+    return 0;
+}
+
+int lqrx_dp_solve_host(const lqrx_dp_desc *d, const void *A, const void *B, const void *Q,
+                       const void *R, const void *Qf, const void *x0, void *K, void *P,
+                       void *X, void *U, int32_t *info)
+{
+    int st = validate_dp(d);
+    if (st) return st;
+    if (d->batch == 0) return 0;
+    const size_t s = dsize(d->dtype), bt = (size_t)d->batch;
+    const size_t n = d->n, m = d->m, N = d->N;
+    const size_t szin[6] = {n * n, n * m, n * n, m * m, n * n, n};
+    const void *hin[6] = {A, B, Q, R, Qf, x0};
+    const size_t szout[4] = {m * n * (N - 1), d->p_mode ? n * n * N : n * n, n * N, m * (N - 1)};
+    void *hout[4] = {K, P, X, U};
+    DevBuf din[6], dout[4], dinfo;
+    for (int i = 0; i < 6; ++i) {
+        if (!hin[i]) return set_err(-(i + 2), "input pointer %d is NULL", i + 2);
+        if ((st = dev_alloc(din[i], szin[i] * s * bt, "hipMalloc input"))) return st;
+        hipError_t e = hipMemcpy(din[i].p, hin[i], szin[i] * s * bt, hipMemcpyHostToDevice);
+        if (e != hipSuccess) return hip_err(e, "H2D");
+    }
+    for (int i = 0; i < 4; ++i) {
+        if (!hout[i]) return set_err(-(i + 8), "output pointer %d is NULL", i + 8);
+        if ((st = dev_alloc(dout[i], szout[i] * s * bt, "hipMalloc output"))) return st;
+    }
+    if ((st = dev_alloc(dinfo, 4 * bt, "hipMalloc info"))) return st;
+    st = lqrx_dp_solve(d, din[0].p, din[1].p, din[2].p, din[3].p, din[4].p, din[5].p, dout[0].p,
+                       dout[1].p, dout[2].p, dout[3].p, (int32_t *)dinfo.p, nullptr);
+    if (st < 0) return st;
+    for (int i = 0; i < 4; ++i) {
+        hipError_t e = hipMemcpy(hout[i], dout[i].p, szout[i] * s * bt, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return hip_err(e, "D2H");
+    }
+    if (info) {
+        hipError_t e = hipMemcpy(info, dinfo.p, 4 * bt, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return hip_err(e, "D2H info");
+    }
+    return st;
+}
+
+
+// ------------------------------------------------------------------ KKT
+namespace {
+struct KktLayout {
+    std::vector<int32_t> meta; // per knot: n1, p, n2, w, oY, oy, oH, og
+    int64_t sY = 0, sy = 0, sH = 0, sg = 0;
+    int maxw = 0, maxrows = 0;
+};
+
+int kkt_layout(const lqrx_kkt_desc *d, KktLayout &L)
+{
+    if (!d) return set_err(-1, "desc is NULL");
+    if (d->N < 1) return set_err(-1, "desc.N must be >= 1");
+    if (d->dtype != LQRX_F64) return set_err(LQRX_ERR_UNSUPPORTED, "KKT path is fp64 only");
+    if (d->batch < 0) return set_err(-1, "desc.batch must be >= 0");
+    if (!d->n1 || !d->p || !d->n2 || !d->w) return set_err(-1, "block-size arrays are NULL");
+    if (d->h_mode < 0 || d->h_mode > 2) return set_err(-1, "desc.h_mode must be 0, 1 or 2");
+    if (d->ginv != 0 && d->ginv != 1) return set_err(-1, "desc.ginv must be 0 or 1");
+    if (d->layout != 0) return set_err(LQRX_ERR_UNSUPPORTED, "desc.layout must be 0");
+    L.meta.assign((size_t)d->N * 8, 0);
+    for (int k = 0; k < d->N; ++k) {
+        int n1 = d->n1[k], p = d->p[k], n2 = d->n2[k], w = d->w[k];
+        if (n1 < 0 || p < 0 || n2 < 0 || w < 1)
+            return set_err(-1, "knot %d: negative block size or w < 1", k);
+        if (k == 0 && n1 != 0) return set_err(-1, "knot 0 must have n1 == 0");
+        if (k > 0 && n1 != d->n2[k - 1])
+            return set_err(-1, "knot %d: n1 (%d) != n2 of knot %d (%d)", k, n1, k - 1, d->n2[k - 1]);
+        if (k == d->N - 1 && n2 != 0) return set_err(-1, "last knot must have n2 == 0");
+        int rows = n1 + p + n2;
+        if (rows > 64 || w > 64)
+            return set_err(LQRX_ERR_UNSUPPORTED, "knot %d: block %dx%d larger than 64", k, rows, w);
+        int32_t *m = &L.meta[(size_t)k * 8];
+        m[0] = n1; m[1] = p; m[2] = n2; m[3] = w;
+        m[4] = (int32_t)L.sY; m[5] = (int32_t)L.sy; m[6] = (int32_t)L.sH; m[7] = (int32_t)L.sg;
+        L.sY += (int64_t)rows * w;
+        L.sy += p + n2;
+        L.sH += d->h_mode == 2 ? w : (int64_t)w * w;
+        L.sg += w;
+        L.maxw = std::max(L.maxw, w);
+        L.maxrows = std::max(L.maxrows, rows);
+    }
+    if (L.sY > INT32_MAX) return set_err(LQRX_ERR_UNSUPPORTED, "trajectory too large");
+    return 0;
+}
+} // namespace
+
+extern "C" int lqrx_kkt_sizes(const lqrx_kkt_desc *d, int64_t *nY, int64_t *ny, int64_t *nH,
+                              int64_t *ng, int64_t *nlam)
+{
+    KktLayout L;
+    int st = kkt_layout(d, L);
+    if (st) return st;
+    if (nY) *nY = L.sY;
+    if (ny) *ny = L.sy;
+    if (nH) *nH = L.sH;
+    if (ng) *ng = L.sg;
+    if (nlam) *nlam = L.sy;
+    return 0;
+}
+
+extern "C" int lqrx_kkt_solve(const lqrx_kkt_desc *d, const void *Y, const void *y, const void *H,
+                              const void *g, void *dz, void *lam, int32_t *info, void *stream)
+{
+    KktLayout L;
+    int st = kkt_layout(d, L);
+    if (st) return st;
+    if (d->batch == 0) return 0;
+    const void *in[4] = {Y, y, H, g};
+    for (int i = 0; i < 4; ++i)
+        if (!in[i]) return set_err(-(i + 2), "input pointer %d is NULL", i + 2);
+    if (!dz) return set_err(-6, "dz is NULL");
+    if (!lam) return set_err(-7, "lam is NULL");
+    hipStream_t s = (hipStream_t)stream;
+    // stream-ordered upload of the block-structure table
+    int32_t *dmeta = nullptr;
+    size_t mb = L.meta.size() * sizeof(int32_t);
+    hipError_t e = hipMallocAsync((void **)&dmeta, mb, s);
+    if (e != hipSuccess) return hip_err(e, "hipMallocAsync meta");
+    e = hipMemcpyAsync(dmeta, L.meta.data(), mb, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return hip_err(e, "meta H2D");
+    lqrx::KktArgs a{};
+    a.Y = (const double *)Y; a.y = (const double *)y; a.H = (const double *)H; a.g = (const double *)g;
+    a.dz = (double *)dz; a.lam = (double *)lam; a.info = info; a.meta = dmeta;
+    a.N = d->N; a.h_mode = d->h_mode; a.ginv = d->ginv; a.batch = d->batch;
+    a.sY = L.sY; a.sy = L.sy; a.sH = L.sH; a.sg = L.sg; a.sl = L.sy;
+    a.maxw = L.maxw; a.maxrows = L.maxrows;
+    e = lqrx::kkt_launch(a, s);
+    hipError_t ef = hipFreeAsync(dmeta, s);
+    if (e == hipErrorNotSupported) return set_err(LQRX_ERR_UNSUPPORTED, "KKT kernel unavailable");
+    if (e != hipSuccess) return hip_err(e, "kkt kernel launch");
+    if (ef != hipSuccess) return hip_err(ef, "hipFreeAsync meta");
+    if (stream == nullptr) {
+        e = hipStreamSynchronize(nullptr);
+        if (e != hipSuccess) return hip_err(e, "kkt kernel");
+        if (info) {
+            std::vector<int32_t> h((size_t)d->batch);
+            e = hipMemcpy(h.data(), info, h.size() * 4, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) return hip_err(e, "info D2H");
+            for (int32_t v : h)
+                if (v) return 1;
+        }
+    }
+    return 0;
+}
+
+extern "C" int lqrx_kkt_solve_host(const lqrx_kkt_desc *d, const void *Y, const void *y,
+                                   const void *H, const void *g, void *dz, void *lam,
+                                   int32_t *info)
+{
+    KktLayout L;
+    int st = kkt_layout(d, L);
+    if (st) return st;
+    if (d->batch == 0) return 0;
+    const size_t bt = (size_t)d->batch;
+    const size_t szin[4] = {(size_t)L.sY, (size_t)L.sy, (size_t)L.sH, (size_t)L.sg};
+    const void *hin[4] = {Y, y, H, g};
+    DevBuf din[4], ddz, dlam, dinfo;
+    for (int i = 0; i < 4; ++i) {
+        if (!hin[i]) return set_err(-(i + 2), "input pointer %d is NULL", i + 2);
+        if ((st = dev_alloc(din[i], szin[i] * 8 * bt, "hipMalloc input"))) return st;
+        hipError_t e = hipMemcpy(din[i].p, hin[i], szin[i] * 8 * bt, hipMemcpyHostToDevice);
+        if (e != hipSuccess) return hip_err(e, "H2D");
+    }
+    if (!dz) return set_err(-6, "dz is NULL");
+    if (!lam) return set_err(-7, "lam is NULL");
+    if ((st = dev_alloc(ddz, (size_t)L.sg * 8 * bt, "hipMalloc dz"))) return st;
+    if ((st = dev_alloc(dlam, (size_t)L.sy * 8 * bt, "hipMalloc lam"))) return st;
+    if ((st = dev_alloc(dinfo, 4 * bt, "hipMalloc info"))) return st;
+    st = lqrx_kkt_solve(d, din[0].p, din[1].p, din[2].p, din[3].p, ddz.p, dlam.p,
+                        (int32_t *)dinfo.p, nullptr);
+    if (st < 0) return st;
+    hipError_t e = hipMemcpy(dz, ddz.p, (size_t)L.sg * 8 * bt, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(lam, dlam.p, (size_t)L.sy * 8 * bt, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && info) e = hipMemcpy(info, dinfo.p, 4 * bt, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_err(e, "D2H");
+    return st;
+}
+
+// ------------------------------------------------------------------ generator
+static inline uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+static inline double gauss(uint64_t seed, uint64_t traj, uint64_t field, uint64_t elem)
+{
+    uint64_t h = splitmix64(seed ^ splitmix64(traj ^ splitmix64((field << 40) ^ elem)));
+    uint64_t h2 = splitmix64(h);
+    double u1 = ((h >> 11) + 1.0) * (1.0 / 9007199254740992.0); // (0, 1]
+    double u2 = (h2 >> 11) * (1.0 / 9007199254740992.0);        // [0, 1)
+    return std::sqrt(-2.0 * std::log(u1)) * std::cos(6.283185307179586 * u2);
+}
+
+static void gen_one(int n, int m, uint64_t seed, uint64_t t, double *A, double *B, double *Q,
+                    double *R, double *Qf, double *x0, std::vector<double> &G)
+{
+    const double sn = std::sqrt((double)n);
+    for (int j = 0; j < n; ++j)
+        for (int i = 0; i < n; ++i)
+            A[i + j * n] = (i == j ? 1.0 : 0.0) + (0.1 / sn) * gauss(seed, t, 0, i + j * n);
+    for (int j = 0; j < m; ++j)
+        for (int i = 0; i < n; ++i) B[i + j * n] = gauss(seed, t, 1, i + j * n) / sn;
+    G.resize((size_t)n * n);
+    for (int e = 0; e < n * n; ++e) G[e] = gauss(seed, t, 2, e);
+    for (int j = 0; j < n; ++j)
+        for (int i = 0; i < n; ++i) {
+            double s = 0.0;
+            for (int p = 0; p < n; ++p) s += G[p + i * n] * G[p + j * n];
+            Q[i + j * n] = (i == j ? 1.0 : 0.0) + s / n;
+        }
+    G.resize((size_t)m * m);
+    for (int e = 0; e < m * m; ++e) G[e] = gauss(seed, t, 3, e);
+    for (int j = 0; j < m; ++j)
+        for (int i = 0; i < m; ++i) {
+            double s = 0.0;
+            for (int p = 0; p < m; ++p) s += G[p + i * m] * G[p + j * m];
+            R[i + j * m] = (i == j ? 1.0 : 0.0) + s / m;
+        }
+    for (int e = 0; e < n * n; ++e) Qf[e] = 10.0 * Q[e];
+    for (int i = 0; i < n; ++i) x0[i] = gauss(seed, t, 4, i);
+}
+
+int lqrx_make_random_dp(int32_t n, int32_t m, int64_t batch, int64_t traj0, uint64_t seed,
+                        int32_t dtype, void *A, void *B, void *Q, void *R, void *Qf, void *x0)
+{
+    if (n < 1) return set_err(-1, "n must be >= 1");
+    if (m < 1) return set_err(-2, "m must be >= 1");
+    if (batch < 0) return set_err(-3, "batch must be >= 0");
+    if (dtype != LQRX_F64 && dtype != LQRX_F32) return set_err(-6, "bad dtype");
+    void *outs[6] = {A, B, Q, R, Qf, x0};
+    for (int i = 0; i < 6; ++i)
+        if (!outs[i]) return set_err(-(7 + i), "output pointer is NULL");
+    const size_t nn = (size_t)n * n, nm = (size_t)n * m, mm = (size_t)m * m;
+    unsigned nth = std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
+    if ((int64_t)nth > batch) nth = (unsigned)std::max<int64_t>(1, batch);
+    auto work = [&](unsigned tid) {
+        std::vector<double> a(nn), b(nm), q(nn), r(mm), qf(nn), x(n), G;
+        for (int64_t t = tid; t < batch; t += nth) {
+            gen_one(n, m, seed, (uint64_t)(traj0 + t), a.data(), b.data(), q.data(), r.data(),
+                    qf.data(), x.data(), G);
+            auto put = [&](void *dst, const std::vector<double> &src, size_t cnt) {
+                if (dtype == LQRX_F64)
+                    std::memcpy((double *)dst + t * cnt, src.data(), cnt * 8);
+                else
+                    for (size_t e = 0; e < cnt; ++e) ((float *)dst)[t * cnt + e] = (float)src[e];
+            };
+            put(A, a, nn); put(B, b, nm); put(Q, q, nn); put(R, r, mm); put(Qf, qf, nn);
+            put(x0, x, n);
+        }
+    };
+    std::vector<std::thread> th;
+    for (unsigned i = 1; i < nth; ++i) th.emplace_back(work, i);
+    work(0);
+    for (auto &t : th) t.join();
+    return 0;
+}
+
+} // extern "C"

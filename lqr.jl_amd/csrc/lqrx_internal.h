@@ -1,0 +1,35 @@
+// lqrx_internal.h — kernel argument blocks shared by the launchers and the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lqrx {
+
+struct DpArgs {
+    const void *A, *B, *Q, *R, *Qf, *x0; // device inputs, layout 0
+    void *K, *P, *X, *U;                 // device outputs
+    int32_t *info;                       // device [batch] or null
+    int n, m, N;
+    int dtype; // 0 f64, 1 f32
+    int p_all;
+    int64_t batch;
+};
+
+hipError_t dp_launch(const DpArgs &a, hipStream_t s);
+bool dp_supported(int dtype, int n, int m);
+
+struct KktArgs {
+    const double *Y, *y, *H, *g; // device, packed per trajectory
+    double *dz, *lam;
+    int32_t *info;
+    const int32_t *meta; // device: per knot {n1, p, n2, w, oY, oy, oH, og(=oz), ol}
+    int N;
+    int h_mode, ginv;
+    int64_t batch;
+    int64_t sY, sy, sH, sg, sl; // per-trajectory strides (elements)
+    int maxw, maxrows;
+};
+
+hipError_t kkt_launch(const KktArgs &a, hipStream_t s);
+
+} // namespace lqrx

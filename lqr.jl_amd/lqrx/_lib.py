@@ -1,0 +1,93 @@
+"""ctypes binding of the lqrx C ABI (include/lqrx.h).
+
+The shared library is built in-tree (``lqr.jl_amd/csrc/Makefile`` → ``lqrx/liblqrx.so``).
+There is no fallback: if the library is missing, importing the compute entry points raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblqrx.so")
+HEADER_PATH = os.path.abspath(os.path.join(_HERE, "..", "..", "include", "lqrx.h"))
+
+F64, F32 = 0, 1
+ERR_HIP, ERR_UNSUPPORTED, ERR_NODEVICE = -100, -101, -102
+
+
+class DpDesc(C.Structure):
+    """Mirror of ``lqrx_dp_desc``."""
+
+    _fields_ = [
+        ("n", C.c_int32), ("m", C.c_int32), ("N", C.c_int32), ("dtype", C.c_int32),
+        ("batch", C.c_int64), ("layout", C.c_int32), ("p_mode", C.c_int32),
+        ("knot_stride_AB", C.c_int64), ("knot_stride_QR", C.c_int64),
+    ]
+
+
+class KktDesc(C.Structure):
+    """Mirror of ``lqrx_kkt_desc``."""
+
+    _fields_ = [
+        ("N", C.c_int32), ("dtype", C.c_int32), ("batch", C.c_int64),
+        ("n1", C.POINTER(C.c_int32)), ("p", C.POINTER(C.c_int32)),
+        ("n2", C.POINTER(C.c_int32)), ("w", C.POINTER(C.c_int32)),
+        ("h_mode", C.c_int32), ("ginv", C.c_int32), ("layout", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+
+_VP = C.c_void_p
+_SIGS = {
+    "lqrx_abi_version": (C.c_int, []),
+    "lqrx_last_error": (C.c_char_p, []),
+    "lqrx_device_available": (C.c_int, []),
+    "lqrx_dp_solve": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 10 + [_VP, _VP]),
+    "lqrx_dp_solve_host": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 10 + [_VP]),
+    "lqrx_kkt_solve": (C.c_int, [C.POINTER(KktDesc)] + [_VP] * 7 + [_VP]),
+    "lqrx_kkt_solve_host": (C.c_int, [C.POINTER(KktDesc)] + [_VP] * 7),
+    "lqrx_kkt_sizes": (C.c_int, [C.POINTER(KktDesc)] + [C.POINTER(C.c_int64)] * 5),
+    "lqrx_make_random_dp": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_uint64,
+                                      C.c_int32] + [_VP] * 6),
+}
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load liblqrx.so (once).  Raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"lqrx native library not built: {LIB_PATH} is missing "
+            "(run `make -C lqr.jl_amd/csrc` or __graft_entry__.build())")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def header_functions() -> list[str]:
+    """Names of every function declared in include/lqrx.h."""
+    src = open(HEADER_PATH).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(lqrx_\w+)\s*\(", src, re.M)))
+
+
+class LqrxError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"lqrx error {code}: {msg}")
+        self.code = code
+
+
+def check(code: int) -> int:
+    """Raise LqrxError for negative return codes; return 0/1 otherwise."""
+    if code < 0:
+        raise LqrxError(code, load().lqrx_last_error().decode())
+    return code

@@ -1,0 +1,217 @@
+"""Host-side mirror of the reference's DP (Riccati) surface, backed by the HIP kernels.
+
+Reference surface (Julia, /root/reference/src):
+  LQRProblem{n,m,T}(Qf, Q, R, A, B, x0, u0, tf, N)        lqr_problem.jl:1-11
+  size(prob) = (n, m, N); num_vars(prob) = N n + (N-1) m   lqr_problem.jl:21-25
+  DPSolver(prob)                                           dynamic_programming.jl:13-23
+  LQRSolution (exported, undefined upstream: fields K, X, U as used by :62-69)
+  solve!(sol, solver, prob)                                dynamic_programming.jl:54-72
+
+Array conventions here: a single problem uses plain (rows, cols) numpy matrices; batches
+use numpy arrays shaped (batch, rows, cols).  The C ABI wants Julia column-major with the
+batch slowest; ``to_abi``/``from_abi`` convert (a transpose of the last two axes).
+Every compute call goes through liblqrx.so — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+
+__all__ = ["LQRProblem", "LQRSolution", "DPSolver", "solve", "solve_batch", "LQRBatch",
+           "random_batch", "to_abi", "from_abi", "dp_solve_device"]
+
+
+def to_abi(a: np.ndarray) -> np.ndarray:
+    """(batch, r, c) row-major logical matrices → contiguous column-major-per-matrix."""
+    a = np.asarray(a)
+    if a.ndim == 2:  # vectors (batch, r)
+        return np.ascontiguousarray(a)
+    return np.ascontiguousarray(np.swapaxes(a, -1, -2))
+
+
+def from_abi(a: np.ndarray, shape: tuple) -> np.ndarray:
+    """Inverse of to_abi: flat ABI buffer → (…, r, c) logical matrices."""
+    *lead, r, c = shape
+    return np.swapaxes(np.asarray(a).reshape(*lead, c, r), -1, -2)
+
+
+@dataclass
+class LQRProblem:
+    """Time-invariant finite-horizon LQR problem (lqr_problem.jl:1-11)."""
+
+    Qf: np.ndarray
+    Q: np.ndarray
+    R: np.ndarray
+    A: np.ndarray
+    B: np.ndarray
+    x0: np.ndarray
+    u0: np.ndarray | None = None
+    tf: float = 1.0
+    N: int = 2
+
+    def size(self):
+        n, m = self.B.shape
+        return n, m, self.N
+
+    def num_vars(self):
+        n, m, N = self.size()
+        return N * n + (N - 1) * m
+
+
+@dataclass
+class LQRSolution:
+    """Output container the reference exports but never defines.
+
+    K[k] (m×n) for k = 1..N-1 stored at index k-1; X[k] (n), U[k] (m); P = P_1 (what
+    solver.P holds after solve!) or all P_k when constructed with all_P=True.
+    """
+
+    K: np.ndarray
+    X: np.ndarray
+    U: np.ndarray
+    P: np.ndarray
+    info: int = 0
+
+    @classmethod
+    def of(cls, prob: LQRProblem, all_P: bool = False):
+        n, m, N = prob.size()
+        return cls(np.zeros((N - 1, m, n)), np.zeros((N, n)), np.zeros((N - 1, m)),
+                   np.zeros((N, n, n)) if all_P else np.zeros((n, n)))
+
+
+@dataclass
+class DPSolver:
+    """DPSolver(prob) (dynamic_programming.jl:13-23).  The Julia struct owns scratch
+    (P, P_, PA, PB, APB, E); here the scratch is registers/LDS inside the kernel, so the
+    solver only records the problem shape and dtype."""
+
+    n: int
+    m: int
+    N: int
+    dtype: int = _lib.F64
+
+    @classmethod
+    def of(cls, prob: LQRProblem, dtype: int = _lib.F64):
+        n, m, N = prob.size()
+        return cls(n, m, N, dtype)
+
+
+@dataclass
+class LQRBatch:
+    """A batch of LQRProblems with the same (n, m, N), arrays shaped (batch, r, c)."""
+
+    A: np.ndarray
+    B: np.ndarray
+    Q: np.ndarray
+    R: np.ndarray
+    Qf: np.ndarray
+    x0: np.ndarray
+    N: int
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def batch(self):
+        return self.A.shape[0]
+
+    def size(self):
+        return self.B.shape[1], self.B.shape[2], self.N
+
+    @classmethod
+    def of(cls, probs: list[LQRProblem]):
+        st = lambda f: np.stack([np.asarray(getattr(p, f), dtype=np.float64) for p in probs])
+        return cls(st("A"), st("B"), st("Q"), st("R"), st("Qf"), st("x0"), probs[0].N)
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def solve_batch(b: LQRBatch, dtype: int = _lib.F64, all_P: bool = False):
+    """Batched solve! through lqrx_dp_solve_host.  Returns dict of logical arrays
+    K (batch, N-1, m, n), P (batch, n, n) or (batch, N, n, n), X (batch, N, n),
+    U (batch, N-1, m), info (batch,), and the ABI return code."""
+    lib = _lib.load()
+    n, m, N = b.size()
+    bt = b.batch
+    npdt = np.float64 if dtype == _lib.F64 else np.float32
+    ins = [to_abi(np.asarray(x, dtype=npdt)) for x in (b.A, b.B, b.Q, b.R, b.Qf)]
+    x0 = np.ascontiguousarray(np.asarray(b.x0, dtype=npdt))
+    K = np.zeros(bt * (N - 1) * m * n, npdt)
+    P = np.zeros(bt * n * n * (N if all_P else 1), npdt)
+    X = np.zeros(bt * N * n, npdt)
+    U = np.zeros(bt * (N - 1) * m, npdt)
+    info = np.zeros(bt, np.int32)
+    d = _lib.DpDesc(n, m, N, dtype, bt, 0, 1 if all_P else 0, 0, 0)
+    rc = _lib.check(lib.lqrx_dp_solve_host(C.byref(d), *[_ptr(a) for a in ins], _ptr(x0),
+                                           _ptr(K), _ptr(P), _ptr(X), _ptr(U), _ptr(info)))
+    return dict(K=from_abi(K, (bt, N - 1, m, n)),
+                P=from_abi(P, (bt, N, n, n) if all_P else (bt, n, n)),
+                X=X.reshape(bt, N, n), U=U.reshape(bt, N - 1, m), info=info, rc=rc)
+
+
+def solve(sol: LQRSolution, solver: DPSolver, prob: LQRProblem) -> LQRSolution:
+    """solve!(sol, solver, prob) — dynamic_programming.jl:54-72 (one problem)."""
+    all_P = sol.P.ndim == 3
+    out = solve_batch(LQRBatch.of([prob]), solver.dtype, all_P)
+    sol.K[...] = out["K"][0]
+    sol.X[...] = out["X"][0]
+    sol.U[...] = out["U"][0]
+    sol.P[...] = out["P"][0]
+    sol.info = int(out["info"][0])
+    return sol
+
+
+def random_batch(n: int, m: int, N: int, batch: int, seed: int, traj0: int = 0,
+                 dtype: int = _lib.F64) -> dict:
+    """Synthetic random-dense batch from the library's counter-based generator, returned
+    in ABI layout (flat arrays) — the same bytes the bench feeds the kernel."""
+    lib = _lib.load()
+    npdt = np.float64 if dtype == _lib.F64 else np.float32
+    A = np.empty(batch * n * n, npdt); B = np.empty(batch * n * m, npdt)
+    Q = np.empty(batch * n * n, npdt); R = np.empty(batch * m * m, npdt)
+    Qf = np.empty(batch * n * n, npdt); x0 = np.empty(batch * n, npdt)
+    _lib.check(lib.lqrx_make_random_dp(n, m, batch, traj0, seed, dtype, _ptr(A), _ptr(B),
+                                       _ptr(Q), _ptr(R), _ptr(Qf), _ptr(x0)))
+    return dict(A=A, B=B, Q=Q, R=R, Qf=Qf, x0=x0, n=n, m=m, N=N, batch=batch)
+
+
+def abi_to_batch(d: dict) -> LQRBatch:
+    n, m, N, bt = d["n"], d["m"], d["N"], d["batch"]
+    return LQRBatch(from_abi(d["A"], (bt, n, n)), from_abi(d["B"], (bt, n, m)),
+                    from_abi(d["Q"], (bt, n, n)), from_abi(d["R"], (bt, m, m)),
+                    from_abi(d["Qf"], (bt, n, n)), d["x0"].reshape(bt, n), N)
+
+
+def dp_solve_device(t: dict, N: int, p_mode: int = 0, stream: int | None = None,
+                    out: dict | None = None) -> dict:
+    """Device-pointer entry point on torch tensors already in ABI layout (flat).
+
+    t: dict with torch tensors A, B, Q, R, Qf, x0 on the GPU and ints n, m, batch.
+    Returns dict of output tensors (K, P, X, U, info).  `stream` is a raw hipStream_t
+    (torch.cuda.current_stream().cuda_stream); None = the null stream, synchronous.
+    """
+    import torch
+
+    lib = _lib.load()
+    n, m, bt = t["n"], t["m"], t["batch"]
+    tdt = t["A"].dtype
+    dtype = _lib.F64 if tdt == torch.float64 else _lib.F32
+    dev = t["A"].device
+    if out is None:
+        out = dict(K=torch.empty(bt * (N - 1) * m * n, dtype=tdt, device=dev),
+                   P=torch.empty(bt * n * n * (N if p_mode else 1), dtype=tdt, device=dev),
+                   X=torch.empty(bt * N * n, dtype=tdt, device=dev),
+                   U=torch.empty(bt * (N - 1) * m, dtype=tdt, device=dev),
+                   info=torch.empty(bt, dtype=torch.int32, device=dev))
+    d = _lib.DpDesc(n, m, N, dtype, bt, 0, p_mode, 0, 0)
+    p = lambda x: C.c_void_p(x.data_ptr())
+    rc = lib.lqrx_dp_solve(C.byref(d), p(t["A"]), p(t["B"]), p(t["Q"]), p(t["R"]), p(t["Qf"]),
+                           p(t["x0"]), p(out["K"]), p(out["P"]), p(out["X"]), p(out["U"]),
+                           p(out["info"]), C.c_void_p(stream) if stream else None)
+    _lib.check(rc)
+    out["rc"] = rc
+    return out

@@ -1,0 +1,191 @@
+"""CPU ORACLE (test infrastructure only) — Python side.
+
+Loaded only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the
+checker.  Wraps oracle/liblqr_oracle.so (the plain-C restatement in lqr_oracle.c, which
+cites the reference lines it follows) and adds numpy identities used to PIN it:
+
+  * dp_dense_kkt:  the DP rollout must equal the optimum of the equality-constrained QP
+      min Σ ½xᵀQx + ½uᵀRu + ½x_Nᵀ Qf x_N  s.t. x1 = x0, x_{k+1} = A x_k + B u_k
+    solved densely (the reference's own DP≡KKT equivalence).
+  * kkt_dense: the dense quantities test/cholesky_solve.jl:18-44 compares against
+      S = D H⁻¹Dᵀ, r = D H⁻¹g − d, λ = −S⁻¹r, δz = −H⁻¹(Dᵀλ + g), full KKT solve.
+Parity status: KKT pinned by the reference's known-answer identities; DP pinned by
+identities only (the reference's DP test holds no assertion and Julia is unavailable).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblqr_oracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return LIB_PATH
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        lib = C.CDLL(LIB_PATH)
+        vp, i32, i64 = C.c_void_p, C.c_int, C.c_int64
+        lib.oracle_dp_solve_batch.restype = i64
+        lib.oracle_dp_solve_batch.argtypes = [i32, i32, i32, i64] + [vp] * 8 + [i32, vp, vp, vp,
+                                                                                 i32]
+        lib.oracle_kkt_solve_one.restype = i32
+        lib.oracle_kkt_solve_one.argtypes = [i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, i32, vp,
+                                             vp, vp, vp, vp]
+        lib.oracle_kkt_solve_batch.restype = i64
+        lib.oracle_kkt_solve_batch.argtypes = [i32, vp, vp, vp, vp, i64, vp, vp, i32, vp, vp,
+                                               i32, vp, vp, vp, i32]
+        lib.oracle_num_threads_max.restype = i32
+        _lib = lib
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+# ------------------------------------------------------------------------- DP
+def dp_solve_abi(d: dict, N: int, all_P: bool = False, nthreads: int = 1) -> dict:
+    """Oracle DP on ABI-layout (flat, column-major, batch slowest) float64 inputs."""
+    lib = load()
+    n, m, bt = d["n"], d["m"], d["batch"]
+    f = lambda k: np.ascontiguousarray(np.asarray(d[k], dtype=np.float64))
+    A, B, Q, R, Qf, x0 = (f(k) for k in ("A", "B", "Q", "R", "Qf", "x0"))
+    K = np.zeros(bt * (N - 1) * m * n)
+    P = np.zeros(bt * n * n * (N if all_P else 1))
+    X = np.zeros(bt * N * n)
+    U = np.zeros(bt * (N - 1) * m)
+    info = np.zeros(bt, np.int32)
+    lib.oracle_dp_solve_batch(n, m, N, bt, _p(A), _p(B), _p(Q), _p(R), _p(Qf), _p(x0), _p(K),
+                              _p(P), 1 if all_P else 0, _p(X), _p(U), _p(info), nthreads)
+    return dict(K=K, P=P, X=X, U=U, info=info)
+
+
+def dp_dense_kkt(A, B, Q, R, Qf, x0, N):
+    """Dense equality-constrained QP optimum of one LQR problem (logical row-major
+    matrices).  Returns (X (N,n), U (N-1,m))."""
+    n, m = B.shape
+    nz = N * n + (N - 1) * m
+    H = np.zeros((nz, nz))
+    ix = lambda k: slice(k * (n + m), k * (n + m) + n)
+    iu = lambda k: slice(k * (n + m) + n, k * (n + m) + n + m)
+    for k in range(N - 1):
+        H[ix(k), ix(k)] = Q
+        H[iu(k), iu(k)] = R
+    H[ix(N - 1), ix(N - 1)] = Qf
+    D = np.zeros((N * n, nz))
+    d = np.zeros(N * n)
+    D[0:n, ix(0)] = np.eye(n)
+    d[0:n] = -x0
+    for k in range(N - 1):
+        r = slice((k + 1) * n, (k + 2) * n)
+        D[r, ix(k)] = A
+        D[r, iu(k)] = B
+        D[r, ix(k + 1)] = -np.eye(n)
+    Kkt = np.block([[H, D.T], [D, np.zeros((N * n, N * n))]])
+    sol = np.linalg.solve(Kkt, np.concatenate([np.zeros(nz), -d]))
+    z = sol[:nz]
+    X = np.stack([z[ix(k)] for k in range(N)])
+    U = np.stack([z[iu(k)] for k in range(N - 1)])
+    return X, U
+
+
+# ------------------------------------------------------------------------- KKT
+class KktStructure:
+    """Per-knot block sizes (conblocks.jl:403-425) for the dynamics + stage-constraint
+    structure: n̄ = n (no Lie group), n1 = n for k>1, n2 = n for k<N, w = n + m·(k<N)."""
+
+    def __init__(self, n: int, m: int, N: int, p):
+        self.n, self.m, self.N = n, m, N
+        p = np.broadcast_to(np.asarray(p, dtype=np.int32), (N,)).copy()
+        self.p = p
+        self.n1 = np.array([0] + [n] * (N - 1), np.int32)
+        self.n2 = np.array([n] * (N - 1) + [0], np.int32)
+        self.w = np.array([n + m] * (N - 1) + [n], np.int32)
+        self.rows = self.n1 + self.p + self.n2
+        self.sY = int(np.sum(self.rows * self.w))
+        self.sy = int(np.sum(self.p + self.n2))
+        self.sg = int(np.sum(self.w))
+        self.P = self.sy
+
+    def sH(self, h_mode):
+        return self.sg if h_mode == 2 else int(np.sum(self.w * self.w))
+
+
+def kkt_solve_one(st: KktStructure, Y, y, H, g, h_mode=2, ginv=1, debug=False):
+    lib = load()
+    dz = np.zeros(st.sg)
+    lam = np.zeros(st.P)
+    S = np.zeros(st.P * st.P) if debug else None
+    U = np.zeros(st.P * st.P) if debug else None
+    r = np.zeros(st.P) if debug else None
+    f = lambda a: np.ascontiguousarray(a, dtype=np.float64)
+    Y, y, H, g = f(Y), f(y), f(H), f(g)
+    info = lib.oracle_kkt_solve_one(st.N, _p(st.n1), _p(st.p), _p(st.n2), _p(st.w), _p(Y), _p(y),
+                                    h_mode, _p(H), _p(g), ginv, _p(dz), _p(lam), _p(S), _p(U),
+                                    _p(r))
+    out = dict(dz=dz, lam=lam, info=info)
+    if debug:
+        out.update(S=S.reshape(st.P, st.P, order="F"), U=U.reshape(st.P, st.P, order="F"), r=r)
+    return out
+
+
+def kkt_solve_batch(st: KktStructure, bt, Y, y, H, g, h_mode=2, ginv=1, nthreads=1):
+    lib = load()
+    dz = np.zeros(bt * st.sg)
+    lam = np.zeros(bt * st.P)
+    info = np.zeros(bt, np.int32)
+    f = lambda a: np.ascontiguousarray(a, dtype=np.float64)
+    Y, y, H, g = f(Y), f(y), f(H), f(g)
+    lib.oracle_kkt_solve_batch(st.N, _p(st.n1), _p(st.p), _p(st.n2), _p(st.w), bt, _p(Y), _p(y),
+                               h_mode, _p(H), _p(g), ginv, _p(dz), _p(lam), _p(info), nthreads)
+    return dict(dz=dz, lam=lam, info=info)
+
+
+def kkt_dense(st: KktStructure, Y, y, H, g, h_mode=2):
+    """Dense assembly (copy_blocks!, conblocks.jl:429-442; build_H!) and the dense
+    quantities of test/cholesky_solve.jl:18-44."""
+    N = st.N
+    NN, P = st.sg, st.P
+    D = np.zeros((P, NN))
+    d = np.zeros(P)
+    Hd = np.zeros((NN, NN))
+    gd = np.zeros(NN)
+    oY = oy = oH = og = 0
+    off1 = off2 = 0
+    for k in range(N):
+        rows, w = int(st.rows[k]), int(st.w[k])
+        Yk = np.asarray(Y[oY:oY + rows * w]).reshape(w, rows).T
+        D[off1:off1 + rows, off2:off2 + w] = Yk
+        n1 = int(st.n1[k])
+        d[off1 + n1:off1 + rows] = y[oy:oy + rows - n1]
+        if h_mode == 2:
+            Hd[off2:off2 + w, off2:off2 + w] = np.diag(H[oH:oH + w])
+            oH += w
+        else:
+            Hd[off2:off2 + w, off2:off2 + w] = np.asarray(H[oH:oH + w * w]).reshape(w, w).T
+            oH += w * w
+        gd[off2:off2 + w] = g[og:og + w]
+        oY += rows * w
+        oy += rows - n1
+        og += w
+        off1 += n1 + int(st.p[k])
+        off2 += w
+    HiDt = np.linalg.solve(Hd, D.T)
+    S = D @ HiDt
+    r = D @ np.linalg.solve(Hd, gd) - d
+    lam = -np.linalg.solve(S, r)
+    dz = -np.linalg.solve(Hd, D.T @ lam + gd)
+    full = np.linalg.solve(np.block([[Hd, D.T], [D, np.zeros((P, P))]]), np.concatenate([-gd, -d]))
+    return dict(D=D, d=d, H=Hd, g=gd, S=S, r=r, lam=lam, dz=dz, full=full)

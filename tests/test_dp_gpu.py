@@ -1,0 +1,98 @@
+"""GPU parity: batched Riccati kernel (liblqrx.so, via the C ABI) vs the CPU oracle.
+
+Oracle = oracle/lqr_oracle.c, restating /root/reference/src/dynamic_programming.jl:28-72.
+Tolerance (north star): max|K − K_ref| / max|K_ref| ≤ 1e-10 per knot in fp64, same for P
+(and X, U); fp32 runs are held to 1e-4 against the fp64 oracle.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL64 = 1e-10
+TOL32 = 1e-4
+
+
+def relerr_per_knot(a, b):
+    """max over knots of max|a−b| / max|b| (leading axes: batch, knot)."""
+    a = a.reshape(a.shape[0], a.shape[1], -1)
+    b = b.reshape(b.shape[0], b.shape[1], -1)
+    num = np.abs(a - b).max(axis=2)
+    den = np.abs(b).max(axis=2)
+    den[den == 0] = 1.0
+    return float((num / den).max())
+
+
+def run_pair(lqrx, oracle, n, m, N, batch, seed, dtype=0, all_P=True):
+    from lqrx.dp import abi_to_batch
+
+    d = lqrx.random_batch(n, m, N, batch, seed)
+    b = abi_to_batch(d)
+    got = lqrx.solve_batch(b, dtype=dtype, all_P=all_P)
+    ref = oracle.dp_solve_abi(d, N, all_P=all_P)
+    from lqrx.dp import from_abi
+
+    refK = from_abi(ref["K"], (batch, N - 1, m, n))
+    refP = from_abi(ref["P"], (batch, N, n, n) if all_P else (batch, n, n))
+    refX = ref["X"].reshape(batch, N, n)
+    refU = ref["U"].reshape(batch, N - 1, m)
+    return got, dict(K=refK, P=refP, X=refX, U=refU, info=ref["info"])
+
+
+@pytest.mark.parametrize("n,m,N,batch", [
+    (4, 1, 101, 64),      # cartpole-sized (cfg1/cfg2 shape)
+    (6, 3, 30, 37),       # DoubleIntegrator(3) shape, ragged batch
+    (16, 16, 12, 5),      # exact single tiles
+    (17, 5, 9, 3),        # padded 2×1 tiles
+    (32, 16, 16, 8),      # cfg4 shape, short horizon
+    (32, 16, 256, 4),     # cfg4 shape, full horizon
+    (32, 32, 20, 3),      # 2×2 tiles
+])
+def test_dp_parity_f64(lqrx, oracle, gpu_ok, n, m, N, batch):
+    got, ref = run_pair(lqrx, oracle, n, m, N, batch, seed=1000 + n * 7 + m)
+    assert got["rc"] == 0 and (got["info"] == 0).all()
+    assert relerr_per_knot(got["K"], ref["K"]) <= TOL64
+    P = got["P"]
+    assert relerr_per_knot(P, ref["P"]) <= TOL64
+    assert relerr_per_knot(got["X"][:, :, None], ref["X"][:, :, None]) <= TOL64 or \
+        np.abs(got["X"] - ref["X"]).max() <= TOL64 * max(1.0, np.abs(ref["X"]).max())
+    assert np.abs(got["U"] - ref["U"]).max() <= TOL64 * max(1.0, np.abs(ref["U"]).max())
+
+
+def test_dp_p1_only(lqrx, oracle, gpu_ok):
+    """p_mode 0 returns P_1 = solver.P after solve! (dynamic_programming.jl:63)."""
+    got, ref = run_pair(lqrx, oracle, 32, 16, 40, 6, seed=5, all_P=False)
+    assert relerr_per_knot(got["P"][:, None], ref["P"][:, None]) <= TOL64
+
+
+@pytest.mark.parametrize("n,m,N,batch", [(32, 16, 64, 4), (4, 1, 101, 16)])
+def test_dp_parity_f32(lqrx, oracle, gpu_ok, n, m, N, batch):
+    got, ref = run_pair(lqrx, oracle, n, m, N, batch, seed=77, dtype=1)
+    assert relerr_per_knot(got["K"].astype(np.float64), ref["K"]) <= TOL32
+    assert relerr_per_knot(got["P"].astype(np.float64), ref["P"]) <= TOL32
+
+
+def test_dp_non_spd_sets_info(lqrx, oracle, gpu_ok):
+    """A non-SPD R makes E = R + BᵀPB indefinite at the first backward knot: the kernel
+    reports it per trajectory (the reference discards potrf's info)."""
+    from lqrx.dp import abi_to_batch
+
+    n, m, N, bt = 6, 3, 10, 4
+    d = lqrx.random_batch(n, m, N, bt, seed=3)
+    b = abi_to_batch(d)
+    b.R[1] = -100.0 * np.eye(m)      # trajectory 1 is broken
+    b.B[1] *= 1e-3
+    got = lqrx.solve_batch(b)
+    assert got["rc"] == 1
+    assert got["info"][1] == N - 1
+    assert got["info"][0] == 0 and got["info"][2] == 0 and got["info"][3] == 0
+
+
+def test_dp_deterministic(lqrx, gpu_ok):
+    from lqrx.dp import abi_to_batch
+
+    d = lqrx.random_batch(32, 16, 32, 16, seed=11)
+    b = abi_to_batch(d)
+    a1 = lqrx.solve_batch(b)
+    a2 = lqrx.solve_batch(b)
+    assert np.array_equal(a1["K"], a2["K"]) and np.array_equal(a1["X"], a2["X"])
