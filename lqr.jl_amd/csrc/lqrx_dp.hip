@@ -25,60 +25,75 @@
 #include "lqrx_tile.h"
 #include "lqrx_internal.h"
 
+#ifndef LQRX_DP_WAVES
+#define LQRX_DP_WAVES 2
+#endif
+#ifndef LQRX_DP_BCAST
+#define LQRX_DP_BCAST 0
+#endif
+#ifndef LQRX_DP_VAR
+#define LQRX_DP_VAR 0
+#endif
+
 namespace lqrx {
 
-// Augmented upper Cholesky solve.  aug (LDS, column-major, column stride CS) holds
-// [E | G] with E MP×MP (upper triangle used, as potrf 'U' does) and G MP×NP.  On return
-// the G columns hold K = E⁻¹G (potrs 'U': Uᵀ Y = G, then U K = Y).  Each lane owns the
-// columns lane + 64q.  Returns false (wave-uniform) if a pivot was not > 0.
-// Also streams K (true m×n part) to global `Kout` (column-major, ld m) when Kout != null.
-template <typename T, int MP, int NP, int CS>
-__device__ __forceinline__ bool aug_chol_solve(T *aug, int lane, int m, int n, T *__restrict__ Kout)
+// Forward LDLᵀ sweep on the augmented matrix [E | G | I] — the factor/solve of
+// chol_solve! (dynamic_programming.jl:28-31: potrf 'U' + potrs 'U'), reorganised so that
+// it costs the fewest VALU instructions (fp64 VALU does not overlap fp64 MFMA on gfx950).
+//
+// E = L D Lᵀ (unit-lower L; D_ii are exactly potrf's squared pivots U_ii², so the
+// potrf failure test "pivot ≤ 0" is unchanged).  One column of [E | G | I] per lane
+// (columns lane + 64q).  Step i:  piv = E'[i][i] (v_readlane of lane i), t = x[i]/piv,
+// x[p] −= E'[i][p]·t for p > i, where the unscaled pivot row E'[i][p] reaches every lane
+// as a uniform LDS read (BCAST = 1) or v_readlane (BCAST = 0).  Afterwards
+//   G columns hold Y = L⁻¹G,  I columns hold W = L⁻¹,  and rinv[i] = 1/piv_i,
+// so  K = E⁻¹G = Wᵀ·(D⁻¹Y)  — finished by the caller as one TN MFMA product.
+// Column images written back to LDS: aug[MP..MP+NP) ← Y, aug[MP+NP..2MP+NP) ← W,
+// rinv (MP values) at aug + (2MP+NP)·CS.  Returns false if a pivot was not > 0.
+template <typename T, int MP, int NP, int CS, int BCAST>
+__device__ __forceinline__ bool aug_ldl_forward(T *aug, int lane)
 {
-    constexpr int NC = MP + NP;
+    constexpr int NC = MP + NP + MP;
     constexpr int CPL = (NC + 63) / 64;
+    T *rowbuf = aug + NC * CS;        // 64-wide broadcast row (reused every step)
+    T *rinv = rowbuf + 64;            // 1/pivot per row
     T x[CPL][MP];
 #pragma unroll
     for (int q = 0; q < CPL; ++q) {
         int c = lane + 64 * q;
+        if (c < MP + NP) {
 #pragma unroll
-        for (int i = 0; i < MP; ++i) x[q][i] = (c < NC) ? aug[c * CS + i] : (T)0;
+            for (int i = 0; i < MP; ++i) x[q][i] = aug[c * CS + i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < MP; ++i) x[q][i] = (c - MP - NP == i) ? (T)1 : (T)0;
+        }
     }
     bool ok = true;
-    T dinv[MP];
-    // forward: upper Cholesky of E and Uᵀ Y = G in one elimination sweep
 #pragma unroll
     for (int i = 0; i < MP; ++i) {
+        if constexpr (BCAST == 1) {
+            // publish row i of E' (final after step i-1) for the uniform reads below
+            rowbuf[lane] = x[0][i];   // 64-wide row buffer: no exec mask
+        }
         T piv = readlane(x[i / 64][i], i % 64);
         ok = ok && (piv > (T)0);
-        T d = sqrt(piv);
-        T di = (T)1 / d;
-        dinv[i] = di;
+        T ri = rcp_nr(piv);
+        if (lane == 0) rinv[i] = ri;
+        T t[CPL];
 #pragma unroll
-        for (int q = 0; q < CPL; ++q) x[q][i] *= di;
+        for (int q = 0; q < CPL; ++q) t[q] = x[q][i] * ri;
+        if constexpr (BCAST == 1) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 #pragma unroll
         for (int p = i + 1; p < MP; ++p) {
-            T u = readlane(x[p / 64][i], p % 64); // U[i][p], held by the owner of column p
+            T e;
+            if constexpr (BCAST == 1) e = rowbuf[p];
+            else e = readlane(x[p / 64][i], p % 64);
 #pragma unroll
-            for (int q = 0; q < CPL; ++q) x[q][p] = fma(-u, x[q][i], x[q][p]);
+            for (int q = 0; q < CPL; ++q) x[q][p] = fma(-e, t[q], x[q][p]);
         }
-    }
-    // backward: U K = Y on the G columns only (E columns keep U for the broadcasts)
-#pragma unroll
-    for (int j = MP - 1; j >= 0; --j) {
-        T kj[CPL];
-#pragma unroll
-        for (int q = 0; q < CPL; ++q) {
-            bool rhs = (lane + 64 * q) >= MP;
-            kj[q] = rhs ? x[q][j] * dinv[j] : (T)0;
-            x[q][j] = rhs ? kj[q] : x[q][j];
-        }
-#pragma unroll
-        for (int p = 0; p < j; ++p) {
-            T u = readlane(x[j / 64][p], j % 64); // U[p][j]
-#pragma unroll
-            for (int q = 0; q < CPL; ++q) x[q][p] = fma(-u, kj[q], x[q][p]);
-        }
+        if constexpr (BCAST == 1) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int q = 0; q < CPL; ++q) {
@@ -86,12 +101,6 @@ __device__ __forceinline__ bool aug_chol_solve(T *aug, int lane, int m, int n, T
         if (c >= MP && c < NC) {
 #pragma unroll
             for (int i = 0; i < MP; ++i) aug[c * CS + i] = x[q][i];
-            int j = c - MP;
-            if (Kout && j < n) {
-#pragma unroll
-                for (int i = 0; i < MP; ++i)
-                    if (i < m) Kout[(size_t)i + (size_t)j * m] = x[q][i];
-            }
         }
     }
     return ok;
@@ -100,20 +109,26 @@ __device__ __forceinline__ bool aug_chol_solve(T *aug, int lane, int m, int n, T
 template <typename T, int NT, int MT> struct DpCfg {
     static constexpr int NP = NT * 16, MP = MT * 16;
     static constexpr int CS = MP + 2;                       // padded LDS column stride
-    static constexpr int AUG = (MP + NP) * CS;              // [E | G] image
+    static constexpr int AUG = (MP + NP + MP) * CS + 64 + MP; // [E | G | I] image + row/rinv
     static constexpr int ROLL = MP * NP + NP + MP;          // K_k + x + u (rollout)
-    static constexpr int LDS_ELEMS = AUG > ROLL ? AUG : ROLL;
+    static constexpr int SYM = NP * (NP + 2);                // symmetrize image
+    static constexpr int LDS_ELEMS = (AUG > ROLL ? AUG : ROLL) > SYM ? (AUG > ROLL ? AUG : ROLL) : SYM;
     static constexpr int KPL = (MP * NP + 63) / 64;         // K elements per lane (rollout)
 };
 
 // Forward rollout  dynamic_programming.jl:66-70 :  u_k = −K_k x_k ; x_{k+1} = A x_k + B u_k.
 // K_k is streamed back from global (written by the backward sweep of this same wave),
-// DEPTH knots ahead, 64 lanes × KPL coalesced elements per knot.
+// DEPTH knots ahead, 64 lanes × KPL coalesced elements per knot, staged through LDS.
+// Dot products are split over the wave: u_i by SU = 64/MP lanes (i = lane % MP), x'_i by
+// SX = 64/NP lanes (i = lane % NP), partial sums combined with xor-shuffles.
 template <typename T, int NT, int MT, int DEPTH>
 __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, int lane)
 {
     using C = DpCfg<T, NT, MT>;
     constexpr int NP = C::NP, MP = C::MP, KPL = C::KPL;
+    constexpr int SU = 64 / MP > 0 ? 64 / MP : 1, SX = 64 / NP > 0 ? 64 / NP : 1;
+    constexpr int JU = NP / SU, JX = NP / SX, PX = MP / SX; // per-lane slice lengths
+    static_assert(MP <= 64 && NP <= 64, "rollout assumes n, m <= 64");
     const int n = a.n, m = a.m, N = a.N;
     const size_t mn = (size_t)m * n;
     const T *__restrict__ Kg = (const T *)a.K + (size_t)b * (size_t)(N - 1) * mn;
@@ -123,19 +138,24 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
     T *__restrict__ Ug = (T *)a.U + (size_t)b * (size_t)(N - 1) * m;
     T *Ks = lds, *xs = lds + MP * NP, *us = xs + NP;
 
-    // rows of A and B for the x-update (lane i < n owns row i)
-    T arow[NP], brow[MP];
+    const int iu = lane % MP, hu = lane / MP;   // u row, column part
+    const int ix = lane % NP, hx = lane / NP;   // x row, column part
+    T arow[JX], brow[PX];
 #pragma unroll
-    for (int j = 0; j < NP; ++j) arow[j] = (lane < n && j < n) ? Ag[lane + (size_t)j * n] : (T)0;
+    for (int t = 0; t < JX; ++t) {
+        int j = hx * JX + t;
+        arow[t] = (ix < n && j < n) ? Ag[ix + (size_t)j * n] : (T)0;
+    }
 #pragma unroll
-    for (int p = 0; p < MP; ++p) brow[p] = (lane < n && p < m) ? Bg[lane + (size_t)p * n] : (T)0;
-
+    for (int t = 0; t < PX; ++t) {
+        int p = hx * PX + t;
+        brow[t] = (ix < n && p < m) ? Bg[ix + (size_t)p * n] : (T)0;
+    }
     const T *x0 = (const T *)a.x0 + (size_t)b * n;
     if (lane < NP) xs[lane] = (lane < n) ? x0[lane] : (T)0;
     if (lane < MP) us[lane] = (T)0;
     if (lane < n) Xg[lane] = x0[lane];
 
-    // ring of DEPTH prefetched K knots
     T ring[DEPTH][KPL];
     auto issue = [&](int kk, T(&dst)[KPL]) {
 #pragma unroll
@@ -153,7 +173,6 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
         for (int d = 0; d < DEPTH; ++d) {
             const int k = k0 + d;
             if (k <= N - 1) {
-                // stage K_k into LDS (col-major m×n), refill this ring slot with K_{k+DEPTH}
 #pragma unroll
                 for (int s = 0; s < KPL; ++s) {
                     size_t e = (size_t)lane + 64 * s;
@@ -161,53 +180,62 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
                 }
                 issue(k + DEPTH, ring[d]);
                 __syncthreads();
-                if (lane < m) {
-                    T s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+                // u_i = −Σ_j K[i][j] x_j   (dynamic_programming.jl:68)
+                T s0 = 0, s1 = 0;
 #pragma unroll
-                    for (int j = 0; j < NP; j += 4) {
-                        if (j + 0 < n) s0 = fma(Ks[lane + (j + 0) * m], xs[j + 0], s0);
-                        if (j + 1 < n) s1 = fma(Ks[lane + (j + 1) * m], xs[j + 1], s1);
-                        if (j + 2 < n) s2 = fma(Ks[lane + (j + 2) * m], xs[j + 2], s2);
-                        if (j + 3 < n) s3 = fma(Ks[lane + (j + 3) * m], xs[j + 3], s3);
-                    }
-                    T u = -((s0 + s1) + (s2 + s3));
-                    us[lane] = u;
-                    Ug[(size_t)(k - 1) * m + lane] = u;
+                for (int t = 0; t < JU; t += 2) {
+                    int j0 = hu * JU + t, j1 = j0 + 1;
+                    if (j0 < n) s0 = fma(Ks[iu + j0 * m], xs[j0], s0);
+                    if (t + 1 < JU && j1 < n) s1 = fma(Ks[iu + j1 * m], xs[j1], s1);
+                }
+                T su = s0 + s1;
+#pragma unroll
+                for (int o = MP; o < 64; o <<= 1) su += __shfl_xor(su, o);
+                if (lane < m) {
+                    us[lane] = -su;
+                    Ug[(size_t)(k - 1) * m + lane] = -su;
                 }
                 __syncthreads();
-                T xn = 0;
+                // x_{k+1} = A x_k + B u_k   (:69)
+                T t0 = 0, t1 = 0;
+#pragma unroll
+                for (int t = 0; t < JX; t += 2) {
+                    t0 = fma(arow[t], xs[hx * JX + t], t0);
+                    if (t + 1 < JX) t1 = fma(arow[t + 1], xs[hx * JX + t + 1], t1);
+                }
+#pragma unroll
+                for (int t = 0; t < PX; ++t) t1 = fma(brow[t], us[hx * PX + t], t1);
+                T xn = t0 + t1;
+#pragma unroll
+                for (int o = NP; o < 64; o <<= 1) xn += __shfl_xor(xn, o);
+                __syncthreads();
                 if (lane < n) {
-                    T s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-#pragma unroll
-                    for (int j = 0; j < NP; j += 4) {
-                        s0 = fma(arow[j + 0], xs[j + 0], s0);
-                        s1 = fma(arow[j + 1], xs[j + 1], s1);
-                        s2 = fma(arow[j + 2], xs[j + 2], s2);
-                        s3 = fma(arow[j + 3], xs[j + 3], s3);
-                    }
-                    T t0 = 0, t1 = 0;
-#pragma unroll
-                    for (int p = 0; p < MP; p += 2) {
-                        t0 = fma(brow[p + 0], us[p + 0], t0);
-                        t1 = fma(brow[p + 1], us[p + 1], t1);
-                    }
-                    xn = ((s0 + s1) + (s2 + s3)) + (t0 + t1);
+                    xs[lane] = xn;
                     Xg[(size_t)k * n + lane] = xn;
                 }
-                __syncthreads();
-                if (lane < n) xs[lane] = xn;
                 __syncthreads();
             }
         }
     }
 }
 
-template <typename T, int NT, int MT>
-__global__ __launch_bounds__(64, 2) void dp_riccati_kernel(const DpArgs a)
+// Kernel variants (compile-time VAR bits):
+//   VAR_EXACT  : reference op order (explicit APB = A'PB, all n×n tiles of P_ computed,
+//                Q register-resident).  Default (0) is the fast form: APBᵀ = PBᵀA equals
+//                G = BᵀPA for symmetric P, so P_ = Q + AᵀPA − GᵀK; P_ is symmetric, so
+//                only its lower tiles are computed and the upper ones mirrored (LDS
+//                transpose); Q is re-read (L2/MALL-resident, 8 KB/traj) into the P_
+//                accumulators each knot so it holds no registers.
+//   VAR_NOSOLVE / VAR_NOROLL / VAR_NOKSTORE : diagnostic ablations (tools/dp_ablate).
+enum : int { VAR_EXACT = 1, VAR_NOSOLVE = 2, VAR_NOROLL = 4, VAR_NOKSTORE = 8 };
+
+template <typename T, int NT, int MT, int WAVES, int VAR, bool FULL>
+__global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
 {
     using C = DpCfg<T, NT, MT>;
     using acc = typename Tile<T>::acc;
-    constexpr int NP = C::NP, MP = C::MP, CS = C::CS;
+    constexpr int MP = C::MP, CS = C::CS;
+    constexpr bool EXACT = (VAR & VAR_EXACT) != 0;
     __shared__ T lds[C::LDS_ELEMS];
 
     const int lane = threadIdx.x;
@@ -215,13 +243,15 @@ __global__ __launch_bounds__(64, 2) void dp_riccati_kernel(const DpArgs a)
     if (b >= a.batch) return;
     const int n = a.n, m = a.m, N = a.N;
     const size_t nn = (size_t)n * n, nm = (size_t)n * m, mm = (size_t)m * m;
+    const T *Qg = (const T *)a.Q + b * nn;
 
-    acc At[NT][NT], Bt[NT][MT], Qt[NT][NT], Rt[MT][MT], P[NT][NT];
-    tiles_load<T, NT, NT>(At, (const T *)a.A + b * nn, n, n, n, lane, false);
-    tiles_load<T, NT, MT>(Bt, (const T *)a.B + b * nm, n, m, n, lane, false);
-    tiles_load<T, NT, NT>(Qt, (const T *)a.Q + b * nn, n, n, n, lane, false);
-    tiles_load<T, MT, MT>(Rt, (const T *)a.R + b * mm, m, m, m, lane, true);
-    tiles_load<T, NT, NT>(P, (const T *)a.Qf + b * nn, n, n, n, lane, false); // :58 P = Qf
+    acc At[NT][NT], Bt[NT][MT], Rt[MT][MT], P[NT][NT];
+    tiles_load<T, NT, NT, FULL>(At, (const T *)a.A + b * nn, n, n, n, lane, false);
+    tiles_load<T, NT, MT, FULL>(Bt, (const T *)a.B + b * nm, n, m, n, lane, false);
+    tiles_load<T, MT, MT, FULL>(Rt, (const T *)a.R + b * mm, m, m, m, lane, true);
+    tiles_load<T, NT, NT, FULL>(P, (const T *)a.Qf + b * nn, n, n, n, lane, false); // :58 P = Qf
+    acc Qt[EXACT ? NT : 1][EXACT ? NT : 1];
+    if constexpr (EXACT) tiles_load<T, NT, NT, FULL>(Qt, Qg, n, n, n, lane, false);
 
     T *Pall = a.p_all ? (T *)a.P + (size_t)b * nn * N : nullptr;
     if (Pall) tiles_store<T, NT, NT>(P, Pall + (size_t)(N - 1) * nn, n, n, n, lane);
@@ -229,60 +259,97 @@ __global__ __launch_bounds__(64, 2) void dp_riccati_kernel(const DpArgs a)
     int info = 0;
 
     for (int k = N - 1; k >= 1; --k) { // :61
-        acc PB[NT][MT], E[MT][MT], PA[NT][NT], G[MT][NT];
+        acc PB[NT][MT], E[MT][MT], PA[NT][NT], G[MT][NT], Pn[NT][NT];
         tiles_zero<T, NT, MT>(PB);
         mma_tn<T, NT, NT, MT>(PB, P, Bt);                          // :38 PB = P B
+        tiles_zero<T, NT, NT>(PA);
+        mma_tn<T, NT, NT, NT>(PA, P, At);                          // :40 PA = P A
+        if constexpr (EXACT) {
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j) Pn[i][j] = Qt[i][j];
+        } else {
+            tiles_load_lower<T, NT, FULL>(Pn, Qg, n, n, lane);            // P_ ← Q (lower tiles)
+        }
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
             for (int j = 0; j < MT; ++j) E[i][j] = Rt[i][j];
         mma_tn<T, NT, MT, MT>(E, Bt, PB);                          // :39 E = R + B'PB
-        tiles_zero<T, NT, NT>(PA);
-        mma_tn<T, NT, NT, NT>(PA, P, At);                          // :40 PA = P A
         tiles_zero<T, MT, NT>(G);
         mma_tn<T, NT, MT, NT>(G, Bt, PA);                          // :41 K = B'PA
+        if constexpr (EXACT) mma_tn<T, NT, NT, NT>(Pn, At, PA);    // :51 Q + A'PA
+        else mma_tn_lower<T, NT, NT>(Pn, At, PA);
 
         // :42 chol_solve!(E, K) — potrf 'U' + potrs 'U'
-        tiles_to_lds<T, MT, MT>(E, lds, CS, lane);
-        tiles_to_lds<T, MT, NT>(G, lds + MP * CS, CS, lane);
-        __syncthreads();
-        bool ok = aug_chol_solve<T, MP, NP, CS>(lds, lane, m, n, Kb + (size_t)(k - 1) * nm);
-        if (!ok && info == 0) info = k;
-        __syncthreads();
         acc Kt[MT][NT];
-        tiles_from_lds<T, MT, NT>(Kt, lds + MP * CS, CS, lane);
-        __syncthreads();
-
-        acc APBt[MT][NT];
-        tiles_zero<T, MT, NT>(APBt);
-        mma_tn<T, NT, MT, NT>(APBt, PB, At);                       // :50 APBᵀ = PBᵀ A
+        if constexpr ((VAR & VAR_NOSOLVE) != 0) {
 #pragma unroll
-        for (int i = 0; i < MT; ++i)
+            for (int i = 0; i < MT; ++i)
 #pragma unroll
-            for (int j = 0; j < NT; ++j) Kt[i][j] = -Kt[i][j];
+                for (int j = 0; j < NT; ++j) Kt[i][j] = G[i][j] * (T)1e-3 + E[0][0] * (T)1e-9;
+        } else {
+            tiles_to_lds<T, MT, MT>(E, lds, CS, lane);
+            tiles_to_lds<T, MT, NT>(G, lds + MP * CS, CS, lane);
+            __syncthreads();
+            bool ok = aug_ldl_forward<T, MP, C::NP, CS, LQRX_DP_BCAST>(lds, lane);
+            if (!ok && info == 0) info = k;
+            __syncthreads();
+            acc Yt[MT][NT], Wt[MT][MT];
+            tiles_from_lds<T, MT, NT>(Yt, lds + MP * CS, CS, lane);
+            tiles_from_lds<T, MT, MT>(Wt, lds + (MP + C::NP) * CS, CS, lane);
+            const T *rinv = lds + (2 * MP + C::NP) * CS + 64;
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    T s = rinv[i * 16 + Tile<T>::row(lane, r)];          // D⁻¹ row scale
+#pragma unroll
+                    for (int j = 0; j < NT; ++j) Yt[i][j][r] *= s;
+                }
+            __syncthreads();
+            tiles_zero<T, MT, NT>(Kt);
+            mma_tn<T, MT, MT, NT>(Kt, Wt, Yt);                     // K = Wᵀ(D⁻¹Y) = E⁻¹G
+            if constexpr ((VAR & VAR_NOKSTORE) == 0)
+                tiles_store<T, MT, NT, FULL>(Kt, Kb + (size_t)(k - 1) * nm, m, n, m, lane);
+        }
+        if constexpr (EXACT) {
+            acc APBt[MT][NT];
+            tiles_zero<T, MT, NT>(APBt);
+            mma_tn<T, NT, MT, NT>(APBt, PB, At);                   // :50 APBᵀ = PBᵀ A
+            mma_tn<T, MT, NT, NT, true>(Pn, APBt, Kt);             // :51 − APB K
+        } else {
+            mma_tn_lower<T, MT, NT, true>(Pn, G, Kt);              //     − GᵀK  (= APB K)
+            tiles_symmetrize_lower<T, NT>(Pn, lds, lane);          // P_ exactly symmetric
+        }
 #pragma unroll
         for (int i = 0; i < NT; ++i)
 #pragma unroll
-            for (int j = 0; j < NT; ++j) P[i][j] = Qt[i][j];
-        mma_tn<T, NT, NT, NT>(P, At, PA);                          // :51 Q + A'PA
-        mma_tn<T, MT, NT, NT>(P, APBt, Kt);                        //     − APB K
+            for (int j = 0; j < NT; ++j) P[i][j] = Pn[i][j];
         if (Pall) tiles_store<T, NT, NT>(P, Pall + (size_t)(k - 1) * nn, n, n, n, lane);
     }
     if (!a.p_all) tiles_store<T, NT, NT>(P, (T *)a.P + (size_t)b * nn, n, n, n, lane);
     if (a.info && lane == 0) a.info[b] = info;
 
-    // make this wave's K stores visible to its own (other-lane) rollout loads
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    dp_rollout<T, NT, MT, 4>(a, b, lds, lane);
+    if constexpr ((VAR & VAR_NOROLL) == 0) {
+        // make this wave's K stores visible to its own (other-lane) rollout loads
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        dp_rollout<T, NT, MT, 4>(a, b, lds, lane);
+    }
 }
 
 // ------------------------------------------------------------------ launcher
-template <typename T, int NT, int MT> static hipError_t launch_dp(const DpArgs &a, hipStream_t s)
+template <typename T, int NT, int MT, int WAVES = 2, int VAR = 0>
+static hipError_t launch_dp(const DpArgs &a, hipStream_t s)
 {
     dim3 grid((unsigned)a.batch), block(64);
-    hipLaunchKernelGGL((dp_riccati_kernel<T, NT, MT>), grid, block, 0, s, a);
+    if (a.n == NT * 16 && a.m == MT * 16)
+        hipLaunchKernelGGL((dp_riccati_kernel<T, NT, MT, WAVES, VAR, true>), grid, block, 0, s, a);
+    else
+        hipLaunchKernelGGL((dp_riccati_kernel<T, NT, MT, WAVES, VAR, false>), grid, block, 0, s, a);
     return hipGetLastError();
 }
 
@@ -291,7 +358,7 @@ hipError_t dp_launch(const DpArgs &a, hipStream_t s)
     const int nt = (a.n + 15) / 16, mt = (a.m + 15) / 16;
     if (a.dtype == 0) {
         if (nt == 1 && mt == 1) return launch_dp<double, 1, 1>(a, s);
-        if (nt == 2 && mt == 1) return launch_dp<double, 2, 1>(a, s);
+        if (nt == 2 && mt == 1) return launch_dp<double, 2, 1, LQRX_DP_WAVES, LQRX_DP_VAR>(a, s);
         if (nt == 2 && mt == 2) return launch_dp<double, 2, 2>(a, s);
     } else {
         if (nt == 1 && mt == 1) return launch_dp<float, 1, 1>(a, s);

@@ -24,6 +24,11 @@ template <> struct Tile<double> {
     {
         return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
     }
+    // D = −A·B + C  (f64 MFMA neg modifier on A: blgp bit 0 → "neg:[1,0,0]")
+    static __device__ __forceinline__ acc mma_nega(double a, double b, acc c)
+    {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 1);
+    }
     static __device__ __forceinline__ int row(int lane, int r) { return (lane >> 4) + 4 * r; }
 };
 
@@ -32,6 +37,11 @@ template <> struct Tile<float> {
     static __device__ __forceinline__ acc mma(float a, float b, acc c)
     {
         return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    // f32 MFMA has no neg modifier (blgp is a broadcast control): negate the operand
+    static __device__ __forceinline__ acc mma_nega(float a, float b, acc c)
+    {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(-a, b, c, 0, 0, 0);
     }
     static __device__ __forceinline__ int row(int lane, int r) { return 4 * (lane >> 4) + r; }
 };
@@ -55,7 +65,7 @@ __device__ __forceinline__ float readlane(float v, int src)
 // D[I][J] += Σ_k M[k][I]ᵀ Y[k][J]  over KT k-tiles; M is KT×I tiles, Y is KT×J tiles.
 // Loop order (k-tile, k-slice outermost, output tiles innermost) keeps consecutive MFMAs
 // on different accumulators wherever I·J > 1.
-template <typename T, int KT, int I, int J>
+template <typename T, int KT, int I, int J, bool NEG = false>
 __device__ __forceinline__ void mma_tn(typename Tile<T>::acc (&D)[I][J],
                                        const typename Tile<T>::acc (&M)[KT][I],
                                        const typename Tile<T>::acc (&Y)[KT][J])
@@ -67,7 +77,9 @@ __device__ __forceinline__ void mma_tn(typename Tile<T>::acc (&D)[I][J],
 #pragma unroll
             for (int i = 0; i < I; ++i)
 #pragma unroll
-                for (int j = 0; j < J; ++j) D[i][j] = Tile<T>::mma(M[k][i][r], Y[k][j][r], D[i][j]);
+                for (int j = 0; j < J; ++j)
+                    D[i][j] = NEG ? Tile<T>::mma_nega(M[k][i][r], Y[k][j][r], D[i][j])
+                                  : Tile<T>::mma(M[k][i][r], Y[k][j][r], D[i][j]);
 }
 
 template <typename T, int I, int J>
@@ -80,8 +92,10 @@ __device__ __forceinline__ void tiles_zero(typename Tile<T>::acc (&D)[I][J])
 }
 
 // Load a rows×cols column-major matrix (leading dim ld) into C-layout tiles, zero padded.
-// If diag_pad, padded diagonal entries are 1 (keeps a padded SPD block SPD).
-template <typename T, int I, int J>
+// If diag_pad, padded diagonal entries are 1 (keeps a padded SPD block SPD).  Loads are
+// unconditional (out-of-range lanes read element 0 and select the pad value) so the tile
+// load is one straight run of global loads; FULL = dimensions are exact multiples of 16.
+template <typename T, int I, int J, bool FULL = false>
 __device__ __forceinline__ void tiles_load(typename Tile<T>::acc (&D)[I][J], const T *__restrict__ src,
                                            int rows, int cols, int ld, int lane, bool diag_pad)
 {
@@ -92,14 +106,14 @@ __device__ __forceinline__ void tiles_load(typename Tile<T>::acc (&D)[I][J], con
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 int row = i * 16 + Tile<T>::row(lane, r), col = j * 16 + tcol(lane);
-                T v = (T)0;
-                if (row < rows && col < cols) v = src[(size_t)row + (size_t)col * ld];
-                else if (diag_pad && row == col) v = (T)1;
+                bool ok = FULL || (row < rows && col < cols);
+                T v = src[ok ? (size_t)row + (size_t)col * ld : 0];
+                if (!FULL) v = ok ? v : ((diag_pad && row == col) ? (T)1 : (T)0);
                 D[i][j][r] = v;
             }
 }
 
-template <typename T, int I, int J>
+template <typename T, int I, int J, bool FULL = false>
 __device__ __forceinline__ void tiles_store(const typename Tile<T>::acc (&D)[I][J], T *__restrict__ dst,
                                             int rows, int cols, int ld, int lane)
 {
@@ -110,7 +124,7 @@ __device__ __forceinline__ void tiles_store(const typename Tile<T>::acc (&D)[I][
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 int row = i * 16 + Tile<T>::row(lane, r), col = j * 16 + tcol(lane);
-                if (row < rows && col < cols) dst[(size_t)row + (size_t)col * ld] = D[i][j][r];
+                if (FULL || (row < rows && col < cols)) dst[(size_t)row + (size_t)col * ld] = D[i][j][r];
             }
 }
 
@@ -143,6 +157,113 @@ __device__ __forceinline__ void tiles_from_lds(typename Tile<T>::acc (&D)[I][J],
                 int row = i * 16 + Tile<T>::row(lane, r), col = j * 16 + tcol(lane);
                 D[i][j][r] = lds[row + col * cs];
             }
+}
+
+// D[i][j] += Σ_k M[k][i]ᵀ Y[k][j] for the lower tiles i >= j only (symmetric results).
+template <typename T, int KT, int NT, bool NEG = false>
+__device__ __forceinline__ void mma_tn_lower(typename Tile<T>::acc (&D)[NT][NT],
+                                             const typename Tile<T>::acc (&M)[KT][NT],
+                                             const typename Tile<T>::acc (&Y)[KT][NT])
+{
+#pragma unroll
+    for (int k = 0; k < KT; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+#pragma unroll
+                for (int j = 0; j <= i; ++j)
+                    D[i][j] = NEG ? Tile<T>::mma_nega(M[k][i][r], Y[k][j][r], D[i][j])
+                                  : Tile<T>::mma(M[k][i][r], Y[k][j][r], D[i][j]);
+}
+
+// Load the lower tiles (i >= j) of a rows×cols column-major matrix; upper tiles zeroed.
+template <typename T, int NT, bool FULL = false>
+__device__ __forceinline__ void tiles_load_lower(typename Tile<T>::acc (&D)[NT][NT], const T *__restrict__ src,
+                                                 int rows, int cols, int lane)
+{
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                int row = i * 16 + Tile<T>::row(lane, r), col = j * 16 + tcol(lane);
+                if (j > i) { D[i][j][r] = (T)0; continue; }
+                bool ok = FULL || (row < rows && col < cols);
+                T v = src[ok ? (size_t)row + (size_t)col * rows : 0];
+                D[i][j][r] = (FULL || ok) ? v : (T)0;
+            }
+}
+
+// Make a tile matrix exactly symmetric from its lower triangle: every element above the
+// diagonal (upper tiles AND the upper half of diagonal tiles) is replaced by its mirror.
+// Needed for the fast form P_ = Q + AᵀPA − GᵀK, whose accuracy relies on P staying
+// symmetric (GᵀK equals the reference's APB·K only for symmetric P).  Goes through an
+// NT·16 × NT·16 column-major LDS image with column stride NT·16 + 2.
+template <typename T, int NT>
+__device__ __forceinline__ void tiles_symmetrize_lower(typename Tile<T>::acc (&D)[NT][NT], T *lds,
+                                                       int lane)
+{
+    constexpr int S = NT * 16 + 2;
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                lds[(i * 16 + Tile<T>::row(lane, r)) + (j * 16 + tcol(lane)) * S] = D[i][j][r];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int j = i; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                int row = i * 16 + Tile<T>::row(lane, r), col = j * 16 + tcol(lane);
+                T v = lds[col + row * S];
+                if (row < col) D[i][j][r] = v;
+            }
+    __syncthreads();
+}
+
+// 1/a: hardware estimate (v_rcp_f64: max rel err 4.6e-8 measured on gfx950, see
+// profiles/r01/lat_probe.txt) + one Newton step → ~2e-15 relative.
+__device__ __forceinline__ double rcp_nr(double a)
+{
+    double y = __builtin_amdgcn_rcp(a);
+#pragma unroll
+    for (int it = 0; it < 1; ++it) {
+        double e = fma(-a, y, 1.0);
+        y = fma(y, e, y);
+    }
+    return y;
+}
+__device__ __forceinline__ float rcp_nr(float a)
+{
+    float y = __builtin_amdgcn_rcpf(a);
+    float e = fmaf(-a, y, 1.0f);
+    return fmaf(y, e, y);
+}
+
+// 1/sqrt(a): hardware estimate + Newton steps to full precision.
+__device__ __forceinline__ double rsqrt_nr(double a)
+{
+    double y = __builtin_amdgcn_rsq(a);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        double h = 0.5 * a * y;
+        double r = fma(-h, y, 0.5);
+        y = fma(y, r, y);
+    }
+    return y;
+}
+__device__ __forceinline__ float rsqrt_nr(float a)
+{
+    float y = __builtin_amdgcn_rsqf(a);
+    float h = 0.5f * a * y;
+    float r = fmaf(-h, y, 0.5f);
+    return fmaf(y, r, y);
 }
 
 } // namespace lqrx
