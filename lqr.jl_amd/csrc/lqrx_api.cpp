@@ -174,7 +174,7 @@ namespace {
 struct KktLayout {
     std::vector<int32_t> meta; // per knot: n1, p, n2, w, oY, oy, oH, og
     int64_t sY = 0, sy = 0, sH = 0, sg = 0;
-    int maxw = 0, maxrows = 0;
+    int maxw = 0, maxrows = 0, max_p1 = 0, max_ps = 0, max_p2 = 0;
 };
 
 int kkt_layout(const lqrx_kkt_desc *d, KktLayout &L)
@@ -208,6 +208,9 @@ int kkt_layout(const lqrx_kkt_desc *d, KktLayout &L)
         L.sg += w;
         L.maxw = std::max(L.maxw, w);
         L.maxrows = std::max(L.maxrows, rows);
+        L.max_p1 = std::max(L.max_p1, n1);
+        L.max_ps = std::max(L.max_ps, p);
+        L.max_p2 = std::max(L.max_p2, n2);
     }
     if (L.sY > INT32_MAX) return set_err(LQRX_ERR_UNSUPPORTED, "trajectory too large");
     return 0;
@@ -254,6 +257,7 @@ extern "C" int lqrx_kkt_solve(const lqrx_kkt_desc *d, const void *Y, const void 
     a.N = d->N; a.h_mode = d->h_mode; a.ginv = d->ginv; a.batch = d->batch;
     a.sY = L.sY; a.sy = L.sy; a.sH = L.sH; a.sg = L.sg; a.sl = L.sy;
     a.maxw = L.maxw; a.maxrows = L.maxrows;
+    a.max_p1 = L.max_p1; a.max_ps = L.max_ps; a.max_p2 = L.max_p2;
     e = lqrx::kkt_launch(a, s);
     hipError_t ef = hipFreeAsync(dmeta, s);
     if (e == hipErrorNotSupported) return set_err(LQRX_ERR_UNSUPPORTED, "KKT kernel unavailable");

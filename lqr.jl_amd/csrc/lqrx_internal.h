@@ -27,7 +27,7 @@ struct KktArgs {
     int h_mode, ginv;
     int64_t batch;
     int64_t sY, sy, sH, sg, sl; // per-trajectory strides (elements)
-    int maxw, maxrows;
+    int maxw, maxrows, max_p1, max_ps, max_p2;
 };
 
 hipError_t kkt_launch(const KktArgs &a, hipStream_t s);

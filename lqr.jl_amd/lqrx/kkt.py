@@ -1,0 +1,190 @@
+"""Host-side mirror of the reference's block-tridiagonal KKT surface (CholeskySolver._solve!).
+
+Reference (Julia, /root/reference/src):
+  ConstraintBlock(n1, p, n2, w): Y = [D2; C; D1], y = [c; d]       conblocks.jl:365-401
+  ConstraintBlocks sizing (n1, p, n2, w per knot)                   conblocks.jl:403-425
+  InvertedQuadratic / BlockCholesky (dense, block-diag, diagonal)   block_cholesky.jl:19-159
+  _solve!(solver): Schur → block Cholesky → fwd/bwd → primals      cholesky_solver.jl:166-182
+  second_order_correction! (Ginv = false)                           cholesky_solver.jl:254-273
+
+`KktProblem` holds one batch in the ABI's packed per-trajectory layout (every knot block
+column-major, concatenated over knots, batch slowest).  Compute goes through liblqrx.so
+(lqrx_kkt_solve / lqrx_kkt_solve_host); there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+
+__all__ = ["KktStructure", "KktProblem", "ConstraintBlocks", "dubins_structure",
+           "double_integrator_structure", "random_kkt", "kkt_solve", "kkt_solve_device",
+           "second_order_correction"]
+
+H_DENSE, H_BLOCKDIAG, H_DIAG = 0, 1, 2
+
+
+@dataclass
+class KktStructure:
+    """Per-knot block sizes shared by the batch (ConstraintBlocks, conblocks.jl:403-425)."""
+
+    n: int
+    m: int
+    N: int
+    n1: np.ndarray
+    p: np.ndarray
+    n2: np.ndarray
+    w: np.ndarray
+
+    @property
+    def rows(self):
+        return self.n1 + self.p + self.n2
+
+    def sizes(self, h_mode):
+        sY = int(np.sum(self.rows * self.w))
+        sy = int(np.sum(self.p + self.n2))
+        sH = int(np.sum(self.w)) if h_mode == H_DIAG else int(np.sum(self.w * self.w))
+        sg = int(np.sum(self.w))
+        return sY, sy, sH, sg
+
+    def desc(self, batch, h_mode, ginv):
+        arrs = [np.ascontiguousarray(a, dtype=np.int32) for a in (self.n1, self.p, self.n2, self.w)]
+        ptr = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32))
+        d = _lib.KktDesc(self.N, _lib.F64, batch, *[ptr(a) for a in arrs], h_mode, ginv, 0, 0)
+        d._keep = arrs  # keep the arrays alive with the descriptor
+        return d
+
+
+def ConstraintBlocks(n, m, N, stage_p):
+    """conblocks.jl:403-425 for a problem whose constraints are the dynamics on 1:N-1 plus
+    stage constraints with stage_p[k] rows at knot k (0-based): n1 = n̄ if dynamics at k−1,
+    n2 = n̄ if dynamics at k, w = n̄ + m·(k < N−1)."""
+    p = np.broadcast_to(np.asarray(stage_p, dtype=np.int32), (N,)).copy()
+    n1 = np.array([0] + [n] * (N - 1), np.int32)
+    n2 = np.array([n] * (N - 1) + [0], np.int32)
+    w = np.array([n + m] * (N - 1) + [n], np.int32)
+    return KktStructure(n, m, N, n1, p, n2, w)
+
+
+def dubins_structure(N=101):
+    """Dubins car n=3, m=2 (BASELINE cfg3): initial-state constraint at knot 1, dynamics,
+    goal at knot N — block 1 (0,3,3), blocks 2..N-1 (3,0,3), block N (3,3,0)."""
+    return ConstraintBlocks(3, 2, N, [3] + [0] * (N - 2) + [3])
+
+
+def double_integrator_structure(D=3, N=101):
+    """test/problems.jl DoubleIntegrator(D, N): n = 2D, m = D; initial condition (n rows) at
+    knot 1, a planar LinearConstraint (max(D−2,1) rows) on 2:N−1, goal (n rows) at N."""
+    n = 2 * D
+    p = max(D - 2, 1)
+    return ConstraintBlocks(n, D, N, [n] + [p] * (N - 2) + [n])
+
+
+@dataclass
+class KktProblem:
+    st: KktStructure
+    batch: int
+    h_mode: int
+    Y: np.ndarray
+    y: np.ndarray
+    H: np.ndarray
+    g: np.ndarray
+
+
+def random_kkt(st: KktStructure, batch: int, seed: int, h_mode: int = H_DIAG) -> KktProblem:
+    """Synthetic KKT data with the reference's Jacobian structure: D1_k = [A_k B_k],
+    D2_{k+1} = [−I 0] (dynamics x_{k+1} = f(x_k, u_k)), stage rows C random (the initial
+    condition / goal rows are [I 0]); H_k SPD (diagonal, block-diagonal or dense)."""
+    rng = np.random.default_rng(seed)
+    n, m, N = st.n, st.m, st.N
+    sY, sy, sH, sg = st.sizes(h_mode)
+    Y = np.zeros((batch, sY))
+    y = np.zeros((batch, sy))
+    H = np.zeros((batch, sH))
+    g = rng.standard_normal((batch, sg))
+    oY = oy = oH = 0
+    for k in range(N):
+        n1, p, n2, w = int(st.n1[k]), int(st.p[k]), int(st.n2[k]), int(st.w[k])
+        rows = n1 + p + n2
+        blk = np.zeros((batch, rows, w))
+        if n1:
+            blk[:, :n1, :n] = -np.eye(n)
+        if p:
+            if k == 0 or k == N - 1:
+                blk[:, n1:n1 + p, :n] = np.eye(n)[:p] if p <= n else 0
+                if p > n:
+                    blk[:, n1:n1 + p, :] = rng.standard_normal((batch, p, w))
+            else:
+                blk[:, n1:n1 + p, :] = rng.standard_normal((batch, p, w))
+        if n2:
+            A = np.eye(n) + 0.1 * rng.standard_normal((batch, n, n))
+            B = 0.1 * rng.standard_normal((batch, n, m))
+            blk[:, n1 + p:, :n] = A
+            blk[:, n1 + p:, n:n + m] = B
+        Y[:, oY:oY + rows * w] = np.swapaxes(blk, 1, 2).reshape(batch, -1)
+        y[:, oy:oy + p + n2] = 0.1 * rng.standard_normal((batch, p + n2))
+        if h_mode == H_DIAG:
+            H[:, oH:oH + w] = 0.1 + rng.random((batch, w))
+            oH += w
+        else:
+            M = rng.standard_normal((batch, w, w)) * 0.3
+            Hk = np.einsum("bij,bkj->bik", M, M) + np.eye(w)
+            if h_mode == H_BLOCKDIAG and w > n:
+                Hk[:, :n, n:] = 0.0
+                Hk[:, n:, :n] = 0.0
+            H[:, oH:oH + w * w] = np.swapaxes(Hk, 1, 2).reshape(batch, -1)
+            oH += w * w
+        oY += rows * w
+        oy += p + n2
+    return KktProblem(st, batch, h_mode, Y, y, H, g)
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def kkt_solve(pb: KktProblem, ginv: int = 1):
+    """Batched _solve! via lqrx_kkt_solve_host.  Returns dict dz (batch, NN), lam
+    (batch, P), info (batch,), rc."""
+    lib = _lib.load()
+    st, bt = pb.st, pb.batch
+    sY, sy, sH, sg = st.sizes(pb.h_mode)
+    d = st.desc(bt, pb.h_mode, ginv)
+    f = lambda a: np.ascontiguousarray(a, dtype=np.float64)
+    Y, y, H, g = f(pb.Y), f(pb.y), f(pb.H), f(pb.g)
+    dz = np.zeros((bt, sg))
+    lam = np.zeros((bt, sy))
+    info = np.zeros(bt, np.int32)
+    rc = _lib.check(lib.lqrx_kkt_solve_host(C.byref(d), _ptr(Y), _ptr(y), _ptr(H), _ptr(g),
+                                            _ptr(dz), _ptr(lam), _ptr(info)))
+    return dict(dz=dz, lam=lam, info=info, rc=rc)
+
+
+def second_order_correction(pb: KktProblem):
+    """second_order_correction! (cholesky_solver.jl:254-273): δẑ = −Dᵀ(DDᵀ)⁻¹d."""
+    return kkt_solve(pb, ginv=0)
+
+
+def kkt_solve_device(st: KktStructure, t: dict, h_mode: int, ginv: int = 1,
+                     stream: int | None = None, out: dict | None = None) -> dict:
+    """Device-pointer entry on torch tensors (flat, ABI layout): t has Y, y, H, g, batch."""
+    import torch
+
+    lib = _lib.load()
+    bt = t["batch"]
+    sY, sy, sH, sg = st.sizes(h_mode)
+    dev = t["Y"].device
+    if out is None:
+        out = dict(dz=torch.empty(bt * sg, dtype=torch.float64, device=dev),
+                   lam=torch.empty(bt * sy, dtype=torch.float64, device=dev),
+                   info=torch.empty(bt, dtype=torch.int32, device=dev))
+    d = st.desc(bt, h_mode, ginv)
+    p = lambda x: C.c_void_p(x.data_ptr())
+    rc = lib.lqrx_kkt_solve(C.byref(d), p(t["Y"]), p(t["y"]), p(t["H"]), p(t["g"]), p(out["dz"]),
+                            p(out["lam"]), p(out["info"]), C.c_void_p(stream) if stream else None)
+    _lib.check(rc)
+    out["rc"] = rc
+    return out

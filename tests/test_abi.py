@@ -1,0 +1,85 @@
+"""CPU tests of the C ABI boundary (no GPU needed): the library loads, exports every
+symbol include/lqrx.h declares, validates arguments (LAPACK-style −i codes) before touching
+a device, and the synthetic generator is deterministic."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+
+def test_exports_every_header_symbol(lqrx):
+    from lqrx import _lib
+
+    lib = _lib.load()
+    names = _lib.header_functions()
+    assert len(names) >= 9
+    for nm in names:
+        assert hasattr(lib, nm), nm
+
+
+def test_abi_version(lqrx):
+    assert lqrx.load().lqrx_abi_version() == 1
+
+
+@pytest.mark.parametrize("field,val,code", [("n", 0, -1), ("m", 0, -1), ("N", 1, -1),
+                                            ("dtype", 7, -1), ("p_mode", 3, -1),
+                                            ("layout", 1, -101), ("knot_stride_AB", 5, -101)])
+def test_dp_validation(lqrx, field, val, code):
+    from lqrx import _lib
+
+    d = _lib.DpDesc(32, 16, 10, 0, 4, 0, 0, 0, 0)
+    setattr(d, field, val)
+    rc = lqrx.load().lqrx_dp_solve(C.byref(d), *([None] * 10), None, None)
+    assert rc == code
+    assert len(lqrx.load().lqrx_last_error()) > 0
+
+
+def test_dp_null_pointer_codes(lqrx):
+    from lqrx import _lib
+
+    d = _lib.DpDesc(8, 4, 10, 0, 4, 0, 0, 0, 0)
+    buf = np.zeros(16)
+    p = buf.ctypes.data_as(C.c_void_p)
+    rc = lqrx.load().lqrx_dp_solve(C.byref(d), None, p, p, p, p, p, p, p, p, p, None, None)
+    assert rc == -2          # A is argument 2
+    rc = lqrx.load().lqrx_dp_solve(C.byref(d), p, p, p, p, p, p, p, None, p, p, None, None)
+    assert rc == -9          # P is argument 9
+
+
+def test_kkt_validation(lqrx):
+    import lqrx.kkt as K
+
+    st = K.dubins_structure(5)
+    d = st.desc(4, 2, 1)
+    d.h_mode = 9
+    assert lqrx.load().lqrx_kkt_solve(C.byref(d), *([None] * 7), None) == -1
+    st2 = K.dubins_structure(5)
+    st2.n1[2] = 2            # breaks the A ≡ previous-C aliasing (n1[k] == n2[k-1])
+    d2 = st2.desc(4, 2, 1)
+    assert lqrx.load().lqrx_kkt_solve(C.byref(d2), *([None] * 7), None) == -1
+
+
+def test_kkt_sizes(lqrx):
+    import lqrx.kkt as K
+
+    st = K.dubins_structure(101)
+    d = st.desc(1, 2, 1)
+    out = [C.c_int64() for _ in range(5)]
+    assert lqrx.load().lqrx_kkt_sizes(C.byref(d), *[C.byref(o) for o in out]) == 0
+    sY, sy, sH, sg = st.sizes(2)
+    assert [o.value for o in out] == [sY, sy, sH, sg, sy]
+    assert sg == 101 * 3 + 100 * 2 and sy == 306        # NN = 503, P = (N+1)·n
+
+
+def test_generator_deterministic_and_sharded(lqrx):
+    a = lqrx.random_batch(6, 3, 10, 8, seed=99)
+    b = lqrx.random_batch(6, 3, 10, 8, seed=99)
+    c = lqrx.random_batch(6, 3, 10, 4, seed=99, traj0=4)   # a shard of the same batch
+    for k in ("A", "B", "Q", "R", "Qf", "x0"):
+        assert np.array_equal(a[k], b[k])
+        assert np.array_equal(a[k][len(a[k]) // 2:], c[k])
+    from lqrx.dp import abi_to_batch
+
+    bb = abi_to_batch(a)
+    assert np.allclose(bb.Q, np.swapaxes(bb.Q, 1, 2))
+    assert (np.linalg.eigvalsh(bb.R) > 0).all()

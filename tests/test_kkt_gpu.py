@@ -1,0 +1,76 @@
+"""GPU parity: batched block-tridiagonal KKT solve (liblqrx.so, C ABI) vs the CPU oracle.
+
+Oracle = oracle/lqr_oracle.c restating cholesky_solver.jl:166-236, jacobian_blocks.jl:
+220-286, cholesky_solve.jl:206-302, block_cholesky.jl:55-101 (pinned in test_oracle.py by
+the reference's test/cholesky_solve.jl:18-44 identities).  Tolerance: fp64, max|δz − ref| /
+max|ref| ≤ 1e-10 and the same for the multipliers.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+
+
+def rel(a, b):
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+def _ref(st, pb, ginv):
+    os_ = orc.KktStructure(st.n, st.m, st.N, st.p)
+    return orc.kkt_solve_batch(os_, pb.batch, pb.Y, pb.y, pb.H, pb.g, h_mode=pb.h_mode, ginv=ginv,
+                               nthreads=8)
+
+
+@pytest.mark.parametrize("N,batch", [(101, 256), (11, 67), (3, 5)])   # N=2 Dubins is over-constrained (9 rows, 8 vars)
+@pytest.mark.parametrize("h_mode", [2, 0, 1])
+def test_kkt_dubins_parity(lqrx, gpu_ok, N, batch, h_mode):
+    import lqrx.kkt as K
+
+    st = K.dubins_structure(N)
+    pb = K.random_kkt(st, batch, seed=100 + N + h_mode, h_mode=h_mode)
+    got = K.kkt_solve(pb)
+    ref = _ref(st, pb, 1)
+    assert got["rc"] == 0 and (got["info"] == 0).all()
+    assert rel(got["dz"], ref["dz"].reshape(batch, -1)) <= TOL
+    assert rel(got["lam"], ref["lam"].reshape(batch, -1)) <= TOL
+
+
+@pytest.mark.parametrize("D,N", [(3, 101), (2, 12)])
+def test_kkt_double_integrator_parity(lqrx, gpu_ok, D, N):
+    """The reference's own known-answer structure (test/cholesky_solve.jl on
+    DoubleIntegrator(3,101))."""
+    import lqrx.kkt as K
+
+    st = K.double_integrator_structure(D, N)
+    pb = K.random_kkt(st, 37, seed=9, h_mode=2)
+    got = K.kkt_solve(pb)
+    ref = _ref(st, pb, 1)
+    assert (got["info"] == 0).all()
+    assert rel(got["dz"], ref["dz"].reshape(37, -1)) <= TOL
+    assert rel(got["lam"], ref["lam"].reshape(37, -1)) <= TOL
+
+
+def test_kkt_soc_parity(lqrx, gpu_ok):
+    """second_order_correction! variant (Ginv = false)."""
+    import lqrx.kkt as K
+
+    st = K.dubins_structure(101)
+    pb = K.random_kkt(st, 128, seed=3, h_mode=2)
+    got = K.second_order_correction(pb)
+    ref = _ref(st, pb, 0)
+    assert rel(got["dz"], ref["dz"].reshape(128, -1)) <= TOL
+    assert rel(got["lam"], ref["lam"].reshape(128, -1)) <= TOL
+
+
+def test_kkt_info_non_spd(lqrx, gpu_ok):
+    import lqrx.kkt as K
+
+    st = K.dubins_structure(11)
+    pb = K.random_kkt(st, 4, seed=2, h_mode=0)
+    pb.H[2, :] = -pb.H[2, :]
+    got = K.kkt_solve(pb)
+    assert got["rc"] == 1 and got["info"][2] != 0
+    assert got["info"][0] == 0 and got["info"][1] == 0 and got["info"][3] == 0

@@ -1,0 +1,153 @@
+"""CPU tests that PIN the oracle (oracle/lqr_oracle.c) before anything is compared to it.
+
+KKT path — pinned by the reference's own known-answer identities,
+/root/reference/test/cholesky_solve.jl:18-44, reproduced on the same problem structure
+(DoubleIntegrator(3,101) from test/problems.jl:14-56) and on the Dubins cfg3 structure:
+  :18  S ≈ D*(H\\D')            :19  D*(H\\g) − d ≈ r
+  :24  cholesky(S).U ≈ U        :25  U'U ≈ S
+  :31  λ ≈ −S\\r                :36  δz ≈ −H\\(D'λ + g)
+  :39  ‖D δz + d‖ < 1e-12      :40  ‖H δz + g + D'λ‖ < 1e-12
+  :42-44 [H D'; D 0] \\ [−g; −d] equals (δz, λ)
+and the second-order-correction variant (cholesky_solver.jl:254-273): δẑ = −Dᵀ(DDᵀ)⁻¹d.
+
+DP path — the reference's DP test (test/dp.jl) has no assertion and Julia is absent, so
+the restatement of dynamic_programming.jl is pinned by identities: (1) the rollout U equals
+the dense equality-constrained QP optimum; (2) for a long horizon K_1 → the DARE gain.
+"""
+import numpy as np
+import pytest
+import scipy.linalg as sla
+
+from oracle import oracle as orc
+
+
+def _struct(name):
+    import lqrx.kkt as K
+
+    return {"di": K.double_integrator_structure(3, 101), "dubins": K.dubins_structure(101),
+            "di_small": K.double_integrator_structure(2, 12)}[name]
+
+
+def _oracle_struct(st):
+    o = orc.KktStructure(st.n, st.m, st.N, st.p)
+    return o
+
+
+@pytest.mark.parametrize("name", ["di", "dubins", "di_small"])
+@pytest.mark.parametrize("h_mode", [0, 1, 2])
+def test_kkt_oracle_known_answers(lqrx, name, h_mode):
+    import lqrx.kkt as K
+
+    st = _struct(name)
+    pb = K.random_kkt(st, 1, seed=17 + h_mode, h_mode=h_mode)
+    os_ = _oracle_struct(st)
+    out = orc.kkt_solve_one(os_, pb.Y[0], pb.y[0], pb.H[0], pb.g[0], h_mode=h_mode, debug=True)
+    assert out["info"] == 0
+    dn = orc.kkt_dense(os_, pb.Y[0], pb.y[0], pb.H[0], pb.g[0], h_mode=h_mode)
+    D, d, H, g = dn["D"], dn["d"], dn["H"], dn["g"]
+    S_dense = D @ np.linalg.solve(H, D.T)
+    rtol = 1e-8  # Julia's default ≈ (√eps) used by the reference script
+    scale = np.abs(S_dense).max()
+    # :18  S ≈ D*(H\D')  (the block storage holds the upper block triangle)
+    assert np.abs(np.triu(out["S"]) - np.triu(S_dense)).max() <= rtol * scale
+    # :19  D*(H\g) − d ≈ r
+    assert np.allclose(out["r"], D @ np.linalg.solve(H, g) - d, rtol=rtol, atol=rtol * np.abs(d).max())
+    # :24-25  cholesky(S).U ≈ U ;  U'U ≈ S
+    U = np.triu(out["U"])
+    Uref = np.linalg.cholesky(S_dense).T
+    assert np.abs(U - Uref).max() <= 1e-7 * np.abs(Uref).max()
+    assert np.abs(U.T @ U - S_dense).max() <= rtol * scale
+    # :31  λ ≈ −S\r
+    lam = out["lam"]
+    assert np.allclose(lam, dn["lam"], rtol=1e-8, atol=1e-9 * np.abs(dn["lam"]).max())
+    # :36  δz ≈ −H\(D'λ + g)
+    dz = out["dz"]
+    assert np.allclose(dz, -np.linalg.solve(H, D.T @ lam + g), rtol=1e-8, atol=1e-10)
+    # :39-40  residuals
+    assert np.linalg.norm(D @ dz + d) < 1e-10 * max(1.0, np.abs(d).max())
+    assert np.linalg.norm(H @ dz + g + D.T @ lam) < 1e-10 * max(1.0, np.abs(g).max())
+    # :42-44 full KKT solve
+    NN = len(g)
+    assert np.allclose(dn["full"][:NN], dz, rtol=1e-8, atol=1e-10)
+    assert np.allclose(dn["full"][NN:], lam, rtol=1e-8, atol=1e-9 * np.abs(lam).max())
+
+
+@pytest.mark.parametrize("name", ["di", "dubins"])
+def test_kkt_oracle_soc(lqrx, name):
+    """second_order_correction! (Ginv=false): δẑ = −Dᵀ(DDᵀ)⁻¹d (cholesky_solver.jl:255)."""
+    import lqrx.kkt as K
+
+    st = _struct(name)
+    pb = K.random_kkt(st, 1, seed=5, h_mode=2)
+    os_ = _oracle_struct(st)
+    out = orc.kkt_solve_one(os_, pb.Y[0], pb.y[0], pb.H[0], pb.g[0], h_mode=2, ginv=0)
+    dn = orc.kkt_dense(os_, pb.Y[0], pb.y[0], pb.H[0], pb.g[0], h_mode=2)
+    D, d = dn["D"], dn["d"]
+    ref = -D.T @ np.linalg.solve(D @ D.T, d)
+    assert np.allclose(out["dz"], ref, rtol=1e-9, atol=1e-11)
+
+
+def test_kkt_oracle_non_spd_info(lqrx):
+    """A negative cost Hessian entry must be reported (the reference discards potrf info)."""
+    import lqrx.kkt as K
+
+    st = K.dubins_structure(11)
+    pb = K.random_kkt(st, 1, seed=2, h_mode=0)
+    pb.H[0, :] = -pb.H[0, :]
+    out = orc.kkt_solve_one(_oracle_struct(st), pb.Y[0], pb.y[0], pb.H[0], pb.g[0], h_mode=0)
+    assert out["info"] != 0
+
+
+def test_dp_oracle_equals_dense_kkt(lqrx):
+    from lqrx.dp import abi_to_batch
+
+    n, m, N, bt = 6, 3, 25, 5
+    d = lqrx.random_batch(n, m, N, bt, seed=31)
+    out = orc.dp_solve_abi(d, N)
+    b = abi_to_batch(d)
+    X = out["X"].reshape(bt, N, n)
+    U = out["U"].reshape(bt, N - 1, m)
+    for t in range(bt):
+        Xd, Ud = orc.dp_dense_kkt(b.A[t], b.B[t], b.Q[t], b.R[t], b.Qf[t], b.x0[t], N)
+        assert np.abs(U[t] - Ud).max() <= 1e-10 * max(1.0, np.abs(Ud).max())
+        assert np.abs(X[t] - Xd).max() <= 1e-10 * max(1.0, np.abs(Xd).max())
+
+
+def test_dp_oracle_dare_limit(lqrx):
+    """Long horizon: K_1 → (R + BᵀP∞B)⁻¹BᵀP∞A and P_1 → P∞ (scipy solve_discrete_are) on
+    well-actuated problems (stable A, full-rank B) whose Riccati recursion
+    converges geometrically."""
+    from lqrx.dp import from_abi, to_abi
+
+    rng = np.random.default_rng(8)
+    n, m, N, bt = 8, 4, 300, 3
+    A = rng.standard_normal((bt, n, n)) * 0.3   # ρ(A) < 1: the reference recursion does not
+    # symmetrise P, so for open-loop-unstable A its skew part grows like ρ(A)^{2k}
+    B = rng.standard_normal((bt, n, m))
+    Q = np.broadcast_to(np.eye(n), (bt, n, n)).copy()
+    R = np.broadcast_to(np.eye(m), (bt, m, m)).copy()
+    d = dict(A=to_abi(A), B=to_abi(B), Q=to_abi(Q), R=to_abi(R), Qf=to_abi(10 * Q),
+             x0=rng.standard_normal((bt, n)), n=n, m=m, batch=bt)
+    out = orc.dp_solve_abi(d, N)
+    K = from_abi(out["K"], (bt, N - 1, m, n))
+    P1 = from_abi(out["P"], (bt, n, n))
+    for t in range(bt):
+        Pinf = sla.solve_discrete_are(A[t], B[t], Q[t], R[t])
+        Kinf = np.linalg.solve(R[t] + B[t].T @ Pinf @ B[t], B[t].T @ Pinf @ A[t])
+        assert np.abs(K[t, 0] - Kinf).max() <= 1e-9 * np.abs(Kinf).max()
+        assert np.abs(P1[t] - Pinf).max() <= 1e-9 * np.abs(Pinf).max()
+
+
+def test_dp_oracle_all_P_consistent(lqrx):
+    """p_mode 1 stores P_k for every knot; P_N = Qf and P_1 equals the p_mode 0 output."""
+    from lqrx.dp import from_abi
+
+    n, m, N, bt = 5, 2, 30, 2
+    d = lqrx.random_batch(n, m, N, bt, seed=4)
+    a = orc.dp_solve_abi(d, N, all_P=True)
+    b = orc.dp_solve_abi(d, N, all_P=False)
+    Pa = from_abi(a["P"], (bt, N, n, n))
+    Pb = from_abi(b["P"], (bt, n, n))
+    Qf = from_abi(d["Qf"], (bt, n, n))
+    assert np.array_equal(Pa[:, N - 1], Qf)
+    assert np.array_equal(Pa[:, 0], Pb)
