@@ -69,6 +69,29 @@ def cpu_baseline(n, m, N, target_s=12.0, threads=None):
                        f"{threads} threads, {dt:.1f} s")
 
 
+def cpu_baseline_kkt(N, target_s=12.0, threads=None):
+    """CPU oracle (C restatement of cholesky_solver.jl _solve!) on a bounded Dubins sample."""
+    import lqrx.kkt as K
+    from oracle import oracle as orc
+
+    threads = threads or max(1, min(16, os.cpu_count() or 1))
+    st = K.dubins_structure(N)
+    os_ = orc.KktStructure(st.n, st.m, st.N, st.p)
+    probe = 256
+    pb = K.random_kkt(st, probe, seed=1, h_mode=K.H_DIAG)
+    t0 = time.perf_counter()
+    orc.kkt_solve_batch(os_, probe, pb.Y, pb.y, pb.H, pb.g, h_mode=2, nthreads=threads)
+    per = (time.perf_counter() - t0) / probe
+    sample = int(max(probe, min(1 << 18, target_s / max(per, 1e-9))))
+    pb = K.random_kkt(st, sample, seed=2, h_mode=K.H_DIAG)
+    t0 = time.perf_counter()
+    orc.kkt_solve_batch(os_, sample, pb.Y, pb.y, pb.H, pb.g, h_mode=2, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return dict(value=sample / dt, unit="trajectories/s", cores=threads, kind="port",
+                sample=f"{sample} Dubins KKT solves N={N}, oracle/lqr_oracle.c (C restatement "
+                       f"of _solve!), OpenMP {threads} threads, {dt:.1f} s")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -83,7 +106,20 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--workload", choices=["dp", "cartpole", "kkt"], default="dp",
+                    help="dp = random dense LQR (BASELINE configs[3], the headline); "
+                         "cartpole = configs[1] (n=4 m=1 N=101 B=4096); "
+                         "kkt = Dubins block-tridiagonal KKT solve (configs[2], B=16384)")
     args = ap.parse_args()
+    if args.workload == "cartpole":
+        args.n, args.m, args.N = 4, 1, 101
+        if args.batch == 65536:
+            args.batch = 4096
+    if args.workload == "kkt":
+        if args.batch == 65536:
+            args.batch = 16384
+        if args.N == 256:
+            args.N = 101
 
     import torch
     import torch.distributed as dist
@@ -101,19 +137,39 @@ def main():
 
     n, m, N, bt = args.n, args.m, args.N, args.batch
     f64 = args.dtype == "f64"
-    tdt = torch.float64 if f64 else torch.float32
-    host = lqrx.random_batch(n, m, N, bt, seed=args.seed, traj0=rank * bt,
-                             dtype=lqrx.F64 if f64 else lqrx.F32)
     dev = torch.device("cuda", local)
-    t = {k: torch.from_numpy(host[k]).to(dev) for k in ("A", "B", "Q", "R", "Qf", "x0")}
-    t.update(n=n, m=m, batch=bt)
-    del host
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
-    out = lqrx.dp_solve_device(t, N, p_mode=0, stream=sh)   # allocates outputs once
+    if args.workload in ("dp", "cartpole"):
+        tdt = torch.float64 if f64 else torch.float32
+        if args.workload == "dp":
+            host = lqrx.random_batch(n, m, N, bt, seed=args.seed, traj0=rank * bt,
+                                     dtype=lqrx.F64 if f64 else lqrx.F32)
+        else:
+            from lqrx.models import cartpole_batch
+            from lqrx.dp import to_abi
+            cb = cartpole_batch(bt, N, seed=args.seed + rank)
+            npdt = "float64" if f64 else "float32"
+            host = {k: to_abi(getattr(cb, k)).astype(npdt).ravel()
+                    for k in ("A", "B", "Q", "R", "Qf")}
+            host["x0"] = cb.x0.astype(npdt).ravel()
+        t = {k: torch.from_numpy(host[k]).to(dev) for k in ("A", "B", "Q", "R", "Qf", "x0")}
+        t.update(n=n, m=m, batch=bt)
+        del host
+        out = lqrx.dp_solve_device(t, N, p_mode=0, stream=sh)   # allocates outputs once
 
-    def step():
-        lqrx.dp_solve_device(t, N, p_mode=0, stream=sh, out=out)
+        def step():
+            lqrx.dp_solve_device(t, N, p_mode=0, stream=sh, out=out)
+    else:
+        import lqrx.kkt as K
+        st = K.dubins_structure(N)
+        pb = K.random_kkt(st, bt, seed=args.seed + rank, h_mode=K.H_DIAG)
+        t = {k: torch.from_numpy(getattr(pb, k).ravel()).to(dev) for k in ("Y", "y", "H", "g")}
+        t["batch"] = bt
+        out = K.kkt_solve_device(st, t, K.H_DIAG, 1, stream=sh)
+
+        def step():
+            K.kkt_solve_device(st, t, K.H_DIAG, 1, stream=sh, out=out)
 
     for _ in range(args.warmup):
         step()
@@ -145,35 +201,52 @@ def main():
     ms_per_step = wall / args.steps * 1e3
 
     if rank == 0:
-        flops = dp_flops_per_traj(n, m, N) * bt
-        achieved = flops / (kern_ms * 1e-3) / 1e12
-        peak = PEAK_FP64_TFLOPS if f64 else PEAK_FP32_TFLOPS
-        traffic = None
-        if os.path.exists(args.traffic_json):
-            try:
-                tj = json.load(open(args.traffic_json))
-                key = f"n{n}_m{m}_N{N}_B{bt}_{args.dtype}"
-                traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(n, m, N, target_s=args.cpu_seconds)
+        if args.workload == "kkt":
+            import lqrx.kkt as K
+            sY, sy, sH, sg = K.dubins_structure(N).sizes(K.H_DIAG)
+            alg_bytes = (sY + sy + sH + sg + sg + sy) * 8 * bt     # inputs + dz + λ
+            achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+                    "kernel": "kkt_lane_kernel", "kernel_ms": kern_ms,
+                    "alg_bytes_per_traj": alg_bytes / bt}
+            metric = "KKT solves/sec (Dubins n=3 m=2 N=101 block-tridiagonal _solve!)"
+            workload = "Dubins constrained KKT inner solve (BASELINE.json configs[2])"
+            cpu = cpu_baseline_kkt(N, target_s=args.cpu_seconds) \
+                if not args.no_cpu_baseline and world == 1 else None
+        else:
+            flops = dp_flops_per_traj(n, m, N) * bt
+            achieved = flops / (kern_ms * 1e-3) / 1e12
+            peak = PEAK_FP64_TFLOPS if f64 else PEAK_FP32_TFLOPS
+            traffic = None
+            if os.path.exists(args.traffic_json):
+                try:
+                    tj = json.load(open(args.traffic_json))
+                    key = f"n{n}_m{m}_N{N}_B{bt}_{args.dtype}"
+                    traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
+                except Exception:
+                    traffic = None
+            roof = {"bound": "mfma", "achieved": achieved, "peak": peak,
+                    "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
+                    "kernel": "dp_riccati_kernel", "kernel_ms": kern_ms,
+                    "flops_per_traj": dp_flops_per_traj(n, m, N),
+                    "alg_bytes_per_launch": dp_bytes_per_traj(n, m, N, 8 if f64 else 4) * bt}
+            metric = METRIC if args.workload == "dp" else \
+                "LQR trajectories/sec (Riccati bwd+fwd), cartpole n=4 m=1 N=101 B=4096"
+            workload = ("random dense time-invariant LQR, Riccati backward pass + forward "
+                        "rollout (BASELINE.json configs[3])") if args.workload == "dp" else \
+                "cartpole LQR, RK3-linearised (BASELINE.json configs[1])"
+            cpu = cpu_baseline(n, m, N, target_s=args.cpu_seconds) \
+                if not args.no_cpu_baseline and world == 1 else None
         line = {
-            "metric": METRIC, "value": value, "unit": "trajectories/s", "n_gpus": world,
+            "metric": metric, "value": value, "unit": "trajectories/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": args.dtype, "data": "synthetic (counter-based random dense LQR, "
+            "dtype": args.dtype, "data": "synthetic (counter-based random problems, "
                                           "SURVEY.md §8(d) generator)",
-            "config": {"workload": "random dense time-invariant LQR, Riccati backward pass "
-                                   "+ forward rollout (BASELINE.json configs[3])",
-                       "n": n, "m": m, "N": N, "batch_per_gpu": bt, "global_batch": bt * world,
-                       "parallelism": f"batch-sharded x{world}"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak,
-                         "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
-                         "kernel": "dp_riccati_kernel", "kernel_ms": kern_ms,
-                         "flops_per_traj": dp_flops_per_traj(n, m, N),
-                         "alg_bytes_per_launch": dp_bytes_per_traj(n, m, N, 8 if f64 else 4) * bt},
+            "config": {"workload": workload, "n": n, "m": m, "N": N, "batch_per_gpu": bt,
+                       "global_batch": bt * world, "parallelism": f"batch-sharded x{world}"},
+            "roofline": roof,
             "cpu_baseline": cpu,
             "nonfinite_or_info": bad,
         }

@@ -355,24 +355,28 @@ static hipError_t launch_dp(const DpArgs &a, hipStream_t s)
 
 hipError_t dp_launch(const DpArgs &a, hipStream_t s)
 {
+    // smallest instantiated tile grid that covers (n, m); padding is exact (zero rows /
+    // columns, unit diagonal in R), see tiles_load
     const int nt = (a.n + 15) / 16, mt = (a.m + 15) / 16;
     if (a.dtype == 0) {
-        if (nt == 1 && mt == 1) return launch_dp<double, 1, 1>(a, s);
-        if (nt == 2 && mt == 1) return launch_dp<double, 2, 1, LQRX_DP_WAVES, LQRX_DP_VAR>(a, s);
-        if (nt == 2 && mt == 2) return launch_dp<double, 2, 2>(a, s);
+        if (nt <= 1 && mt <= 1) return launch_dp<double, 1, 1>(a, s);
+        if (nt <= 2 && mt <= 1) return launch_dp<double, 2, 1, LQRX_DP_WAVES, LQRX_DP_VAR>(a, s);
+        if (nt <= 2 && mt <= 2) return launch_dp<double, 2, 2>(a, s);
+        if (nt <= 4 && mt <= 2) return launch_dp<double, 4, 2, 1>(a, s);   // n ≤ 64: 1 wave/SIMD
     } else {
-        if (nt == 1 && mt == 1) return launch_dp<float, 1, 1>(a, s);
-        if (nt == 2 && mt == 1) return launch_dp<float, 2, 1>(a, s);
-        if (nt == 2 && mt == 2) return launch_dp<float, 2, 2>(a, s);
+        if (nt <= 1 && mt <= 1) return launch_dp<float, 1, 1>(a, s);
+        if (nt <= 2 && mt <= 1) return launch_dp<float, 2, 1>(a, s);
+        if (nt <= 2 && mt <= 2) return launch_dp<float, 2, 2>(a, s);
+        if (nt <= 4 && mt <= 2) return launch_dp<float, 4, 2, 1>(a, s);    // cfg5: n=64 m=32
     }
     return hipErrorNotSupported;
 }
 
 bool dp_supported(int dtype, int n, int m)
 {
+    (void)dtype;
     const int nt = (n + 15) / 16, mt = (m + 15) / 16;
-    if (n < 1 || m < 1) return false;
-    return (nt == 1 && mt == 1) || (nt == 2 && mt == 1) || (nt == 2 && mt == 2);
+    return n >= 1 && m >= 1 && nt <= 4 && mt <= 2;
 }
 
 } // namespace lqrx

@@ -142,74 +142,132 @@ __device__ __forceinline__ void hinv_apply(const HFac<WM> &hf, double *x, int w,
     trsv_un<WM>(hf.f, w, x);
 }
 
-// Schur pieces of one knot: YYt = Y H⁻¹ Yᵀ (rows×rows) and r = Y H⁻¹ g (shur!, :231-242)
-template <int RM, int WM> struct Shur {
-    double S[RM * RM];
-    double r[RM];
+// Schur pieces of one knot in block form (shur! + copy_shur!, jacobian_blocks.jl:231-286):
+// with Y = [D2; C; D1] (segments 1, s, 2 of p1, ps, p2 rows) and YYt = Y H⁻¹ Yᵀ:
+//   A = YYt[1,1] (added to the previous knot's C),  B = YYt[s,s],  C = YYt[2,2],
+//   D = YYt[1,s],  E = YYt[s,2],  F = YYt[1,2];   r = Y H⁻¹ g split as r1, rs, r2.
+// All register arrays are indexed statically (the segment offsets are runtime values, so
+// they only ever enter global addresses).
+template <int P1M, int PSM, int P2M> struct ShurBlk {
+    double A[P1M * P1M], B[PSM * PSM], C[P2M * P2M], D[P1M * PSM], E[PSM * P2M], F[P1M * P2M];
+    double r1[P1M], rs[PSM], r2[P2M];
 };
 
-template <int RM, int WM>
-__device__ __forceinline__ bool compute_shur(Shur<RM, WM> &s, const double *Yk, const double *Hk,
-                                             const double *gk, const KMeta &km, int hmode, int ginv)
+template <int M1, int M2>
+__device__ __forceinline__ void outer_acc(double *X, const double *u, const double *v, double s)
 {
-    const int rows = km.n1 + km.p + km.n2, w = km.w;
+#pragma unroll
+    for (int j = 0; j < M2; ++j)
+#pragma unroll
+        for (int i = 0; i < M1; ++i) X[KIDX(i, j, M1)] += u[i] * v[j] * s;
+}
+
+template <int P1M, int PSM, int P2M, int WM>
+__device__ __forceinline__ bool compute_shur(ShurBlk<P1M, PSM, P2M> &s, const double *Yk,
+                                             const double *Hk, const double *gk, const KMeta &km,
+                                             int hmode, int ginv)
+{
+    const int p1 = km.n1, ps = km.p, p2 = km.n2, rows = p1 + ps + p2, w = km.w;
     HFac<WM> hf;
     bool ok = true;
     if (ginv) ok = load_hfac<WM>(hf, Hk, w, hmode);
 #pragma unroll
-    for (int i = 0; i < RM * RM; ++i) s.S[i] = 0.0;
+    for (int i = 0; i < P1M * P1M; ++i) s.A[i] = 0.0;
 #pragma unroll
-    for (int i = 0; i < RM; ++i) s.r[i] = 0.0;
+    for (int i = 0; i < PSM * PSM; ++i) s.B[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < P2M * P2M; ++i) s.C[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < P1M * PSM; ++i) s.D[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < PSM * P2M; ++i) s.E[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < P1M * P2M; ++i) s.F[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < P1M; ++i) s.r1[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < PSM; ++i) s.rs[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < P2M; ++i) s.r2[i] = 0.0;
+    auto seg = [&](double *dst, int M, int off, int cnt, int j) {
+        for (int a = 0; a < M; ++a) dst[a] = (a < cnt) ? Yk[(off + a) + j * rows] : 0.0;
+    };
     if (!ginv || hmode == 2) {
-        // stream Y column by column: S += y_j h_j y_jᵀ, r += y_j h_j g_j
+        // stream Y column by column:  YYt += y_j h_j y_jᵀ,  r += y_j h_j g_j
 #pragma unroll
         for (int j = 0; j < WM; ++j)
             if (j < w) {
-                double hj = ginv ? hf.f[j] : 1.0, gj = ginv ? gk[j] * hj : 0.0;
-                double col[RM];
+                const double hj = ginv ? hf.f[j] : 1.0, gj = ginv ? gk[j] * hj : 0.0;
+                double c1[P1M], cs[PSM], c2[P2M];
 #pragma unroll
-                for (int a = 0; a < RM; ++a) col[a] = (a < rows) ? Yk[a + j * rows] : 0.0;
+                for (int a = 0; a < P1M; ++a) c1[a] = (a < p1) ? Yk[a + j * rows] : 0.0;
 #pragma unroll
-                for (int b = 0; b < RM; ++b)
-                    if (b < rows) {
-                        double cb = col[b] * hj;
+                for (int a = 0; a < PSM; ++a) cs[a] = (a < ps) ? Yk[(p1 + a) + j * rows] : 0.0;
 #pragma unroll
-                        for (int a = 0; a < RM; ++a)
-                            if (a <= b) s.S[KIDX(a, b, RM)] += col[a] * cb;
-                        s.r[b] += col[b] * gj;
-                    }
+                for (int a = 0; a < P2M; ++a) c2[a] = (a < p2) ? Yk[(p1 + ps + a) + j * rows] : 0.0;
+                outer_acc<P1M, P1M>(s.A, c1, c1, hj);
+                outer_acc<PSM, PSM>(s.B, cs, cs, hj);
+                outer_acc<P2M, P2M>(s.C, c2, c2, hj);
+                outer_acc<P1M, PSM>(s.D, c1, cs, hj);
+                outer_acc<PSM, P2M>(s.E, cs, c2, hj);
+                outer_acc<P1M, P2M>(s.F, c1, c2, hj);
+#pragma unroll
+                for (int a = 0; a < P1M; ++a) s.r1[a] += c1[a] * gj;
+#pragma unroll
+                for (int a = 0; a < PSM; ++a) s.rs[a] += cs[a] * gj;
+#pragma unroll
+                for (int a = 0; a < P2M; ++a) s.r2[a] += c2[a] * gj;
             }
     } else {
-        // dense / block-diagonal H: JYt = H⁻¹ Yᵀ row by row of Y (one rows-vector per column)
+        // dense / block-diagonal H: W = H⁻¹Yᵀ one row of Y at a time, per segment
+        double W1[P1M * WM], Ws[PSM * WM], W2[P2M * WM];
+        auto hrow = [&](double *Wr, int off, int cnt, int M) {
 #pragma unroll
-        for (int a = 0; a < RM; ++a)
-            if (a < rows) {
+            for (int a = 0; a < M; ++a) {
                 double v[WM];
 #pragma unroll
-                for (int j = 0; j < WM; ++j) v[j] = (j < w) ? Yk[a + j * rows] : 0.0;
-                hinv_apply<WM>(hf, v, w, hmode);          // v = H⁻¹ Y[a,:]ᵀ
-                double ra = 0.0;
+                for (int j = 0; j < WM; ++j) v[j] = (a < cnt && j < w) ? Yk[(off + a) + j * rows] : 0.0;
+                hinv_apply<WM>(hf, v, w, hmode);
 #pragma unroll
-                for (int j = 0; j < WM; ++j)
-                    if (j < w) ra += v[j] * gk[j];
-                s.r[a] = ra;
+                for (int j = 0; j < WM; ++j) Wr[a * WM + j] = v[j];
+            }
+        };
+        hrow(W1, 0, p1, P1M);
+        hrow(Ws, p1, ps, PSM);
+        hrow(W2, p1 + ps, p2, P2M);
 #pragma unroll
-                for (int b = 0; b < RM; ++b)
-                    if (b < rows && a <= b) {
-                        double acc = 0.0;
+        for (int j = 0; j < WM; ++j)
+            if (j < w) {
+                double c1[P1M], cs[PSM], c2[P2M];
 #pragma unroll
-                        for (int j = 0; j < WM; ++j)
-                            if (j < w) acc += Yk[b + j * rows] * v[j];
-                        s.S[KIDX(a, b, RM)] = acc;
-                    }
+                for (int a = 0; a < P1M; ++a) c1[a] = (a < p1) ? Yk[a + j * rows] : 0.0;
+#pragma unroll
+                for (int a = 0; a < PSM; ++a) cs[a] = (a < ps) ? Yk[(p1 + a) + j * rows] : 0.0;
+#pragma unroll
+                for (int a = 0; a < P2M; ++a) c2[a] = (a < p2) ? Yk[(p1 + ps + a) + j * rows] : 0.0;
+                double w1[P1M], ws[PSM], w2[P2M];
+#pragma unroll
+                for (int a = 0; a < P1M; ++a) w1[a] = W1[a * WM + j];
+#pragma unroll
+                for (int a = 0; a < PSM; ++a) ws[a] = Ws[a * WM + j];
+#pragma unroll
+                for (int a = 0; a < P2M; ++a) w2[a] = W2[a * WM + j];
+                outer_acc<P1M, P1M>(s.A, c1, w1, 1.0);
+                outer_acc<PSM, PSM>(s.B, cs, ws, 1.0);
+                outer_acc<P2M, P2M>(s.C, c2, w2, 1.0);
+                outer_acc<P1M, PSM>(s.D, c1, ws, 1.0);
+                outer_acc<PSM, P2M>(s.E, cs, w2, 1.0);
+                outer_acc<P1M, P2M>(s.F, c1, w2, 1.0);
+                const double gj = gk[j];
+#pragma unroll
+                for (int a = 0; a < P1M; ++a) s.r1[a] += w1[a] * gj;
+#pragma unroll
+                for (int a = 0; a < PSM; ++a) s.rs[a] += ws[a] * gj;
+#pragma unroll
+                for (int a = 0; a < P2M; ++a) s.r2[a] += w2[a] * gj;
             }
     }
-    // mirror to the lower triangle
-#pragma unroll
-    for (int b = 0; b < RM; ++b)
-#pragma unroll
-        for (int a = 0; a < RM; ++a)
-            if (a > b) s.S[KIDX(a, b, RM)] = s.S[KIDX(b, a, RM)];
+    (void)seg;
     return ok;
 }
 
@@ -234,9 +292,9 @@ __global__ __launch_bounds__(64) void kkt_lane_kernel(const KktArgs a, double *_
     int info = 0;
 
     // ---------------- forward sweep ----------------
-    Shur<RM, WM> cur, nxt;
+    ShurBlk<P1M, PSM, P2M> cur, nxt;
     KMeta km = kmeta(a.meta, 0);
-    if (!compute_shur<RM, WM>(cur, Y + km.oY, H + km.oH, g + km.og, km, hmode, ginv) && !info) info = -1;
+    if (!compute_shur<P1M, PSM, P2M, WM>(cur, Y + km.oY, H + km.oH, g + km.og, km, hmode, ginv) && !info) info = -1;
     double Ua[PM * PM];      // factor of the previous C block (A ≡ previous C)
     double lprev[PM];        // forward λ of the previous knot
 #pragma unroll
@@ -250,43 +308,35 @@ __global__ __launch_bounds__(64) void kkt_lane_kernel(const KktArgs a, double *_
         KMeta kn{};
         if (k + 1 < N) {
             kn = kmeta(a.meta, k + 1);
-            if (!compute_shur<RM, WM>(nxt, Y + kn.oY, H + kn.oH, g + kn.og, kn, hmode, ginv) && !info)
+            if (!compute_shur<P1M, PSM, P2M, WM>(nxt, Y + kn.oY, H + kn.oH, g + kn.og, kn, hmode, ginv) && !info)
                 info = -(k + 2);
         }
-        // copy_shur!(F[k], block[k], block[k+1])  (:249-286)
+        // copy_shur!(F[k], block[k], block[k+1])  (:249-286): C gets knot k+1's A-part
+        // (A_{k+1} ≡ C_k, jacobian_blocks.jl:166), d gets knot k+1's r_[1] (:251)
         double FB[PSM * PSM], FC[P2M * P2M], FD[P1M * PSM], FE[PSM * P2M], FF[P1M * P2M], c[PSM], d[P2M];
 #pragma unroll
-        for (int j = 0; j < PSM; ++j)
-#pragma unroll
-            for (int i = 0; i < PSM; ++i) FB[KIDX(i, j, PSM)] = (i < ps && j < ps) ? cur.S[KIDX(os + i, os + j, RM)] : 0.0;
+        for (int i = 0; i < PSM * PSM; ++i) FB[i] = cur.B[i];
 #pragma unroll
         for (int j = 0; j < P2M; ++j)
 #pragma unroll
-            for (int i = 0; i < P2M; ++i) {
-                double v = (i < p2 && j < p2) ? cur.S[KIDX(o2 + i, o2 + j, RM)] : 0.0;
-                if (k + 1 < N && i < p2 && j < p2) v += nxt.S[KIDX(i, j, RM)]; // A_{k+1} += YYt[p1,p1]
-                FC[KIDX(i, j, P2M)] = v;
-            }
+            for (int i = 0; i < P2M; ++i)
+                FC[KIDX(i, j, P2M)] = cur.C[KIDX(i, j, P2M)] +
+                    ((k + 1 < N && i < P1M && j < P1M) ? nxt.A[KIDX(i < P1M ? i : 0, j < P1M ? j : 0, P1M)] : 0.0);
 #pragma unroll
-        for (int j = 0; j < PSM; ++j)
+        for (int i = 0; i < P1M * PSM; ++i) FD[i] = cur.D[i];
 #pragma unroll
-            for (int i = 0; i < P1M; ++i) FD[KIDX(i, j, P1M)] = (i < p1 && j < ps) ? cur.S[KIDX(o1 + i, os + j, RM)] : 0.0;
+        for (int i = 0; i < PSM * P2M; ++i) FE[i] = cur.E[i];
 #pragma unroll
-        for (int j = 0; j < P2M; ++j)
+        for (int i = 0; i < P1M * P2M; ++i) FF[i] = cur.F[i];
 #pragma unroll
-            for (int i = 0; i < PSM; ++i) FE[KIDX(i, j, PSM)] = (i < ps && j < p2) ? cur.S[KIDX(os + i, o2 + j, RM)] : 0.0;
-#pragma unroll
-        for (int j = 0; j < P2M; ++j)
-#pragma unroll
-            for (int i = 0; i < P1M; ++i) FF[KIDX(i, j, P1M)] = (i < p1 && j < p2) ? cur.S[KIDX(o1 + i, o2 + j, RM)] : 0.0;
-#pragma unroll
-        for (int i = 0; i < PSM; ++i) c[i] = (i < ps) ? cur.r[os + i] - yv[km.oy + i] : 0.0;
+        for (int i = 0; i < PSM; ++i) c[i] = (i < ps) ? cur.rs[i] - yv[km.oy + i] : 0.0;
 #pragma unroll
         for (int i = 0; i < P2M; ++i) {
-            double v = (i < p2) ? cur.r[o2 + i] - yv[km.oy + ps + i] : 0.0;
-            if (k + 1 < N && i < p2) v += nxt.r[i];                             // :251 d += r_[1]
+            double v = (i < p2) ? cur.r2[i] - yv[km.oy + ps + i] : 0.0;
+            if (k + 1 < N && i < P1M) v += nxt.r1[i < P1M ? i : 0];
             d[i] = v;
         }
+        (void)o1; (void)os; (void)o2;
 
         // cholesky!(U[k], F[k])  (cholesky_solve.jl:206-226)
         if (p1 > 0) {

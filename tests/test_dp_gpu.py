@@ -47,6 +47,8 @@ def run_pair(lqrx, oracle, n, m, N, batch, seed, dtype=0, all_P=True):
     (32, 16, 16, 8),      # cfg4 shape, short horizon
     (32, 16, 256, 4),     # cfg4 shape, full horizon
     (32, 32, 20, 3),      # 2×2 tiles
+    (64, 32, 12, 2),      # cfg5 shape (4×2 tiles), fp64
+    (48, 20, 9, 3),       # padded 3×2 → 4×2 tiles
 ])
 def test_dp_parity_f64(lqrx, oracle, gpu_ok, n, m, N, batch):
     got, ref = run_pair(lqrx, oracle, n, m, N, batch, seed=1000 + n * 7 + m)
@@ -65,7 +67,7 @@ def test_dp_p1_only(lqrx, oracle, gpu_ok):
     assert relerr_per_knot(got["P"][:, None], ref["P"][:, None]) <= TOL64
 
 
-@pytest.mark.parametrize("n,m,N,batch", [(32, 16, 64, 4), (4, 1, 101, 16)])
+@pytest.mark.parametrize("n,m,N,batch", [(32, 16, 64, 4), (4, 1, 101, 16), (64, 32, 40, 3)])
 def test_dp_parity_f32(lqrx, oracle, gpu_ok, n, m, N, batch):
     got, ref = run_pair(lqrx, oracle, n, m, N, batch, seed=77, dtype=1)
     assert relerr_per_knot(got["K"].astype(np.float64), ref["K"]) <= TOL32
