@@ -1,0 +1,63 @@
+"""World-size-2 `gloo` tests (CPU) of the multi-GPU bench path: ranks shard the batch by
+trajectory index (traj0 = rank·batch) with no data-path collective; the only collectives
+are the timing barrier and the MAX-over-ranks of the wall time.  The shards must tile the
+single-process batch exactly, and per-rank oracle solves of the shards must equal the
+single-process solve (independent problems ⇒ sharding cannot change results)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, root, q):
+    import sys
+
+    sys.path[:0] = [os.path.join(root, "lqr.jl_amd"), root]
+    import torch
+    import lqrx
+    from oracle import oracle as orc
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n, m, N, per = 6, 3, 12, 5
+    d = lqrx.random_batch(n, m, N, per, seed=77, traj0=rank * per)
+    out = orc.dp_solve_abi(d, N)
+    wall = torch.tensor([0.1 * (rank + 1)], dtype=torch.float64)
+    dist.barrier()
+    dist.all_reduce(wall, op=dist.ReduceOp.MAX)
+    q.put((rank, d["A"], out["K"], float(wall.item())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharding_gloo(lqrx):
+    import lqrx as L
+    from oracle import oracle as orc
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, root, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full = L.random_batch(6, 3, 12, 10, seed=77)
+    ref = orc.dp_solve_abi(full, 12)
+    assert np.array_equal(np.concatenate([res[0][1], res[1][1]]), full["A"])
+    assert np.array_equal(np.concatenate([res[0][2], res[1][2]]), ref["K"])
+    assert res[0][3] == pytest.approx(0.2) and res[1][3] == pytest.approx(0.2)

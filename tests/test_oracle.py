@@ -151,3 +151,56 @@ def test_dp_oracle_all_P_consistent(lqrx):
     Qf = from_abi(d["Qf"], (bt, n, n))
     assert np.array_equal(Pa[:, N - 1], Qf)
     assert np.array_equal(Pa[:, 0], Pb)
+
+
+def lqr_as_kkt(A, B, Q, R, Qf, x0, N):
+    """The LQR as the reference's KKT problem (conblocks.jl:403-425 block structure):
+    initial-condition stage rows [I 0] at knot 1 (value −x0), dynamics D1_k = [A B],
+    D2_{k+1} = [−I 0], H_k = blockdiag(Q, R) (Qf at N), g = 0, linearised at z = 0."""
+    import lqrx.kkt as K
+
+    n, m = B.shape
+    st = K.ConstraintBlocks(n, m, N, [n] + [0] * (N - 1))
+    Y, y, H = [], [], []
+    for k in range(N):
+        n1, p, n2, w = int(st.n1[k]), int(st.p[k]), int(st.n2[k]), int(st.w[k])
+        blk = np.zeros((n1 + p + n2, w))
+        if n1:
+            blk[:n1, :n] = -np.eye(n)
+        if p:
+            blk[n1:n1 + p, :n] = np.eye(n)
+        if n2:
+            blk[n1 + p:, :n] = A
+            blk[n1 + p:, n:] = B
+        Y.append(blk.T.ravel())
+        y.append(np.concatenate([-x0 if p else np.zeros(0), np.zeros(n2)]))
+        Hk = np.zeros((w, w))
+        Hk[:n, :n] = Qf if k == N - 1 else Q
+        if w > n:
+            Hk[n:, n:] = R
+        H.append(Hk.T.ravel())
+    g = np.zeros(int(np.sum(st.w)))
+    return st, np.concatenate(Y), np.concatenate(y), np.concatenate(H), g
+
+
+def test_dp_oracle_equals_kat_pinned_kkt_oracle(lqrx):
+    """Transitive pin of the DP restatement: its rollout (X, U) must equal the primal step of
+    the KKT restatement — itself pinned above by the reference's test/cholesky_solve.jl
+    known answers — on the same LQR written as a constrained QP."""
+    from lqrx.dp import abi_to_batch
+
+    n, m, N, bt = 6, 3, 30, 4
+    d = lqrx.random_batch(n, m, N, bt, seed=12)
+    out = orc.dp_solve_abi(d, N)
+    b = abi_to_batch(d)
+    X = out["X"].reshape(bt, N, n)
+    U = out["U"].reshape(bt, N - 1, m)
+    for t in range(bt):
+        st, Y, y, H, g = lqr_as_kkt(b.A[t], b.B[t], b.Q[t], b.R[t], b.Qf[t], b.x0[t], N)
+        kk = orc.kkt_solve_one(_oracle_struct(st), Y, y, H, g, h_mode=0)
+        assert kk["info"] == 0
+        z = kk["dz"]
+        Xk = np.stack([z[k * (n + m):k * (n + m) + n] for k in range(N)])
+        Uk = np.stack([z[k * (n + m) + n:(k + 1) * (n + m)] for k in range(N - 1)])
+        assert np.abs(Xk - X[t]).max() <= 1e-10 * max(1.0, np.abs(X[t]).max())
+        assert np.abs(Uk - U[t]).max() <= 1e-10 * max(1.0, np.abs(U[t]).max())
