@@ -1,0 +1,134 @@
+# LQRX.jl — the reference-side binding a LQR.jl maintainer would add to route the hot path
+# through liblqrx.so (include/lqrx.h).  Text only: Julia is not installed in this image, so
+# this file is not executed by the test-suite; the same C ABI is exercised from Python
+# (ctypes, lqr.jl_amd/lqrx/_lib.py) and by the GPU parity tests.
+#
+# It keeps the reference surface:
+#   LQRProblem / DPSolver / solve!(sol, solver, prob)   src/lqr_problem.jl:1-11,
+#                                                        src/dynamic_programming.jl:2-72
+#   LQRSolution (exported by src/LQR.jl:19 but never defined upstream; fields K, X, U)
+# and adds batched forms over Array{T,3}/Array{T,4}, whose column-major memory with the
+# batch index last is exactly the ABI's layout 0 (no copies).
+module LQRX
+
+using LinearAlgebra
+
+const liblqrx = get(ENV, "LQRX_LIB", joinpath(@__DIR__, "..", "lqr.jl_amd", "lqrx", "liblqrx.so"))
+
+# ---- lqrx_dp_desc (include/lqrx.h) ----
+struct DpDesc
+    n::Int32; m::Int32; N::Int32; dtype::Int32
+    batch::Int64
+    layout::Int32; p_mode::Int32
+    knot_stride_AB::Int64; knot_stride_QR::Int64
+end
+
+lasterror() = unsafe_string(ccall((:lqrx_last_error, liblqrx), Cstring, ()))
+
+function check(rc::Cint)
+    rc < 0 && error("lqrx error $rc: $(lasterror())")
+    return rc
+end
+
+dtypecode(::Type{Float64}) = Int32(0)
+dtypecode(::Type{Float32}) = Int32(1)
+
+"""
+    LQRSolution(n, m, N, batch=1; T=Float64, all_P=false)
+
+K[:,:,k,b] = gain of knot k (m×n); X[:,k,b]; U[:,k,b]; P = P₁ (or all P_k); info[b].
+"""
+struct LQRSolution{T}
+    K::Array{T,4}
+    P::Array{T}
+    X::Array{T,3}
+    U::Array{T,3}
+    info::Vector{Int32}
+end
+LQRSolution(n, m, N, batch=1; T=Float64, all_P=false) =
+    LQRSolution{T}(zeros(T, m, n, N - 1, batch),
+                   all_P ? zeros(T, n, n, N, batch) : zeros(T, n, n, batch),
+                   zeros(T, n, N, batch), zeros(T, m, N - 1, batch), zeros(Int32, batch))
+
+"""
+    LQRBatch(A, B, Q, R, Qf, x0, N)   A: n×n×batch, B: n×m×batch, …, x0: n×batch
+"""
+struct LQRBatch{T}
+    A::Array{T,3}; B::Array{T,3}; Q::Array{T,3}; R::Array{T,3}; Qf::Array{T,3}
+    x0::Matrix{T}; N::Int
+end
+
+"DPSolver(prob): the Julia struct owned the per-knot scratch; here it lives in registers/LDS."
+struct DPSolver{T}
+    n::Int; m::Int; N::Int
+end
+DPSolver(b::LQRBatch{T}) where T = DPSolver{T}(size(b.B, 1), size(b.B, 2), b.N)
+
+"""
+    solve!(sol, solver, prob)
+
+Batched Riccati backward pass + forward rollout on the GPU (host arrays in, host arrays
+out; lqrx_dp_solve_host).  Same outputs as src/dynamic_programming.jl:54-72 for every
+problem in the batch; returns 1 if some trajectory had a non-SPD R + BᵀPB (see sol.info).
+"""
+function solve!(sol::LQRSolution{T}, solver::DPSolver{T}, prob::LQRBatch{T}) where T
+    n, m, N = solver.n, solver.m, solver.N
+    batch = size(prob.A, 3)
+    all_P = ndims(sol.P) == 4
+    d = Ref(DpDesc(n, m, N, dtypecode(T), batch, 0, all_P ? 1 : 0, 0, 0))
+    GC.@preserve prob sol begin
+        rc = ccall((:lqrx_dp_solve_host, liblqrx), Cint,
+                   (Ref{DpDesc}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T},
+                    Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{Int32}),
+                   d, prob.A, prob.B, prob.Q, prob.R, prob.Qf, prob.x0,
+                   sol.K, sol.P, sol.X, sol.U, sol.info)
+    end
+    return check(rc)
+end
+
+# Single-problem form with the reference's LQRProblem fields (lqr_problem.jl:1-11)
+struct LQRProblem{n,m,T}
+    Qf::Matrix{T}; Q::Matrix{T}; R::Matrix{T}; A::Matrix{T}; B::Matrix{T}
+    x0::Vector{T}; u0::Vector{T}; tf::T; N::Int
+end
+function solve!(sol::LQRSolution{T}, prob::LQRProblem{n,m,T}) where {n,m,T}
+    b = LQRBatch{T}(reshape(prob.A, n, n, 1), reshape(prob.B, n, m, 1), reshape(prob.Q, n, n, 1),
+                    reshape(prob.R, m, m, 1), reshape(prob.Qf, n, n, 1), reshape(prob.x0, n, 1), prob.N)
+    solve!(sol, DPSolver(b), b)
+end
+
+# ---- KKT: lqrx_kkt_desc ----
+struct KktDesc
+    N::Int32; dtype::Int32
+    batch::Int64
+    n1::Ptr{Int32}; p::Ptr{Int32}; n2::Ptr{Int32}; w::Ptr{Int32}
+    h_mode::Int32; ginv::Int32; layout::Int32; reserved::Int32
+end
+
+"""
+    kkt_solve!(dz, lam, info, n1, p, n2, w, Y, y, H, g; h_mode=2, ginv=1)
+
+One CholeskySolver._solve! (src/cholesky_solver.jl:166-182) per trajectory: Y, y, H, g are
+the per-knot ConstraintBlock.Y / .y, cost Hessian and gradient, packed (column-major
+blocks, concatenated over knots) with the batch as the last dimension.  ginv=0 is the
+second_order_correction! variant (:254-273).
+"""
+function kkt_solve!(dz::Matrix{Float64}, lam::Matrix{Float64}, info::Vector{Int32},
+                    n1::Vector{Int32}, p::Vector{Int32}, n2::Vector{Int32}, w::Vector{Int32},
+                    Y::Matrix{Float64}, y::Matrix{Float64}, H::Matrix{Float64}, g::Matrix{Float64};
+                    h_mode::Integer=2, ginv::Integer=1)
+    batch = size(Y, 2)
+    GC.@preserve n1 p n2 w Y y H g dz lam info begin
+        d = Ref(KktDesc(length(n1), 0, batch, pointer(n1), pointer(p), pointer(n2), pointer(w),
+                        h_mode, ginv, 0, 0))
+        rc = ccall((:lqrx_kkt_solve_host, liblqrx), Cint,
+                   (Ref{KktDesc}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                    Ptr{Float64}, Ptr{Float64}, Ptr{Int32}),
+                   d, Y, y, H, g, dz, lam, info)
+    end
+    return check(rc)
+end
+
+export LQRProblem, LQRSolution, LQRBatch, DPSolver, solve!, kkt_solve!
+
+end # module
