@@ -106,6 +106,45 @@ __device__ __forceinline__ bool aug_ldl_forward(T *aug, int lane)
     return ok;
 }
 
+// Newton–Schulz refinement of X ≈ E⁻¹ (E SPD, MT×MT tiles), warm-started from the previous
+// knot's inverse.  One step: R = I − EᵀX (4·MT³ MFMAs, neg-A with C = I), X ← X + XᵀR.
+// Returns true once the step just taken is converged to working precision: with
+// ρ = 16·MT·max|R| ≥ ‖R‖∞ the new residual is ≤ cond(E)·ρ², so ρ ≤ tol (1e-11 in fp64:
+// cond·1e-22, far below the rounding floor) accepts.  Not converged after `it` steps
+// (e.g. a cold or poor start) → false, and the caller runs the exact sweep.
+template <typename T> struct NsTol;
+template <> struct NsTol<double> { static constexpr double v = 1e-11; static constexpr int it = 6; };
+template <> struct NsTol<float> { static constexpr float v = 3e-4f; static constexpr int it = 6; };
+
+template <typename T, int MT>
+__device__ __forceinline__ bool ns_refine(typename Tile<T>::acc (&X)[MT][MT],
+                                          const typename Tile<T>::acc (&E)[MT][MT],
+                                          const typename Tile<T>::acc (&Id)[MT][MT], int lane)
+{
+    using acc = typename Tile<T>::acc;
+    for (int it = 0; it < NsTol<T>::it; ++it) {
+        acc R[MT][MT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < MT; ++j) R[i][j] = Id[i][j];
+        mma_tn<T, MT, MT, MT, true>(R, E, X);                   // R = I − EᵀX
+        T mx = (T)0;
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < MT; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) mx = fmax(mx, fabs(R[i][j][r]));
+        mx = wave_max(mx);
+        mma_tn<T, MT, MT, MT>(X, X, R);                         // X ← X + XᵀR
+        const T rho = (T)(16 * MT) * mx;
+        if (rho <= NsTol<T>::v) return true;
+    }
+    (void)lane;
+    return false;
+}
+
 template <typename T, int NT, int MT> struct DpCfg {
     static constexpr int NP = NT * 16, MP = MT * 16;
     static constexpr int CS = MP + 2;                       // padded LDS column stride
@@ -227,7 +266,7 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
 //                transpose); Q is re-read (L2/MALL-resident, 8 KB/traj) into the P_
 //                accumulators each knot so it holds no registers.
 //   VAR_NOSOLVE / VAR_NOROLL / VAR_NOKSTORE : diagnostic ablations (tools/dp_ablate).
-enum : int { VAR_EXACT = 1, VAR_NOSOLVE = 2, VAR_NOROLL = 4, VAR_NOKSTORE = 8 };
+enum : int { VAR_EXACT = 1, VAR_NOSOLVE = 2, VAR_NOROLL = 4, VAR_NOKSTORE = 8, VAR_SWEEPONLY = 16 };
 
 template <typename T, int NT, int MT, int WAVES, int VAR, bool FULL>
 __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
@@ -257,6 +296,16 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
     if (Pall) tiles_store<T, NT, NT>(P, Pall + (size_t)(N - 1) * nn, n, n, n, lane);
     T *Kb = (T *)a.K + (size_t)b * (size_t)(N - 1) * nm;
     int info = 0;
+    acc Xi[MT][MT], Id[MT][MT];                 // running E⁻¹ (warm start), identity tiles
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < MT; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                Id[i][j][r] = (i == j && Tile<T>::row(lane, r) == tcol(lane)) ? (T)1 : (T)0;
+                Xi[i][j][r] = (T)0;
+            }
 
     for (int k = N - 1; k >= 1; --k) { // :61
         acc PB[NT][MT], E[MT][MT], PA[NT][NT], G[MT][NT], Pn[NT][NT];
@@ -282,7 +331,12 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
         if constexpr (EXACT) mma_tn<T, NT, NT, NT>(Pn, At, PA);    // :51 Q + A'PA
         else mma_tn_lower<T, NT, NT>(Pn, At, PA);
 
-        // :42 chol_solve!(E, K) — potrf 'U' + potrs 'U'
+        // :42 chol_solve!(E, K) — potrf 'U' + potrs 'U', as K = E⁻¹G with X ≈ E⁻¹:
+        //  * warm start: Newton–Schulz from the previous knot's inverse, all MFMA
+        //      R = I − EᵀX (neg-A modifier, C = I),  X ← X + XᵀR   (quadratic; no symmetry
+        //      needed: X⁺ − E⁻¹ = −ΔᵀEΔ), accepted at working precision (see NsTol)
+        //  * the first knot, and any knot whose iteration does not converge, run the exact
+        //    LDLᵀ sweep of [E | I] (potrf's pivot test → info) and X = Wᵀ D⁻¹ W.
         acc Kt[MT][NT];
         if constexpr ((VAR & VAR_NOSOLVE) != 0) {
 #pragma unroll
@@ -290,27 +344,33 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
 #pragma unroll
                 for (int j = 0; j < NT; ++j) Kt[i][j] = G[i][j] * (T)1e-3 + E[0][0] * (T)1e-9;
         } else {
-            tiles_to_lds<T, MT, MT>(E, lds, CS, lane);
-            tiles_to_lds<T, MT, NT>(G, lds + MP * CS, CS, lane);
-            __syncthreads();
-            bool ok = aug_ldl_forward<T, MP, C::NP, CS, LQRX_DP_BCAST>(lds, lane);
-            if (!ok && info == 0) info = k;
-            __syncthreads();
-            acc Yt[MT][NT], Wt[MT][MT];
-            tiles_from_lds<T, MT, NT>(Yt, lds + MP * CS, CS, lane);
-            tiles_from_lds<T, MT, MT>(Wt, lds + (MP + C::NP) * CS, CS, lane);
-            const T *rinv = lds + (2 * MP + C::NP) * CS + 64;
+            bool have = false;
+            if constexpr ((VAR & VAR_SWEEPONLY) == 0) {
+                if (k < N - 1) have = ns_refine<T, MT>(Xi, E, Id, lane);
+            }
+            if (!have) {
+                tiles_to_lds<T, MT, MT>(E, lds, CS, lane);
+                __syncthreads();
+                bool ok = aug_ldl_forward<T, MP, 0, CS, LQRX_DP_BCAST>(lds, lane);
+                if (!ok && info == 0) info = k;
+                __syncthreads();
+                acc Wt[MT][MT], DW[MT][MT];
+                tiles_from_lds<T, MT, MT>(Wt, lds + MP * CS, CS, lane);
+                const T *rinv = lds + (2 * MP) * CS + 64;
 #pragma unroll
-            for (int i = 0; i < MT; ++i)
+                for (int i = 0; i < MT; ++i)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    T s = rinv[i * 16 + Tile<T>::row(lane, r)];          // D⁻¹ row scale
+                    for (int r = 0; r < 4; ++r) {
+                        T sc = rinv[i * 16 + Tile<T>::row(lane, r)];         // D⁻¹ row scale
 #pragma unroll
-                    for (int j = 0; j < NT; ++j) Yt[i][j][r] *= s;
-                }
-            __syncthreads();
+                        for (int j = 0; j < MT; ++j) DW[i][j][r] = Wt[i][j][r] * sc;
+                    }
+                __syncthreads();
+                tiles_zero<T, MT, MT>(Xi);
+                mma_tn<T, MT, MT, MT>(Xi, Wt, DW);                      // X = Wᵀ D⁻¹ W = E⁻¹
+            }
             tiles_zero<T, MT, NT>(Kt);
-            mma_tn<T, MT, MT, NT>(Kt, Wt, Yt);                     // K = Wᵀ(D⁻¹Y) = E⁻¹G
+            mma_tn<T, MT, MT, NT>(Kt, Xi, G);                          // K = XᵀG = E⁻¹G
             if constexpr ((VAR & VAR_NOKSTORE) == 0)
                 tiles_store<T, MT, NT, FULL>(Kt, Kb + (size_t)(k - 1) * nm, m, n, m, lane);
         }

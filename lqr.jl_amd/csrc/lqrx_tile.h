@@ -227,6 +227,20 @@ __device__ __forceinline__ void tiles_symmetrize_lower(typename Tile<T>::acc (&D
     __syncthreads();
 }
 
+// wave-wide max (xor butterfly; every lane gets the result)
+__device__ __forceinline__ double wave_max(double v)
+{
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v)
+{
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+
 // 1/a: hardware estimate (v_rcp_f64: max rel err 4.6e-8 measured on gfx950, see
 // profiles/r01/lat_probe.txt) + one Newton step → ~2e-15 relative.
 __device__ __forceinline__ double rcp_nr(double a)

@@ -33,7 +33,7 @@ int main(int argc, char **argv) {
     a.n = (int)n; a.m = (int)m; a.N = (int)N; a.dtype = 0; a.p_all = 0; a.batch = B;
     hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
     const char *names[] = {"W2 fast", "W3 fast", "W2 exact", "W3 exact", "W3 nosolve", "W3 noroll",
-                           "W3 nosolve+noroll", "W3 noKstore", "W2 noroll", "W4 fast"};
+                           "W3 nosolve+noroll", "W3 noKstore", "W2 noroll", "W2 sweeponly"};
     std::vector<std::vector<float>> t(10);
     for (int rep = 0; rep < 4; ++rep) {
         t[0].push_back(run<2, 0>(a, e0, e1));
@@ -45,7 +45,7 @@ int main(int argc, char **argv) {
         t[6].push_back(run<3, VAR_NOSOLVE | VAR_NOROLL>(a, e0, e1));
         t[7].push_back(run<3, VAR_NOKSTORE | VAR_NOROLL>(a, e0, e1));
         t[8].push_back(run<2, VAR_NOROLL>(a, e0, e1));
-        t[9].push_back(run<4, 0>(a, e0, e1));
+        t[9].push_back(run<2, VAR_SWEEPONLY>(a, e0, e1));
     }
     double fl = (double)B * (N - 1) * (4.0*n*n*n + 8.0*n*n*m + 4.0*n*m*m + m*m*m/3.0 + 2.0*n*n + 2.0*m*m + 2.0*n*n + 4.0*n*m);
     for (int v = 0; v < 10; ++v) {
