@@ -113,8 +113,12 @@ __device__ __forceinline__ bool aug_ldl_forward(T *aug, int lane)
 // cond·1e-22, far below the rounding floor) accepts.  Not converged after `it` steps
 // (e.g. a cold or poor start) → false, and the caller runs the exact sweep.
 template <typename T> struct NsTol;
-template <> struct NsTol<double> { static constexpr double v = 1e-11; static constexpr int it = 6; };
-template <> struct NsTol<float> { static constexpr float v = 3e-4f; static constexpr int it = 6; };
+template <> struct NsTol<double> {
+    static constexpr double v = 1e-11, one_step = 1e-9; static constexpr int it = 6;
+};
+template <> struct NsTol<float> {
+    static constexpr float v = 3e-4f, one_step = 1e-5f; static constexpr int it = 6;
+};
 
 template <typename T, int MT>
 __device__ __forceinline__ bool ns_refine(typename Tile<T>::acc (&X)[MT][MT],
@@ -136,10 +140,10 @@ __device__ __forceinline__ bool ns_refine(typename Tile<T>::acc (&X)[MT][MT],
             for (int j = 0; j < MT; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) mx = fmax(mx, fabs(R[i][j][r]));
-        mx = wave_max(mx);
+        const T rho = (T)(16 * MT) * wave_max(mx);
+        if (rho <= NsTol<T>::v) return true;                    // X already at working precision
         mma_tn<T, MT, MT, MT>(X, X, R);                         // X ← X + XᵀR
-        const T rho = (T)(16 * MT) * mx;
-        if (rho <= NsTol<T>::v) return true;
+        if (rho <= NsTol<T>::one_step) return true;             // new residual ≤ cond·ρ² ≪ eps
     }
     (void)lane;
     return false;
@@ -296,7 +300,7 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
     if (Pall) tiles_store<T, NT, NT>(P, Pall + (size_t)(N - 1) * nn, n, n, n, lane);
     T *Kb = (T *)a.K + (size_t)b * (size_t)(N - 1) * nm;
     int info = 0;
-    acc Xi[MT][MT], Id[MT][MT];                 // running E⁻¹ (warm start), identity tiles
+    acc Xi[MT][MT], Xp[MT][MT], Id[MT][MT];     // E⁻¹ of the last two knots, identity tiles
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -305,6 +309,7 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
             for (int r = 0; r < 4; ++r) {
                 Id[i][j][r] = (i == j && Tile<T>::row(lane, r) == tcol(lane)) ? (T)1 : (T)0;
                 Xi[i][j][r] = (T)0;
+                Xp[i][j][r] = (T)0;
             }
 
     for (int k = N - 1; k >= 1; --k) { // :61
@@ -346,7 +351,22 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
         } else {
             bool have = false;
             if constexpr ((VAR & VAR_SWEEPONLY) == 0) {
-                if (k < N - 1) have = ns_refine<T, MT>(Xi, E, Id, lane);
+                if (k < N - 1) {
+                    // warm start: linear extrapolation 2X_{k+1} − X_{k+2} once both exist
+                    acc X0[MT][MT];
+#pragma unroll
+                    for (int i = 0; i < MT; ++i)
+#pragma unroll
+                        for (int j = 0; j < MT; ++j) {
+                            X0[i][j] = Xi[i][j];
+                            if (k < N - 2) Xi[i][j] = (T)2 * Xi[i][j] - Xp[i][j];
+                        }
+                    have = ns_refine<T, MT>(Xi, E, Id, lane);
+#pragma unroll
+                    for (int i = 0; i < MT; ++i)
+#pragma unroll
+                        for (int j = 0; j < MT; ++j) Xp[i][j] = X0[i][j];
+                }
             }
             if (!have) {
                 tiles_to_lds<T, MT, MT>(E, lds, CS, lane);
