@@ -19,6 +19,7 @@
 // each lane on its own trajectory; register arrays are sized by compile-time maxima of the
 // block dimensions (template), loops run to the runtime sizes.
 #include "lqrx_internal.h"
+#include "lqrx_tile.h"
 #include <hip/hip_runtime.h>
 
 namespace lqrx {
@@ -40,7 +41,7 @@ __device__ __forceinline__ bool potrf_u(double *A, int n)
                 if (p < j) d -= A[KIDX(p, j, NM)] * A[KIDX(p, j, NM)];
             ok = ok && (d > 0.0);
             double s = sqrt(d);
-            double si = 1.0 / s;
+            double si = rcp_nr2(s);
             A[KIDX(j, j, NM)] = s;
 #pragma unroll
             for (int c = 0; c < NM; ++c)
@@ -70,7 +71,7 @@ __device__ __forceinline__ void trsm_ut(const double *U, int n, double *X, int n
 #pragma unroll
                     for (int p = 0; p < UM; ++p)
                         if (p < i) s -= U[KIDX(p, i, UM)] * X[KIDX(p, c, XM)];
-                    X[KIDX(i, c, XM)] = s / U[KIDX(i, i, UM)];
+                    X[KIDX(i, c, XM)] = s * rcp_nr2(U[KIDX(i, i, UM)]);
                 }
         }
 }
@@ -86,7 +87,7 @@ __device__ __forceinline__ void trsv_un(const double *U, int n, double *x)
 #pragma unroll
             for (int p = 0; p < UM; ++p)
                 if (p > ii && p < n) s -= U[KIDX(ii, p, UM)] * x[p];
-            x[ii] = s / U[KIDX(ii, ii, UM)];
+            x[ii] = s * rcp_nr2(U[KIDX(ii, ii, UM)]);
         }
 }
 
@@ -110,7 +111,7 @@ __device__ __forceinline__ bool load_hfac(HFac<WM> &hf, const double *H, int w, 
 {
     if (hmode == 2) {
 #pragma unroll
-        for (int i = 0; i < WM; ++i) hf.f[i] = (i < w) ? 1.0 / H[i] : 0.0; // block_cholesky.jl:86
+        for (int i = 0; i < WM; ++i) hf.f[i] = (i < w) ? rcp_nr2(H[i]) : 0.0; // block_cholesky.jl:86 inv
         return true;
     }
 #pragma unroll
@@ -137,7 +138,7 @@ __device__ __forceinline__ void hinv_apply(const HFac<WM> &hf, double *x, int w,
 #pragma unroll
             for (int p = 0; p < WM; ++p)
                 if (p < i) s -= hf.f[KIDX(p, i, WM)] * x[p];
-            x[i] = s / hf.f[KIDX(i, i, WM)];
+            x[i] = s * rcp_nr2(hf.f[KIDX(i, i, WM)]);
         }
     trsv_un<WM>(hf.f, w, x);
 }
@@ -160,6 +161,25 @@ __device__ __forceinline__ void outer_acc(double *X, const double *u, const doub
     for (int j = 0; j < M2; ++j)
 #pragma unroll
         for (int i = 0; i < M1; ++i) X[KIDX(i, j, M1)] += u[i] * v[j] * s;
+}
+
+template <int M>
+__device__ __forceinline__ void sym_acc(double *X, const double *u, double s)
+{
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        const double uj = u[j] * s;
+#pragma unroll
+        for (int i = 0; i <= j; ++i) X[KIDX(i, j, M)] = fma(u[i], uj, X[KIDX(i, j, M)]);
+    }
+}
+
+template <int M> __device__ __forceinline__ void sym_mirror(double *X)
+{
+#pragma unroll
+    for (int j = 0; j < M; ++j)
+#pragma unroll
+        for (int i = j + 1; i < M; ++i) X[KIDX(i, j, M)] = X[KIDX(j, i, M)];
 }
 
 template <int P1M, int PSM, int P2M, int WM>
@@ -205,12 +225,14 @@ __device__ __forceinline__ bool compute_shur(ShurBlk<P1M, PSM, P2M> &s, const do
                 for (int a = 0; a < PSM; ++a) cs[a] = (a < ps) ? Yk[(p1 + a) + j * rows] : 0.0;
 #pragma unroll
                 for (int a = 0; a < P2M; ++a) c2[a] = (a < p2) ? Yk[(p1 + ps + a) + j * rows] : 0.0;
-                outer_acc<P1M, P1M>(s.A, c1, c1, hj);
-                outer_acc<PSM, PSM>(s.B, cs, cs, hj);
-                outer_acc<P2M, P2M>(s.C, c2, c2, hj);
-                outer_acc<P1M, PSM>(s.D, c1, cs, hj);
-                outer_acc<PSM, P2M>(s.E, cs, c2, hj);
-                outer_acc<P1M, P2M>(s.F, c1, c2, hj);
+                // block sizes are wave-uniform (shared structure): empty blocks are skipped
+                // by scalar branches; symmetric blocks accumulate the upper triangle only
+                if (p1) sym_acc<P1M>(s.A, c1, hj);
+                if (ps) sym_acc<PSM>(s.B, cs, hj);
+                if (p2) sym_acc<P2M>(s.C, c2, hj);
+                if (p1 && ps) outer_acc<P1M, PSM>(s.D, c1, cs, hj);
+                if (ps && p2) outer_acc<PSM, P2M>(s.E, cs, c2, hj);
+                if (p1 && p2) outer_acc<P1M, P2M>(s.F, c1, c2, hj);
 #pragma unroll
                 for (int a = 0; a < P1M; ++a) s.r1[a] += c1[a] * gj;
 #pragma unroll
@@ -218,6 +240,9 @@ __device__ __forceinline__ bool compute_shur(ShurBlk<P1M, PSM, P2M> &s, const do
 #pragma unroll
                 for (int a = 0; a < P2M; ++a) s.r2[a] += c2[a] * gj;
             }
+        sym_mirror<P1M>(s.A);
+        sym_mirror<PSM>(s.B);
+        sym_mirror<P2M>(s.C);
     } else {
         // dense / block-diagonal H: W = H⁻¹Yᵀ one row of Y at a time, per segment
         double W1[P1M * WM], Ws[PSM * WM], W2[P2M * WM];
