@@ -9,9 +9,12 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
+#include <map>
+#include <mutex>
 #include <vector>
 
 namespace {
@@ -215,6 +218,40 @@ int kkt_layout(const lqrx_kkt_desc *d, KktLayout &L)
     if (L.sY > INT32_MAX) return set_err(LQRX_ERR_UNSUPPORTED, "trajectory too large");
     return 0;
 }
+// Per-device cache of uploaded structure tables.  The upload is a blocking hipMemcpy on
+// first use of a structure; afterwards a solve issues no host→device traffic besides the
+// launch.  (A per-call stream-ordered alloc + pageable async copy was observed to leave
+// the device table stale on repeated calls with alternating structures.)
+int device_meta(const std::vector<int32_t> &meta, const int32_t **out)
+{
+    static std::mutex mu;
+    static std::map<std::pair<int, std::vector<int32_t>>, int32_t *> cache;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_err(e, "hipGetDevice");
+    std::lock_guard<std::mutex> lock(mu);
+    auto key = std::make_pair(dev, meta);
+    auto it = cache.find(key);
+    if (it != cache.end()) {
+        *out = it->second;
+        return 0;
+    }
+    if (cache.size() >= 4096) { // bound the cache: drop every table (all work must be done)
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_err(e, "hipDeviceSynchronize");
+        for (auto &kv : cache) (void)hipFree(kv.second);
+        cache.clear();
+    }
+    int32_t *d = nullptr;
+    const size_t bytes = meta.size() * sizeof(int32_t);
+    if ((e = hipMalloc((void **)&d, bytes)) != hipSuccess) return hip_err(e, "hipMalloc meta");
+    if ((e = hipMemcpy(d, meta.data(), bytes, hipMemcpyHostToDevice)) != hipSuccess) {
+        (void)hipFree(d);
+        return hip_err(e, "meta H2D");
+    }
+    cache.emplace(std::move(key), d);
+    *out = d;
+    return 0;
+}
 } // namespace
 
 extern "C" int lqrx_kkt_sizes(const lqrx_kkt_desc *d, int64_t *nY, int64_t *ny, int64_t *nH,
@@ -244,13 +281,10 @@ extern "C" int lqrx_kkt_solve(const lqrx_kkt_desc *d, const void *Y, const void 
     if (!dz) return set_err(-6, "dz is NULL");
     if (!lam) return set_err(-7, "lam is NULL");
     hipStream_t s = (hipStream_t)stream;
-    // stream-ordered upload of the block-structure table
-    int32_t *dmeta = nullptr;
-    size_t mb = L.meta.size() * sizeof(int32_t);
-    hipError_t e = hipMallocAsync((void **)&dmeta, mb, s);
-    if (e != hipSuccess) return hip_err(e, "hipMallocAsync meta");
-    e = hipMemcpyAsync(dmeta, L.meta.data(), mb, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return hip_err(e, "meta H2D");
+    // device copy of the block-structure table, uploaded once per distinct structure
+    const int32_t *dmeta = nullptr;
+    if ((st = device_meta(L.meta, &dmeta))) return st;
+    hipError_t e;
     lqrx::KktArgs a{};
     a.Y = (const double *)Y; a.y = (const double *)y; a.H = (const double *)H; a.g = (const double *)g;
     a.dz = (double *)dz; a.lam = (double *)lam; a.info = info; a.meta = dmeta;
@@ -258,11 +292,18 @@ extern "C" int lqrx_kkt_solve(const lqrx_kkt_desc *d, const void *Y, const void 
     a.sY = L.sY; a.sy = L.sy; a.sH = L.sH; a.sg = L.sg; a.sl = L.sy;
     a.maxw = L.maxw; a.maxrows = L.maxrows;
     a.max_p1 = L.max_p1; a.max_ps = L.max_ps; a.max_p2 = L.max_p2;
+    static const int force_lane = [] { const char *v = std::getenv("LQRX_KKT_FORCE_LANE"); return v && *v == '1'; }();
+    static const int debug_meta = [] { const char *v = std::getenv("LQRX_DEBUG_META"); return v && *v == '1'; }();
+    a.force_lane = force_lane;
     e = lqrx::kkt_launch(a, s);
-    hipError_t ef = hipFreeAsync(dmeta, s);
+    if (debug_meta) {
+        std::vector<int32_t> back(L.meta.size());
+        (void)hipStreamSynchronize(s);
+        (void)hipMemcpy(back.data(), dmeta, L.meta.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
+        if (back != L.meta) std::fprintf(stderr, "LQRX_DEBUG_META: device meta differs from host\n");
+    }
     if (e == hipErrorNotSupported) return set_err(LQRX_ERR_UNSUPPORTED, "KKT kernel unavailable");
     if (e != hipSuccess) return hip_err(e, "kkt kernel launch");
-    if (ef != hipSuccess) return hip_err(ef, "hipFreeAsync meta");
     if (stream == nullptr) {
         e = hipStreamSynchronize(nullptr);
         if (e != hipSuccess) return hip_err(e, "kkt kernel");

@@ -28,6 +28,7 @@ struct KktArgs {
     int64_t batch;
     int64_t sY, sy, sH, sg, sl; // per-trajectory strides (elements)
     int maxw, maxrows, max_p1, max_ps, max_p2;
+    int force_lane; // debug: LQRX_KKT_FORCE_LANE=1 selects the register-only kernel
 };
 
 hipError_t kkt_launch(const KktArgs &a, hipStream_t s);

@@ -578,6 +578,443 @@ __global__ __launch_bounds__(64) void kkt_lane_kernel(const KktArgs a, double *_
     if (a.info) a.info[t] = info;
 }
 
+// ---------------------------------------------------------------------------------------
+// Staged variant: identical arithmetic, but every per-knot input (Y_k, y_k, H_k, g_k of the
+// wave's 64 trajectories) is brought into LDS by coalesced LDS-DMA (global_load_lds), one
+// knot ahead in a double buffer, and the factor slab is batch-fastest (coalesced).  The
+// per-trajectory packed layout keeps each trajectory's knot block contiguous, so the wave
+// reads 64 contiguous chunks (dense, lane-linear [t][L] image in LDS).
+using gptr_t = const __attribute__((address_space(1))) void *;
+using lptr_t = __attribute__((address_space(3))) void *;
+
+// stage L doubles at element offset `off` of each of the wave's 64 trajectories (stride s
+// elements) into lds[t*L + e].  16-byte pieces when every chunk is 16-B aligned, else dwords.
+__device__ __forceinline__ void stage_chunk(const double *X, int64_t s, int64_t off, int L,
+                                            int64_t t0, int64_t batch, double *lds, int lane)
+{
+    if (L <= 0) return;
+    const bool wide = ((s | off | L) & 1) == 0;                 // uniform
+    const int unit = wide ? 16 : 4;
+    const int per = L * 8 / unit;                               // pieces per trajectory
+    const int q = 64 / per, r = 64 - q * per;                   // uniform
+    int tl = lane / per, e = lane - tl * per;
+    const bool full = t0 + 64 <= batch;                         // uniform: no clamp needed
+    // running byte address; advancing by (q trajectories, r pieces) per instruction
+    const int64_t sb = s * 8;
+    const char *gp = (const char *)X + (t0 + tl) * sb + off * 8 + (int64_t)e * unit;
+    const int64_t step = q * sb + (int64_t)r * unit, wrap = sb - (int64_t)per * unit;
+    for (int i = 0; i < 64 * per; i += 64) {
+        const char *src = gp;
+        if (!full && t0 + tl >= batch)
+            src = (const char *)X + (batch - 1) * sb + off * 8 + (int64_t)e * unit;
+        char *lp = (char *)lds + (int64_t)i * unit;
+        if (wide)
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lp, 16, 0, 0);
+        else
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lp, 4, 0, 0);
+        tl += q;
+        e += r;
+        gp += step;
+        if (e >= per) {
+            e -= per;
+            tl += 1;
+            gp += wrap;
+        }
+    }
+}
+
+template <int WM, int RM, int YM> struct StageCfg {
+    static constexpr int LY = RM * WM, Ly = YM, LH = WM * WM, Lg = WM;
+    static constexpr int SIZE = 64 * (LY + Ly + LH + Lg); // doubles per buffer
+};
+
+__device__ __forceinline__ void stage_knot(const KktArgs &a, const KMeta &km, int64_t t0, double *buf,
+                                           int LYm, int Lym, int LHm, int lane)
+{
+    const int rows = km.n1 + km.p + km.n2;
+    const int LH = a.h_mode == 2 ? km.w : km.w * km.w;
+    stage_chunk(a.Y, a.sY, km.oY, rows * km.w, t0, a.batch, buf, lane);
+    stage_chunk(a.y, a.sy, km.oy, km.p + km.n2, t0, a.batch, buf + 64 * LYm, lane);
+    stage_chunk(a.H, a.sH, km.oH, LH, t0, a.batch, buf + 64 * (LYm + Lym), lane);
+    stage_chunk(a.g, a.sg, km.og, km.w, t0, a.batch, buf + 64 * (LYm + Lym + LHm), lane);
+}
+
+// LDS-DMA completion is ordered for ds_read only by vmcnt; and a ds_read still in flight
+// when a DMA is issued into its buffer may return the new bytes, so every wait that
+// precedes a restage also drains lgkmcnt.
+__device__ __forceinline__ void dma_wait()
+{
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+// wait for everything but the N most recent vector-memory ops (the previous knot's slab
+// stores, issued after the DMA being waited for)
+template <int NST> __device__ __forceinline__ void dma_wait_but()
+{
+    static_assert(NST >= 0 && NST < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NST) : "memory");
+}
+
+#ifndef LQRX_KKT_DMACHECK
+#define LQRX_KKT_DMACHECK 0
+#endif
+// Debug build only (-DLQRX_KKT_DMACHECK=1): compare a staged knot image against a plain
+// global read of the same bytes; a mismatch means a staging/wait bug.  Returns 0 if clean.
+__device__ __noinline__ int dma_verify(const KktArgs &a, const KMeta &km, int64_t t, bool live,
+                                       const double *Yl, const double *yl, const double *Hl,
+                                       const double *gl, int k, int where)
+{
+    if (!live) return 0;
+    const int rows = km.n1 + km.p + km.n2;
+    const int LH = a.h_mode == 2 ? km.w : km.w * km.w;
+    const double *src[4] = {a.Y + t * a.sY + km.oY, a.y + t * a.sy + km.oy, a.H + t * a.sH + km.oH,
+                            a.g + t * a.sg + km.og};
+    const double *lds[4] = {Yl, yl, Hl, gl};
+    const int L[4] = {rows * km.w, km.p + km.n2, LH, km.w};
+    int bad = 0;
+    for (int f = 0; f < 4; ++f)
+        for (int e = 0; e < L[f]; ++e)
+            if (__double_as_longlong(src[f][e]) != __double_as_longlong(lds[f][e])) {
+                if (!bad)
+                    printf("DMACHECK where=%d knot=%d t=%ld field=%d e=%d lds=%g glob=%g\n", where, k,
+                           (long)t, f, e, lds[f][e], src[f][e]);
+                bad = 1;
+            }
+    return bad;
+}
+
+template <int P1M, int PSM, int P2M, int WM, int RM>
+__global__ __launch_bounds__(64) void kkt_staged_kernel(const KktArgs a, const int32_t *__restrict__ meta,
+                                                        double *__restrict__ scratch)
+{
+    using SL = Slab<P1M, PSM, P2M>;
+    constexpr int PM = (P1M > P2M ? P1M : P2M);
+    using SC = StageCfg<WM, RM, PSM + P2M>;
+    constexpr int LYm = SC::LY, Lym = SC::Ly, LHm = SC::LH;
+    __shared__ double stg[2 * SC::SIZE];
+    const int lane = threadIdx.x;
+    const int64_t t0 = (int64_t)blockIdx.x * 64, t = t0 + lane;
+    const bool live = t < a.batch;
+    const int N = a.N, hmode = a.h_mode, ginv = a.ginv;
+    const int64_t Bp = (a.batch + 63) & ~(int64_t)63;           // slab batch stride
+    double *dz = a.dz + t * a.sg, *lam = a.lam + t * a.sl;
+    auto slab = [&](int k, int f) -> double & { return scratch[((int64_t)k * SL::SIZE + f) * Bp + t]; };
+    auto Yb = [&](int b, const KMeta &km) { return stg + b * SC::SIZE + lane * ((km.n1 + km.p + km.n2) * km.w); };
+    auto yb = [&](int b, const KMeta &km) { return stg + b * SC::SIZE + 64 * LYm + lane * (km.p + km.n2); };
+    auto Hb = [&](int b, const KMeta &km) {
+        return stg + b * SC::SIZE + 64 * (LYm + Lym) + lane * (hmode == 2 ? km.w : km.w * km.w);
+    };
+    auto gb = [&](int b, const KMeta &km) { return stg + b * SC::SIZE + 64 * (LYm + Lym + LHm) + lane * km.w; };
+    int info = 0;
+
+    // ---------------- forward sweep ----------------
+    ShurBlk<P1M, PSM, P2M> cur, nxt;
+    KMeta km = kmeta(meta, 0);
+    double ycur[PSM + P2M];                                     // y_k of the current knot
+    stage_knot(a, km, t0, stg, LYm, Lym, LHm, lane);
+    dma_wait();
+    if (N > 1) stage_knot(a, kmeta(meta, 1), t0, stg + SC::SIZE, LYm, Lym, LHm, lane);
+    if (LQRX_KKT_DMACHECK && dma_verify(a, km, t, live, Yb(0, km), yb(0, km), Hb(0, km), gb(0, km), 0, 0))
+        info = 9999;
+    if (!compute_shur<P1M, PSM, P2M, WM>(cur, Yb(0, km), Hb(0, km), gb(0, km), km, hmode, ginv) && !info)
+        info = -1;
+    {
+        const double *yk = yb(0, km);
+#pragma unroll
+        for (int i = 0; i < PSM + P2M; ++i) ycur[i] = (i < km.p + km.n2) ? yk[i] : 0.0;
+    }
+    double Ua[PM * PM], lprev[PM];
+#pragma unroll
+    for (int i = 0; i < PM * PM; ++i) Ua[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < PM; ++i) lprev[i] = 0.0;
+
+    for (int k = 0; k < N; ++k) {
+        const int p1 = km.n1, ps = km.p, p2 = km.n2;
+        KMeta kn{};
+        double ynxt[PSM + P2M];
+        if (k + 1 < N) {
+            kn = kmeta(meta, k + 1);
+            // knot k+1 has landed (the previous knot's slab stores may still fly) and every
+            // ds_read of the buffer about to be restaged has returned (WAR vs the DMA)
+            if (k == 0) dma_wait();
+            else dma_wait_but<SL::SIZE>();
+            if (k + 2 < N) stage_knot(a, kmeta(meta, k + 2), t0, stg + (k & 1) * SC::SIZE, LYm, Lym, LHm, lane);
+            asm volatile("" ::: "memory");                      // keep the DMAs before the stores
+            const int b = (k + 1) & 1;
+            if (LQRX_KKT_DMACHECK && dma_verify(a, kn, t, live, Yb(b, kn), yb(b, kn), Hb(b, kn), gb(b, kn), k + 1, 1))
+                info = 9999;
+            if (!compute_shur<P1M, PSM, P2M, WM>(nxt, Yb(b, kn), Hb(b, kn), gb(b, kn), kn, hmode, ginv) && !info)
+                info = -(k + 2);
+            const double *yk = yb(b, kn);
+#pragma unroll
+            for (int i = 0; i < PSM + P2M; ++i) ynxt[i] = (i < kn.p + kn.n2) ? yk[i] : 0.0;
+        }
+        double FB[PSM * PSM], FC[P2M * P2M], FD[P1M * PSM], FE[PSM * P2M], FF[P1M * P2M], c[PSM], d[P2M];
+#pragma unroll
+        for (int i = 0; i < PSM * PSM; ++i) FB[i] = cur.B[i];
+#pragma unroll
+        for (int j = 0; j < P2M; ++j)
+#pragma unroll
+            for (int i = 0; i < P2M; ++i)
+                FC[KIDX(i, j, P2M)] = cur.C[KIDX(i, j, P2M)] +
+                    ((k + 1 < N && i < P1M && j < P1M) ? nxt.A[KIDX(i < P1M ? i : 0, j < P1M ? j : 0, P1M)] : 0.0);
+#pragma unroll
+        for (int i = 0; i < P1M * PSM; ++i) FD[i] = cur.D[i];
+#pragma unroll
+        for (int i = 0; i < PSM * P2M; ++i) FE[i] = cur.E[i];
+#pragma unroll
+        for (int i = 0; i < P1M * P2M; ++i) FF[i] = cur.F[i];
+#pragma unroll
+        for (int i = 0; i < PSM; ++i) c[i] = (i < ps) ? cur.rs[i] - ycur[i] : 0.0;
+        // y_d starts at index ps (runtime): select statically
+#pragma unroll
+        for (int i = 0; i < P2M; ++i) {
+            double yd = 0.0;
+#pragma unroll
+            for (int q = 0; q < PSM + P2M; ++q)
+                if (q == ps + i) yd = ycur[q];
+            d[i] = (i < p2) ? cur.r2[i] - yd : 0.0;
+            if (k + 1 < N && i < P1M) d[i] += nxt.r1[i < P1M ? i : 0];
+        }
+        // cholesky!(U[k], F[k])
+        if (p1 > 0) {
+            if (ps) trsm_ut<PM, P1M, PSM>(Ua, p1, FD, ps);
+            if (p2) trsm_ut<PM, P1M, P2M>(Ua, p1, FF, p2);
+        }
+        if (ps) {
+#pragma unroll
+            for (int j = 0; j < PSM; ++j)
+#pragma unroll
+                for (int i = 0; i < PSM; ++i) {
+                    double s = FB[KIDX(i, j, PSM)];
+#pragma unroll
+                    for (int q = 0; q < P1M; ++q) s -= FD[KIDX(q, i, P1M)] * FD[KIDX(q, j, P1M)];
+                    FB[KIDX(i, j, PSM)] = s;
+                }
+            if (!potrf_u<PSM>(FB, ps) && !info) info = k + 1;
+#pragma unroll
+            for (int j = 0; j < P2M; ++j)
+#pragma unroll
+                for (int i = 0; i < PSM; ++i) {
+                    double s = FE[KIDX(i, j, PSM)];
+#pragma unroll
+                    for (int q = 0; q < P1M; ++q) s -= FD[KIDX(q, i, P1M)] * FF[KIDX(q, j, P1M)];
+                    FE[KIDX(i, j, PSM)] = s;
+                }
+            if (p2) trsm_ut<PSM, PSM, P2M>(FB, ps, FE, p2);
+        }
+        if (p2) {
+#pragma unroll
+            for (int j = 0; j < P2M; ++j)
+#pragma unroll
+                for (int i = 0; i <= j; ++i) {
+                    double s = FC[KIDX(i, j, P2M)];
+#pragma unroll
+                    for (int q = 0; q < P1M; ++q) s -= FF[KIDX(q, i, P1M)] * FF[KIDX(q, j, P1M)];
+#pragma unroll
+                    for (int q = 0; q < PSM; ++q) s -= FE[KIDX(q, i, PSM)] * FE[KIDX(q, j, PSM)];
+                    FC[KIDX(i, j, P2M)] = s;
+                }
+            if (!potrf_u<P2M>(FC, p2) && !info) info = k + 1;
+        }
+        // forward_substitution!
+        double mu[PSM], la[P2M];
+#pragma unroll
+        for (int i = 0; i < PSM; ++i) {
+            double s = c[i];
+#pragma unroll
+            for (int q = 0; q < P1M; ++q)
+                if (q < p1) s -= FD[KIDX(q, i, P1M)] * lprev[q < PM ? q : 0];
+            mu[i] = s;
+        }
+        if (ps > 0) trsm_ut<PSM, PSM, 1>(FB, ps, mu, 1);
+#pragma unroll
+        for (int i = 0; i < P2M; ++i) {
+            double s = d[i];
+#pragma unroll
+            for (int q = 0; q < P1M; ++q)
+                if (q < p1) s -= FF[KIDX(q, i, P1M)] * lprev[q < PM ? q : 0];
+#pragma unroll
+            for (int q = 0; q < PSM; ++q)
+                if (q < ps) s -= FE[KIDX(q, i, PSM)] * mu[q];
+            la[i] = s;
+        }
+        if (p2 > 0) trsm_ut<P2M, P2M, 1>(FC, p2, la, 1);
+        // factor slab (batch-fastest → coalesced)
+#pragma unroll
+        for (int i = 0; i < PSM * PSM; ++i) slab(k, SL::B + i) = FB[i];
+#pragma unroll
+        for (int i = 0; i < P2M * P2M; ++i) slab(k, SL::C + i) = FC[i];
+#pragma unroll
+        for (int i = 0; i < P1M * PSM; ++i) slab(k, SL::D + i) = FD[i];
+#pragma unroll
+        for (int i = 0; i < PSM * P2M; ++i) slab(k, SL::E + i) = FE[i];
+#pragma unroll
+        for (int i = 0; i < P1M * P2M; ++i) slab(k, SL::F + i) = FF[i];
+#pragma unroll
+        for (int i = 0; i < PSM; ++i) slab(k, SL::MU + i) = mu[i];
+#pragma unroll
+        for (int i = 0; i < P2M; ++i) slab(k, SL::LAM + i) = la[i];
+#pragma unroll
+        for (int j = 0; j < PM; ++j)
+#pragma unroll
+            for (int i = 0; i < PM; ++i) Ua[KIDX(i, j, PM)] = (i < P2M && j < P2M) ? FC[KIDX(i < P2M ? i : 0, j < P2M ? j : 0, P2M)] : 0.0;
+#pragma unroll
+        for (int i = 0; i < PM; ++i) lprev[i] = (i < P2M) ? la[i < P2M ? i : 0] : 0.0;
+        if (k + 1 < N) {
+            cur = nxt;
+            km = kn;
+#pragma unroll
+            for (int i = 0; i < PSM + P2M; ++i) ycur[i] = ynxt[i];
+        }
+    }
+
+    // ---------------- backward sweep + primal recovery ----------------
+    double nD[P1M * PSM], nF[P1M * P2M], nmu[PSM], nla[P2M];
+    int nps = 0, np2 = 0;
+#pragma unroll
+    for (int i = 0; i < P1M * PSM; ++i) nD[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < P1M * P2M; ++i) nF[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < PSM; ++i) nmu[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < P2M; ++i) nla[i] = 0.0;
+    dma_wait();
+    __syncthreads();
+    stage_knot(a, kmeta(meta, N - 1), t0, stg + ((N - 1) & 1) * SC::SIZE, LYm, Lym, LHm, lane);
+
+    for (int k = N - 1; k >= -1; --k) {
+        double mu[PSM] = {}, la[P2M] = {};
+        KMeta kk{};
+        if (k >= 0) {
+            kk = kmeta(meta, k);
+            const int ps = kk.p, p2 = kk.n2;
+            double FB[PSM * PSM], FC[P2M * P2M], FE[PSM * P2M];
+#pragma unroll
+            for (int i = 0; i < PSM * PSM; ++i) FB[i] = slab(k, SL::B + i);
+#pragma unroll
+            for (int i = 0; i < P2M * P2M; ++i) FC[i] = slab(k, SL::C + i);
+#pragma unroll
+            for (int i = 0; i < PSM * P2M; ++i) FE[i] = slab(k, SL::E + i);
+#pragma unroll
+            for (int i = 0; i < PSM; ++i) mu[i] = slab(k, SL::MU + i);
+#pragma unroll
+            for (int i = 0; i < P2M; ++i) la[i] = slab(k, SL::LAM + i);
+            if (k < N - 1) {
+#pragma unroll
+                for (int i = 0; i < P2M; ++i) {
+                    double v = la[i];
+#pragma unroll
+                    for (int q = 0; q < PSM; ++q)
+                        if (q < nps) v += nD[KIDX(i < P1M ? i : 0, q, P1M)] * nmu[q];
+#pragma unroll
+                    for (int q = 0; q < P2M; ++q)
+                        if (q < np2) v += nF[KIDX(i < P1M ? i : 0, q, P1M)] * nla[q];
+                    la[i] = v;
+                }
+                if (p2 > 0) trsv_un<P2M>(FC, p2, la);
+#pragma unroll
+                for (int i = 0; i < PSM; ++i) {
+                    double v = mu[i];
+#pragma unroll
+                    for (int q = 0; q < P2M; ++q)
+                        if (q < p2) v -= FE[KIDX(i, q, PSM)] * la[q];
+                    mu[i] = v;
+                }
+                if (ps > 0) trsv_un<PSM>(FB, ps, mu);
+#pragma unroll
+                for (int i = 0; i < P2M; ++i) la[i] = -la[i];
+#pragma unroll
+                for (int i = 0; i < PSM; ++i) mu[i] = -mu[i];
+            } else {
+                if (ps > 0) trsv_un<PSM>(FB, ps, mu);
+#pragma unroll
+                for (int i = 0; i < PSM; ++i) mu[i] = -mu[i];
+            }
+            if (live) {
+#pragma unroll
+                for (int i = 0; i < PSM; ++i)
+                    if (i < ps) lam[kk.oy + i] = mu[i];
+#pragma unroll
+                for (int i = 0; i < P2M; ++i)
+                    if (i < p2) lam[kk.oy + ps + i] = la[i];
+            }
+        }
+        if (k + 1 <= N - 1) {
+            const int kp = k + 1;
+            KMeta m1 = kmeta(meta, kp);
+            dma_wait();                                          // knot k+1 landed, reads retired
+            if (k >= 0) stage_knot(a, kk, t0, stg + (k & 1) * SC::SIZE, LYm, Lym, LHm, lane);
+            const int b = kp & 1;
+            const int rows = m1.n1 + m1.p + m1.n2, w = m1.w;
+            const double *Yk = Yb(b, m1), *Hk = Hb(b, m1), *gk = gb(b, m1);
+            if (LQRX_KKT_DMACHECK && dma_verify(a, m1, t, live, Yk, yb(b, m1), Hk, gk, kp, 2)) info = 9999;
+            double z[WM];
+#pragma unroll
+            for (int j = 0; j < WM; ++j)
+                if (j < w) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int i = 0; i < P2M; ++i)
+                        if (i < m1.n2) v += Yk[(m1.n1 + m1.p + i) + j * rows] * nla[i];
+#pragma unroll
+                    for (int i = 0; i < PSM; ++i)
+                        if (i < m1.p) v += Yk[(m1.n1 + i) + j * rows] * nmu[i];
+                    if (kp > 0) {
+#pragma unroll
+                        for (int i = 0; i < P1M; ++i)
+                            if (i < m1.n1) v += Yk[i + j * rows] * la[i < P2M ? i : 0];
+                    }
+                    if (ginv) v += gk[j];
+                    z[j] = v;
+                } else {
+                    z[j] = 0.0;
+                }
+            if (ginv) {
+                HFac<WM> hf;
+                load_hfac<WM>(hf, Hk, w, hmode);
+                hinv_apply<WM>(hf, z, w, hmode);
+            }
+            if (live) {
+#pragma unroll
+                for (int j = 0; j < WM; ++j)
+                    if (j < w) dz[m1.og + j] = -z[j];
+            }
+        }
+        if (k >= 0) {
+#pragma unroll
+            for (int i = 0; i < P1M * PSM; ++i) nD[i] = slab(k, SL::D + i);
+#pragma unroll
+            for (int i = 0; i < P1M * P2M; ++i) nF[i] = slab(k, SL::F + i);
+#pragma unroll
+            for (int i = 0; i < PSM; ++i) nmu[i] = mu[i];
+#pragma unroll
+            for (int i = 0; i < P2M; ++i) nla[i] = la[i];
+            nps = kk.p;
+            np2 = kk.n2;
+        }
+    }
+    dma_wait();
+    if (a.info && live) a.info[t] = info;
+}
+
+template <int P1M, int PSM, int P2M, int WM, int RM>
+static hipError_t launch_staged(const KktArgs &a, hipStream_t s)
+{
+    using SL = Slab<P1M, PSM, P2M>;
+    double *scratch = nullptr;
+    const size_t Bp = ((size_t)a.batch + 63) & ~(size_t)63;
+    size_t bytes = Bp * (size_t)a.N * SL::SIZE * sizeof(double);
+    hipError_t e = hipMallocAsync((void **)&scratch, bytes, s);
+    if (e != hipSuccess) return e;
+    dim3 grid((unsigned)((a.batch + 63) / 64)), block(64);
+    hipLaunchKernelGGL((kkt_staged_kernel<P1M, PSM, P2M, WM, RM>), grid, block, 0, s, a, a.meta, scratch);
+    e = hipGetLastError();
+    hipError_t ef = hipFreeAsync(scratch, s);
+    return e != hipSuccess ? e : ef;
+}
+
 template <int P1M, int PSM, int P2M, int WM, int RM>
 static hipError_t launch_lane(const KktArgs &a, hipStream_t s)
 {
@@ -597,7 +1034,7 @@ hipError_t kkt_launch(const KktArgs &a, hipStream_t s)
 {
     // block-size maxima from the structure (host copy in a.hmeta)
     const int P1 = a.max_p1, PS = a.max_ps, P2 = a.max_p2, W = a.maxw, R = a.maxrows;
-    if (P1 <= 3 && PS <= 3 && P2 <= 3 && W <= 5 && R <= 6) return launch_lane<3, 3, 3, 5, 6>(a, s);
+    if (!a.force_lane && P1 <= 3 && PS <= 3 && P2 <= 3 && W <= 5 && R <= 6) return launch_staged<3, 3, 3, 5, 6>(a, s);
     if (P1 <= 4 && PS <= 4 && P2 <= 4 && W <= 8 && R <= 8) return launch_lane<4, 4, 4, 8, 8>(a, s);
     if (P1 <= 8 && PS <= 8 && P2 <= 8 && W <= 12 && R <= 16) return launch_lane<8, 8, 8, 12, 16>(a, s);
     return hipErrorNotSupported;

@@ -10,7 +10,7 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblqrx.so")
+LIB_PATH = os.environ.get("LQRX_LIB") or os.path.join(_HERE, "liblqrx.so")
 HEADER_PATH = os.path.abspath(os.path.join(_HERE, "..", "..", "include", "lqrx.h"))
 
 F64, F32 = 0, 1
