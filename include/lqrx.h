@@ -23,6 +23,7 @@
 #ifndef LQRX_H
 #define LQRX_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -129,6 +130,10 @@ int lqrx_kkt_sizes(const lqrx_kkt_desc *desc, int64_t *nY, int64_t *ny, int64_t 
  * ------------------------------------------------------------------------------------ */
 int lqrx_abi_version(void);
 const char *lqrx_last_error(void);
+/* copy the calling thread's last error message into buf (NUL-terminated, truncated to
+ * len-1 bytes); returns the full message length.  For bindings that cannot hold a
+ * pointer into library memory (SURVEY.md §8(b) lqrx_get_last_error). */
+int lqrx_get_last_error(char *buf, size_t len);
 /* 1 if the HIP runtime sees a gfx950 device, else 0 (no compute; safe without a GPU) */
 int lqrx_device_available(void);
 

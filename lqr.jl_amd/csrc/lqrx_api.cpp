@@ -83,6 +83,16 @@ int lqrx_abi_version(void) { return LQRX_ABI_VERSION; }
 
 const char *lqrx_last_error(void) { return g_err.c_str(); }
 
+int lqrx_get_last_error(char *buf, size_t len)
+{
+    if (buf && len > 0) {
+        const size_t k = std::min(len - 1, g_err.size());
+        std::memcpy(buf, g_err.data(), k);
+        buf[k] = '\0';
+    }
+    return (int)g_err.size();
+}
+
 int lqrx_device_available(void)
 {
     int n = 0;

@@ -43,6 +43,7 @@ _VP = C.c_void_p
 _SIGS = {
     "lqrx_abi_version": (C.c_int, []),
     "lqrx_last_error": (C.c_char_p, []),
+    "lqrx_get_last_error": (C.c_int, [C.c_char_p, C.c_size_t]),
     "lqrx_device_available": (C.c_int, []),
     "lqrx_dp_solve": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 10 + [_VP, _VP]),
     "lqrx_dp_solve_host": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 10 + [_VP]),

@@ -83,3 +83,17 @@ def test_generator_deterministic_and_sharded(lqrx):
     bb = abi_to_batch(a)
     assert np.allclose(bb.Q, np.swapaxes(bb.Q, 1, 2))
     assert (np.linalg.eigvalsh(bb.R) > 0).all()
+
+
+def test_get_last_error_copies(lqrx):
+    from lqrx import _lib
+
+    lib = lqrx.load()
+    d = _lib.DpDesc(32, 16, 0, 0, 4, 0, 0, 0, 0)          # N = 0 is invalid
+    assert lib.lqrx_dp_solve(C.byref(d), *([None] * 10), None, None) < 0
+    full = lib.lqrx_last_error()
+    buf = C.create_string_buffer(8)
+    n = lib.lqrx_get_last_error(buf, 8)
+    assert n == len(full) and buf.value == full[:7]
+    big = C.create_string_buffer(1024)
+    assert lib.lqrx_get_last_error(big, 1024) == len(full) and big.value == full

@@ -74,3 +74,21 @@ def test_kkt_info_non_spd(lqrx, gpu_ok):
     got = K.kkt_solve(pb)
     assert got["rc"] == 1 and got["info"][2] != 0
     assert got["info"][0] == 0 and got["info"][1] == 0 and got["info"][3] == 0
+
+
+def test_kkt_alternating_structures(lqrx, gpu_ok):
+    """Repeated solves that alternate block structures and batch sizes in one process.
+    Regression for a stale device structure table (per-call pool allocation + async copy
+    from pageable memory) that corrupted every later solve of one structure."""
+    import lqrx.kkt as K
+
+    cases = []
+    for N, batch, h, seed in [(11, 4, 0, 18), (101, 256, 2, 5), (11, 67, 1, 3), (3, 5, 2, 4)]:
+        st = K.dubins_structure(N)
+        pb = K.random_kkt(st, batch, seed=seed, h_mode=h)
+        ref = _ref(st, pb, 1)
+        cases.append((pb, ref["dz"].reshape(batch, -1), ref["lam"].reshape(batch, -1)))
+    for _ in range(8):
+        for pb, rd, rl in cases:
+            got = K.kkt_solve(pb)
+            assert rel(got["dz"], rd) <= TOL and rel(got["lam"], rl) <= TOL
