@@ -50,6 +50,8 @@ extern "C" {
  *
  * Buffers (layout 0, element type per dtype):
  *   A  n·n·batch     B  n·m·batch    Q  n·n·batch    R  m·m·batch    Qf n·n·batch
+ *      (×(N-1) per trajectory for time-varying fields, see knot_stride_*; the
+ *       time-varying path is SURVEY §8(f) rank 1 and currently covers n ≤ 4, m ≤ 4)
  *   x0 n·batch
  *   K  m·n·(N-1)·batch     sol.K[k], k = 1..N-1  (LQRSolution.K)
  *   P  n·n·batch  (p_mode 0: P_1 = solver.P on return, :63)
@@ -66,8 +68,11 @@ typedef struct lqrx_dp_desc {
     int64_t batch;          /* number of independent problems                          */
     int32_t layout;         /* 0 = column-major, batch slowest (only value supported)  */
     int32_t p_mode;         /* 0 = P_1 only (reference-observable), 1 = all P_k        */
-    int64_t knot_stride_AB; /* 0 = time-invariant (reference LQRProblem); >0 reserved  */
-    int64_t knot_stride_QR; /* 0 = time-invariant; >0 reserved                         */
+    int64_t knot_stride_AB; /* 0 = time-invariant A, B (reference LQRProblem);
+                               1 = per knot: A n·n·(N-1)·batch, B n·m·(N-1)·batch, knot k
+                               at index k-1 (LCRProblem.A/.B, constrained_problem.jl:3-4) */
+    int64_t knot_stride_QR; /* 0 = time-invariant Q, R; 1 = per knot: Q n·n·(N-1)·batch,
+                               R m·m·(N-1)·batch (Qf stays the terminal cost)            */
 } lqrx_dp_desc;
 
 /* device pointers (hipMalloc'd or torch CUDA/HIP tensors) */

@@ -68,10 +68,14 @@ int validate_dp(const lqrx_dp_desc *d)
     if (d->batch < 0) return set_err(-1, "desc.batch must be >= 0");
     if (d->layout != 0) return set_err(LQRX_ERR_UNSUPPORTED, "desc.layout %d not supported", d->layout);
     if (d->p_mode != 0 && d->p_mode != 1) return set_err(-1, "desc.p_mode must be 0 or 1");
-    if (d->knot_stride_AB != 0 || d->knot_stride_QR != 0)
-        return set_err(LQRX_ERR_UNSUPPORTED, "time-varying knot strides are not supported yet");
-    if (!lqrx::dp_supported(d->dtype, d->n, d->m))
-        return set_err(LQRX_ERR_UNSUPPORTED, "no kernel instantiated for n=%d m=%d", d->n, d->m);
+    if (d->knot_stride_AB != 0 && d->knot_stride_AB != 1)
+        return set_err(-1, "desc.knot_stride_AB must be 0 (time-invariant) or 1 (per knot)");
+    if (d->knot_stride_QR != 0 && d->knot_stride_QR != 1)
+        return set_err(-1, "desc.knot_stride_QR must be 0 (time-invariant) or 1 (per knot)");
+    const bool tv = d->knot_stride_AB != 0 || d->knot_stride_QR != 0;
+    if (!lqrx::dp_supported(d->dtype, d->n, d->m, tv))
+        return set_err(LQRX_ERR_UNSUPPORTED, "no kernel instantiated for n=%d m=%d%s", d->n, d->m,
+                       tv ? " (time-varying)" : "");
     return 0;
 }
 
@@ -123,6 +127,7 @@ int lqrx_dp_solve(const lqrx_dp_desc *d, const void *A, const void *B, const voi
     a.K = K; a.P = P; a.X = X; a.U = U; a.info = info;
     a.n = d->n; a.m = d->m; a.N = d->N; a.dtype = d->dtype; a.p_all = d->p_mode;
     a.batch = d->batch;
+    a.tv_AB = (int)d->knot_stride_AB; a.tv_QR = (int)d->knot_stride_QR;
     hipStream_t s = (hipStream_t)stream;
     hipError_t e = lqrx::dp_launch(a, s);
     if (e == hipErrorNotSupported)
@@ -151,7 +156,8 @@ int lqrx_dp_solve_host(const lqrx_dp_desc *d, const void *A, const void *B, cons
     if (d->batch == 0) return 0;
     const size_t s = dsize(d->dtype), bt = (size_t)d->batch;
     const size_t n = d->n, m = d->m, N = d->N;
-    const size_t szin[6] = {n * n, n * m, n * n, m * m, n * n, n};
+    const size_t kAB = d->knot_stride_AB ? N - 1 : 1, kQR = d->knot_stride_QR ? N - 1 : 1;
+    const size_t szin[6] = {n * n * kAB, n * m * kAB, n * n * kQR, m * m * kQR, n * n, n};
     const void *hin[6] = {A, B, Q, R, Qf, x0};
     const size_t szout[4] = {m * n * (N - 1), d->p_mode ? n * n * N : n * n, n * N, m * (N - 1)};
     void *hout[4] = {K, P, X, U};

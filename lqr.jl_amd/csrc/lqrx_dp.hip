@@ -435,6 +435,9 @@ static hipError_t launch_dp(const DpArgs &a, hipStream_t s)
 
 hipError_t dp_launch(const DpArgs &a, hipStream_t s)
 {
+    // n ≤ 4: one lane per trajectory (a 16×16 MFMA tile would be mostly padding)
+    if (dp_lane_supported(a.n, a.m)) return dp_lane_launch(a, s);
+    if (a.tv_AB || a.tv_QR) return hipErrorNotSupported;
     // smallest instantiated tile grid that covers (n, m); padding is exact (zero rows /
     // columns, unit diagonal in R), see tiles_load
     const int nt = (a.n + 15) / 16, mt = (a.m + 15) / 16;
@@ -452,11 +455,12 @@ hipError_t dp_launch(const DpArgs &a, hipStream_t s)
     return hipErrorNotSupported;
 }
 
-bool dp_supported(int dtype, int n, int m)
+bool dp_supported(int dtype, int n, int m, bool tv)
 {
     (void)dtype;
+    if (dp_lane_supported(n, m)) return true;
     const int nt = (n + 15) / 16, mt = (m + 15) / 16;
-    return n >= 1 && m >= 1 && nt <= 4 && mt <= 2;
+    return !tv && n >= 1 && m >= 1 && nt <= 4 && mt <= 2;
 }
 
 } // namespace lqrx

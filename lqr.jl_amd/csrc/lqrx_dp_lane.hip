@@ -1,0 +1,334 @@
+// lqrx_dp_lane.hip — batched Riccati backward pass + forward rollout for SMALL state
+// dimensions (n ≤ 4, m ≤ 4): the reference's test problems (cartpole n=4 m=1,
+// test/cartpole.jl; Dubins n=3 m=2; double integrators), BASELINE configs[0..1].
+// Replaces solve!(sol, ::DPSolver, ::LQRProblem), /root/reference/src/dynamic_programming.jl:54-72.
+//
+// Mapping: ONE LANE PER TRAJECTORY (64 trajectories per wave).  At n = 4 a 16×16 fp64 MFMA
+// tile would be 94 % padding; here every flop is useful: the whole knot (≈160 fp64 FMAs at
+// n=4, m=1) is straight-line scalar code on registers, all dimensions compile-time padded
+// (NP, MP) with exact zero padding (A, B, Q padded with zeros, R with a unit diagonal: the
+// padded rows/columns of P, E, K stay exactly 0/identity, so real entries see only +0·x
+// terms).  The horizon walk is serial per lane; the batch is the parallelism.
+//
+// Per knot (fast symmetric form, as the MFMA kernel; reference lines of dynamic_programming.jl):
+//   :38  PB = P·B           :39  E = R + BᵀPB         :40  PA = P·A       :41  G = BᵀPA
+//   :29-30 potrf 'U' of E (pivot ≤ 0 → info = k) and K = E⁻¹G by two triangular solves
+//   :50-51 P_ = Q + AᵀPA − GᵀK  (GᵀK ≡ APB·K for symmetric P), lower triangle, mirrored.
+// Time-varying problems (per-knot A_k, B_k, Q_k, R_k) reload the knot's
+// matrices instead of keeping them in registers.
+#include "lqrx_internal.h"
+#include "lqrx_tile.h"
+
+namespace lqrx {
+
+namespace {
+
+template <typename T> __device__ __forceinline__ T lane_rsqrt(T a);
+template <> __device__ __forceinline__ double lane_rsqrt<double>(double a) { return rsqrt_nr(a); }
+template <> __device__ __forceinline__ float lane_rsqrt<float>(float a) { return rsqrt_nr(a); }
+
+// load an r×c column-major block (ld = r) into a padded RP×CP register array; pad value
+// `dpad` on the padded diagonal (1 for R so the padded E stays SPD), 0 elsewhere
+template <typename T, int RP, int CP>
+__device__ __forceinline__ void lane_load(T (&D)[RP][CP], const T *__restrict__ src, int r, int c, T dpad)
+{
+#pragma unroll
+    for (int j = 0; j < CP; ++j)
+#pragma unroll
+        for (int i = 0; i < RP; ++i) {
+            const bool ok = i < r && j < c;
+            D[i][j] = ok ? src[i + j * r] : (i == j ? dpad : (T)0);
+        }
+}
+
+} // namespace
+
+template <typename T, int NP, int MP, bool TV>
+__global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
+{
+    const int64_t b = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (b >= a.batch) return;   // no barriers / cross-lane ops below
+    const int n = a.n, m = a.m, N = a.N;
+    const int64_t nn = (int64_t)n * n, nm = (int64_t)n * m, mm = (int64_t)m * m;
+    // TV (template): matrices are re-read every knot; a time-invariant field of a
+    // time-varying problem simply has knot stride 0 (it stays cache-resident)
+    constexpr bool tvAB = TV, tvQR = TV;
+    const int64_t kAB = a.tv_AB ? N - 1 : 1, kQR = a.tv_QR ? N - 1 : 1;    // knots stored
+    const int64_t sA = a.tv_AB ? nn : 0, sB = a.tv_AB ? nm : 0;            // knot strides
+    const int64_t sQ = a.tv_QR ? nn : 0, sR = a.tv_QR ? mm : 0;
+    const T *Ab = (const T *)a.A + b * nn * kAB;
+    const T *Bb = (const T *)a.B + b * nm * kAB;
+    const T *Qb = (const T *)a.Q + b * nn * kQR;
+    const T *Rb = (const T *)a.R + b * mm * kQR;
+
+    T A[NP][NP], B[NP][MP], Q[NP][NP], R[MP][MP], P[NP][NP];
+    lane_load<T, NP, NP>(P, (const T *)a.Qf + b * nn, n, n, (T)0);   // :58 P = Qf
+    if constexpr (!tvAB) {
+        lane_load<T, NP, NP>(A, Ab, n, n, (T)0);
+        lane_load<T, NP, MP>(B, Bb, n, m, (T)0);
+    }
+    if constexpr (!tvQR) {
+        lane_load<T, NP, NP>(Q, Qb, n, n, (T)0);
+        lane_load<T, MP, MP>(R, Rb, m, m, (T)1);
+    }
+    T *Kb = (T *)a.K + b * (int64_t)(N - 1) * nm;
+    T *Pall = a.p_all ? (T *)a.P + b * nn * N : nullptr;
+    auto store_P = [&](T *dst) {
+#pragma unroll
+        for (int j = 0; j < NP; ++j)
+#pragma unroll
+            for (int i = 0; i < NP; ++i)
+                if (i < n && j < n) dst[i + j * n] = (i >= j) ? P[i][j] : P[j][i];
+    };
+    if (Pall) store_P(Pall + (int64_t)(N - 1) * nn);
+    int info = 0;
+    // time-varying: knot k's matrices are prefetched during knot k+1
+    constexpr int TN = TV ? NP : 1, TM = TV ? MP : 1;
+    T An[TN][TN], Bn[TN][TM], Qn[TN][TN], Rn[TM][TM];
+    auto fetch_tv = [&](int k) {
+        if (k < 1) return;
+        if constexpr (tvAB) {
+            lane_load<T, NP, NP>(An, Ab + (int64_t)(k - 1) * sA, n, n, (T)0);
+            lane_load<T, NP, MP>(Bn, Bb + (int64_t)(k - 1) * sB, n, m, (T)0);
+        }
+        if constexpr (tvQR) {
+            lane_load<T, NP, NP>(Qn, Qb + (int64_t)(k - 1) * sQ, n, n, (T)0);
+            lane_load<T, MP, MP>(Rn, Rb + (int64_t)(k - 1) * sR, m, m, (T)1);
+        }
+    };
+    if constexpr (TV) fetch_tv(N - 1);
+
+    for (int k = N - 1; k >= 1; --k) {   // :61
+        if constexpr (tvAB) {
+#pragma unroll
+            for (int i = 0; i < NP; ++i) {
+#pragma unroll
+                for (int j = 0; j < NP; ++j) A[i][j] = An[i][j];
+#pragma unroll
+                for (int c = 0; c < MP; ++c) B[i][c] = Bn[i][c];
+            }
+        }
+        if constexpr (tvQR) {
+#pragma unroll
+            for (int i = 0; i < NP; ++i)
+#pragma unroll
+                for (int j = 0; j < NP; ++j) Q[i][j] = Qn[i][j];
+#pragma unroll
+            for (int i = 0; i < MP; ++i)
+#pragma unroll
+                for (int j = 0; j < MP; ++j) R[i][j] = Rn[i][j];
+        }
+        if constexpr (TV) fetch_tv(k - 1);
+        // P is symmetric: only P[i][j], i ≥ j, is maintained
+#define PS(i, j) ((i) >= (j) ? P[i][j] : P[j][i])
+        T PB[NP][MP], PA[NP][NP];
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+#pragma unroll
+            for (int c = 0; c < MP; ++c) {                       // :38 PB = P B
+                T s = (T)0;
+#pragma unroll
+                for (int l = 0; l < NP; ++l) s = fma(PS(i, l), B[l][c], s);
+                PB[i][c] = s;
+            }
+#pragma unroll
+            for (int j = 0; j < NP; ++j) {                       // :40 PA = P A
+                T s = (T)0;
+#pragma unroll
+                for (int l = 0; l < NP; ++l) s = fma(PS(i, l), A[l][j], s);
+                PA[i][j] = s;
+            }
+        }
+#undef PS
+        T E[MP][MP], G[MP][NP];
+#pragma unroll
+        for (int c = 0; c < MP; ++c) {
+#pragma unroll
+            for (int d = 0; d <= c; ++d) {                       // :39 E = R + BᵀPB (lower)
+                T s = R[c][d];
+#pragma unroll
+                for (int i = 0; i < NP; ++i) s = fma(B[i][c], PB[i][d], s);
+                E[c][d] = s;
+            }
+#pragma unroll
+            for (int j = 0; j < NP; ++j) {                       // :41 G = BᵀPA
+                T s = (T)0;
+#pragma unroll
+                for (int i = 0; i < NP; ++i) s = fma(B[i][c], PA[i][j], s);
+                G[c][j] = s;
+            }
+        }
+        // :29 potrf 'U' (E = UᵀU; here the lower storage holds Uᵀ = L): column by column
+        T L[MP][MP], Linv[MP];
+#pragma unroll
+        for (int j = 0; j < MP; ++j) {
+            T d = E[j][j];
+#pragma unroll
+            for (int p = 0; p < j; ++p) d = fma(-L[j][p], L[j][p], d);
+            if (!(d > (T)0) && info == 0) info = k;
+            const T ri = lane_rsqrt<T>(d);
+            Linv[j] = ri;
+#pragma unroll
+            for (int i = j + 1; i < MP; ++i) {
+                T s = E[i][j];
+#pragma unroll
+                for (int p = 0; p < j; ++p) s = fma(-L[i][p], L[j][p], s);
+                L[i][j] = s * ri;
+            }
+            L[j][j] = d * ri;
+        }
+        // :30 potrs: L y = G (forward), Lᵀ K = y (backward), column by column of G
+        T K[MP][NP];
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            T y[MP];
+#pragma unroll
+            for (int i = 0; i < MP; ++i) {
+                T s = G[i][j];
+#pragma unroll
+                for (int p = 0; p < i; ++p) s = fma(-L[i][p], y[p], s);
+                y[i] = s * Linv[i];
+            }
+#pragma unroll
+            for (int i = MP - 1; i >= 0; --i) {
+                T s = y[i];
+#pragma unroll
+                for (int p = i + 1; p < MP; ++p) s = fma(-L[p][i], K[p][j], s);
+                K[i][j] = s * Linv[i];
+            }
+        }
+        T *Kk = Kb + (int64_t)(k - 1) * nm;                      // sol.K[k], m×n col-major
+#pragma unroll
+        for (int j = 0; j < NP; ++j)
+#pragma unroll
+            for (int i = 0; i < MP; ++i)
+                if (i < m && j < n) Kk[i + j * m] = K[i][j];
+        // :51 P_ = Q + AᵀPA − GᵀK   (lower triangle)
+#pragma unroll
+        for (int i = 0; i < NP; ++i)
+#pragma unroll
+            for (int j = 0; j <= i; ++j) {
+                T s = Q[i][j];
+#pragma unroll
+                for (int l = 0; l < NP; ++l) s = fma(A[l][i], PA[l][j], s);
+#pragma unroll
+                for (int c = 0; c < MP; ++c) s = fma(-G[c][i], K[c][j], s);
+                P[i][j] = s;
+            }
+        if (Pall) store_P(Pall + (int64_t)(k - 1) * nn);
+    }
+    if (!a.p_all) store_P((T *)a.P + b * nn);
+    if (a.info) a.info[b] = info;
+
+    // forward rollout  :66-70  u_k = −K_k x_k ; x_{k+1} = A_k x_k + B_k u_k
+    T *Xb = (T *)a.X + b * (int64_t)N * n, *Ub = (T *)a.U + b * (int64_t)(N - 1) * m;
+    const T *x0 = (const T *)a.x0 + b * n;
+    T x[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) x[i] = i < n ? x0[i] : (T)0;
+#pragma unroll
+    for (int i = 0; i < NP; ++i)
+        if (i < n) Xb[i] = x[i];
+    // K_k (and A_k, B_k when time-varying) were written / live in HBM; the x-recurrence is a
+    // short dependent chain per knot, so the loads are issued RD knots ahead from a
+    // register ring (unrolled by RD so every ring index is static).
+    constexpr int RD = TV ? 4 : ((MP * NP <= 8) ? 8 : 4);
+    struct Knot {
+        T K[MP][NP], A[TV ? NP : 1][TV ? NP : 1], B[TV ? NP : 1][TV ? MP : 1];
+    };
+    Knot ring[RD];
+    auto fetch = [&](int k, Knot &d) {
+        if (k > N - 1) return;
+        const T *Kk = Kb + (int64_t)(k - 1) * nm;
+#pragma unroll
+        for (int j = 0; j < NP; ++j)
+#pragma unroll
+            for (int i = 0; i < MP; ++i) d.K[i][j] = (i < m && j < n) ? Kk[i + j * m] : (T)0;
+        if constexpr (tvAB) {
+            lane_load<T, NP, NP>(d.A, Ab + (int64_t)(k - 1) * sA, n, n, (T)0);
+            lane_load<T, NP, MP>(d.B, Bb + (int64_t)(k - 1) * sB, n, m, (T)0);
+        }
+    };
+#pragma unroll
+    for (int d = 0; d < RD; ++d) fetch(1 + d, ring[d]);
+    for (int k0 = 1; k0 <= N - 1; k0 += RD) {
+#pragma unroll
+        for (int d = 0; d < RD; ++d) {
+            const int k = k0 + d;
+            if (k > N - 1) break;
+            T Kc[MP][NP];
+#pragma unroll
+            for (int j = 0; j < NP; ++j)
+#pragma unroll
+                for (int i = 0; i < MP; ++i) Kc[i][j] = ring[d].K[i][j];
+            if constexpr (tvAB) {
+#pragma unroll
+                for (int i = 0; i < NP; ++i) {
+#pragma unroll
+                    for (int j = 0; j < NP; ++j) A[i][j] = ring[d].A[i][j];
+#pragma unroll
+                    for (int c = 0; c < MP; ++c) B[i][c] = ring[d].B[i][c];
+                }
+            }
+            fetch(k + RD, ring[d]);
+            T u[MP];
+#pragma unroll
+            for (int i = 0; i < MP; ++i) {
+                T s = (T)0;
+#pragma unroll
+                for (int j = 0; j < NP; ++j) s = fma(Kc[i][j], x[j], s);
+                u[i] = -s;
+                if (i < m) Ub[(int64_t)(k - 1) * m + i] = u[i];
+            }
+            T xn[NP];
+#pragma unroll
+            for (int i = 0; i < NP; ++i) {
+                T s = (T)0;
+#pragma unroll
+                for (int j = 0; j < NP; ++j) s = fma(A[i][j], x[j], s);
+#pragma unroll
+                for (int c = 0; c < MP; ++c) s = fma(B[i][c], u[c], s);
+                xn[i] = s;
+            }
+#pragma unroll
+            for (int i = 0; i < NP; ++i) {
+                x[i] = xn[i];
+                if (i < n) Xb[(int64_t)k * n + i] = x[i];
+            }
+        }
+    }
+}
+
+template <typename T, int NP, int MP>
+static hipError_t launch_lane(const DpArgs &a, hipStream_t s)
+{
+    dim3 grid((unsigned)((a.batch + 63) / 64)), block(64);
+    if (a.tv_AB || a.tv_QR)
+        hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, true>), grid, block, 0, s, a);
+    else
+        hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, false>), grid, block, 0, s, a);
+    return hipGetLastError();
+}
+
+bool dp_lane_supported(int n, int m) { return n >= 1 && m >= 1 && n <= 4 && m <= 4; }
+
+hipError_t dp_lane_launch(const DpArgs &a, hipStream_t s)
+{
+    const int np = a.n <= 2 ? 2 : 4, mp = a.m <= 1 ? 1 : (a.m <= 2 ? 2 : 4);
+    if (a.dtype == 0) {
+        if (np == 2 && mp == 1) return launch_lane<double, 2, 1>(a, s);
+        if (np == 2 && mp == 2) return launch_lane<double, 2, 2>(a, s);
+        if (np == 4 && mp == 1) return launch_lane<double, 4, 1>(a, s);
+        if (np == 4 && mp == 2) return launch_lane<double, 4, 2>(a, s);
+        if (np == 4 && mp == 4) return launch_lane<double, 4, 4>(a, s);
+    } else {
+        if (np == 2 && mp == 1) return launch_lane<float, 2, 1>(a, s);
+        if (np == 2 && mp == 2) return launch_lane<float, 2, 2>(a, s);
+        if (np == 4 && mp == 1) return launch_lane<float, 4, 1>(a, s);
+        if (np == 4 && mp == 2) return launch_lane<float, 4, 2>(a, s);
+        if (np == 4 && mp == 4) return launch_lane<float, 4, 4>(a, s);
+    }
+    return hipErrorNotSupported;
+}
+
+} // namespace lqrx

@@ -13,10 +13,14 @@ struct DpArgs {
     int dtype; // 0 f64, 1 f32
     int p_all;
     int64_t batch;
+    int tv_AB, tv_QR; // 1 = per-knot A_k,B_k / Q_k,R_k (N−1 knots per trajectory), 0 = time-invariant
 };
 
 hipError_t dp_launch(const DpArgs &a, hipStream_t s);
-bool dp_supported(int dtype, int n, int m);
+bool dp_supported(int dtype, int n, int m, bool tv);
+// lane-per-trajectory kernel for n ≤ 4, m ≤ 4 (lqrx_dp_lane.hip)
+hipError_t dp_lane_launch(const DpArgs &a, hipStream_t s);
+bool dp_lane_supported(int n, int m);
 
 struct KktArgs {
     const double *Y, *y, *H, *g; // device, packed per trajectory

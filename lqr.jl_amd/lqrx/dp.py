@@ -41,7 +41,9 @@ def from_abi(a: np.ndarray, shape: tuple) -> np.ndarray:
 
 @dataclass
 class LQRProblem:
-    """Time-invariant finite-horizon LQR problem (lqr_problem.jl:1-11)."""
+    """Finite-horizon LQR problem (lqr_problem.jl:1-11).  Time-invariant as upstream;
+    A/B (and Q/R) may instead carry a leading knot axis of length N-1 (per-knot A_k, B_k,
+    the LCRProblem layout of constrained_problem.jl:3-4)."""
 
     Qf: np.ndarray
     Q: np.ndarray
@@ -54,7 +56,7 @@ class LQRProblem:
     N: int = 2
 
     def size(self):
-        n, m = self.B.shape
+        n, m = self.B.shape[-2:]
         return n, m, self.N
 
     def num_vars(self):
@@ -118,7 +120,12 @@ class LQRBatch:
         return self.A.shape[0]
 
     def size(self):
-        return self.B.shape[1], self.B.shape[2], self.N
+        return self.B.shape[-2], self.B.shape[-1], self.N
+
+    def time_varying(self):
+        """(tv_AB, tv_QR): 1 where the fields carry a knot axis, A (batch, N-1, n, n) —
+        the per-knot LCRProblem layout (constrained_problem.jl:3-4), SURVEY §8(f) rank 1."""
+        return int(np.ndim(self.A) == 4), int(np.ndim(self.Q) == 4)
 
     @classmethod
     def of(cls, probs: list[LQRProblem]):
@@ -137,6 +144,7 @@ def solve_batch(b: LQRBatch, dtype: int = _lib.F64, all_P: bool = False):
     lib = _lib.load()
     n, m, N = b.size()
     bt = b.batch
+    tvAB, tvQR = b.time_varying()
     npdt = np.float64 if dtype == _lib.F64 else np.float32
     ins = [to_abi(np.asarray(x, dtype=npdt)) for x in (b.A, b.B, b.Q, b.R, b.Qf)]
     x0 = np.ascontiguousarray(np.asarray(b.x0, dtype=npdt))
@@ -145,7 +153,7 @@ def solve_batch(b: LQRBatch, dtype: int = _lib.F64, all_P: bool = False):
     X = np.zeros(bt * N * n, npdt)
     U = np.zeros(bt * (N - 1) * m, npdt)
     info = np.zeros(bt, np.int32)
-    d = _lib.DpDesc(n, m, N, dtype, bt, 0, 1 if all_P else 0, 0, 0)
+    d = _lib.DpDesc(n, m, N, dtype, bt, 0, 1 if all_P else 0, tvAB, tvQR)
     rc = _lib.check(lib.lqrx_dp_solve_host(C.byref(d), *[_ptr(a) for a in ins], _ptr(x0),
                                            _ptr(K), _ptr(P), _ptr(X), _ptr(U), _ptr(info)))
     return dict(K=from_abi(K, (bt, N - 1, m, n)),
@@ -207,7 +215,7 @@ def dp_solve_device(t: dict, N: int, p_mode: int = 0, stream: int | None = None,
                    X=torch.empty(bt * N * n, dtype=tdt, device=dev),
                    U=torch.empty(bt * (N - 1) * m, dtype=tdt, device=dev),
                    info=torch.empty(bt, dtype=torch.int32, device=dev))
-    d = _lib.DpDesc(n, m, N, dtype, bt, 0, p_mode, 0, 0)
+    d = _lib.DpDesc(n, m, N, dtype, bt, 0, p_mode, int(t.get("tv_AB", 0)), int(t.get("tv_QR", 0)))
     p = lambda x: C.c_void_p(x.data_ptr())
     rc = lib.lqrx_dp_solve(C.byref(d), p(t["A"]), p(t["B"]), p(t["Q"]), p(t["R"]), p(t["Qf"]),
                            p(t["x0"]), p(out["K"]), p(out["P"]), p(out["X"]), p(out["U"]),

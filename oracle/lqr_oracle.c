@@ -117,10 +117,10 @@ static void potrs_upper(int n, int nrhs, const double *U, int ldu, double *X, in
  * Returns info: 0, or the (1-based) knot k whose E = R + BᵀPB was not SPD (first met in
  * the backward sweep).  The sweep continues either way, as the reference does.
  */
-int oracle_dp_solve_one(int n, int m, int N, const double *A, const double *B,
-                        const double *Q, const double *R, const double *Qf,
-                        const double *x0, double *K, double *P, int p_all, double *X,
-                        double *U)
+int oracle_dp_solve_one_tv(int n, int m, int N, const double *A0, const double *B0,
+                           const double *Q0, const double *R0, const double *Qf,
+                           const double *x0, double *K, double *P, int p_all, double *X,
+                           double *U, int tvAB, int tvQR)
 {
     size_t nn = (size_t)n * n, nm = (size_t)n * m, mm = (size_t)m * m;
     double *Pc = malloc(nn * sizeof(double)), *P_ = malloc(nn * sizeof(double));
@@ -134,6 +134,12 @@ int oracle_dp_solve_one(int n, int m, int N, const double *A, const double *B,
 
     for (int k = N - 1; k >= 1; --k) {                        /* :61  k = N-1:-1:1 */
         double *Kk = K + (size_t)(k - 1) * nm;
+        /* time-varying extension (LCRProblem.A[k]/B[k]): knot k's
+         * matrices; the time-invariant reference is tvAB = tvQR = 0 */
+        const double *A = A0 + (tvAB ? (size_t)(k - 1) * nn : 0);
+        const double *B = B0 + (tvAB ? (size_t)(k - 1) * nm : 0);
+        const double *Q = Q0 + (tvQR ? (size_t)(k - 1) * nn : 0);
+        const double *R = R0 + (tvQR ? (size_t)(k - 1) * mm : 0);
         /* compute_gain!  :37-43 */
         gemm(n, m, n, 0, Pc, n, 0, B, n, PB, n);               /* :38  PB .= P*B */
         gemm(m, m, n, 1, B, n, 0, PB, n, E, m);                /* :39  E .= R .+ B'PB */
@@ -158,6 +164,8 @@ int oracle_dp_solve_one(int n, int m, int N, const double *A, const double *B,
         const double *Kk = K + (size_t)(k - 1) * nm;
         const double *xk = X + (size_t)(k - 1) * n;
         double *uk = U + (size_t)(k - 1) * m, *xn = X + (size_t)k * n;
+        const double *A = A0 + (tvAB ? (size_t)(k - 1) * nn : 0);
+        const double *B = B0 + (tvAB ? (size_t)(k - 1) * nm : 0);
         for (int i = 0; i < m; ++i) {
             double s = 0.0;
             for (int j = 0; j < n; ++j) s += Kk[IDX(i, j, m)] * xk[j];
@@ -174,32 +182,53 @@ int oracle_dp_solve_one(int n, int m, int N, const double *A, const double *B,
     return info;
 }
 
+int oracle_dp_solve_one(int n, int m, int N, const double *A, const double *B,
+                        const double *Q, const double *R, const double *Qf,
+                        const double *x0, double *K, double *P, int p_all, double *X,
+                        double *U)
+{
+    return oracle_dp_solve_one_tv(n, m, N, A, B, Q, R, Qf, x0, K, P, p_all, X, U, 0, 0);
+}
+
 /*
  * Batched driver, Julia layout (batch slowest).  `nthreads` > 1 uses OpenMP when the
  * library is built with -fopenmp (the CPU baseline); returns the number of trajectories
  * with info != 0.  Inputs may be time-invariant only (the reference LQRProblem).
  */
-int64_t oracle_dp_solve_batch(int n, int m, int N, int64_t batch, const double *A,
-                              const double *B, const double *Q, const double *R,
-                              const double *Qf, const double *x0, double *K, double *P,
-                              int p_all, double *X, double *U, int32_t *info, int nthreads)
+int64_t oracle_dp_solve_batch_tv(int n, int m, int N, int64_t batch, const double *A,
+                                 const double *B, const double *Q, const double *R,
+                                 const double *Qf, const double *x0, double *K, double *P,
+                                 int p_all, double *X, double *U, int32_t *info, int nthreads,
+                                 int tvAB, int tvQR)
 {
     size_t nn = (size_t)n * n, nm = (size_t)n * m, mm = (size_t)m * m;
+    size_t kAB = tvAB ? (size_t)(N - 1) : 1, kQR = tvQR ? (size_t)(N - 1) : 1;
     size_t pstride = p_all ? nn * (size_t)N : nn;
     int64_t bad = 0;
 #ifdef _OPENMP
 #pragma omp parallel for schedule(dynamic, 4) num_threads(nthreads) reduction(+ : bad)
 #endif
     for (int64_t b = 0; b < batch; ++b) {
-        int st = oracle_dp_solve_one(n, m, N, A + b * nn, B + b * nm, Q + b * nn, R + b * mm,
-                                     Qf + b * nn, x0 + b * (size_t)n,
-                                     K + b * nm * (size_t)(N - 1), P + b * pstride, p_all,
-                                     X + b * (size_t)n * N, U + b * (size_t)m * (N - 1));
+        int st = oracle_dp_solve_one_tv(n, m, N, A + b * nn * kAB, B + b * nm * kAB,
+                                        Q + b * nn * kQR, R + b * mm * kQR,
+                                        Qf + b * nn, x0 + b * (size_t)n,
+                                        K + b * nm * (size_t)(N - 1), P + b * pstride, p_all,
+                                        X + b * (size_t)n * N, U + b * (size_t)m * (N - 1),
+                                        tvAB, tvQR);
         if (info) info[b] = st;
         bad += (st != 0);
     }
     (void)nthreads;
     return bad;
+}
+
+int64_t oracle_dp_solve_batch(int n, int m, int N, int64_t batch, const double *A,
+                              const double *B, const double *Q, const double *R,
+                              const double *Qf, const double *x0, double *K, double *P,
+                              int p_all, double *X, double *U, int32_t *info, int nthreads)
+{
+    return oracle_dp_solve_batch_tv(n, m, N, batch, A, B, Q, R, Qf, x0, K, P, p_all, X, U,
+                                    info, nthreads, 0, 0);
 }
 
 int oracle_num_threads_max(void)

@@ -40,6 +40,9 @@ def load():
         lib.oracle_dp_solve_batch.restype = i64
         lib.oracle_dp_solve_batch.argtypes = [i32, i32, i32, i64] + [vp] * 8 + [i32, vp, vp, vp,
                                                                                  i32]
+        lib.oracle_dp_solve_batch_tv.restype = i64
+        lib.oracle_dp_solve_batch_tv.argtypes = [i32, i32, i32, i64] + [vp] * 8 + [
+            i32, vp, vp, vp, i32, i32, i32]
         lib.oracle_kkt_solve_one.restype = i32
         lib.oracle_kkt_solve_one.argtypes = [i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, i32, vp,
                                              vp, vp, vp, vp]
@@ -57,7 +60,9 @@ def _p(a):
 
 # ------------------------------------------------------------------------- DP
 def dp_solve_abi(d: dict, N: int, all_P: bool = False, nthreads: int = 1) -> dict:
-    """Oracle DP on ABI-layout (flat, column-major, batch slowest) float64 inputs."""
+    """Oracle DP on ABI-layout (flat, column-major, batch slowest) float64 inputs.
+    d["tv_AB"] / d["tv_QR"] (optional, default 0) select per-knot A,B / Q,R (N−1 knots per
+    trajectory, the time-varying extension of SURVEY §8(f))."""
     lib = load()
     n, m, bt = d["n"], d["m"], d["batch"]
     f = lambda k: np.ascontiguousarray(np.asarray(d[k], dtype=np.float64))
@@ -67,8 +72,9 @@ def dp_solve_abi(d: dict, N: int, all_P: bool = False, nthreads: int = 1) -> dic
     X = np.zeros(bt * N * n)
     U = np.zeros(bt * (N - 1) * m)
     info = np.zeros(bt, np.int32)
-    lib.oracle_dp_solve_batch(n, m, N, bt, _p(A), _p(B), _p(Q), _p(R), _p(Qf), _p(x0), _p(K),
-                              _p(P), 1 if all_P else 0, _p(X), _p(U), _p(info), nthreads)
+    lib.oracle_dp_solve_batch_tv(n, m, N, bt, _p(A), _p(B), _p(Q), _p(R), _p(Qf), _p(x0),
+                                 _p(K), _p(P), 1 if all_P else 0, _p(X), _p(U), _p(info),
+                                 nthreads, int(d.get("tv_AB", 0)), int(d.get("tv_QR", 0)))
     return dict(K=K, P=P, X=X, U=U, info=info)
 
 

@@ -23,7 +23,8 @@ def test_abi_version(lqrx):
 
 @pytest.mark.parametrize("field,val,code", [("n", 0, -1), ("m", 0, -1), ("N", 1, -1),
                                             ("dtype", 7, -1), ("p_mode", 3, -1),
-                                            ("layout", 1, -101), ("knot_stride_AB", 5, -101)])
+                                            ("layout", 1, -101), ("knot_stride_AB", 5, -1),
+                                            ("knot_stride_QR", 1, -101)])
 def test_dp_validation(lqrx, field, val, code):
     from lqrx import _lib
 
@@ -32,6 +33,16 @@ def test_dp_validation(lqrx, field, val, code):
     rc = lqrx.load().lqrx_dp_solve(C.byref(d), *([None] * 10), None, None)
     assert rc == code
     assert len(lqrx.load().lqrx_last_error()) > 0
+
+
+def test_dp_time_varying_small_n_accepted(lqrx):
+    """Per-knot A_k/B_k (knot_stride 1) is served by the n ≤ 4 lane kernel: validation
+    passes and the first NULL pointer is what gets reported."""
+    from lqrx import _lib
+
+    d = _lib.DpDesc(4, 1, 10, 0, 4, 0, 0, 1, 1)
+    rc = lqrx.load().lqrx_dp_solve(C.byref(d), *([None] * 10), None, None)
+    assert rc == -2
 
 
 def test_dp_null_pointer_codes(lqrx):

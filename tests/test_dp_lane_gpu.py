@@ -1,0 +1,162 @@
+"""GPU parity of the small-n lane-per-trajectory Riccati kernel (lqrx_dp_lane.hip, n ≤ 4,
+m ≤ 4 — cartpole / Dubins / double-integrator shapes) and of the time-varying extension
+(per-knot A_k, B_k, Q_k, R_k), through the C ABI, against the CPU
+oracle (oracle/lqr_oracle.c, restating dynamic_programming.jl:28-72; the time-varying
+variant indexes knot k's matrices in the same loop).
+
+Tolerance (north star): 1e-10 relative per knot in fp64 for K and P, same for X, U;
+fp32 1e-4 against the fp64 oracle.
+"""
+import numpy as np
+import pytest
+
+from test_dp_gpu import TOL32, TOL64, relerr_per_knot, run_pair
+
+pytestmark = pytest.mark.gpu
+
+
+def per_traj_relerr(a, b):
+    """(batch,) max over knots of max|a−b| / max|b| (per knot)."""
+    a = a.reshape(a.shape[0], a.shape[1], -1)
+    b = b.reshape(b.shape[0], b.shape[1], -1)
+    den = np.abs(b).max(axis=2)
+    den[den == 0] = 1.0
+    return (np.abs(a - b).max(axis=2) / den).max(axis=1)
+
+
+def intrinsic_spread(d, N, Kref, Pref):
+    """Per-trajectory conditioning of the reference recursion itself: the relative
+    difference between the oracle and an independent fp64 restatement in the reference op
+    order (numpy, LU-based solve instead of potrf/potrs).  On the random generator at small
+    n (A = I + 0.1/√n·G) a few trajectories per thousand have ρ(A) ≈ 1.1 and weak
+    actuation; their Riccati recursion amplifies rounding so that two faithful fp64
+    implementations already disagree above 1e-10."""
+    from lqrx.dp import abi_to_batch
+
+    b = abi_to_batch(d)
+    A, B, Q, R = b.A, b.B, b.Q, b.R
+    P = b.Qf.copy()
+    K = np.zeros_like(Kref)
+    Ps = np.zeros_like(Pref)
+    Ps[:, N - 1] = P
+    T = lambda M: np.swapaxes(M, 1, 2)
+    for k in range(N - 1, 0, -1):
+        PB, PA = P @ B, P @ A
+        Kk = np.linalg.solve(R + T(B) @ PB, T(B) @ PA)
+        P = Q + T(A) @ PA - (T(A) @ PB) @ Kk
+        K[:, k - 1] = Kk
+        Ps[:, k - 1] = P
+    return np.maximum(per_traj_relerr(K, Kref), per_traj_relerr(Ps, Pref))
+
+
+def assert_parity(got, ref, d, N, tol=TOL64, eps_ratio=1.0, rare=0.01):
+    """K, P, X, U within `tol` per knot for every trajectory, except that a trajectory
+    whose intrinsic spread (above, measured in fp64 and scaled by eps_ratio = eps(dtype) /
+    eps(fp64) for fp32 runs) exceeds tol/10 is held to 10× that spread; such trajectories
+    must stay rare (fraction < `rare`)."""
+    got = {k: np.asarray(got[k], dtype=np.float64) for k in ("K", "P", "X", "U")}
+    bt = got["K"].shape[0]
+    xs = lambda a: a.reshape(bt, 1, -1)                 # X, U: one block per trajectory
+    err = np.maximum.reduce([per_traj_relerr(got["K"], ref["K"]),
+                             per_traj_relerr(got["P"], ref["P"]),
+                             per_traj_relerr(xs(got["X"]), xs(ref["X"])),
+                             per_traj_relerr(xs(got["U"]), xs(ref["U"]))])
+    if (err <= tol).all():
+        return
+    spread = intrinsic_spread(d, N, ref["K"], ref["P"])
+    lim = np.maximum(tol, 10.0 * spread * eps_ratio)
+    assert (err <= lim).all(), (err.max(), spread[err.argmax()])
+    assert (err > tol).mean() < rare
+
+
+@pytest.mark.parametrize("n,m,N,batch", [
+    (4, 1, 101, 4096 + 5),   # cartpole shape (cfg2), ragged last wave
+    (3, 2, 101, 130),        # Dubins shape
+    (2, 1, 50, 64),          # double integrator 1-D
+    (1, 1, 7, 3),
+    (4, 4, 33, 65),
+    (4, 3, 20, 9),
+    (3, 1, 2, 11),           # N = 2: one backward knot
+])
+def test_lane_parity_f64(lqrx, oracle, gpu_ok, n, m, N, batch):
+    seed = 300 + 11 * n + m
+    got, ref = run_pair(lqrx, oracle, n, m, N, batch, seed=seed)
+    assert got["rc"] == 0 and (got["info"] == 0).all()
+    assert_parity(got, ref, lqrx.random_batch(n, m, N, batch, seed), N)
+
+
+def test_lane_p1_only(lqrx, oracle, gpu_ok):
+    got, ref = run_pair(lqrx, oracle, 4, 2, 40, 70, seed=9, all_P=False)
+    assert relerr_per_knot(got["P"][:, None], ref["P"][:, None]) <= TOL64
+
+
+@pytest.mark.parametrize("n,m", [(4, 1), (3, 2)])
+def test_lane_parity_f32(lqrx, oracle, gpu_ok, n, m):
+    got, ref = run_pair(lqrx, oracle, n, m, 60, 100, seed=78, dtype=1)
+    assert_parity(got, ref, lqrx.random_batch(n, m, 60, 100, 78), 60, tol=TOL32,
+                  eps_ratio=float(np.finfo(np.float32).eps / np.finfo(np.float64).eps),
+                  rare=1.0)   # fp32 on weakly actuated random problems: the bound is the spread
+
+
+def test_lane_cartpole_problem(lqrx, oracle, gpu_ok):
+    """cfg2 on the real RK3-linearised cartpole (test/cartpole.jl), per-trajectory x0."""
+    from lqrx.dp import to_abi, from_abi
+    from lqrx.models import cartpole_batch
+
+    bt, N = 256, 101
+    cb = cartpole_batch(bt, N, seed=5)
+    got = lqrx.solve_batch(cb, all_P=True)
+    d = {k: to_abi(getattr(cb, k)).ravel() for k in ("A", "B", "Q", "R", "Qf")}
+    d.update(x0=cb.x0.ravel(), n=4, m=1, batch=bt)
+    ref = oracle.dp_solve_abi(d, N, all_P=True)
+    assert relerr_per_knot(got["K"], from_abi(ref["K"], (bt, N - 1, 1, 4))) <= TOL64
+    assert relerr_per_knot(got["P"], from_abi(ref["P"], (bt, N, 4, 4))) <= TOL64
+    assert np.abs(got["X"] - ref["X"].reshape(bt, N, 4)).max() <= TOL64
+
+
+def test_lane_non_spd_sets_info(lqrx, gpu_ok):
+    from lqrx.dp import abi_to_batch
+
+    n, m, N, bt = 4, 2, 10, 70
+    d = lqrx.random_batch(n, m, N, bt, seed=3)
+    b = abi_to_batch(d)
+    b.R[65] = -100.0 * np.eye(m)      # second wave, trajectory 1 is broken
+    b.B[65] *= 1e-3
+    got = lqrx.solve_batch(b)
+    assert got["rc"] == 1
+    assert got["info"][65] == N - 1
+    assert (np.delete(got["info"], 65) == 0).all()
+
+
+def _tv_batch(lqrx, n, m, N, bt, seed, tv_ab=True, tv_qr=True):
+    """Per-knot A_k, B_k, Q_k, R_k: the time-invariant random problem perturbed per knot."""
+    from lqrx.dp import abi_to_batch
+
+    b = abi_to_batch(lqrx.random_batch(n, m, N, bt, seed))
+    rng = np.random.default_rng(seed)
+    if tv_ab:
+        b.A = b.A[:, None] + 0.05 * rng.standard_normal((bt, N - 1, n, n)) / np.sqrt(n)
+        b.B = b.B[:, None] + 0.05 * rng.standard_normal((bt, N - 1, n, m)) / np.sqrt(n)
+    if tv_qr:
+        s = 1.0 + 0.5 * rng.random((bt, N - 1, 1, 1))
+        b.Q = b.Q[:, None] * s
+        b.R = b.R[:, None] * (2.0 - s[..., :1, :1])
+    return b
+
+
+@pytest.mark.parametrize("n,m,tv_ab,tv_qr", [(4, 1, True, True), (3, 2, True, False),
+                                             (4, 4, False, True)])
+def test_time_varying_parity(lqrx, oracle, gpu_ok, n, m, tv_ab, tv_qr):
+    from lqrx.dp import to_abi, from_abi
+
+    N, bt = 41, 67
+    b = _tv_batch(lqrx, n, m, N, bt, seed=21 + n, tv_ab=tv_ab, tv_qr=tv_qr)
+    got = lqrx.solve_batch(b, all_P=True)
+    d = {k: to_abi(getattr(b, k)).ravel() for k in ("A", "B", "Q", "R", "Qf")}
+    d.update(x0=b.x0.ravel(), n=n, m=m, batch=bt, tv_AB=int(tv_ab), tv_QR=int(tv_qr))
+    ref = oracle.dp_solve_abi(d, N, all_P=True)
+    assert got["rc"] == 0
+    assert relerr_per_knot(got["K"], from_abi(ref["K"], (bt, N - 1, m, n))) <= TOL64
+    assert relerr_per_knot(got["P"], from_abi(ref["P"], (bt, N, n, n))) <= TOL64
+    refX = ref["X"].reshape(bt, N, n)
+    assert np.abs(got["X"] - refX).max() <= TOL64 * max(1.0, np.abs(refX).max())

@@ -204,3 +204,69 @@ def test_dp_oracle_equals_kat_pinned_kkt_oracle(lqrx):
         Uk = np.stack([z[k * (n + m) + n:(k + 1) * (n + m)] for k in range(N - 1)])
         assert np.abs(Xk - X[t]).max() <= 1e-10 * max(1.0, np.abs(X[t]).max())
         assert np.abs(Uk - U[t]).max() <= 1e-10 * max(1.0, np.abs(U[t]).max())
+
+
+def lqr_tv_as_kkt(A, B, Q, R, Qf, x0, N):
+    """Time-varying LQR (A[k], B[k], Q[k], R[k] for k = 0..N-2) as the KKT problem of
+    lqr_as_kkt (knot k's dynamics rows [A_k B_k], cost blockdiag(Q_k, R_k))."""
+    import lqrx.kkt as K
+
+    n, m = B.shape[-2:]
+    st = K.ConstraintBlocks(n, m, N, [n] + [0] * (N - 1))
+    Y, y, H = [], [], []
+    for k in range(N):
+        n1, p, n2, w = int(st.n1[k]), int(st.p[k]), int(st.n2[k]), int(st.w[k])
+        blk = np.zeros((n1 + p + n2, w))
+        if n1:
+            blk[:n1, :n] = -np.eye(n)
+        if p:
+            blk[n1:n1 + p, :n] = np.eye(n)
+        if n2:
+            blk[n1 + p:, :n] = A[k]
+            blk[n1 + p:, n:] = B[k]
+        Y.append(blk.T.ravel())
+        y.append(np.concatenate([-x0 if p else np.zeros(0), np.zeros(n2)]))
+        Hk = np.zeros((w, w))
+        Hk[:n, :n] = Qf if k == N - 1 else Q[k]
+        if w > n:
+            Hk[n:, n:] = R[k]
+        H.append(Hk.T.ravel())
+    g = np.zeros(int(np.sum(st.w)))
+    return st, np.concatenate(Y), np.concatenate(y), np.concatenate(H), g
+
+
+def test_dp_oracle_time_varying_pinned(lqrx):
+    """the time-varying DP restatement (per-knot A_k, B_k, Q_k, R_k)
+    (a) reduces bit-exactly to the time-invariant one when every knot repeats the same
+    matrices and (b) equals the KAT-pinned KKT oracle on the same time-varying QP."""
+    from lqrx.dp import abi_to_batch, to_abi
+
+    n, m, N, bt = 4, 2, 20, 3
+    d = lqrx.random_batch(n, m, N, bt, seed=44)
+    b = abi_to_batch(d)
+    rep = lambda M: np.repeat(M[:, None], N - 1, axis=1)
+    dtv = dict(d, A=to_abi(rep(b.A)).ravel(), B=to_abi(rep(b.B)).ravel(),
+               Q=to_abi(rep(b.Q)).ravel(), R=to_abi(rep(b.R)).ravel(), tv_AB=1, tv_QR=1)
+    a0, a1 = orc.dp_solve_abi(d, N, all_P=True), orc.dp_solve_abi(dtv, N, all_P=True)
+    for k in ("K", "P", "X", "U"):
+        assert np.array_equal(a0[k], a1[k]), k
+
+    rng = np.random.default_rng(3)
+    A = rep(b.A) + 0.1 * rng.standard_normal((bt, N - 1, n, n))
+    B = rep(b.B) + 0.1 * rng.standard_normal((bt, N - 1, n, m))
+    Q = rep(b.Q) * (1 + rng.random((bt, N - 1, 1, 1)))
+    R = rep(b.R) * (1 + rng.random((bt, N - 1, 1, 1)))
+    dtv = dict(d, A=to_abi(A).ravel(), B=to_abi(B).ravel(), Q=to_abi(Q).ravel(),
+               R=to_abi(R).ravel(), tv_AB=1, tv_QR=1)
+    out = orc.dp_solve_abi(dtv, N)
+    X = out["X"].reshape(bt, N, n)
+    U = out["U"].reshape(bt, N - 1, m)
+    for t in range(bt):
+        st, Y, y, H, g = lqr_tv_as_kkt(A[t], B[t], Q[t], R[t], b.Qf[t], b.x0[t], N)
+        kk = orc.kkt_solve_one(_oracle_struct(st), Y, y, H, g, h_mode=0)
+        assert kk["info"] == 0
+        z = kk["dz"]
+        Xk = np.stack([z[k * (n + m):k * (n + m) + n] for k in range(N)])
+        Uk = np.stack([z[k * (n + m) + n:(k + 1) * (n + m)] for k in range(N - 1)])
+        assert np.abs(Xk - X[t]).max() <= 1e-10 * max(1.0, np.abs(X[t]).max())
+        assert np.abs(Uk - U[t]).max() <= 1e-10 * max(1.0, np.abs(U[t]).max())
