@@ -116,6 +116,7 @@ def main():
         if args.batch == 65536:
             args.batch = 4096
     if args.workload == "kkt":
+        args.n, args.m = 3, 2                       # Dubins car (test/dubins.jl)
         if args.batch == 65536:
             args.batch = 16384
         if args.N == 256:
@@ -208,7 +209,8 @@ def main():
             achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": achieved / PEAK_HBM_GBS, "traffic": None,
-                    "kernel": "kkt_lane_kernel", "kernel_ms": kern_ms,
+                    "kernel": "kkt_fil_kernel" if N >= 4 else "kkt_staged_kernel",
+                    "kernel_ms": kern_ms,
                     "alg_bytes_per_traj": alg_bytes / bt}
             metric = "KKT solves/sec (Dubins n=3 m=2 N=101 block-tridiagonal _solve!)"
             workload = "Dubins constrained KKT inner solve (BASELINE.json configs[2])"
@@ -228,7 +230,8 @@ def main():
                     traffic = None
             roof = {"bound": "mfma", "achieved": achieved, "peak": peak,
                     "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
-                    "kernel": "dp_riccati_kernel", "kernel_ms": kern_ms,
+                    "kernel": "dp_lane_kernel" if (n <= 4 and m <= 4) else "dp_riccati_kernel",
+                    "kernel_ms": kern_ms,
                     "flops_per_traj": dp_flops_per_traj(n, m, N),
                     "alg_bytes_per_launch": dp_bytes_per_traj(n, m, N, 8 if f64 else 4) * bt}
             metric = METRIC if args.workload == "dp" else \

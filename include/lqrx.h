@@ -89,7 +89,7 @@ int lqrx_dp_solve_host(const lqrx_dp_desc *desc, const void *A, const void *B, c
  * KKT path: one inner solve of CholeskySolver._solve!(solver)
  *   /root/reference/src/cholesky_solver.jl:166-182
  * = calculate_shur_factors! (jacobian_blocks.jl:220-286) → cholesky!(chol, shur)
- *   (cholesky_solve.jl:206-226) → forward_/backward_substitution! (:252-302) →
+ *   (cholesky_solve.jl:47-67) → forward_/backward_substitution! (:93-143) →
  *   calculate_primals! (cholesky_solver.jl:185-236); ginv = 0 gives the
  *   second_order_correction! variant (cholesky_solver.jl:254-273): δẑ = −Dᵀ(DDᵀ)⁻¹d.
  *

@@ -311,7 +311,10 @@ extern "C" int lqrx_kkt_solve(const lqrx_kkt_desc *d, const void *Y, const void 
     static const int force_lane = [] { const char *v = std::getenv("LQRX_KKT_FORCE_LANE"); return v && *v == '1'; }();
     static const int debug_meta = [] { const char *v = std::getenv("LQRX_DEBUG_META"); return v && *v == '1'; }();
     a.force_lane = force_lane;
-    e = lqrx::kkt_launch(a, s);
+    // LQRX_KKT_GENERIC=1 forces the generic (runtime-shaped) kernel, for A/B checks
+    static const int force_generic = [] { const char *v = std::getenv("LQRX_KKT_GENERIC"); return v && *v == '1'; }();
+    if (force_lane || force_generic || !lqrx::kkt_fil_launch(a, d->n1, d->p, d->n2, d->w, s, &e))
+        e = lqrx::kkt_launch(a, s);
     if (debug_meta) {
         std::vector<int32_t> back(L.meta.size());
         (void)hipStreamSynchronize(s);

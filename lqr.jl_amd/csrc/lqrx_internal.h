@@ -36,5 +36,9 @@ struct KktArgs {
 };
 
 hipError_t kkt_launch(const KktArgs &a, hipStream_t s);
+// compile-time-shaped kernel for first/interior/last structures (lqrx_kkt_fil.hip); returns
+// false (and launches nothing) when the structure has no instantiation
+bool kkt_fil_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
+                    const int32_t *w, hipStream_t s, hipError_t *err);
 
 } // namespace lqrx

@@ -8,11 +8,11 @@
 //     shur!/copy_shur!  (jacobian_blocks.jl:231-286) for knot k+1 — YYt = Y H⁻¹ Yᵀ and
 //       r = Y H⁻¹ g streamed column by column from HBM (H diagonal: h_mode 2, or dense /
 //       block-diagonal factored by a w×w Cholesky, block_cholesky.jl:55-101);
-//     cholesky!(U[k], F[k])  (cholesky_solve.jl:206-226);
-//     forward_substitution!  (cholesky_solve.jl:252-276);
+//     cholesky!(U[k], F[k])  (cholesky_solve.jl:47-67);
+//     forward_substitution!  (cholesky_solve.jl:93-117);
 //     the factor blocks B, C, D, E, F and the forward μ, λ go to a scratch slab.
 //   backward k = N-1 … 0:
-//     backward_substitution!  (cholesky_solve.jl:278-302), and with a one-knot lag
+//     backward_substitution!  (cholesky_solve.jl:119-143), and with a one-knot lag
 //     calc_residual! + calc_primals!  (cholesky_solver.jl:195-236): δz_k = −H_k⁻¹ res_k.
 //
 // Every per-knot operation is the oracle's (oracle/lqr_oracle.c) scalar loop, executed by
@@ -20,6 +20,7 @@
 // block dimensions (template), loops run to the runtime sizes.
 #include "lqrx_internal.h"
 #include "lqrx_tile.h"
+#include "lqrx_stage.h"
 #include <hip/hip_runtime.h>
 
 namespace lqrx {
@@ -363,7 +364,7 @@ __global__ __launch_bounds__(64) void kkt_lane_kernel(const KktArgs a, double *_
         }
         (void)o1; (void)os; (void)o2;
 
-        // cholesky!(U[k], F[k])  (cholesky_solve.jl:206-226)
+        // cholesky!(U[k], F[k])  (cholesky_solve.jl:47-67)
         if (p1 > 0) {
             trsm_ut<PM, P1M, PSM>(Ua, p1, FD, ps);                             // D = A⁻ᵀ F.D
             trsm_ut<PM, P1M, P2M>(Ua, p1, FF, p2);                             // F = A⁻ᵀ F.F
@@ -401,7 +402,7 @@ __global__ __launch_bounds__(64) void kkt_lane_kernel(const KktArgs a, double *_
             }
         if (p2 > 0 && !potrf_u<P2M>(FC, p2) && !info) info = k + 1;
 
-        // forward_substitution!  (:252-276)
+        // forward_substitution!  (:93-117)
         double mu[PSM], la[P2M];
 #pragma unroll
         for (int i = 0; i < PSM; ++i) {
@@ -584,45 +585,6 @@ __global__ __launch_bounds__(64) void kkt_lane_kernel(const KktArgs a, double *_
 // knot ahead in a double buffer, and the factor slab is batch-fastest (coalesced).  The
 // per-trajectory packed layout keeps each trajectory's knot block contiguous, so the wave
 // reads 64 contiguous chunks (dense, lane-linear [t][L] image in LDS).
-using gptr_t = const __attribute__((address_space(1))) void *;
-using lptr_t = __attribute__((address_space(3))) void *;
-
-// stage L doubles at element offset `off` of each of the wave's 64 trajectories (stride s
-// elements) into lds[t*L + e].  16-byte pieces when every chunk is 16-B aligned, else dwords.
-__device__ __forceinline__ void stage_chunk(const double *X, int64_t s, int64_t off, int L,
-                                            int64_t t0, int64_t batch, double *lds, int lane)
-{
-    if (L <= 0) return;
-    const bool wide = ((s | off | L) & 1) == 0;                 // uniform
-    const int unit = wide ? 16 : 4;
-    const int per = L * 8 / unit;                               // pieces per trajectory
-    const int q = 64 / per, r = 64 - q * per;                   // uniform
-    int tl = lane / per, e = lane - tl * per;
-    const bool full = t0 + 64 <= batch;                         // uniform: no clamp needed
-    // running byte address; advancing by (q trajectories, r pieces) per instruction
-    const int64_t sb = s * 8;
-    const char *gp = (const char *)X + (t0 + tl) * sb + off * 8 + (int64_t)e * unit;
-    const int64_t step = q * sb + (int64_t)r * unit, wrap = sb - (int64_t)per * unit;
-    for (int i = 0; i < 64 * per; i += 64) {
-        const char *src = gp;
-        if (!full && t0 + tl >= batch)
-            src = (const char *)X + (batch - 1) * sb + off * 8 + (int64_t)e * unit;
-        char *lp = (char *)lds + (int64_t)i * unit;
-        if (wide)
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lp, 16, 0, 0);
-        else
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lp, 4, 0, 0);
-        tl += q;
-        e += r;
-        gp += step;
-        if (e >= per) {
-            e -= per;
-            tl += 1;
-            gp += wrap;
-        }
-    }
-}
-
 template <int WM, int RM, int YM> struct StageCfg {
     static constexpr int LY = RM * WM, Ly = YM, LH = WM * WM, Lg = WM;
     static constexpr int SIZE = 64 * (LY + Ly + LH + Lg); // doubles per buffer

@@ -1,0 +1,916 @@
+// lqrx_kkt_fil.hip — batched block-tridiagonal KKT solve (CholeskySolver._solve!,
+// /root/reference/src/cholesky_solver.jl:166-182) for block structures of the
+// "first / interior / last" form that ConstraintBlocks produces for trajectory problems
+// (conblocks.jl:403-425): knot 0 = (n1 0, p P0, n2 n̄, w n̄+m), knots 1..N-2 = (n̄, PK, n̄,
+// n̄+m), knot N-1 = (n̄, PN, 0, n̄).  Dubins (BASELINE cfg3: n̄=3, m=2, P0=3, PK=0, PN=3) and
+// the double integrators of test/problems.jl have this form.
+//
+// Why a separate kernel: with every block size a compile-time constant, each knot's work is
+// straight-line register code (no runtime-size predication, no selects), which is ~5× fewer
+// VALU instructions per knot than the generic kernel (lqrx_kkt.hip) — and the per-wave
+// instruction stream IS the cost here: one lane per trajectory, the horizon serial.
+//
+// Mapping: ONE LANE PER TRAJECTORY, 64 per wave (one wave per workgroup).  Per-knot inputs
+// (Y_k, y_k, H_k, g_k of the wave's 64 trajectories, packed per trajectory in the ABI) are
+// brought to LDS by coalesced LDS-DMA (lqrx_stage.h) two knots ahead into a ring of three
+// buffers; the factor slab is batch-fastest (coalesced stores/loads).
+//
+//   forward  k = 0..N-1: shur!/copy_shur! of knot k+1 (jacobian_blocks.jl:231-286; its
+//            A block and r1 fold into knot k's C and d — the aliasing of :166/:251),
+//            cholesky! of knot k (cholesky_solve.jl:47-67), forward_substitution!
+//            (:93-117); factor blocks + forward μ, λ → slab.
+//   backward k = N-1..0: backward_substitution! (:119-143) and, one knot behind,
+//            calc_residual!/calc_primals! (cholesky_solver.jl:195-236) from re-staged
+//            Y, H, g: δz_k = −H_k⁻¹(D2ᵀλ_{k-1} + Cᵀμ_k + D1ᵀλ_k + g_k).
+// Triangular factors keep 1/U_ii on the diagonal (multiplies instead of divides).
+#include "lqrx_internal.h"
+#include "lqrx_stage.h"
+#include "lqrx_tile.h"
+#include <type_traits>
+
+namespace lqrx {
+namespace fil {
+
+#ifndef LQRX_FIL_N12
+#define LQRX_FIL_N12 1   // 12-byte LDS-DMA pieces for the short chunks (0: dwords only)
+#endif
+constexpr int Z(int x) { return x > 0 ? x : 1; }
+constexpr int tri(int x) { return x * (x + 1) / 2; }
+
+template <int P1_, int PS_, int P2_, int W_> struct Cls {
+    static constexpr int P1 = P1_, PS = PS_, P2 = P2_, W = W_, R = P1_ + PS_ + P2_;
+    static constexpr int O1 = 0, OS = P1_, O2 = P1_ + PS_;     // row segments of Y = [D2; C; D1]
+    static constexpr bool none = (W_ == 0);
+};
+using NoCls = Cls<0, 0, 0, 0>;
+
+template <int NX_, int M_, int P0_, int PK_, int PN_, bool HDIAG_, bool GINV_> struct Shape {
+    static constexpr int NX = NX_, M = M_;
+    static constexpr bool HDIAG = HDIAG_, GINV = GINV_;
+    using F = Cls<0, P0_, NX_, NX_ + M_>;
+    using I = Cls<NX_, PK_, NX_, NX_ + M_>;
+    using L = Cls<NX_, PN_, 0, NX_>;
+    template <class C> static constexpr int LY() { return C::R * C::W; }
+    template <class C> static constexpr int Ly() { return C::PS + C::P2; }
+    template <class C> static constexpr int LH() { return HDIAG ? C::W : C::W * C::W; }
+    template <class C> static constexpr int Lg() { return C::W; }
+    // Y goes in 16-byte pieces when every knot's Y block has an even length (then every
+    // knot offset and the trajectory stride are even); the short y/H/g chunks in dwords
+    static constexpr bool WIDE_Y = (LY<F>() % 2 == 0) && (LY<I>() % 2 == 0) && (LY<L>() % 2 == 0);
+    static constexpr int nsplit(int L) { return LQRX_FIL_N12 ? (8 * L) / 12 + ((8 * L) % 12) / 4 : 2 * L; }   // = Split<L>::instrs
+    template <class C> static constexpr int Dmin()   // DMA instructions of a forward restage
+    {
+        return C::none ? 0 : (WIDE_Y ? LY<C>() / 2 : 2 * LY<C>()) + nsplit(Ly<C>()) +
+                                 (GINV ? nsplit(LH<C>()) + nsplit(Lg<C>()) : 0);
+    }
+    template <class C> static constexpr int Dbwd()   // … of a backward restage (no y)
+    {
+        return C::none ? 0 : (WIDE_Y ? LY<C>() / 2 : 2 * LY<C>()) + (GINV ? nsplit(LH<C>()) + nsplit(Lg<C>()) : 0);
+    }
+    template <int A, int B, int C> static constexpr int mx3() { return A > B ? (A > C ? A : C) : (B > C ? B : C); }
+    static constexpr int LYm = mx3<LY<F>(), LY<I>(), LY<L>()>();
+    static constexpr int Lym = mx3<Ly<F>(), Ly<I>(), Ly<L>()>();
+    static constexpr int LHm = mx3<LH<F>(), LH<I>(), LH<L>()>();
+    static constexpr int Lgm = mx3<Lg<F>(), Lg<I>(), Lg<L>()>();
+    // staging buffer (bytes): Y image (16-B pieces, dense) | y | H | g split images
+    static constexpr int sb(int L) { return LQRX_FIL_N12 ? 16 * ((8 * L) / 12) + 4 * (((8 * L) % 12) / 4) : 8 * L; }
+    static constexpr int OFF_y = 64 * 8 * LYm;
+    static constexpr int OFF_H = OFF_y + 64 * mx3<sb(Ly<F>()), sb(Ly<I>()), sb(Ly<L>())>();
+    static constexpr int OFF_g = OFF_H + 64 * mx3<sb(LH<F>()), sb(LH<I>()), sb(LH<L>())>();
+    static constexpr int BUF_BYTES = OFF_g + 64 * mx3<sb(Lg<F>()), sb(Lg<I>()), sb(Lg<L>())>();
+    static constexpr int BUF = (BUF_BYTES + 15) / 16 * 2;       // doubles per staging buffer
+    // slab slot: B̃ (tri) | C̃ (tri) | D̃ | Ẽ | F̃ | μ | λ  (max over the classes)
+    template <class C> static constexpr int slab()
+    {
+        return tri(C::PS) + tri(C::P2) + C::P1 * C::PS + C::PS * C::P2 + C::P1 * C::P2 + C::PS + C::P2;
+    }
+    static constexpr int SLOT = mx3<slab<F>(), slab<I>(), slab<L>()>();
+};
+
+// per-knot offsets (elements) in the packed per-trajectory arrays: knot 0 is class F,
+// knots 1.. follow with class I sizes (the last knot starts where an I knot would)
+template <class S> struct Off {
+    __device__ static int64_t Y(int k) { return k == 0 ? 0 : S::template LY<typename S::F>() + (int64_t)(k - 1) * S::template LY<typename S::I>(); }
+    __device__ static int64_t y(int k) { return k == 0 ? 0 : S::template Ly<typename S::F>() + (int64_t)(k - 1) * S::template Ly<typename S::I>(); }
+    __device__ static int64_t H(int k) { return k == 0 ? 0 : S::template LH<typename S::F>() + (int64_t)(k - 1) * S::template LH<typename S::I>(); }
+    __device__ static int64_t g(int k) { return k == 0 ? 0 : S::template Lg<typename S::F>() + (int64_t)(k - 1) * S::template Lg<typename S::I>(); }
+};
+
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void *base)
+{
+    // raw buffer (stride 0), full 31-bit range; gfx9 dword-3 format bits
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+
+// DMA pattern of one packed array for a chunk of L doubles per trajectory: the wave's 64
+// chunks form a dense [t][L] image of `per` pieces per trajectory (16 B pieces when WIDE,
+// else dwords); instruction i moves pieces 64i .. 64i+63, lane l piece 64i + l.  The per-lane
+// byte offsets are knot-invariant (only the scalar soffset changes per knot), so once
+// initialised an issue costs no VALU work.  Lanes past the batch end read the last live
+// trajectory (clamped) so no out-of-range access is ever issued.
+template <int L, bool WIDE> struct Pat {
+    static constexpr int unit = WIDE ? 16 : 4;
+    static constexpr int per = L * 8 / unit;
+    uint32_t vo[per > 0 ? per : 1];
+    __device__ __forceinline__ void init(int64_t s, int lane, int nlive)
+    {
+#pragma unroll
+        for (int i = 0; i < per; ++i) {
+            const uint32_t p = 64u * (uint32_t)i + (uint32_t)lane;
+            uint32_t tr = p / (uint32_t)per;
+            const uint32_t e = p - tr * (uint32_t)per;
+            tr = tr < (uint32_t)nlive ? tr : (uint32_t)(nlive - 1);
+            vo[i] = tr * (uint32_t)(s * 8) + e * (uint32_t)unit;
+        }
+    }
+    __device__ __forceinline__ void issue(rsrc_t r, int64_t off_elems, double *lds) const
+    {
+        const uint32_t so = (uint32_t)(off_elems * 8);
+#pragma unroll
+        for (int i = 0; i < per; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lptr_t)((char *)lds + i * 64 * unit), unit, vo[i], so, 0, 0);
+    }
+};
+
+// Short chunks (y, H, g: odd numbers of doubles, so 16-B alignment is impossible) go as
+// 12-byte pieces (buffer_load_dwordx3 … lds, gfx950) plus a dword tail: L doubles = 8L bytes
+// = n12·12 + n4·4.  A 12-byte LDS-DMA lands each lane's piece in a 16-byte LDS slot
+// (measured: tools/dma12_probe.hip, profiles/r01/dma12_probe.txt), so the images are
+// A = [t][n12][16 B] (12 valid) and B = [t][n4][4 B].  The reader (SImg) reassembles a
+// double from its two dwords.  5 doubles cost 3 + 1 instructions instead of 10 dwords.
+template <int L> struct Split {
+    static constexpr int B = 8 * L, n12 = LQRX_FIL_N12 ? B / 12 : 0, n4 = (B - 12 * n12) / 4;
+    static constexpr int bytesA = 64 * 16 * n12;
+    static constexpr int lane_bytes = 16 * n12 + 4 * n4;       // LDS bytes per trajectory
+    static constexpr int instrs = n12 + n4;
+};
+template <int L> struct PatS {
+    using SP = Split<L>;
+    uint32_t voA[SP::n12 > 0 ? SP::n12 : 1], voB[SP::n4 > 0 ? SP::n4 : 1];
+    __device__ __forceinline__ void init(int64_t s, int lane, int nlive)
+    {
+        const uint32_t sb = (uint32_t)(s * 8);
+#pragma unroll
+        for (int i = 0; i < SP::n12; ++i) {
+            const uint32_t p = 64u * (uint32_t)i + (uint32_t)lane;
+            uint32_t tr = p / (uint32_t)(SP::n12 > 0 ? SP::n12 : 1);
+            const uint32_t e = p - tr * (uint32_t)(SP::n12 > 0 ? SP::n12 : 1);
+            tr = tr < (uint32_t)nlive ? tr : (uint32_t)(nlive - 1);
+            voA[i] = tr * sb + 12u * e;
+        }
+#pragma unroll
+        for (int i = 0; i < SP::n4; ++i) {
+            const uint32_t p = 64u * (uint32_t)i + (uint32_t)lane;
+            uint32_t tr = p / (uint32_t)(SP::n4 > 0 ? SP::n4 : 1);
+            const uint32_t e = p - tr * (uint32_t)(SP::n4 > 0 ? SP::n4 : 1);
+            tr = tr < (uint32_t)nlive ? tr : (uint32_t)(nlive - 1);
+            voB[i] = tr * sb + 12u * SP::n12 + 4u * e;
+        }
+    }
+    __device__ __forceinline__ void issue(rsrc_t r, int64_t off_elems, double *lds) const
+    {
+        const uint32_t so = (uint32_t)(off_elems * 8);
+#pragma unroll
+        for (int i = 0; i < SP::n12; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lptr_t)((char *)lds + i * 64 * 16), 12, voA[i], so, 0, 0);
+#pragma unroll
+        for (int i = 0; i < SP::n4; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lptr_t)((char *)lds + SP::bytesA + i * 64 * 4), 4, voB[i],
+                                                     so, 0, 0);
+    }
+};
+// reader of a split image: element j of this lane's chunk
+typedef const __attribute__((address_space(3))) uint32_t lds_u32;
+template <int L> struct SImg {
+    using SP = Split<L>;
+    uint32_t base;                                                  // LDS byte address
+    int lane;
+    __device__ __forceinline__ uint32_t dw(int x) const
+    {
+        // explicit LDS (address-space 3) access: a generic-pointer form of this read trips
+        // an instruction-selection bug in this compiler (src_shared_base compare)
+        const uint32_t a = x < 12 * SP::n12 ? base + (lane * SP::n12 + x / 12) * 16 + x % 12
+                                            : base + SP::bytesA + lane * (4 * SP::n4) + (x - 12 * SP::n12);
+        return *(lds_u32 *)(size_t)a;
+    }
+    __device__ __forceinline__ double operator[](int j) const
+    {
+        const uint64_t lo = dw(8 * j), hi = dw(8 * j + 4);
+        return __builtin_bit_cast(double, lo | (hi << 32));
+    }
+};
+
+// staging buffer views (lane-linear [t][L] images)
+template <class S> struct Buf {
+    double *base;
+    __device__ const double *Y(int lane, int L) const { return base + lane * L; }
+    __device__ uint32_t lds() const { return (uint32_t)(size_t)(lptr_t)base; }
+    template <int L> __device__ SImg<L> y(int lane) const { return SImg<L>{lds() + S::OFF_y, lane}; }
+    template <int L> __device__ SImg<L> H(int lane) const { return SImg<L>{lds() + S::OFF_H, lane}; }
+    template <int L> __device__ SImg<L> g(int lane) const { return SImg<L>{lds() + S::OFF_g, lane}; }
+};
+
+// per-wave context: buffer resources, lane facts, the DMA patterns of interior knots
+template <class S> struct Ctx {
+    using I = typename S::I;
+    const double *bY, *by, *bH, *bg;              // wave bases (→ buffer resources at use)
+    double *bS, *bdz, *blam;
+    int lane, nlive;
+    bool live;
+    uint32_t vS, vdz, vlam;                        // per-lane byte offsets: slab, dz, lam
+    Pat<S::template LY<I>(), S::WIDE_Y> pY;
+    PatS<S::template Ly<I>()> py;
+    PatS<S::template LH<I>()> pH;
+    PatS<S::template Lg<I>()> pg;
+};
+
+// interior knots: the precomputed patterns of the context
+template <class S>
+__device__ __forceinline__ void stage_I(const Ctx<S> &c, int k, double *buf, bool fwd)
+{
+    using O = Off<S>;
+    c.pY.issue(make_rsrc(c.bY), O::Y(k), buf);
+    if (fwd) c.py.issue(make_rsrc(c.by), O::y(k), buf + S::OFF_y / 8);
+    if constexpr (S::GINV) {
+        c.pH.issue(make_rsrc(c.bH), O::H(k), buf + S::OFF_H / 8);
+        c.pg.issue(make_rsrc(c.bg), O::g(k), buf + S::OFF_g / 8);
+    }
+}
+
+// first / last knot (class C): one-off patterns
+template <class S, class C>
+__device__ __forceinline__ void stage(const KktArgs &a, const Ctx<S> &c, int k, double *buf, bool fwd)
+{
+    using O = Off<S>;
+    Pat<S::template LY<C>(), S::WIDE_Y> pY;
+    pY.init(a.sY, c.lane, c.nlive);
+    pY.issue(make_rsrc(c.bY), O::Y(k), buf);
+    if (fwd) {
+        PatS<S::template Ly<C>()> py;
+        py.init(a.sy, c.lane, c.nlive);
+        py.issue(make_rsrc(c.by), O::y(k), buf + S::OFF_y / 8);
+    }
+    if constexpr (S::GINV) {
+        PatS<S::template LH<C>()> pH;
+        pH.init(a.sH, c.lane, c.nlive);
+        pH.issue(make_rsrc(c.bH), O::H(k), buf + S::OFF_H / 8);
+        PatS<S::template Lg<C>()> pg;
+        pg.init(a.sg, c.lane, c.nlive);
+        pg.issue(make_rsrc(c.bg), O::g(k), buf + S::OFF_g / 8);
+    }
+}
+
+typedef unsigned int u2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void bstore(double v, rsrc_t r, uint32_t vo, uint32_t so)
+{
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2_t, v), r, vo, so, 0);
+}
+__device__ __forceinline__ double bload(rsrc_t r, uint32_t vo, uint32_t so)
+{
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
+}
+
+// wait until at most N vector-memory ops are outstanding (N ≤ 63) and all LDS ops are done
+template <int N> __device__ __forceinline__ void vm_wait()
+{
+    constexpr int n = N > 63 ? 63 : (N < 0 ? 0 : N);
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(n) : "memory");
+}
+
+// ------------------------------------------------------------------ small dense kernels
+// upper Cholesky X = UᵀU in place (upper triangle, i ≤ j); diagonal replaced by 1/U_ii.
+// Returns false on a non-positive pivot (potrf info; the sweep continues like the caller).
+template <int M>
+__device__ __forceinline__ bool potrf_inv(double (&X)[Z(M)][Z(M)])
+{
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        double d = X[j][j];
+#pragma unroll
+        for (int p = 0; p < j; ++p) d = fma(-X[p][j], X[p][j], d);
+        ok = ok && (d > 0.0);
+        const double ri = rsqrt_nr(d);
+        X[j][j] = ri;
+#pragma unroll
+        for (int c = j + 1; c < M; ++c) {
+            double v = X[j][c];
+#pragma unroll
+            for (int p = 0; p < j; ++p) v = fma(-X[p][j], X[p][c], v);
+            X[j][c] = v * ri;
+        }
+    }
+    return ok;
+}
+
+// X ← U⁻ᵀX (X is M×NR); U from potrf_inv (inverse diagonal)
+template <int M, int NR>
+__device__ __forceinline__ void trsm_t(const double (&U)[Z(M)][Z(M)], double (&X)[Z(M)][Z(NR)])
+{
+#pragma unroll
+    for (int c = 0; c < NR; ++c)
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+            double s = X[i][c];
+#pragma unroll
+            for (int p = 0; p < i; ++p) s = fma(-U[p][i], X[p][c], s);
+            X[i][c] = s * U[i][i];
+        }
+}
+// x ← U⁻ᵀx
+template <int M> __device__ __forceinline__ void trsv_t(const double (&U)[Z(M)][Z(M)], double (&x)[Z(M)])
+{
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        double s = x[i];
+#pragma unroll
+        for (int p = 0; p < i; ++p) s = fma(-U[p][i], x[p], s);
+        x[i] = s * U[i][i];
+    }
+}
+// x ← U⁻¹x
+template <int M> __device__ __forceinline__ void trsv_n(const double (&U)[Z(M)][Z(M)], double (&x)[Z(M)])
+{
+#pragma unroll
+    for (int i = M - 1; i >= 0; --i) {
+        double s = x[i];
+#pragma unroll
+        for (int p = i + 1; p < M; ++p) s = fma(-U[i][p], x[p], s);
+        x[i] = s * U[i][i];
+    }
+}
+
+// ------------------------------------------------------------------ Schur pieces
+// shur! (jacobian_blocks.jl:231-242): S = Y H⁻¹ Yᵀ (upper triangle), r = Y H⁻¹ g;
+// Ginv = false (SOC variant): S = Y Yᵀ, r = 0.  Y is R×W column-major in LDS.
+template <class C> struct Shur {
+    double S[Z(C::R)][Z(C::R)];
+    double r[Z(C::R)];
+};
+
+template <class S, class C>
+__device__ __forceinline__ bool compute_shur(Shur<C> &s, const double *Y, const SImg<S::template LH<C>()> &H,
+                                             const SImg<S::template Lg<C>()> &g)
+{
+    constexpr int R = C::R, W = C::W;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        s.r[i] = 0.0;
+#pragma unroll
+        for (int j = i; j < R; ++j) s.S[i][j] = 0.0;
+    }
+    bool ok = true;
+    if constexpr (!S::GINV || S::HDIAG) {
+        // stream Y column by column: S += y_j h_j y_jᵀ, r += y_j h_j g_j  (h = 1/H_jj)
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            double v[R], vh[R];
+#pragma unroll
+            for (int i = 0; i < R; ++i) v[i] = Y[i + j * R];
+            if constexpr (S::GINV) {
+                const double h = rcp_nr2(H[j]);               // block_cholesky.jl:86 inv
+                const double gh = g[j];
+#pragma unroll
+                for (int i = 0; i < R; ++i) {
+                    vh[i] = v[i] * h;
+                    s.r[i] = fma(vh[i], gh, s.r[i]);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < R; ++i) vh[i] = v[i];
+            }
+#pragma unroll
+            for (int i = 0; i < R; ++i)
+#pragma unroll
+                for (int i2 = i; i2 < R; ++i2) s.S[i][i2] = fma(vh[i], v[i2], s.S[i][i2]);
+        }
+    } else {
+        // dense / block-diagonal H (block_cholesky.jl:55-77): potrf, then Wt = H⁻¹Yᵀ row by row
+        double U[W][W];
+#pragma unroll
+        for (int j = 0; j < W; ++j)
+#pragma unroll
+            for (int i = 0; i <= j; ++i) U[i][j] = H[i + j * W];
+        ok = potrf_inv<W>(U);
+        double Wt[R][W];
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            double x[W];
+#pragma unroll
+            for (int j = 0; j < W; ++j) x[j] = Y[i + j * R];
+            trsv_t<W>(U, x);
+            trsv_n<W>(U, x);
+#pragma unroll
+            for (int j = 0; j < W; ++j) Wt[i][j] = x[j];
+        }
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            const double gj = g[j];
+#pragma unroll
+            for (int i = 0; i < R; ++i) {
+                const double y = Y[i + j * R];
+                s.r[i] = fma(Wt[i][j], gj, s.r[i]);
+#pragma unroll
+                for (int i2 = i; i2 < R; ++i2) s.S[i][i2] = fma(y, Wt[i2][j], s.S[i][i2]);
+            }
+        }
+    }
+    return ok;
+}
+
+// ------------------------------------------------------------------ forward step
+// Carried between knots: Ua = C̃_{k-1} (factor, inverse diagonal) and λ_{k-1} (forward).
+template <class S> struct Carry {
+    double Ua[Z(S::NX)][Z(S::NX)];
+    double lprev[Z(S::NX)];
+};
+
+// slab: wave-major [k][field][64 lanes] doubles (coalesced; 32-bit offsets per wave)
+template <class S> __device__ __forceinline__ uint32_t slab_so(int k, int f)
+{
+    return (uint32_t)((k * S::SLOT + f) * 64 * 8);
+}
+
+// cholesky! + forward_substitution! of knot k (class C), given its Schur pieces sc, y_k
+// (yc), and the Schur pieces of knot k+1 (sn, class Cn; NoCls at the last knot).
+// Returns the number of slab stores issued (all single doubles).
+template <class S, class C, class Cn>
+__device__ __forceinline__ void factor_knot(int k, const Shur<C> &sc, const double (&yc)[Z(C::PS + C::P2)],
+                                            const Shur<Cn> &sn, Carry<S> &cy, const Ctx<S> &c, int &info)
+{
+    constexpr int p1 = C::P1, ps = C::PS, p2 = C::P2;
+    constexpr int O1 = C::O1, OS = C::OS, O2 = C::O2;
+    static_assert(Cn::none || Cn::P1 == p2, "n1[k+1] == n2[k]");
+    double D[Z(p1)][Z(ps)], Bm[Z(ps)][Z(ps)], E[Z(ps)][Z(p2)], F[Z(p1)][Z(p2)], Cm[Z(p2)][Z(p2)];
+    double cc[Z(ps)], d[Z(p2)];
+#pragma unroll
+    for (int i = 0; i < p1; ++i) {
+#pragma unroll
+        for (int j = 0; j < ps; ++j) D[i][j] = sc.S[O1 + i][OS + j];
+#pragma unroll
+        for (int j = 0; j < p2; ++j) F[i][j] = sc.S[O1 + i][O2 + j];
+    }
+#pragma unroll
+    for (int i = 0; i < ps; ++i) {
+#pragma unroll
+        for (int j = i; j < ps; ++j) Bm[i][j] = sc.S[OS + i][OS + j];
+#pragma unroll
+        for (int j = 0; j < p2; ++j) E[i][j] = sc.S[OS + i][O2 + j];
+        cc[i] = sc.r[OS + i] - yc[i];                             // copy_shur! :284
+    }
+#pragma unroll
+    for (int i = 0; i < p2; ++i) {
+#pragma unroll
+        for (int j = i; j < p2; ++j) {
+            double v = sc.S[O2 + i][O2 + j];
+            if constexpr (!Cn::none) v += sn.S[i][j];             // A_{k+1} ≡ C_k  (:166, :277)
+            Cm[i][j] = v;
+        }
+        double dv = sc.r[O2 + i] - yc[ps + i];                    // :285
+        if constexpr (!Cn::none) dv += sn.r[i];                   // d .+= r_D2 of k+1  (:251)
+        d[i] = dv;
+    }
+    // cholesky!(U[k], F[k])  cholesky_solve.jl:47-67
+    if constexpr (p1 > 0) {
+        if constexpr (ps > 0) trsm_t<p1, ps>(cy.Ua, D);              // :49  D̃ = A⁻ᵀD
+        if constexpr (p2 > 0) trsm_t<p1, p2>(cy.Ua, F);              // :57  F̃ = A⁻ᵀF
+    }
+    if constexpr (ps > 0) {
+#pragma unroll
+        for (int i = 0; i < ps; ++i)
+#pragma unroll
+            for (int j = i; j < ps; ++j) {
+                double v = Bm[i][j];
+#pragma unroll
+                for (int q = 0; q < p1; ++q) v = fma(-D[q][i], D[q][j], v);   // :50-53
+                Bm[i][j] = v;
+            }
+        if (!potrf_inv<ps>(Bm) && info == 0) info = k + 1;
+#pragma unroll
+        for (int i = 0; i < ps; ++i)
+#pragma unroll
+            for (int j = 0; j < p2; ++j) {
+                double v = E[i][j];
+#pragma unroll
+                for (int q = 0; q < p1; ++q) v = fma(-D[q][i], F[q][j], v);   // :59
+                E[i][j] = v;
+            }
+        if constexpr (p2 > 0) trsm_t<ps, p2>(Bm, E);                   // :60
+    }
+    if constexpr (p2 > 0) {
+#pragma unroll
+        for (int i = 0; i < p2; ++i)
+#pragma unroll
+            for (int j = i; j < p2; ++j) {
+                double v = Cm[i][j];
+#pragma unroll
+                for (int q = 0; q < p1; ++q) v = fma(-F[q][i], F[q][j], v);   // :61-62
+#pragma unroll
+                for (int q = 0; q < ps; ++q) v = fma(-E[q][i], E[q][j], v);
+                Cm[i][j] = v;
+            }
+        if (!potrf_inv<p2>(Cm) && info == 0) info = k + 1;
+    }
+    // forward_substitution!  cholesky_solve.jl:93-117
+    double mu[Z(ps)], la[Z(p2)];
+#pragma unroll
+    for (int i = 0; i < ps; ++i) {
+        double v = cc[i];
+#pragma unroll
+        for (int q = 0; q < p1; ++q) v = fma(-D[q][i], cy.lprev[q], v);
+        mu[i] = v;
+    }
+    if constexpr (ps > 0) trsv_t<ps>(Bm, mu);
+#pragma unroll
+    for (int i = 0; i < p2; ++i) {
+        double v = d[i];
+#pragma unroll
+        for (int q = 0; q < p1; ++q) v = fma(-F[q][i], cy.lprev[q], v);
+#pragma unroll
+        for (int q = 0; q < ps; ++q) v = fma(-E[q][i], mu[q], v);
+        la[i] = v;
+    }
+    if constexpr (p2 > 0) trsv_t<p2>(Cm, la);
+    // slab (batch-fastest, coalesced): B̃ | C̃ | D̃ | Ẽ | F̃ | μ | λ
+    int f = 0;
+#pragma unroll
+    for (int i = 0; i < ps; ++i)
+#pragma unroll
+        for (int j = i; j < ps; ++j) bstore(Bm[i][j], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
+#pragma unroll
+    for (int i = 0; i < p2; ++i)
+#pragma unroll
+        for (int j = i; j < p2; ++j) bstore(Cm[i][j], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
+#pragma unroll
+    for (int i = 0; i < p1; ++i)
+#pragma unroll
+        for (int j = 0; j < ps; ++j) bstore(D[i][j], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
+#pragma unroll
+    for (int i = 0; i < ps; ++i)
+#pragma unroll
+        for (int j = 0; j < p2; ++j) bstore(E[i][j], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
+#pragma unroll
+    for (int i = 0; i < p1; ++i)
+#pragma unroll
+        for (int j = 0; j < p2; ++j) bstore(F[i][j], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
+#pragma unroll
+    for (int i = 0; i < ps; ++i) bstore(mu[i], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
+#pragma unroll
+    for (int i = 0; i < p2; ++i) bstore(la[i], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
+    // carry C̃_k, λ_k to knot k+1
+    if constexpr (p2 > 0) {
+#pragma unroll
+        for (int i = 0; i < p2; ++i) {
+            cy.lprev[i] = la[i];
+#pragma unroll
+            for (int j = i; j < p2; ++j) cy.Ua[i][j] = Cm[i][j];
+        }
+    }
+}
+
+// forward step k (class C; next class Cn, class after next Cnn for the DMA issued here)
+template <class S, class C, class Cn, class Cnn, bool FIRST = false>
+__device__ __forceinline__ void fwd_step(const KktArgs &a, const Ctx<S> &c, int k, double *stg,
+                                         Shur<C> &sc, double (&yc)[Z(C::PS + C::P2)], Shur<Cn> &sn,
+                                         double (&yn)[Z(Cn::PS + Cn::P2)], Carry<S> &cy, int &info)
+{
+    if constexpr (!Cn::none) {
+        Buf<S> b{stg + ((k + 1) % 3) * S::BUF};
+        const bool ok = compute_shur<S, Cn>(sn, b.Y(c.lane, S::template LY<Cn>()),
+                                           b.template H<S::template LH<Cn>()>(c.lane),
+                                           b.template g<S::template Lg<Cn>()>(c.lane));
+        if (!ok && info == 0) info = -(k + 2);
+        const auto yk = b.template y<S::template Ly<Cn>()>(c.lane);
+#pragma unroll
+        for (int i = 0; i < Cn::PS + Cn::P2; ++i) yn[i] = yk[i];
+    }
+    factor_knot<S, C, Cn>(k, sc, yc, sn, cy, c, info);
+}
+
+// ------------------------------------------------------------------ backward step
+template <class C> struct SlabV {        // slab contents of one knot, in registers
+    double Bm[Z(C::PS)][Z(C::PS)], Cm[Z(C::P2)][Z(C::P2)], D[Z(C::P1)][Z(C::PS)], E[Z(C::PS)][Z(C::P2)],
+        F[Z(C::P1)][Z(C::P2)], mu[Z(C::PS)], la[Z(C::P2)];
+};
+
+template <class S, class C>
+__device__ __forceinline__ void slab_load(SlabV<C> &v, const Ctx<S> &c, int k)
+{
+    constexpr int p1 = C::P1, ps = C::PS, p2 = C::P2;
+    int f = 0;
+    auto at = [&](int ff) { return bload(make_rsrc(c.bS), c.vS, slab_so<S>(k, ff)); };
+#pragma unroll
+    for (int i = 0; i < ps; ++i)
+#pragma unroll
+        for (int j = i; j < ps; ++j) v.Bm[i][j] = at(f++);
+#pragma unroll
+    for (int i = 0; i < p2; ++i)
+#pragma unroll
+        for (int j = i; j < p2; ++j) v.Cm[i][j] = at(f++);
+#pragma unroll
+    for (int i = 0; i < p1; ++i)
+#pragma unroll
+        for (int j = 0; j < ps; ++j) v.D[i][j] = at(f++);
+#pragma unroll
+    for (int i = 0; i < ps; ++i)
+#pragma unroll
+        for (int j = 0; j < p2; ++j) v.E[i][j] = at(f++);
+#pragma unroll
+    for (int i = 0; i < p1; ++i)
+#pragma unroll
+        for (int j = 0; j < p2; ++j) v.F[i][j] = at(f++);
+#pragma unroll
+    for (int i = 0; i < ps; ++i) v.mu[i] = at(f++);
+#pragma unroll
+    for (int i = 0; i < p2; ++i) v.la[i] = at(f++);
+}
+
+// final multipliers of knot k (class C) from its slab and knot k+1's (class Cn, final μ, λ
+// already in vn.mu / vn.la).  backward_substitution!, cholesky_solve.jl:119-143.
+template <class C, class Cn>
+__device__ __forceinline__ void bwd_knot(SlabV<C> &v, const SlabV<Cn> &vn)
+{
+    constexpr int ps = C::PS, p2 = C::P2;
+    if constexpr (!Cn::none) {
+#pragma unroll
+        for (int i = 0; i < p2; ++i) {                            // λ += D' μ' + F' λ'
+            double s = v.la[i];
+#pragma unroll
+            for (int q = 0; q < Cn::PS; ++q) s = fma(vn.D[i][q], vn.mu[q], s);
+#pragma unroll
+            for (int q = 0; q < Cn::P2; ++q) s = fma(vn.F[i][q], vn.la[q], s);
+            v.la[i] = s;
+        }
+        if constexpr (p2 > 0) trsv_n<p2>(v.Cm, v.la);
+#pragma unroll
+        for (int i = 0; i < ps; ++i) {                            // μ -= E λ
+            double s = v.mu[i];
+#pragma unroll
+            for (int q = 0; q < p2; ++q) s = fma(-v.E[i][q], v.la[q], s);
+            v.mu[i] = s;
+        }
+        if constexpr (ps > 0) trsv_n<ps>(v.Bm, v.mu);
+#pragma unroll
+        for (int i = 0; i < p2; ++i) v.la[i] = -v.la[i];
+#pragma unroll
+        for (int i = 0; i < ps; ++i) v.mu[i] = -v.mu[i];
+    } else {                                                       // terminal :139-143
+        if constexpr (ps > 0) trsv_n<ps>(v.Bm, v.mu);
+#pragma unroll
+        for (int i = 0; i < ps; ++i) v.mu[i] = -v.mu[i];
+    }
+}
+
+// calc_residual! + calc_primals! of knot k (class C): needs λ_{k-1} (lp, class Cp's λ),
+// μ_k, λ_k (v).  cholesky_solver.jl:195-236 (SOC: :263-266).
+template <class S, class C, int NLP>
+__device__ __forceinline__ void primal_knot(const Ctx<S> &c, int k, const SlabV<C> &v, const double (&lp)[Z(NLP)],
+                                            const Buf<S> &b)
+{
+    constexpr int R = C::R, W = C::W;
+    static_assert(NLP == C::P1, "λ_{k-1} has n1[k] entries");
+    const double *Y = b.Y(c.lane, S::template LY<C>());
+    double z[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < C::P2; ++i) s = fma(Y[(C::O2 + i) + j * R], v.la[i], s);   // D1ᵀλ_k
+#pragma unroll
+        for (int i = 0; i < C::PS; ++i) s = fma(Y[(C::OS + i) + j * R], v.mu[i], s);   // Cᵀμ_k
+#pragma unroll
+        for (int i = 0; i < C::P1; ++i) s = fma(Y[(C::O1 + i) + j * R], lp[i], s);     // D2ᵀλ_{k-1}
+        z[j] = s;
+    }
+    if constexpr (S::GINV) {
+        const auto g = b.template g<S::template Lg<C>()>(c.lane);
+        const auto H = b.template H<S::template LH<C>()>(c.lane);
+#pragma unroll
+        for (int j = 0; j < W; ++j) z[j] += g[j];                                     // add_gradient!
+        if constexpr (S::HDIAG) {
+#pragma unroll
+            for (int j = 0; j < W; ++j) z[j] *= rcp_nr2(H[j]);
+        } else {
+            double U[W][W];
+#pragma unroll
+            for (int j = 0; j < W; ++j)
+#pragma unroll
+                for (int i = 0; i <= j; ++i) U[i][j] = H[i + j * W];
+            (void)potrf_inv<W>(U);
+            trsv_t<W>(U, z);
+            trsv_n<W>(U, z);
+        }
+    }
+    if (c.live) {
+        const uint32_t so = (uint32_t)(Off<S>::g(k) * 8);
+#pragma unroll
+        for (int j = 0; j < W; ++j) bstore(-z[j], make_rsrc(c.bdz), c.vdz + 8 * j, so);
+    }
+}
+
+template <class S, class C>
+__device__ __forceinline__ void store_lam(const Ctx<S> &c, int k, const SlabV<C> &v)
+{
+    if (!c.live) return;
+    const uint32_t so = (uint32_t)(Off<S>::y(k) * 8);
+#pragma unroll
+    for (int i = 0; i < C::PS; ++i) bstore(v.mu[i], make_rsrc(c.blam), c.vlam + 8 * i, so);
+#pragma unroll
+    for (int i = 0; i < C::P2; ++i) bstore(v.la[i], make_rsrc(c.blam), c.vlam + 8 * (C::PS + i), so);
+}
+
+// Start of forward step k (class C; Cnn = class of knot k+2): knot k+1 must have landed.
+// After its DMA (issued at step k-2) came the slab stores of step k-2 (not counted:
+// conservative), the DMA of knot k+2 (≥ Dmin<Cnn> instructions) and the slab stores of
+// step k-1 (single-double stores, ≥ the smaller of the F / C slab sizes).  Step 0 has no
+// stores before it.  Then knot k+3 is restaged into knot k's (consumed) buffer.
+template <class S, class C, class Cnn, bool FIRST>
+__device__ __forceinline__ void fwd_wait()
+{
+    constexpr int sF = S::template slab<typename S::F>(), sC = S::template slab<C>();
+    constexpr int Sprev = FIRST ? 0 : (sF < sC ? sF : sC);
+    vm_wait<S::template Dmin<Cnn>() + Sprev>();
+}
+
+// ------------------------------------------------------------------ the kernel
+template <class S>
+__global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__restrict__ scratch)
+{
+    using F = typename S::F;
+    using I = typename S::I;
+    using L = typename S::L;
+    __shared__ double stg[3 * S::BUF];
+    const int N = a.N;                                          // ≥ 4 (host-checked)
+    const int64_t t0 = (int64_t)blockIdx.x * 64;
+    Ctx<S> c;
+    c.lane = threadIdx.x;
+    c.nlive = (int)(a.batch - t0 < 64 ? a.batch - t0 : 64);
+    c.live = c.lane < c.nlive;
+    c.bY = a.Y + t0 * a.sY;
+    c.by = a.y + t0 * a.sy;
+    c.bH = a.H + t0 * a.sH;
+    c.bg = a.g + t0 * a.sg;
+    c.bdz = a.dz + t0 * a.sg;
+    c.blam = a.lam + t0 * a.sl;
+    c.bS = scratch + (int64_t)blockIdx.x * N * S::SLOT * 64;
+    c.vS = 8u * c.lane;
+    c.vdz = (uint32_t)(c.lane * a.sg * 8);
+    c.vlam = (uint32_t)(c.lane * a.sl * 8);
+    c.pY.init(a.sY, c.lane, c.nlive);
+    c.py.init(a.sy, c.lane, c.nlive);
+    c.pH.init(a.sH, c.lane, c.nlive);
+    c.pg.init(a.sg, c.lane, c.nlive);
+    int info = 0;
+
+    // ---------------- forward ----------------
+    stage<S, F>(a, c, 0, stg, true);
+    stage_I<S>(c, 1, stg + S::BUF, true);
+    stage_I<S>(c, 2, stg + 2 * S::BUF, true);               // N ≥ 4: knot 2 is interior
+    vm_wait<S::template Dmin<I>() * 2>();
+    Shur<F> s0;
+    double y0[Z(F::PS + F::P2)];
+    {
+        Buf<S> b{stg};
+        if (!compute_shur<S, F>(s0, b.Y(c.lane, S::template LY<F>()), b.template H<S::template LH<F>()>(c.lane),
+                                b.template g<S::template Lg<F>()>(c.lane)) && info == 0)
+            info = -1;
+        const auto yk = b.template y<S::template Ly<F>()>(c.lane);
+#pragma unroll
+        for (int i = 0; i < F::PS + F::P2; ++i) y0[i] = yk[i];
+    }
+    Carry<S> cy;
+#pragma unroll
+    for (int i = 0; i < S::NX; ++i) {
+        cy.lprev[i] = 0.0;
+#pragma unroll
+        for (int j = 0; j < S::NX; ++j) cy.Ua[i][j] = 0.0;
+    }
+    Shur<I> sI;
+    double yI[Z(I::PS + I::P2)];
+    fwd_wait<S, F, I, true>();
+    if (3 == N - 1) stage<S, L>(a, c, 3, stg, true);
+    else stage_I<S>(c, 3, stg, true);
+    fwd_step<S, F, I, I, true>(a, c, 0, stg, s0, y0, sI, yI, cy, info);
+    for (int k = 1; k <= N - 3; ++k) {
+        Shur<I> sn;
+        double yn[Z(I::PS + I::P2)];
+        double *rb = stg + ((k + 3) % 3) * S::BUF;
+        if (k == N - 3) {
+            fwd_wait<S, I, L, false>();                         // (no restage: k+3 = N)
+            fwd_step<S, I, I, L>(a, c, k, stg, sI, yI, sn, yn, cy, info);
+        } else {
+            fwd_wait<S, I, I, false>();
+            if (k + 3 == N - 1) stage<S, L>(a, c, k + 3, rb, true);
+            else stage_I<S>(c, k + 3, rb, true);
+            fwd_step<S, I, I, I>(a, c, k, stg, sI, yI, sn, yn, cy, info);
+        }
+        sI = sn;
+#pragma unroll
+        for (int i = 0; i < I::PS + I::P2; ++i) yI[i] = yn[i];
+    }
+    Shur<L> sL;
+    double yL[Z(L::PS + L::P2)];
+    fwd_wait<S, I, NoCls, false>();
+    fwd_step<S, I, L, NoCls>(a, c, N - 2, stg, sI, yI, sL, yL, cy, info);
+    {
+        Shur<NoCls> none;
+        factor_knot<S, L, NoCls>(N - 1, sL, yL, none, cy, c, info);
+    }
+
+    // ---------------- backward + primal recovery ----------------
+    // step j finalises μ_j, λ_j and recovers δz_{j+1} from staged knot j+1; the DMA issued
+    // at step j is knot j-1's (used at step j-2)
+    vm_wait<0>();
+    stage<S, L>(a, c, N - 1, stg + ((N - 1) % 3) * S::BUF, false);
+    SlabV<L> vL;
+    slab_load<S, L>(vL, c, N - 1);
+    SlabV<NoCls> vnone;
+    bwd_knot<L, NoCls>(vL, vnone);                              // step N-1 (no primal yet)
+    store_lam<S, L>(c, N - 1, vL);
+    stage_I<S>(c, N - 2, stg + ((N - 2) % 3) * S::BUF, false);
+
+    SlabV<I> vI, vpre;
+    slab_load<S, I>(vI, c, N - 2);
+    slab_load<S, I>(vpre, c, N - 3);                            // knot N-3 ≥ 1 is interior
+    {
+        // step N-2: multipliers of N-2, primal of N-1 (needs knot N-1 staged)
+        vm_wait<0>();
+        stage_I<S>(c, N - 3, stg + ((N - 3) % 3) * S::BUF, false);
+        bwd_knot<I, L>(vI, vL);
+        Buf<S> b{stg + ((N - 1) % 3) * S::BUF};
+        primal_knot<S, L, L::P1>(c, N - 1, vL, vI.la, b);
+        store_lam<S, I>(c, N - 2, vI);
+    }
+    for (int j = N - 3; j >= 1; --j) {
+        SlabV<I> v = vpre;
+        if (j - 1 >= 1) slab_load<S, I>(vpre, c, j - 1);         // next step's slab
+        // knot j+1 landed: after its DMA came (at least) the DMA of knot j
+        vm_wait<S::template Dbwd<I>()>();
+        if (j - 1 >= 1) stage_I<S>(c, j - 1, stg + ((j - 1) % 3) * S::BUF, false);
+        else stage<S, F>(a, c, 0, stg, false);
+        bwd_knot<I, I>(v, vI);
+        Buf<S> b{stg + ((j + 1) % 3) * S::BUF};
+        primal_knot<S, I, I::P1>(c, j + 1, vI, v.la, b);
+        store_lam<S, I>(c, j, v);
+        vI = v;
+    }
+    {
+        // step 0: multipliers of knot 0, primal of knot 1, then primal of knot 0
+        SlabV<F> v0;
+        slab_load<S, F>(v0, c, 0);
+        vm_wait<S::template Dbwd<F>()>();                        // knot 1 landed (DMA of 0 after it)
+        bwd_knot<F, I>(v0, vI);
+        Buf<S> b1{stg + (1 % 3) * S::BUF};
+        primal_knot<S, I, I::P1>(c, 1, vI, v0.la, b1);
+        store_lam<S, F>(c, 0, v0);
+        vm_wait<0>();
+        Buf<S> b0{stg};
+        double none[1] = {0.0};
+        primal_knot<S, F, 0>(c, 0, v0, none, b0);
+    }
+    if (a.info && c.live) a.info[t0 + c.lane] = info;
+}
+
+template <class S>
+hipError_t launch(const KktArgs &a, hipStream_t s)
+{
+    double *scratch = nullptr;
+    const size_t Bp = ((size_t)a.batch + 63) & ~(size_t)63;   // wave-major slab, 64 lanes/wave
+    const size_t bytes = Bp * (size_t)a.N * S::SLOT * sizeof(double);
+    hipError_t e = hipMallocAsync((void **)&scratch, bytes, s);
+    if (e != hipSuccess) return e;
+    dim3 grid((unsigned)((a.batch + 63) / 64)), block(64);
+    hipLaunchKernelGGL((kkt_fil_kernel<S>), grid, block, 0, s, a, scratch);
+    e = hipGetLastError();
+    hipError_t ef = hipFreeAsync(scratch, s);
+    return e != hipSuccess ? e : ef;
+}
+
+} // namespace fil
+
+// Dispatch: the FIL kernel serves a structure iff every knot matches one of the
+// instantiated (n̄, m, P0, PK, PN) shapes; otherwise the generic kernel (lqrx_kkt.hip) runs.
+bool kkt_fil_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
+                    const int32_t *w, hipStream_t s, hipError_t *err)
+{
+    const int N = a.N;
+    if (N < 4) return false;
+    const int nx = n2[0], m = w[0] - nx, P0 = p[0], PK = p[1], PN = p[N - 1];
+    if (n1[0] != 0 || w[N - 1] != nx || n2[N - 1] != 0 || n1[N - 1] != nx) return false;
+    for (int k = 1; k < N - 1; ++k)
+        if (n1[k] != nx || n2[k] != nx || p[k] != PK || w[k] != nx + m) return false;
+    const bool diag = a.h_mode == 2, ginv = a.ginv != 0;
+#define LQRX_FIL(NX, M, A0, AK, AN)                                                                      \
+    if (nx == NX && m == M && P0 == A0 && PK == AK && PN == AN) {                                        \
+        if (diag && ginv) *err = fil::launch<fil::Shape<NX, M, A0, AK, AN, true, true>>(a, s);          \
+        else if (ginv) *err = fil::launch<fil::Shape<NX, M, A0, AK, AN, false, true>>(a, s);            \
+        else *err = fil::launch<fil::Shape<NX, M, A0, AK, AN, true, false>>(a, s);                      \
+        return true;                                                                                     \
+    }
+    LQRX_FIL(3, 2, 3, 0, 3)   // Dubins car (BASELINE cfg3), test/dubins.jl
+#undef LQRX_FIL
+    return false;
+}
+
+} // namespace lqrx

@@ -15,8 +15,8 @@
  *
  *   KKT (block-tridiagonal Schur complement + block upper Cholesky + substitutions)
  *     /root/reference/src/jacobian_blocks.jl:220-286   calculate_shur_factors!/shur!/copy_shur!
- *     /root/reference/src/cholesky_solve.jl:206-226     cholesky!(U, F)   (block upper recurrence)
- *     /root/reference/src/cholesky_solve.jl:252-302     forward_/backward_substitution!
+ *     /root/reference/src/cholesky_solve.jl:47-67     cholesky!(U, F)   (block upper recurrence)
+ *     /root/reference/src/cholesky_solve.jl:93-143     forward_/backward_substitution!
  *     /root/reference/src/cholesky_solver.jl:185-236    calculate_primals!/calc_residual!
  *     /root/reference/src/block_cholesky.jl:55-101      H_k factor modes (dense / block-diag / diag)
  *
@@ -388,29 +388,29 @@ int oracle_kkt_solve_one(int N, const int *n1, const int *p, const int *n2, cons
     if (Sd) memset(Sd, 0, Ptot * Ptot * sizeof(double));
     if (Ud) memset(Ud, 0, Ptot * Ptot * sizeof(double));
 
-    /* KKT-7: cholesky!(U, F)  (cholesky_solve.jl:206-226) */
+    /* KKT-7: cholesky!(U, F)  (cholesky_solve.jl:47-67) */
     for (int k = 0; k < N; ++k) {
         oblk *u = &U[k], *f = &F[k];
         int p1 = u->p1, ps = u->ps, p2 = u->p2;
-        memcpy(u->D, f->D, (size_t)p1 * ps * sizeof(double));            /* :207 */
-        if (p1) trsm_ut(p1, ps, u->A, p1, u->D, p1);                      /* :208 A⁻ᵀD */
-        for (int j = 0; j < ps; ++j)                                      /* :209-211 B - D'D */
+        memcpy(u->D, f->D, (size_t)p1 * ps * sizeof(double));            /* :48 */
+        if (p1) trsm_ut(p1, ps, u->A, p1, u->D, p1);                      /* :49 A⁻ᵀD */
+        for (int j = 0; j < ps; ++j)                                      /* :50-53 B - D'D */
             for (int i = 0; i < ps; ++i) {
                 double s = f->B[IDX(i, j, ps)];
                 for (int q = 0; q < p1; ++q) s -= u->D[IDX(q, i, p1)] * u->D[IDX(q, j, p1)];
                 u->B[IDX(i, j, ps)] = s;
             }
         if (ps) { int st = oracle_potrf_upper(ps, u->B, ps); if (st && !info) info = k + 1; }
-        memcpy(u->F, f->F, (size_t)p1 * p2 * sizeof(double));            /* :215 */
-        if (p1) trsm_ut(p1, p2, u->A, p1, u->F, p1);                      /* :216 */
-        for (int j = 0; j < p2; ++j)                                      /* :218 E - D'F */
+        memcpy(u->F, f->F, (size_t)p1 * p2 * sizeof(double));            /* :56 */
+        if (p1) trsm_ut(p1, p2, u->A, p1, u->F, p1);                      /* :57 */
+        for (int j = 0; j < p2; ++j)                                      /* :59 E - D'F */
             for (int i = 0; i < ps; ++i) {
                 double s = f->E[IDX(i, j, ps)];
                 for (int q = 0; q < p1; ++q) s -= u->D[IDX(q, i, p1)] * u->F[IDX(q, j, p1)];
                 u->E[IDX(i, j, ps)] = s;
             }
-        if (ps) trsm_ut(ps, p2, u->B, ps, u->E, ps);                      /* :219 */
-        for (int j = 0; j < p2; ++j)                                      /* :220 C - F'F - E'E */
+        if (ps) trsm_ut(ps, p2, u->B, ps, u->E, ps);                      /* :60 */
+        for (int j = 0; j < p2; ++j)                                      /* :61-62 C - F'F - E'E */
             for (int i = 0; i < p2; ++i) {
                 double s = f->C[IDX(i, j, p2)];
                 for (int q = 0; q < p1; ++q) s -= u->F[IDX(q, i, p1)] * u->F[IDX(q, j, p1)];
@@ -418,11 +418,11 @@ int oracle_kkt_solve_one(int N, const int *n1, const int *p, const int *n2, cons
                 u->C[IDX(i, j, p2)] = s;
             }
         if (p2) { int st = oracle_potrf_upper(p2, u->C, p2); if (st && !info) info = k + 1; }
-        memcpy(u->c, f->c, (size_t)ps * sizeof(double));                 /* :223-224 */
+        memcpy(u->c, f->c, (size_t)ps * sizeof(double));                 /* :64-65 */
         memcpy(u->d, f->d, (size_t)p2 * sizeof(double));
     }
 
-    /* KKT-8: forward_substitution!  (cholesky_solve.jl:252-276) */
+    /* KKT-8: forward_substitution!  (cholesky_solve.jl:93-117) */
     for (int k = 0; k < N; ++k) {
         oblk *u = &U[k];
         int p1 = u->p1, ps = u->ps, p2 = u->p2;
@@ -441,7 +441,7 @@ int oracle_kkt_solve_one(int N, const int *n1, const int *p, const int *n2, cons
         }
         if (p2) trsm_ut(p2, 1, u->C, p2, u->lam, p2);                     /* C⁻ᵀ */
     }
-    /* KKT-9: backward_substitution!  (cholesky_solve.jl:278-302) */
+    /* KKT-9: backward_substitution!  (cholesky_solve.jl:119-143) */
     for (int k = N - 1; k >= 0; --k) {
         oblk *u = &U[k];
         int ps = u->ps, p2 = u->p2;
@@ -462,7 +462,7 @@ int oracle_kkt_solve_one(int N, const int *n1, const int *p, const int *n2, cons
             if (ps) trsm_un(ps, 1, u->B, ps, u->mu, ps);
             for (int i = 0; i < p2; ++i) u->lam[i] = -u->lam[i];
             for (int i = 0; i < ps; ++i) u->mu[i] = -u->mu[i];
-        } else {                                                          /* terminal :298-302 */
+        } else {                                                          /* terminal :139-143 */
             if (ps) trsm_un(ps, 1, u->B, ps, u->mu, ps);
             for (int i = 0; i < ps; ++i) u->mu[i] = -u->mu[i];
             /* λ_N (p2 == 0 for the reference's terminal block) is left as forward gave it */

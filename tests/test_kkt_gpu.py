@@ -1,7 +1,7 @@
 """GPU parity: batched block-tridiagonal KKT solve (liblqrx.so, C ABI) vs the CPU oracle.
 
 Oracle = oracle/lqr_oracle.c restating cholesky_solver.jl:166-236, jacobian_blocks.jl:
-220-286, cholesky_solve.jl:206-302, block_cholesky.jl:55-101 (pinned in test_oracle.py by
+220-286, cholesky_solve.jl:47-143, block_cholesky.jl:55-101 (pinned in test_oracle.py by
 the reference's test/cholesky_solve.jl:18-44 identities).  Tolerance: fp64, max|δz − ref| /
 max|ref| ≤ 1e-10 and the same for the multipliers.
 """
@@ -92,3 +92,20 @@ def test_kkt_alternating_structures(lqrx, gpu_ok):
         for pb, rd, rl in cases:
             got = K.kkt_solve(pb)
             assert rel(got["dz"], rd) <= TOL and rel(got["lam"], rl) <= TOL
+
+
+@pytest.mark.parametrize("N,batch", [(4, 130), (5, 64), (6, 1), (101, 16384 + 3)])
+@pytest.mark.parametrize("h_mode,ginv", [(2, 1), (0, 1), (2, 0)])
+def test_kkt_fil_shapes(lqrx, gpu_ok, N, batch, h_mode, ginv):
+    """The compile-time-shaped first/interior/last kernel (lqrx_kkt_fil.hip) at its edge
+    cases: the shortest horizon it serves (N = 4), one trajectory, ragged last waves, the
+    full cfg3 batch; Ginv = 0 is the second-order-correction variant."""
+    import lqrx.kkt as K
+
+    st = K.dubins_structure(N)
+    pb = K.random_kkt(st, batch, seed=7 * N + h_mode, h_mode=h_mode)
+    got = K.kkt_solve(pb, ginv=ginv)
+    ref = _ref(st, pb, ginv)
+    assert got["rc"] == 0 and (got["info"] == 0).all()
+    assert rel(got["dz"], ref["dz"].reshape(batch, -1)) <= TOL
+    assert rel(got["lam"], ref["lam"].reshape(batch, -1)) <= TOL
