@@ -34,6 +34,9 @@
 #ifndef LQRX_DP_VAR
 #define LQRX_DP_VAR 0
 #endif
+#ifndef LQRX_DP_DPPMAX
+#define LQRX_DP_DPPMAX 1
+#endif
 
 namespace lqrx {
 
@@ -140,10 +143,18 @@ __device__ __forceinline__ bool ns_refine(typename Tile<T>::acc (&X)[MT][MT],
             for (int j = 0; j < MT; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) mx = fmax(mx, fabs(R[i][j][r]));
+#if LQRX_DP_DPPMAX
+        // uniform (SGPR) residual bound: float precision is ample for a threshold test
+        const float rho = (float)(16 * MT) * wave_max_uniform((float)mx);
+        if (rho <= (float)NsTol<T>::v) return true;             // X already at working precision
+        mma_tn<T, MT, MT, MT>(X, X, R);                         // X ← X + XᵀR
+        if (rho <= (float)NsTol<T>::one_step) return true;      // new residual ≤ cond·ρ² ≪ eps
+#else
         const T rho = (T)(16 * MT) * wave_max(mx);
         if (rho <= NsTol<T>::v) return true;                    // X already at working precision
         mma_tn<T, MT, MT, MT>(X, X, R);                         // X ← X + XᵀR
         if (rho <= NsTol<T>::one_step) return true;             // new residual ≤ cond·ρ² ≪ eps
+#endif
     }
     (void)lane;
     return false;
@@ -156,6 +167,8 @@ template <typename T, int NT, int MT> struct DpCfg {
     static constexpr int ROLL = MP * NP + NP + MP;          // K_k + x + u (rollout)
     static constexpr int SYM = NP * (NP + 2);                // symmetrize image
     static constexpr int LDS_ELEMS = (AUG > ROLL ? AUG : ROLL) > SYM ? (AUG > ROLL ? AUG : ROLL) : SYM;
+    static constexpr int QCS = NP + 2;                      // LDS-resident Q image: column stride
+    static constexpr int QIMG = NP * QCS;
     static constexpr int KPL = (MP * NP + 63) / 64;         // K elements per lane (rollout)
 };
 
@@ -280,6 +293,9 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
     constexpr int MP = C::MP, CS = C::CS;
     constexpr bool EXACT = (VAR & VAR_EXACT) != 0;
     __shared__ T lds[C::LDS_ELEMS];
+    // Q (time-invariant, read every knot as the P_ accumulator start) lives in LDS for the
+    // horizon: an LDS read per element instead of an L2 round trip per knot
+    __shared__ T qimg[(VAR & VAR_EXACT) ? 1 : C::QIMG];
 
     const int lane = threadIdx.x;
     const int64_t b = blockIdx.x;
@@ -295,6 +311,14 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
     tiles_load<T, NT, NT, FULL>(P, (const T *)a.Qf + b * nn, n, n, n, lane, false); // :58 P = Qf
     acc Qt[EXACT ? NT : 1][EXACT ? NT : 1];
     if constexpr (EXACT) tiles_load<T, NT, NT, FULL>(Qt, Qg, n, n, n, lane, false);
+    else {
+        // zero-padded NP×NP image of Q (padding rows/cols 0, as tiles_load_lower)
+        for (int e = lane; e < C::NP * C::NP; e += 64) {
+            const int i = e % C::NP, j = e / C::NP;
+            qimg[i + j * C::QCS] = (i < n && j < n) ? Qg[i + (size_t)j * n] : (T)0;
+        }
+        __syncthreads();
+    }
 
     T *Pall = a.p_all ? (T *)a.P + (size_t)b * nn * N : nullptr;
     if (Pall) tiles_store<T, NT, NT>(P, Pall + (size_t)(N - 1) * nn, n, n, n, lane);
@@ -324,7 +348,7 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
 #pragma unroll
                 for (int j = 0; j < NT; ++j) Pn[i][j] = Qt[i][j];
         } else {
-            tiles_load_lower<T, NT, FULL>(Pn, Qg, n, n, lane);            // P_ ← Q (lower tiles)
+            tiles_lower_from_lds<T, NT>(Pn, qimg, C::QCS, lane);         // P_ ← Q (lower tiles)
         }
 #pragma unroll
         for (int i = 0; i < MT; ++i)

@@ -200,7 +200,20 @@ __device__ __forceinline__ void tiles_load_lower(typename Tile<T>::acc (&D)[NT][
 // diagonal (upper tiles AND the upper half of diagonal tiles) is replaced by its mirror.
 // Needed for the fast form P_ = Q + AᵀPA − GᵀK, whose accuracy relies on P staying
 // symmetric (GᵀK equals the reference's APB·K only for symmetric P).  Goes through an
-// NT·16 × NT·16 column-major LDS image with column stride NT·16 + 2.
+// NT·16 × NT·16 column-major LDS image with column stride NT·16 + 2.  Every LDS read is
+// unconditional and the diagonal tiles blend with a bit mask (no exec-mask branches: a
+// predicated read costs ~6 scalar/VALU instructions plus an SGPR-spill readlane).
+__device__ __forceinline__ double blend_upper(double keep, double mirror, bool take)
+{
+    const long long m = -(long long)take;                       // all-ones when take
+    return __longlong_as_double((__double_as_longlong(mirror) & m) | (__double_as_longlong(keep) & ~m));
+}
+__device__ __forceinline__ float blend_upper(float keep, float mirror, bool take)
+{
+    const int m = -(int)take;
+    return __int_as_float((__float_as_int(mirror) & m) | (__float_as_int(keep) & ~m));
+}
+
 template <typename T, int NT>
 __device__ __forceinline__ void tiles_symmetrize_lower(typename Tile<T>::acc (&D)[NT][NT], T *lds,
                                                        int lane)
@@ -220,11 +233,27 @@ __device__ __forceinline__ void tiles_symmetrize_lower(typename Tile<T>::acc (&D
         for (int j = i; j < NT; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                int row = i * 16 + Tile<T>::row(lane, r), col = j * 16 + tcol(lane);
-                T v = lds[col + row * S];
-                if (row < col) D[i][j][r] = v;
+                const int row = i * 16 + Tile<T>::row(lane, r), col = j * 16 + tcol(lane);
+                const T v = lds[col + row * S];
+                if (j > i) D[i][j][r] = v;                       // strictly upper tile: all mirrored
+                else D[i][j][r] = blend_upper(D[i][j][r], v, row < col);
             }
     __syncthreads();
+}
+
+// Load the lower tiles (i >= j) of an LDS-resident column-major image (column stride cs);
+// upper tiles zeroed.
+template <typename T, int NT>
+__device__ __forceinline__ void tiles_lower_from_lds(typename Tile<T>::acc (&D)[NT][NT], const T *lds, int cs,
+                                                     int lane)
+{
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                D[i][j][r] = (j > i) ? (T)0 : lds[(i * 16 + Tile<T>::row(lane, r)) + (j * 16 + tcol(lane)) * cs];
 }
 
 // wave-wide max (xor butterfly; every lane gets the result)
@@ -239,6 +268,22 @@ __device__ __forceinline__ float wave_max(float v)
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) v = fmaxf(v, __shfl_xor(v, o));
     return v;
+}
+
+// Wave-wide max of a NON-NEGATIVE value as a wave-uniform scalar (lands in an SGPR, so a
+// branch on it is uniform): integer max on the float bit pattern (order-preserving for
+// x ≥ 0) through DPP row shifts and row broadcasts (gfx9 DPP), then v_readlane of lane 63.
+// 6 VALU + 1 readlane, no LDS (the xor-butterfly above costs 12 ds_bpermute for a double).
+__device__ __forceinline__ float wave_max_uniform(float x)
+{
+    int v = __float_as_int(x);
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x111, 0xf, 0xf, false));   // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x112, 0xf, 0xf, false));   // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x114, 0xf, 0xf, false));   // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x118, 0xf, 0xf, false));   // row_shr:8
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return __int_as_float(__builtin_amdgcn_readlane(v, 63));
 }
 
 // 1/a: hardware estimate (v_rcp_f64: max rel err 4.6e-8 measured on gfx950, see
