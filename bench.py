@@ -207,8 +207,15 @@ def main():
             sY, sy, sH, sg = K.dubins_structure(N).sizes(K.H_DIAG)
             alg_bytes = (sY + sy + sH + sg + sg + sy) * 8 * bt     # inputs + dz + λ
             achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+            traffic = None
+            if os.path.exists(args.traffic_json):
+                try:
+                    traffic = json.load(open(args.traffic_json)).get(
+                        f"kkt_dubins_N{N}_B{bt}_f64", {}).get("hbm_bytes_per_launch")
+                except Exception:
+                    traffic = None
             roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+                    "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                     "kernel": "kkt_fil_kernel" if N >= 4 else "kkt_staged_kernel",
                     "kernel_ms": kern_ms,
                     "alg_bytes_per_traj": alg_bytes / bt}

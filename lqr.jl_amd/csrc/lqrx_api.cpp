@@ -81,6 +81,36 @@ int validate_dp(const lqrx_dp_desc *d)
 
 } // namespace
 
+namespace lqrx {
+hipError_t scratch_alloc(void **p, size_t bytes, hipStream_t s)
+{
+    static std::mutex mu;
+    static std::map<int, hipMemPool_t> pools;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    hipMemPool_t pool = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        auto it = pools.find(dev);
+        if (it == pools.end()) {
+            hipMemPoolProps props{};
+            props.allocType = hipMemAllocationTypePinned;
+            props.location.type = hipMemLocationTypeDevice;
+            props.location.id = dev;
+            if ((e = hipMemPoolCreate(&pool, &props)) != hipSuccess) return e;
+            uint64_t keep = UINT64_MAX;                     // never trim freed blocks
+            if ((e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep)) != hipSuccess) return e;
+            pools.emplace(dev, pool);
+        } else {
+            pool = it->second;
+        }
+    }
+    return hipMallocFromPoolAsync(p, bytes, pool, s);
+}
+hipError_t scratch_free(void *p, hipStream_t s) { return hipFreeAsync(p, s); }
+} // namespace lqrx
+
 extern "C" {
 
 int lqrx_abi_version(void) { return LQRX_ABI_VERSION; }

@@ -968,12 +968,12 @@ static hipError_t launch_staged(const KktArgs &a, hipStream_t s)
     double *scratch = nullptr;
     const size_t Bp = ((size_t)a.batch + 63) & ~(size_t)63;
     size_t bytes = Bp * (size_t)a.N * SL::SIZE * sizeof(double);
-    hipError_t e = hipMallocAsync((void **)&scratch, bytes, s);
+    hipError_t e = scratch_alloc((void **)&scratch, bytes, s);
     if (e != hipSuccess) return e;
     dim3 grid((unsigned)((a.batch + 63) / 64)), block(64);
     hipLaunchKernelGGL((kkt_staged_kernel<P1M, PSM, P2M, WM, RM>), grid, block, 0, s, a, a.meta, scratch);
     e = hipGetLastError();
-    hipError_t ef = hipFreeAsync(scratch, s);
+    hipError_t ef = scratch_free(scratch, s);
     return e != hipSuccess ? e : ef;
 }
 
@@ -983,12 +983,12 @@ static hipError_t launch_lane(const KktArgs &a, hipStream_t s)
     using SL = Slab<P1M, PSM, P2M>;
     double *scratch = nullptr;
     size_t bytes = (size_t)a.batch * (size_t)a.N * SL::SIZE * sizeof(double);
-    hipError_t e = hipMallocAsync((void **)&scratch, bytes, s);
+    hipError_t e = scratch_alloc((void **)&scratch, bytes, s);
     if (e != hipSuccess) return e;
     dim3 grid((unsigned)((a.batch + 63) / 64)), block(64);
     hipLaunchKernelGGL((kkt_lane_kernel<P1M, PSM, P2M, WM, RM>), grid, block, 0, s, a, scratch);
     e = hipGetLastError();
-    hipError_t ef = hipFreeAsync(scratch, s);
+    hipError_t ef = scratch_free(scratch, s);
     return e != hipSuccess ? e : ef;
 }
 

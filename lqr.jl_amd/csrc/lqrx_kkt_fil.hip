@@ -878,12 +878,12 @@ hipError_t launch(const KktArgs &a, hipStream_t s)
     double *scratch = nullptr;
     const size_t Bp = ((size_t)a.batch + 63) & ~(size_t)63;   // wave-major slab, 64 lanes/wave
     const size_t bytes = Bp * (size_t)a.N * S::SLOT * sizeof(double);
-    hipError_t e = hipMallocAsync((void **)&scratch, bytes, s);
+    hipError_t e = scratch_alloc((void **)&scratch, bytes, s);
     if (e != hipSuccess) return e;
     dim3 grid((unsigned)((a.batch + 63) / 64)), block(64);
     hipLaunchKernelGGL((kkt_fil_kernel<S>), grid, block, 0, s, a, scratch);
     e = hipGetLastError();
-    hipError_t ef = hipFreeAsync(scratch, s);
+    hipError_t ef = scratch_free(scratch, s);
     return e != hipSuccess ? e : ef;
 }
 
