@@ -51,7 +51,7 @@ extern "C" {
  * Buffers (layout 0, element type per dtype):
  *   A  n·n·batch     B  n·m·batch    Q  n·n·batch    R  m·m·batch    Qf n·n·batch
  *      (×(N-1) per trajectory for time-varying fields, see knot_stride_*; the
- *       time-varying path is SURVEY §8(f) rank 1 and currently covers n ≤ 4, m ≤ 4)
+ *       time-varying path is SURVEY §8(f) rank 1; every supported n, m)
  *   x0 n·batch
  *   K  m·n·(N-1)·batch     sol.K[k], k = 1..N-1  (LQRSolution.K)
  *   P  n·n·batch  (p_mode 0: P_1 = solver.P on return, :63)

@@ -34,8 +34,8 @@
 #ifndef LQRX_DP_VAR
 #define LQRX_DP_VAR 0
 #endif
-#ifndef LQRX_DP_DPPMAX
-#define LQRX_DP_DPPMAX 1
+#ifndef LQRX_DP_TVWAIT
+#define LQRX_DP_TVWAIT 0
 #endif
 
 namespace lqrx {
@@ -123,6 +123,15 @@ template <> struct NsTol<float> {
     static constexpr float v = 3e-4f, one_step = 1e-5f; static constexpr int it = 6;
 };
 
+// NaN-propagating magnitude key: the high word of |v| (sign cleared) — order-preserving
+// for magnitudes, and every NaN key exceeds +inf's.  (fmax() would silently DROP a NaN
+// element — IEEE maxNum — and let a diverged iterate pass the convergence test.)
+// key_bound(k) is the largest double with that high word: an upper bound of the magnitude.
+__device__ __forceinline__ int mag_key(double v) { return __double2hiint(v) & 0x7fffffff; }
+__device__ __forceinline__ double key_bound(int k, double) { return __hiloint2double(k, -1); }
+__device__ __forceinline__ int mag_key(float v) { return __float_as_int(v) & 0x7fffffff; }
+__device__ __forceinline__ float key_bound(int k, float) { return __int_as_float(k); }
+
 template <typename T, int MT>
 __device__ __forceinline__ bool ns_refine(typename Tile<T>::acc (&X)[MT][MT],
                                           const typename Tile<T>::acc (&E)[MT][MT],
@@ -136,25 +145,19 @@ __device__ __forceinline__ bool ns_refine(typename Tile<T>::acc (&X)[MT][MT],
 #pragma unroll
             for (int j = 0; j < MT; ++j) R[i][j] = Id[i][j];
         mma_tn<T, MT, MT, MT, true>(R, E, X);                   // R = I − EᵀX
-        T mx = (T)0;
+        int key = 0;
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
             for (int j = 0; j < MT; ++j)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) mx = fmax(mx, fabs(R[i][j][r]));
-#if LQRX_DP_DPPMAX
-        // uniform (SGPR) residual bound: float precision is ample for a threshold test
-        const float rho = (float)(16 * MT) * wave_max_uniform((float)mx);
-        if (rho <= (float)NsTol<T>::v) return true;             // X already at working precision
-        mma_tn<T, MT, MT, MT>(X, X, R);                         // X ← X + XᵀR
-        if (rho <= (float)NsTol<T>::one_step) return true;      // new residual ≤ cond·ρ² ≪ eps
-#else
-        const T rho = (T)(16 * MT) * wave_max(mx);
+                for (int r = 0; r < 4; ++r) key = max(key, mag_key(R[i][j][r]));
+        // uniform (SGPR) residual bound ρ ≥ ‖R‖∞ (NaN if any element is NaN)
+        const T rho = (T)(16 * MT) * key_bound(wave_max_uniform_i(key), (T)0);
         if (rho <= NsTol<T>::v) return true;                    // X already at working precision
+        if (!(rho < (T)1)) return false;                        // no contraction (or NaN): exact sweep
         mma_tn<T, MT, MT, MT>(X, X, R);                         // X ← X + XᵀR
         if (rho <= NsTol<T>::one_step) return true;             // new residual ≤ cond·ρ² ≪ eps
-#endif
     }
     (void)lane;
     return false;
@@ -177,7 +180,7 @@ template <typename T, int NT, int MT> struct DpCfg {
 // DEPTH knots ahead, 64 lanes × KPL coalesced elements per knot, staged through LDS.
 // Dot products are split over the wave: u_i by SU = 64/MP lanes (i = lane % MP), x'_i by
 // SX = 64/NP lanes (i = lane % NP), partial sums combined with xor-shuffles.
-template <typename T, int NT, int MT, int DEPTH>
+template <typename T, int NT, int MT, int DEPTH, bool TV = false>
 __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, int lane)
 {
     using C = DpCfg<T, NT, MT>;
@@ -188,25 +191,31 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
     const int n = a.n, m = a.m, N = a.N;
     const size_t mn = (size_t)m * n;
     const T *__restrict__ Kg = (const T *)a.K + (size_t)b * (size_t)(N - 1) * mn;
-    const T *__restrict__ Ag = (const T *)a.A + (size_t)b * n * n;
-    const T *__restrict__ Bg = (const T *)a.B + (size_t)b * n * m;
+    // time-varying (TV): knot k's A_k, B_k at knot stride sA, sB (0 for a time-invariant field)
+    const int64_t sA = (TV && a.tv_AB) ? (int64_t)n * n : 0, sB = (TV && a.tv_AB) ? (int64_t)n * m : 0;
+    const T *__restrict__ Ag = (const T *)a.A + (size_t)b * n * n * (TV && a.tv_AB ? N - 1 : 1);
+    const T *__restrict__ Bg = (const T *)a.B + (size_t)b * n * m * (TV && a.tv_AB ? N - 1 : 1);
     T *__restrict__ Xg = (T *)a.X + (size_t)b * (size_t)N * n;
     T *__restrict__ Ug = (T *)a.U + (size_t)b * (size_t)(N - 1) * m;
     T *Ks = lds, *xs = lds + MP * NP, *us = xs + NP;
 
     const int iu = lane % MP, hu = lane / MP;   // u row, column part
     const int ix = lane % NP, hx = lane / NP;   // x row, column part
-    T arow[JX], brow[PX];
+    T arow[JX], brow[PX], arow_n[TV ? JX : 1], brow_n[TV ? PX : 1];
+    auto load_rows = [&](int kk, T *ar, T *br) {   // row ix of A_kk, B_kk (this lane's part)
+        const T *Ak = Ag + (int64_t)(kk - 1) * sA, *Bk = Bg + (int64_t)(kk - 1) * sB;
 #pragma unroll
-    for (int t = 0; t < JX; ++t) {
-        int j = hx * JX + t;
-        arow[t] = (ix < n && j < n) ? Ag[ix + (size_t)j * n] : (T)0;
-    }
+        for (int t = 0; t < JX; ++t) {
+            int j = hx * JX + t;
+            ar[t] = (ix < n && j < n) ? Ak[ix + (size_t)j * n] : (T)0;
+        }
 #pragma unroll
-    for (int t = 0; t < PX; ++t) {
-        int p = hx * PX + t;
-        brow[t] = (ix < n && p < m) ? Bg[ix + (size_t)p * n] : (T)0;
-    }
+        for (int t = 0; t < PX; ++t) {
+            int p = hx * PX + t;
+            br[t] = (ix < n && p < m) ? Bk[ix + (size_t)p * n] : (T)0;
+        }
+    };
+    load_rows(1, arow, brow);
     const T *x0 = (const T *)a.x0 + (size_t)b * n;
     if (lane < NP) xs[lane] = (lane < n) ? x0[lane] : (T)0;
     if (lane < MP) us[lane] = (T)0;
@@ -235,6 +244,9 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
                     if (e < mn) Ks[e] = ring[d][s];
                 }
                 issue(k + DEPTH, ring[d]);
+                if constexpr (TV) {
+                    if (k + 1 <= N - 1) load_rows(k + 1, arow_n, brow_n);   // next knot's rows
+                }
                 __syncthreads();
                 // u_i = −Σ_j K[i][j] x_j   (dynamic_programming.jl:68)
                 T s0 = 0, s1 = 0;
@@ -269,6 +281,12 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
                     xs[lane] = xn;
                     Xg[(size_t)k * n + lane] = xn;
                 }
+                if constexpr (TV) {
+#pragma unroll
+                    for (int t = 0; t < JX; ++t) arow[t] = arow_n[t];
+#pragma unroll
+                    for (int t = 0; t < PX; ++t) brow[t] = brow_n[t];
+                }
                 __syncthreads();
             }
         }
@@ -283,7 +301,11 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
 //                transpose); Q is re-read (L2/MALL-resident, 8 KB/traj) into the P_
 //                accumulators each knot so it holds no registers.
 //   VAR_NOSOLVE / VAR_NOROLL / VAR_NOKSTORE : diagnostic ablations (tools/dp_ablate).
-enum : int { VAR_EXACT = 1, VAR_NOSOLVE = 2, VAR_NOROLL = 4, VAR_NOKSTORE = 8, VAR_SWEEPONLY = 16 };
+//   VAR_TV     : time-varying A_k, B_k, Q_k, R_k (ABI knot strides 1):
+//                knot k-1's A, B, R are loaded into the same registers right after knot k's
+//                last product that reads them (the load hides behind the rest of the knot);
+//                Q_k is loaded from global straight into the P_ accumulators.
+enum : int { VAR_EXACT = 1, VAR_NOSOLVE = 2, VAR_NOROLL = 4, VAR_NOKSTORE = 8, VAR_SWEEPONLY = 16, VAR_TV = 32 };
 
 template <typename T, int NT, int MT, int WAVES, int VAR, bool FULL>
 __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
@@ -292,26 +314,33 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
     using acc = typename Tile<T>::acc;
     constexpr int MP = C::MP, CS = C::CS;
     constexpr bool EXACT = (VAR & VAR_EXACT) != 0;
+    constexpr bool TV = (VAR & VAR_TV) != 0;
     __shared__ T lds[C::LDS_ELEMS];
     // Q (time-invariant, read every knot as the P_ accumulator start) lives in LDS for the
     // horizon: an LDS read per element instead of an L2 round trip per knot
-    __shared__ T qimg[(VAR & VAR_EXACT) ? 1 : C::QIMG];
+    __shared__ T qimg[(EXACT || TV) ? 1 : C::QIMG];
 
     const int lane = threadIdx.x;
     const int64_t b = blockIdx.x;
     if (b >= a.batch) return;
     const int n = a.n, m = a.m, N = a.N;
     const size_t nn = (size_t)n * n, nm = (size_t)n * m, mm = (size_t)m * m;
-    const T *Qg = (const T *)a.Q + b * nn;
+    // per-trajectory bases; time-varying fields hold N-1 knots (knot k at index k-1)
+    const size_t kAB = (TV && a.tv_AB) ? (size_t)(N - 1) : 1, kQR = (TV && a.tv_QR) ? (size_t)(N - 1) : 1;
+    const size_t sA = kAB > 1 ? nn : 0, sB = kAB > 1 ? nm : 0, sQ = kQR > 1 ? nn : 0, sR = kQR > 1 ? mm : 0;
+    const T *Ab = (const T *)a.A + b * nn * kAB, *Bb = (const T *)a.B + b * nm * kAB;
+    const T *Qb = (const T *)a.Q + b * nn * kQR, *Rb = (const T *)a.R + b * mm * kQR;
+    const T *Qg = Qb;
 
     acc At[NT][NT], Bt[NT][MT], Rt[MT][MT], P[NT][NT];
-    tiles_load<T, NT, NT, FULL>(At, (const T *)a.A + b * nn, n, n, n, lane, false);
-    tiles_load<T, NT, MT, FULL>(Bt, (const T *)a.B + b * nm, n, m, n, lane, false);
-    tiles_load<T, MT, MT, FULL>(Rt, (const T *)a.R + b * mm, m, m, m, lane, true);
+    const size_t k0 = TV ? (size_t)(N - 2) : 0;                 // first backward knot k = N-1
+    tiles_load<T, NT, NT, FULL>(At, Ab + k0 * sA, n, n, n, lane, false);
+    tiles_load<T, NT, MT, FULL>(Bt, Bb + k0 * sB, n, m, n, lane, false);
+    tiles_load<T, MT, MT, FULL>(Rt, Rb + k0 * sR, m, m, m, lane, true);
     tiles_load<T, NT, NT, FULL>(P, (const T *)a.Qf + b * nn, n, n, n, lane, false); // :58 P = Qf
     acc Qt[EXACT ? NT : 1][EXACT ? NT : 1];
     if constexpr (EXACT) tiles_load<T, NT, NT, FULL>(Qt, Qg, n, n, n, lane, false);
-    else {
+    else if constexpr (!TV) {
         // zero-padded NP×NP image of Q (padding rows/cols 0, as tiles_load_lower)
         for (int e = lane; e < C::NP * C::NP; e += 64) {
             const int i = e % C::NP, j = e / C::NP;
@@ -348,7 +377,13 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
 #pragma unroll
                 for (int j = 0; j < NT; ++j) Pn[i][j] = Qt[i][j];
         } else {
-            tiles_lower_from_lds<T, NT>(Pn, qimg, C::QCS, lane);         // P_ ← Q (lower tiles)
+            if constexpr (TV) {
+                tiles_load_lower<T, NT, FULL>(Pn, Qb + (size_t)(k - 1) * sQ, n, n, lane);
+#if LQRX_DP_TVWAIT
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+            }
+            else tiles_lower_from_lds<T, NT>(Pn, qimg, C::QCS, lane);   // P_ ← Q (lower tiles)
         }
 #pragma unroll
         for (int i = 0; i < MT; ++i)
@@ -359,6 +394,14 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
         mma_tn<T, NT, MT, NT>(G, Bt, PA);                          // :41 K = B'PA
         if constexpr (EXACT) mma_tn<T, NT, NT, NT>(Pn, At, PA);    // :51 Q + A'PA
         else mma_tn_lower<T, NT, NT>(Pn, At, PA);
+        if constexpr (TV) {
+            // knot k's A, B, R are consumed: bring in knot k-1's (lands during the solve)
+            if (k > 1) {
+                tiles_load<T, NT, NT, FULL>(At, Ab + (size_t)(k - 2) * sA, n, n, n, lane, false);
+                tiles_load<T, NT, MT, FULL>(Bt, Bb + (size_t)(k - 2) * sB, n, m, n, lane, false);
+                tiles_load<T, MT, MT, FULL>(Rt, Rb + (size_t)(k - 2) * sR, m, m, m, lane, true);
+            }
+        }
 
         // :42 chol_solve!(E, K) — potrf 'U' + potrs 'U', as K = E⁻¹G with X ≈ E⁻¹:
         //  * warm start: Newton–Schulz from the previous knot's inverse, all MFMA
@@ -441,12 +484,23 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        dp_rollout<T, NT, MT, 4>(a, b, lds, lane);
+        dp_rollout<T, NT, MT, 4, TV>(a, b, lds, lane);
     }
 }
 
 // ------------------------------------------------------------------ launcher
 template <typename T, int NT, int MT, int WAVES = 2, int VAR = 0>
+static hipError_t launch_dp(const DpArgs &a, hipStream_t s);
+
+// time-varying problems take the VAR_TV variant of the same tile grid
+template <typename T, int NT, int MT, int WAVES = 2, int VAR = 0>
+static hipError_t launch_dp_tv(const DpArgs &a, hipStream_t s)
+{
+    if (a.tv_AB || a.tv_QR) return launch_dp<T, NT, MT, 1, VAR_TV>(a, s);   // 1 wave/SIMD: no spills
+    return launch_dp<T, NT, MT, WAVES, VAR>(a, s);
+}
+
+template <typename T, int NT, int MT, int WAVES, int VAR>
 static hipError_t launch_dp(const DpArgs &a, hipStream_t s)
 {
     dim3 grid((unsigned)a.batch), block(64);
@@ -461,20 +515,19 @@ hipError_t dp_launch(const DpArgs &a, hipStream_t s)
 {
     // n ≤ 4: one lane per trajectory (a 16×16 MFMA tile would be mostly padding)
     if (dp_lane_supported(a.n, a.m)) return dp_lane_launch(a, s);
-    if (a.tv_AB || a.tv_QR) return hipErrorNotSupported;
     // smallest instantiated tile grid that covers (n, m); padding is exact (zero rows /
     // columns, unit diagonal in R), see tiles_load
     const int nt = (a.n + 15) / 16, mt = (a.m + 15) / 16;
     if (a.dtype == 0) {
-        if (nt <= 1 && mt <= 1) return launch_dp<double, 1, 1>(a, s);
-        if (nt <= 2 && mt <= 1) return launch_dp<double, 2, 1, LQRX_DP_WAVES, LQRX_DP_VAR>(a, s);
-        if (nt <= 2 && mt <= 2) return launch_dp<double, 2, 2>(a, s);
-        if (nt <= 4 && mt <= 2) return launch_dp<double, 4, 2, 1>(a, s);   // n ≤ 64: 1 wave/SIMD
+        if (nt <= 1 && mt <= 1) return launch_dp_tv<double, 1, 1>(a, s);
+        if (nt <= 2 && mt <= 1) return launch_dp_tv<double, 2, 1, LQRX_DP_WAVES, LQRX_DP_VAR>(a, s);
+        if (nt <= 2 && mt <= 2) return launch_dp_tv<double, 2, 2>(a, s);
+        if (nt <= 4 && mt <= 2) return launch_dp_tv<double, 4, 2, 1>(a, s);   // n ≤ 64: 1 wave/SIMD
     } else {
-        if (nt <= 1 && mt <= 1) return launch_dp<float, 1, 1>(a, s);
-        if (nt <= 2 && mt <= 1) return launch_dp<float, 2, 1>(a, s);
-        if (nt <= 2 && mt <= 2) return launch_dp<float, 2, 2>(a, s);
-        if (nt <= 4 && mt <= 2) return launch_dp<float, 4, 2, 1>(a, s);    // cfg5: n=64 m=32
+        if (nt <= 1 && mt <= 1) return launch_dp_tv<float, 1, 1>(a, s);
+        if (nt <= 2 && mt <= 1) return launch_dp_tv<float, 2, 1>(a, s);
+        if (nt <= 2 && mt <= 2) return launch_dp_tv<float, 2, 2>(a, s);
+        if (nt <= 4 && mt <= 2) return launch_dp_tv<float, 4, 2, 1>(a, s);    // cfg5: n=64 m=32
     }
     return hipErrorNotSupported;
 }
@@ -482,9 +535,10 @@ hipError_t dp_launch(const DpArgs &a, hipStream_t s)
 bool dp_supported(int dtype, int n, int m, bool tv)
 {
     (void)dtype;
+    (void)tv;
     if (dp_lane_supported(n, m)) return true;
     const int nt = (n + 15) / 16, mt = (m + 15) / 16;
-    return !tv && n >= 1 && m >= 1 && nt <= 4 && mt <= 2;
+    return n >= 1 && m >= 1 && nt <= 4 && mt <= 2;
 }
 
 } // namespace lqrx

@@ -274,16 +274,19 @@ __device__ __forceinline__ float wave_max(float v)
 // branch on it is uniform): integer max on the float bit pattern (order-preserving for
 // x ≥ 0) through DPP row shifts and row broadcasts (gfx9 DPP), then v_readlane of lane 63.
 // 6 VALU + 1 readlane, no LDS (the xor-butterfly above costs 12 ds_bpermute for a double).
-__device__ __forceinline__ float wave_max_uniform(float x)
+__device__ __forceinline__ int wave_max_uniform_i(int v)
 {
-    int v = __float_as_int(x);
     v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x111, 0xf, 0xf, false));   // row_shr:1
     v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x112, 0xf, 0xf, false));   // row_shr:2
     v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x114, 0xf, 0xf, false));   // row_shr:4
     v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x118, 0xf, 0xf, false));   // row_shr:8
     v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
     v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
-    return __int_as_float(__builtin_amdgcn_readlane(v, 63));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ float wave_max_uniform(float x)
+{
+    return __int_as_float(wave_max_uniform_i(__float_as_int(x)));
 }
 
 // 1/a: hardware estimate (v_rcp_f64: max rel err 4.6e-8 measured on gfx950, see

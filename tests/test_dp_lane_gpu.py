@@ -144,12 +144,14 @@ def _tv_batch(lqrx, n, m, N, bt, seed, tv_ab=True, tv_qr=True):
     return b
 
 
-@pytest.mark.parametrize("n,m,tv_ab,tv_qr", [(4, 1, True, True), (3, 2, True, False),
-                                             (4, 4, False, True)])
-def test_time_varying_parity(lqrx, oracle, gpu_ok, n, m, tv_ab, tv_qr):
+@pytest.mark.parametrize("n,m,tv_ab,tv_qr,N,bt", [
+    (4, 1, True, True, 41, 67), (3, 2, True, False, 41, 67), (4, 4, False, True, 41, 67),
+    # the MFMA kernel's VAR_TV variant (n ≥ 5): 1×1, 2×1 (cfg4 shape), padded, 4×2 tiles
+    (6, 3, True, True, 30, 5), (32, 16, True, True, 40, 3), (20, 5, False, True, 25, 4),
+    (17, 3, True, False, 12, 2), (64, 32, True, True, 9, 2)])
+def test_time_varying_parity(lqrx, oracle, gpu_ok, n, m, tv_ab, tv_qr, N, bt):
     from lqrx.dp import to_abi, from_abi
 
-    N, bt = 41, 67
     b = _tv_batch(lqrx, n, m, N, bt, seed=21 + n, tv_ab=tv_ab, tv_qr=tv_qr)
     got = lqrx.solve_batch(b, all_P=True)
     d = {k: to_abi(getattr(b, k)).ravel() for k in ("A", "B", "Q", "R", "Qf")}
