@@ -27,6 +27,7 @@
 #include "lqrx_stage.h"
 #include "lqrx_tile.h"
 #include <type_traits>
+#include <cstdlib>
 
 namespace lqrx {
 namespace fil {
@@ -102,6 +103,47 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void *base)
     // raw buffer (stride 0), full 31-bit range; gfx9 dword-3 format bits
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7fffffff, 0x00020000);
 }
+// the same descriptor as four SGPRs, for the inline-asm DMA below
+typedef uint32_t u4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u4_t make_rsrc4(const void *base)
+{
+    const uint64_t a = (uint64_t)base;
+    u4_t r;
+    r.x = (uint32_t)a;
+    r.y = (uint32_t)(a >> 32) & 0xffffu;
+    r.z = 0x7fffffffu;
+    r.w = 0x00020000u;
+    return r;
+}
+
+// One LDS-DMA instruction (buffer_load_dword{,x3,x4} … lds; M0 = the wave's LDS destination,
+// each lane's piece lands at M0 + lane·slot).  Issued as inline asm ON PURPOSE: the compiler's
+// wait-count pass cannot tell which LDS bytes a DMA writes, so after a DMA issued through the
+// builtin it makes EVERY later LDS read wait for it (vmcnt(0) before the first read of the
+// knot staged two steps earlier) — which defeats the ring's prefetch entirely.  Issued here the
+// DMA is invisible to that pass: completion is tracked by hand (vm_wait<N>, which counts these
+// like any vector-memory op), the "memory" clobber keeps LDS accesses from moving across it,
+// and M0 is restored for the compiler.
+template <int BYTES>
+__device__ __forceinline__ void dma_lds(u4_t r, uint32_t vo, uint32_t so, uint32_t lds)
+{
+    uint32_t keep;
+    if constexpr (BYTES == 16)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, %4 offen lds\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(vo), "s"(lds), "s"(r), "s"(so) : "memory");
+    else if constexpr (BYTES == 12)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx3 %1, %3, %4 offen lds\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(vo), "s"(lds), "s"(r), "s"(so) : "memory");
+    else {
+        static_assert(BYTES == 4, "LDS-DMA piece of 4, 12 or 16 bytes");
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %1, %3, %4 offen lds\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(vo), "s"(lds), "s"(r), "s"(so) : "memory");
+    }
+}
+__device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(size_t)(lptr_t)p; }
 
 // DMA pattern of one packed array for a chunk of L doubles per trajectory: the wave's 64
 // chunks form a dense [t][L] image of `per` pieces per trajectory (16 B pieces when WIDE,
@@ -124,12 +166,11 @@ template <int L, bool WIDE> struct Pat {
             vo[i] = tr * (uint32_t)(s * 8) + e * (uint32_t)unit;
         }
     }
-    __device__ __forceinline__ void issue(rsrc_t r, int64_t off_elems, double *lds) const
+    __device__ __forceinline__ void issue(u4_t r, int64_t off_elems, double *lds) const
     {
-        const uint32_t so = (uint32_t)(off_elems * 8);
+        const uint32_t so = (uint32_t)(off_elems * 8), l0 = lds_addr(lds);
 #pragma unroll
-        for (int i = 0; i < per; ++i)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lptr_t)((char *)lds + i * 64 * unit), unit, vo[i], so, 0, 0);
+        for (int i = 0; i < per; ++i) dma_lds<unit>(r, vo[i], so, l0 + i * 64 * unit);
     }
 };
 
@@ -168,16 +209,13 @@ template <int L> struct PatS {
             voB[i] = tr * sb + 12u * SP::n12 + 4u * e;
         }
     }
-    __device__ __forceinline__ void issue(rsrc_t r, int64_t off_elems, double *lds) const
+    __device__ __forceinline__ void issue(u4_t r, int64_t off_elems, double *lds) const
     {
-        const uint32_t so = (uint32_t)(off_elems * 8);
+        const uint32_t so = (uint32_t)(off_elems * 8), l0 = lds_addr(lds);
 #pragma unroll
-        for (int i = 0; i < SP::n12; ++i)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lptr_t)((char *)lds + i * 64 * 16), 12, voA[i], so, 0, 0);
+        for (int i = 0; i < SP::n12; ++i) dma_lds<12>(r, voA[i], so, l0 + i * 64 * 16);
 #pragma unroll
-        for (int i = 0; i < SP::n4; ++i)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lptr_t)((char *)lds + SP::bytesA + i * 64 * 4), 4, voB[i],
-                                                     so, 0, 0);
+        for (int i = 0; i < SP::n4; ++i) dma_lds<4>(r, voB[i], so, l0 + SP::bytesA + i * 64 * 4);
     }
 };
 // reader of a split image: element j of this lane's chunk
@@ -223,43 +261,49 @@ template <class S> struct Ctx {
     PatS<S::template Ly<I>()> py;
     PatS<S::template LH<I>()> pH;
     PatS<S::template Lg<I>()> pg;
+
+    // interior knot k: the precomputed patterns
+    __device__ __forceinline__ void stage_I(int k, double *buf, bool fwd) const
+    {
+        using O = Off<S>;
+        pY.issue(make_rsrc4(bY), O::Y(k), buf);
+        if (fwd) py.issue(make_rsrc4(by), O::y(k), buf + S::OFF_y / 8);
+        if constexpr (S::GINV) {
+            pH.issue(make_rsrc4(bH), O::H(k), buf + S::OFF_H / 8);
+            pg.issue(make_rsrc4(bg), O::g(k), buf + S::OFF_g / 8);
+        }
+    }
+    // first / last knot (class C): one-off patterns
+    template <class C>
+    __device__ __forceinline__ void stage(const KktArgs &a, int k, double *buf, bool fwd) const
+    {
+        using O = Off<S>;
+        Pat<S::template LY<C>(), S::WIDE_Y> qY;
+        qY.init(a.sY, lane, nlive);
+        qY.issue(make_rsrc4(bY), O::Y(k), buf);
+        if (fwd) {
+            PatS<S::template Ly<C>()> qy;
+            qy.init(a.sy, lane, nlive);
+            qy.issue(make_rsrc4(by), O::y(k), buf + S::OFF_y / 8);
+        }
+        if constexpr (S::GINV) {
+            PatS<S::template LH<C>()> qH;
+            qH.init(a.sH, lane, nlive);
+            qH.issue(make_rsrc4(bH), O::H(k), buf + S::OFF_H / 8);
+            PatS<S::template Lg<C>()> qg;
+            qg.init(a.sg, lane, nlive);
+            qg.issue(make_rsrc4(bg), O::g(k), buf + S::OFF_g / 8);
+        }
+    }
+    // any knot into its ring buffer (stg + (k mod 3)·BUF)
+    __device__ __forceinline__ void stage_any(const KktArgs &a, int k, double *stg, bool fwd) const
+    {
+        double *buf = stg + (k % 3) * S::BUF;
+        if (k == 0) stage<typename S::F>(a, 0, buf, fwd);
+        else if (k == a.N - 1) stage<typename S::L>(a, k, buf, fwd);
+        else stage_I(k, buf, fwd);
+    }
 };
-
-// interior knots: the precomputed patterns of the context
-template <class S>
-__device__ __forceinline__ void stage_I(const Ctx<S> &c, int k, double *buf, bool fwd)
-{
-    using O = Off<S>;
-    c.pY.issue(make_rsrc(c.bY), O::Y(k), buf);
-    if (fwd) c.py.issue(make_rsrc(c.by), O::y(k), buf + S::OFF_y / 8);
-    if constexpr (S::GINV) {
-        c.pH.issue(make_rsrc(c.bH), O::H(k), buf + S::OFF_H / 8);
-        c.pg.issue(make_rsrc(c.bg), O::g(k), buf + S::OFF_g / 8);
-    }
-}
-
-// first / last knot (class C): one-off patterns
-template <class S, class C>
-__device__ __forceinline__ void stage(const KktArgs &a, const Ctx<S> &c, int k, double *buf, bool fwd)
-{
-    using O = Off<S>;
-    Pat<S::template LY<C>(), S::WIDE_Y> pY;
-    pY.init(a.sY, c.lane, c.nlive);
-    pY.issue(make_rsrc(c.bY), O::Y(k), buf);
-    if (fwd) {
-        PatS<S::template Ly<C>()> py;
-        py.init(a.sy, c.lane, c.nlive);
-        py.issue(make_rsrc(c.by), O::y(k), buf + S::OFF_y / 8);
-    }
-    if constexpr (S::GINV) {
-        PatS<S::template LH<C>()> pH;
-        pH.init(a.sH, c.lane, c.nlive);
-        pH.issue(make_rsrc(c.bH), O::H(k), buf + S::OFF_H / 8);
-        PatS<S::template Lg<C>()> pg;
-        pg.init(a.sg, c.lane, c.nlive);
-        pg.issue(make_rsrc(c.bg), O::g(k), buf + S::OFF_g / 8);
-    }
-}
 
 typedef unsigned int u2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void bstore(double v, rsrc_t r, uint32_t vo, uint32_t so)
@@ -626,6 +670,61 @@ __device__ __forceinline__ void slab_load(SlabV<C> &v, const Ctx<S> &c, int k)
     for (int i = 0; i < p2; ++i) v.la[i] = at(f++);
 }
 
+// Backward slab ring: interior / last knots' slab chunks come back by LDS-DMA (16-B pieces;
+// the wave-major chunk [field][64 lanes] of a knot is contiguous, so piece p = 16·p bytes and
+// the LDS image is the same [field][64] layout), issued two steps before use like the knot
+// data.  Register loads (slab_load) would be tracked by the compiler, whose wait for them also
+// drains every DMA issued after them (it does not count the asm DMA), i.e. one-step prefetch.
+template <class S> constexpr int slab_ring_fields()
+{
+    return S::template slab<typename S::I>() > S::template slab<typename S::L>() ? S::template slab<typename S::I>()
+                                                                                 : S::template slab<typename S::L>();
+}
+template <class S> constexpr int slab_dma_instrs() { return (slab_ring_fields<S>() + 1) / 2; }
+template <class S> constexpr int SLB = slab_dma_instrs<S>() * 128;     // doubles per ring slot
+
+template <class S>
+__device__ __forceinline__ void stage_slab(const Ctx<S> &c, int k, double *ring)
+{
+    const u4_t r = make_rsrc4(c.bS);
+    const uint32_t so = slab_so<S>(k, 0), l0 = lds_addr(ring + (k % 3) * SLB<S>);
+#pragma unroll
+    for (int i = 0; i < slab_dma_instrs<S>(); ++i) dma_lds<16>(r, 2u * c.vS, so + 1024u * i, l0 + 1024u * i);
+}
+
+template <class S, class C>
+__device__ __forceinline__ void slab_read(SlabV<C> &v, const Ctx<S> &c, int k, const double *ring)
+{
+    static_assert(S::template slab<C>() <= slab_ring_fields<S>(), "slab chunk fits a ring slot");
+    constexpr int p1 = C::P1, ps = C::PS, p2 = C::P2;
+    const double *b = ring + (k % 3) * SLB<S> + c.lane;
+    int f = 0;
+#pragma unroll
+    for (int i = 0; i < ps; ++i)
+#pragma unroll
+        for (int j = i; j < ps; ++j) v.Bm[i][j] = b[64 * f++];
+#pragma unroll
+    for (int i = 0; i < p2; ++i)
+#pragma unroll
+        for (int j = i; j < p2; ++j) v.Cm[i][j] = b[64 * f++];
+#pragma unroll
+    for (int i = 0; i < p1; ++i)
+#pragma unroll
+        for (int j = 0; j < ps; ++j) v.D[i][j] = b[64 * f++];
+#pragma unroll
+    for (int i = 0; i < ps; ++i)
+#pragma unroll
+        for (int j = 0; j < p2; ++j) v.E[i][j] = b[64 * f++];
+#pragma unroll
+    for (int i = 0; i < p1; ++i)
+#pragma unroll
+        for (int j = 0; j < p2; ++j) v.F[i][j] = b[64 * f++];
+#pragma unroll
+    for (int i = 0; i < ps; ++i) v.mu[i] = b[64 * f++];
+#pragma unroll
+    for (int i = 0; i < p2; ++i) v.la[i] = b[64 * f++];
+}
+
 // final multipliers of knot k (class C) from its slab and knot k+1's (class Cn, final μ, λ
 // already in vn.mu / vn.la).  backward_substitution!, cholesky_solve.jl:119-143.
 template <class C, class Cn>
@@ -741,6 +840,7 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     using I = typename S::I;
     using L = typename S::L;
     __shared__ double stg[3 * S::BUF];
+    __shared__ double sl[3 * SLB<S>];
     const int N = a.N;                                          // ≥ 4 (host-checked)
     const int64_t t0 = (int64_t)blockIdx.x * 64;
     Ctx<S> c;
@@ -764,9 +864,9 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     int info = 0;
 
     // ---------------- forward ----------------
-    stage<S, F>(a, c, 0, stg, true);
-    stage_I<S>(c, 1, stg + S::BUF, true);
-    stage_I<S>(c, 2, stg + 2 * S::BUF, true);               // N ≥ 4: knot 2 is interior
+    c.stage_any(a, 0, stg, true);
+    c.stage_I(1, stg + S::BUF, true);
+    c.stage_I(2, stg + 2 * S::BUF, true);               // N ≥ 4: knot 2 is interior
     vm_wait<S::template Dmin<I>() * 2>();
     Shur<F> s0;
     double y0[Z(F::PS + F::P2)];
@@ -789,20 +889,17 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     Shur<I> sI;
     double yI[Z(I::PS + I::P2)];
     fwd_wait<S, F, I, true>();
-    if (3 == N - 1) stage<S, L>(a, c, 3, stg, true);
-    else stage_I<S>(c, 3, stg, true);
+    c.stage_any(a, 3, stg, true);
     fwd_step<S, F, I, I, true>(a, c, 0, stg, s0, y0, sI, yI, cy, info);
     for (int k = 1; k <= N - 3; ++k) {
         Shur<I> sn;
         double yn[Z(I::PS + I::P2)];
-        double *rb = stg + ((k + 3) % 3) * S::BUF;
         if (k == N - 3) {
             fwd_wait<S, I, L, false>();                         // (no restage: k+3 = N)
             fwd_step<S, I, I, L>(a, c, k, stg, sI, yI, sn, yn, cy, info);
         } else {
             fwd_wait<S, I, I, false>();
-            if (k + 3 == N - 1) stage<S, L>(a, c, k + 3, rb, true);
-            else stage_I<S>(c, k + 3, rb, true);
+            c.stage_any(a, k + 3, stg, true);
             fwd_step<S, I, I, I>(a, c, k, stg, sI, yI, sn, yn, cy, info);
         }
         sI = sn;
@@ -819,36 +916,53 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     }
 
     // ---------------- backward + primal recovery ----------------
-    // step j finalises μ_j, λ_j and recovers δz_{j+1} from staged knot j+1; the DMA issued
-    // at step j is knot j-1's (used at step j-2)
-    vm_wait<0>();
-    stage<S, L>(a, c, N - 1, stg + ((N - 1) % 3) * S::BUF, false);
+    // Step j finalises μ_j, λ_j (slab j) and recovers δz_{j+1} (staged knot j+1); it issues
+    // the slab of j-2 and knot j-1, both consumed two steps later.  Stores per step: λ/μ of
+    // knot j and δz of knot j+1; all of them count in vmcnt like the DMA (lower bounds below).
+    constexpr int nS = slab_dma_instrs<S>(), nK = S::template Dbwd<I>();
+    constexpr int stL = L::PS + L::P2, stI = I::PS + I::P2;             // store_lam
+    vm_wait<0>();                                               // forward slab stores landed
+    stage_slab<S>(c, N - 1, sl);
+    stage_slab<S>(c, N - 2, sl);
+    c.stage_any(a, N - 1, stg, false);
+    vm_wait<nS + S::template Dbwd<L>()>();                      // slab N-1
     SlabV<L> vL;
-    slab_load<S, L>(vL, c, N - 1);
+    slab_read<S, L>(vL, c, N - 1, sl);
+    stage_slab<S>(c, N - 3, sl);                                // N-3 ≥ 1: interior
+    c.stage_I(N - 2, stg + ((N - 2) % 3) * S::BUF, false);
     SlabV<NoCls> vnone;
-    bwd_knot<L, NoCls>(vL, vnone);                              // step N-1 (no primal yet)
+    bwd_knot<L, NoCls>(vL, vnone);                              // step N-1 (no primal)
     store_lam<S, L>(c, N - 1, vL);
-    stage_I<S>(c, N - 2, stg + ((N - 2) % 3) * S::BUF, false);
-
-    SlabV<I> vI, vpre;
-    slab_load<S, I>(vI, c, N - 2);
-    slab_load<S, I>(vpre, c, N - 3);                            // knot N-3 ≥ 1 is interior
+    // step N-2: slab N-2, knot N-1 (issued before step N-1's DMA and stores)
+    vm_wait<nS + nK + stL>();
+    SlabV<I> vI;
+    slab_read<S, I>(vI, c, N - 2, sl);
+    if (N - 4 >= 1) stage_slab<S>(c, N - 4, sl);
+    c.stage_I(N - 3, stg + ((N - 3) % 3) * S::BUF, false);
+    bwd_knot<I, L>(vI, vL);
     {
-        // step N-2: multipliers of N-2, primal of N-1 (needs knot N-1 staged)
-        vm_wait<0>();
-        stage_I<S>(c, N - 3, stg + ((N - 3) % 3) * S::BUF, false);
-        bwd_knot<I, L>(vI, vL);
         Buf<S> b{stg + ((N - 1) % 3) * S::BUF};
         primal_knot<S, L, L::P1>(c, N - 1, vL, vI.la, b);
-        store_lam<S, I>(c, N - 2, vI);
     }
+    store_lam<S, I>(c, N - 2, vI);
     for (int j = N - 3; j >= 1; --j) {
-        SlabV<I> v = vpre;
-        if (j - 1 >= 1) slab_load<S, I>(vpre, c, j - 1);         // next step's slab
-        // knot j+1 landed: after its DMA came (at least) the DMA of knot j
-        vm_wait<S::template Dbwd<I>()>();
-        if (j - 1 >= 1) stage_I<S>(c, j - 1, stg + ((j - 1) % 3) * S::BUF, false);
-        else stage<S, F>(a, c, 0, stg, false);
+        // slab j, knot j+1 were issued at step j+2; after them: stores of step j+2, the DMA
+        // of step j+1 (knot j; slab j-1 only when j ≥ 2) and its stores.
+        // Lower bounds: the slab of step N-2 is not counted at j = N-3.
+        constexpr int stp = stI + I::W;                         // stores of an interior step
+        if (j == N - 3) vm_wait<stL + nK + L::W + stI>();
+        else if (j == N - 4) {
+            if (j >= 2) vm_wait<L::W + stI + nS + nK + stp>();
+            else vm_wait<L::W + stI + nK + stp>();
+        } else {
+            if (j >= 2) vm_wait<stp + nS + nK + stp>();
+            else vm_wait<stp + nK + stp>();
+        }
+        SlabV<I> v;
+        slab_read<S, I>(v, c, j, sl);
+        if (j - 2 >= 1) stage_slab<S>(c, j - 2, sl);
+        if (j - 1 >= 1) c.stage_I(j - 1, stg + ((j - 1) % 3) * S::BUF, false);
+        else c.stage_any(a, 0, stg, false);
         bwd_knot<I, I>(v, vI);
         Buf<S> b{stg + ((j + 1) % 3) * S::BUF};
         primal_knot<S, I, I::P1>(c, j + 1, vI, v.la, b);
@@ -856,20 +970,305 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
         vI = v;
     }
     {
-        // step 0: multipliers of knot 0, primal of knot 1, then primal of knot 0
+        // step 0: multipliers of knot 0 (its class-F slab is the wider one: a register load,
+        // once), primal of knot 1, then primal of knot 0
         SlabV<F> v0;
         slab_load<S, F>(v0, c, 0);
-        vm_wait<S::template Dbwd<F>()>();                        // knot 1 landed (DMA of 0 after it)
+        vm_wait<0>();
         bwd_knot<F, I>(v0, vI);
         Buf<S> b1{stg + (1 % 3) * S::BUF};
         primal_knot<S, I, I::P1>(c, 1, vI, v0.la, b1);
         store_lam<S, F>(c, 0, v0);
-        vm_wait<0>();
         Buf<S> b0{stg};
         double none[1] = {0.0};
         primal_knot<S, F, 0>(c, 0, v0, none, b0);
     }
     if (a.info && c.live) a.info[t0 + c.lane] = info;
+}
+
+// ------------------------------------------------------------------ warp-specialised variant
+// The single-wave kernel above runs every knot's whole instruction stream on ONE wave, and a
+// lone wave issues fp64 VALU work at ~1/8–1/10 per cycle (profiles/r01/mfma_probe.txt: 32.5
+// TF/s at 1 wave/SIMD) — with B = 16384 there is one wave per CU, so the kernel is bound by
+// that serial stream, not by HBM.  Here a workgroup of TWO waves shares the same 64
+// trajectories (same lane = same trajectory) and splits each knot's work between two SIMDs:
+//   producer wave (P): LDS-DMA staging, Schur pieces of knot s (shur!/copy_shur!) → LDS ring;
+//                      backward: primal recovery δz (calc_residual!/calc_primals!)
+//   chain wave    (C): block Cholesky + forward substitution (the serial recurrence) and the
+//                      factor slab; backward: backward substitution → final μ, λ → LDS ring
+// in lock-step (one s_barrier per step):
+//   forward  step s = 0..N+1: P builds Shur(s) [s ≤ N-1]; C factors knot s-2 from the ring
+//   backward step t = 0..N+1: C finalises knot N-1-t [t ≤ N-1]; P recovers δz of knot N+1-t [t ≥ 2]
+// Rings of three slots make every read one step behind its write.
+template <class S> struct WsCfg {
+    using F = typename S::F;
+    using I = typename S::I;
+    using L = typename S::L;
+    template <class C> static constexpr int rec() { return tri(C::R) + C::R + C::PS + C::P2; }
+    static constexpr int SH = S::template mx3<rec<F>(), rec<I>(), rec<L>()>();   // Schur record (doubles)
+    static constexpr int FM = S::template mx3<F::PS + F::P2, I::PS + I::P2, L::PS + L::P2>(); // μ, λ record
+};
+
+template <class C, int L>
+__device__ __forceinline__ void shur_put(const Shur<C> &s, const SImg<L> &y, double *rec)
+{
+    int f = 0;
+#pragma unroll
+    for (int i = 0; i < C::R; ++i)
+#pragma unroll
+        for (int j = i; j < C::R; ++j) rec[f++] = s.S[i][j];
+#pragma unroll
+    for (int i = 0; i < C::R; ++i) rec[f++] = s.r[i];
+#pragma unroll
+    for (int i = 0; i < C::PS + C::P2; ++i) rec[f++] = y[i];
+}
+template <class C>
+__device__ __forceinline__ void shur_get(Shur<C> &s, double (&y)[Z(C::PS + C::P2)], const double *rec)
+{
+    int f = 0;
+#pragma unroll
+    for (int i = 0; i < C::R; ++i)
+#pragma unroll
+        for (int j = i; j < C::R; ++j) s.S[i][j] = rec[f++];
+#pragma unroll
+    for (int i = 0; i < C::R; ++i) s.r[i] = rec[f++];
+#pragma unroll
+    for (int i = 0; i < C::PS + C::P2; ++i) y[i] = rec[f++];
+}
+
+template <class S>
+__global__ __launch_bounds__(128) void kkt_fil_ws_kernel(const KktArgs a, double *__restrict__ scratch)
+{
+    using F = typename S::F;
+    using I = typename S::I;
+    using L = typename S::L;
+    using W = WsCfg<S>;
+    __shared__ double stg[3 * S::BUF];
+    __shared__ double shr[3 * 64 * W::SH];
+    __shared__ double fml[3 * 64 * W::FM];
+    const int N = a.N;                                          // ≥ 4 (host-checked)
+    const int64_t t0 = (int64_t)blockIdx.x * 64;
+    const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
+    Ctx<S> c;
+    c.lane = threadIdx.x & 63;
+    c.nlive = (int)(a.batch - t0 < 64 ? a.batch - t0 : 64);
+    c.live = c.lane < c.nlive;
+    c.bY = a.Y + t0 * a.sY;
+    c.by = a.y + t0 * a.sy;
+    c.bH = a.H + t0 * a.sH;
+    c.bg = a.g + t0 * a.sg;
+    c.bdz = a.dz + t0 * a.sg;
+    c.blam = a.lam + t0 * a.sl;
+    c.bS = scratch + (int64_t)blockIdx.x * N * S::SLOT * 64;
+    c.vS = 8u * c.lane;
+    c.vdz = (uint32_t)(c.lane * a.sg * 8);
+    c.vlam = (uint32_t)(c.lane * a.sl * 8);
+    if (producer) {
+        c.pY.init(a.sY, c.lane, c.nlive);
+        c.py.init(a.sy, c.lane, c.nlive);
+        c.pH.init(a.sH, c.lane, c.nlive);
+        c.pg.init(a.sg, c.lane, c.nlive);
+    }
+    auto shr_rec = [&](int k) { return shr + ((k % 3) * 64 + c.lane) * W::SH; };
+    auto fm_rec = [&](int k) { return fml + ((k % 3) * 64 + c.lane) * W::FM; };
+    int info = 0;
+
+    // ---------------- forward ----------------
+    if (producer) {
+        c.stage_any(a, 0, stg, true);
+        c.stage_any(a, 1, stg, true);
+    }
+    Carry<S> cy;
+#pragma unroll
+    for (int i = 0; i < S::NX; ++i) {
+        cy.lprev[i] = 0.0;
+#pragma unroll
+        for (int j = 0; j < S::NX; ++j) cy.Ua[i][j] = 0.0;
+    }
+    for (int s = 0; s <= N + 1; ++s) {
+        if (producer) {
+            if (s <= N - 1) {
+                // knot s landed: after its DMA (step s-2) came only the DMA of knot s+1
+                if (s + 1 <= N - 1) {
+                    if (s + 1 == N - 1) vm_wait<S::template Dmin<L>()>();
+                    else vm_wait<S::template Dmin<I>()>();
+                } else {
+                    vm_wait<0>();
+                }
+                if (s + 2 <= N - 1) c.stage_any(a, s + 2, stg, true);
+                Buf<S> b{stg + (s % 3) * S::BUF};
+                double *rec = shr_rec(s);
+                bool ok;
+                if (s == 0) {
+                    Shur<F> sh;
+                    ok = compute_shur<S, F>(sh, b.Y(c.lane, S::template LY<F>()), b.template H<S::template LH<F>()>(c.lane),
+                                            b.template g<S::template Lg<F>()>(c.lane));
+                    shur_put<F>(sh, b.template y<S::template Ly<F>()>(c.lane), rec);
+                } else if (s == N - 1) {
+                    Shur<L> sh;
+                    ok = compute_shur<S, L>(sh, b.Y(c.lane, S::template LY<L>()), b.template H<S::template LH<L>()>(c.lane),
+                                            b.template g<S::template Lg<L>()>(c.lane));
+                    shur_put<L>(sh, b.template y<S::template Ly<L>()>(c.lane), rec);
+                } else {
+                    Shur<I> sh;
+                    ok = compute_shur<S, I>(sh, b.Y(c.lane, S::template LY<I>()), b.template H<S::template LH<I>()>(c.lane),
+                                            b.template g<S::template Lg<I>()>(c.lane));
+                    shur_put<I>(sh, b.template y<S::template Ly<I>()>(c.lane), rec);
+                }
+                if (!ok && info == 0) info = -(s + 1);
+            }
+        } else if (s >= 2) {
+            const int k = s - 2;                                // factor knot k with Shur(k), Shur(k+1)
+            if (k == 0) {
+                Shur<F> sc; Shur<I> sn;
+                double yc[Z(F::PS + F::P2)], yn[Z(I::PS + I::P2)];
+                shur_get<F>(sc, yc, shr_rec(0));
+                shur_get<I>(sn, yn, shr_rec(1));
+                factor_knot<S, F, I>(0, sc, yc, sn, cy, c, info);
+            } else if (k == N - 1) {
+                Shur<L> sc; Shur<NoCls> sn;
+                double yc[Z(L::PS + L::P2)];
+                shur_get<L>(sc, yc, shr_rec(k));
+                factor_knot<S, L, NoCls>(k, sc, yc, sn, cy, c, info);
+            } else if (k == N - 2) {
+                Shur<I> sc; Shur<L> sn;
+                double yc[Z(I::PS + I::P2)], yn[Z(L::PS + L::P2)];
+                shur_get<I>(sc, yc, shr_rec(k));
+                shur_get<L>(sn, yn, shr_rec(k + 1));
+                factor_knot<S, I, L>(k, sc, yc, sn, cy, c, info);
+            } else {
+                Shur<I> sc, sn;
+                double yc[Z(I::PS + I::P2)], yn[Z(I::PS + I::P2)];
+                shur_get<I>(sc, yc, shr_rec(k));
+                shur_get<I>(sn, yn, shr_rec(k + 1));
+                factor_knot<S, I, I>(k, sc, yc, sn, cy, c, info);
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---------------- backward + primal recovery ----------------
+    // (the chain wave's slab stores are its own: same-lane loads see them in order)
+    SlabV<I> vI, vpre;
+    SlabV<L> vL;
+    SlabV<F> v0;
+    auto fm_put = [&](int k, const double *mu, int ps, const double *la, int p2) {
+        double *r = fm_rec(k);
+        for (int i = 0; i < ps; ++i) r[i] = mu[i];
+        for (int i = 0; i < p2; ++i) r[ps + i] = la[i];
+    };
+    if (producer) {
+        vm_wait<0>();
+        c.stage_any(a, N - 1, stg, false);
+        c.stage_any(a, N - 2, stg, false);
+    } else {
+        vm_wait<0>();
+        slab_load<S, L>(vL, c, N - 1);
+        slab_load<S, I>(vI, c, N - 2);
+    }
+    for (int t = 0; t <= N + 1; ++t) {
+        if (!producer) {
+            const int j = N - 1 - t;
+            if (j == N - 1) {
+                SlabV<NoCls> vn;
+                bwd_knot<L, NoCls>(vL, vn);
+                store_lam<S, L>(c, j, vL);
+#pragma unroll
+                for (int i = 0; i < L::PS; ++i) fm_rec(j)[i] = vL.mu[i];
+            } else if (j == N - 2) {
+                if (N - 3 >= 1) slab_load<S, I>(vpre, c, N - 3);
+                bwd_knot<I, L>(vI, vL);
+                store_lam<S, I>(c, j, vI);
+#pragma unroll
+                for (int i = 0; i < I::PS; ++i) fm_rec(j)[i] = vI.mu[i];
+#pragma unroll
+                for (int i = 0; i < I::P2; ++i) fm_rec(j)[I::PS + i] = vI.la[i];
+            } else if (j >= 1) {
+                SlabV<I> v = vpre;
+                if (j - 1 >= 1) slab_load<S, I>(vpre, c, j - 1);
+                bwd_knot<I, I>(v, vI);
+                store_lam<S, I>(c, j, v);
+#pragma unroll
+                for (int i = 0; i < I::PS; ++i) fm_rec(j)[i] = v.mu[i];
+#pragma unroll
+                for (int i = 0; i < I::P2; ++i) fm_rec(j)[I::PS + i] = v.la[i];
+                vI = v;
+            } else if (j == 0) {
+                slab_load<S, F>(v0, c, 0);
+                bwd_knot<F, I>(v0, vI);
+                store_lam<S, F>(c, 0, v0);
+#pragma unroll
+                for (int i = 0; i < F::PS; ++i) fm_rec(0)[i] = v0.mu[i];
+#pragma unroll
+                for (int i = 0; i < F::P2; ++i) fm_rec(0)[F::PS + i] = v0.la[i];
+            }
+        } else if (t >= 2) {
+            const int q = N + 1 - t;                            // δz of knot q
+            // knot q landed: after its DMA (step t-2 or the prologue) came the DMA of knot q-1
+            // (≥ Dbwd of its class) — or nothing at q = 0
+            if (q >= 2) vm_wait<S::template Dbwd<I>()>();
+            else if (q == 1) vm_wait<S::template Dbwd<F>()>();
+            else vm_wait<0>();
+            if (q - 2 >= 0) c.stage_any(a, q - 2, stg, false);
+            Buf<S> b{stg + (q % 3) * S::BUF};
+            const double *rq = fm_rec(q);
+            if (q == N - 1) {
+                SlabV<L> v;
+#pragma unroll
+                for (int i = 0; i < L::PS; ++i) v.mu[i] = rq[i];
+                double lp[Z(L::P1)];
+#pragma unroll
+                for (int i = 0; i < L::P1; ++i) lp[i] = fm_rec(q - 1)[I::PS + i];
+                primal_knot<S, L, L::P1>(c, q, v, lp, b);
+            } else if (q >= 1) {
+                SlabV<I> v;
+#pragma unroll
+                for (int i = 0; i < I::PS; ++i) v.mu[i] = rq[i];
+#pragma unroll
+                for (int i = 0; i < I::P2; ++i) v.la[i] = rq[I::PS + i];
+                double lp[Z(I::P1)];
+                const int ps_prev = (q - 1 == 0) ? F::PS : I::PS;
+#pragma unroll
+                for (int i = 0; i < I::P1; ++i) lp[i] = fm_rec(q - 1)[ps_prev + i];
+                primal_knot<S, I, I::P1>(c, q, v, lp, b);
+            } else {
+                SlabV<F> v;
+#pragma unroll
+                for (int i = 0; i < F::PS; ++i) v.mu[i] = rq[i];
+#pragma unroll
+                for (int i = 0; i < F::P2; ++i) v.la[i] = rq[F::PS + i];
+                double none[1] = {0.0};
+                primal_knot<S, F, 0>(c, 0, v, none, b);
+            }
+        }
+        __syncthreads();
+    }
+    (void)fm_put;
+    // info: the producer saw H failures (−(k+1)), the chain wave Schur-pivot failures (k+1);
+    // H failures take precedence, as in the oracle (all H_k are factored before the Schur
+    // complement is formed)
+    __shared__ int infos[2][64];
+    infos[producer ? 0 : 1][c.lane] = info;
+    __syncthreads();
+    if (producer && a.info && c.live) {
+        const int ip = infos[0][c.lane], ic = infos[1][c.lane];
+        a.info[t0 + c.lane] = ip != 0 ? ip : ic;
+    }
+}
+
+template <class S>
+hipError_t launch_ws(const KktArgs &a, hipStream_t s)
+{
+    double *scratch = nullptr;
+    const size_t Bp = ((size_t)a.batch + 63) & ~(size_t)63;
+    const size_t bytes = Bp * (size_t)a.N * S::SLOT * sizeof(double);
+    hipError_t e = scratch_alloc((void **)&scratch, bytes, s);
+    if (e != hipSuccess) return e;
+    dim3 grid((unsigned)((a.batch + 63) / 64)), block(128);
+    hipLaunchKernelGGL((kkt_fil_ws_kernel<S>), grid, block, 0, s, a, scratch);
+    e = hipGetLastError();
+    hipError_t ef = scratch_free(scratch, s);
+    return e != hipSuccess ? e : ef;
 }
 
 template <class S>
@@ -887,6 +1286,17 @@ hipError_t launch(const KktArgs &a, hipStream_t s)
     return e != hipSuccess ? e : ef;
 }
 
+// Explicit instantiations: clang drops the host stub of an implicitly instantiated kernel
+// template that is launched from both arms of a conditional alongside a second kernel.
+#define LQRX_FIL_INST(NX, M, A0, AK, AN)                                                                 \
+    template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, true>>(const KktArgs, double *__restrict__);  \
+    template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, false, true>>(const KktArgs, double *__restrict__); \
+    template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, false>>(const KktArgs, double *__restrict__); \
+    template __global__ void kkt_fil_ws_kernel<Shape<NX, M, A0, AK, AN, true, true>>(const KktArgs, double *__restrict__); \
+    template __global__ void kkt_fil_ws_kernel<Shape<NX, M, A0, AK, AN, true, false>>(const KktArgs, double *__restrict__);
+LQRX_FIL_INST(3, 2, 3, 0, 3)
+#undef LQRX_FIL_INST
+
 } // namespace fil
 
 // Dispatch: the FIL kernel serves a structure iff every knot matches one of the
@@ -901,11 +1311,17 @@ bool kkt_fil_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const
     for (int k = 1; k < N - 1; ++k)
         if (n1[k] != nx || n2[k] != nx || p[k] != PK || w[k] != nx + m) return false;
     const bool diag = a.h_mode == 2, ginv = a.ginv != 0;
+    // the warp-specialised variant is opt-in (LQRX_KKT_WS=1): measured slower on cfg3
+    // (0.53 vs 0.45 ms)
+    static const bool ws = [] { const char *v = std::getenv("LQRX_KKT_WS"); return v && *v == '1'; }();
 #define LQRX_FIL(NX, M, A0, AK, AN)                                                                      \
     if (nx == NX && m == M && P0 == A0 && PK == AK && PN == AN) {                                        \
-        if (diag && ginv) *err = fil::launch<fil::Shape<NX, M, A0, AK, AN, true, true>>(a, s);          \
-        else if (ginv) *err = fil::launch<fil::Shape<NX, M, A0, AK, AN, false, true>>(a, s);            \
-        else *err = fil::launch<fil::Shape<NX, M, A0, AK, AN, true, false>>(a, s);                      \
+        using SD = fil::Shape<NX, M, A0, AK, AN, true, true>;                                            \
+        using SH = fil::Shape<NX, M, A0, AK, AN, false, true>;                                           \
+        using SS = fil::Shape<NX, M, A0, AK, AN, true, false>;                                           \
+        if (diag && ginv) *err = ws ? fil::launch_ws<SD>(a, s) : fil::launch<SD>(a, s);                  \
+        else if (ginv) *err = fil::launch<SH>(a, s);   /* dense H: the WS rings exceed LDS */          \
+        else *err = ws ? fil::launch_ws<SS>(a, s) : fil::launch<SS>(a, s);                               \
         return true;                                                                                     \
     }
     LQRX_FIL(3, 2, 3, 0, 3)   // Dubins car (BASELINE cfg3), test/dubins.jl
