@@ -27,7 +27,6 @@
 #include "lqrx_stage.h"
 #include "lqrx_tile.h"
 #include <type_traits>
-#include <cstdlib>
 
 namespace lqrx {
 namespace fil {
@@ -986,291 +985,6 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     if (a.info && c.live) a.info[t0 + c.lane] = info;
 }
 
-// ------------------------------------------------------------------ warp-specialised variant
-// The single-wave kernel above runs every knot's whole instruction stream on ONE wave, and a
-// lone wave issues fp64 VALU work at ~1/8–1/10 per cycle (profiles/r01/mfma_probe.txt: 32.5
-// TF/s at 1 wave/SIMD) — with B = 16384 there is one wave per CU, so the kernel is bound by
-// that serial stream, not by HBM.  Here a workgroup of TWO waves shares the same 64
-// trajectories (same lane = same trajectory) and splits each knot's work between two SIMDs:
-//   producer wave (P): LDS-DMA staging, Schur pieces of knot s (shur!/copy_shur!) → LDS ring;
-//                      backward: primal recovery δz (calc_residual!/calc_primals!)
-//   chain wave    (C): block Cholesky + forward substitution (the serial recurrence) and the
-//                      factor slab; backward: backward substitution → final μ, λ → LDS ring
-// in lock-step (one s_barrier per step):
-//   forward  step s = 0..N+1: P builds Shur(s) [s ≤ N-1]; C factors knot s-2 from the ring
-//   backward step t = 0..N+1: C finalises knot N-1-t [t ≤ N-1]; P recovers δz of knot N+1-t [t ≥ 2]
-// Rings of three slots make every read one step behind its write.
-template <class S> struct WsCfg {
-    using F = typename S::F;
-    using I = typename S::I;
-    using L = typename S::L;
-    template <class C> static constexpr int rec() { return tri(C::R) + C::R + C::PS + C::P2; }
-    static constexpr int SH = S::template mx3<rec<F>(), rec<I>(), rec<L>()>();   // Schur record (doubles)
-    static constexpr int FM = S::template mx3<F::PS + F::P2, I::PS + I::P2, L::PS + L::P2>(); // μ, λ record
-};
-
-template <class C, int L>
-__device__ __forceinline__ void shur_put(const Shur<C> &s, const SImg<L> &y, double *rec)
-{
-    int f = 0;
-#pragma unroll
-    for (int i = 0; i < C::R; ++i)
-#pragma unroll
-        for (int j = i; j < C::R; ++j) rec[f++] = s.S[i][j];
-#pragma unroll
-    for (int i = 0; i < C::R; ++i) rec[f++] = s.r[i];
-#pragma unroll
-    for (int i = 0; i < C::PS + C::P2; ++i) rec[f++] = y[i];
-}
-template <class C>
-__device__ __forceinline__ void shur_get(Shur<C> &s, double (&y)[Z(C::PS + C::P2)], const double *rec)
-{
-    int f = 0;
-#pragma unroll
-    for (int i = 0; i < C::R; ++i)
-#pragma unroll
-        for (int j = i; j < C::R; ++j) s.S[i][j] = rec[f++];
-#pragma unroll
-    for (int i = 0; i < C::R; ++i) s.r[i] = rec[f++];
-#pragma unroll
-    for (int i = 0; i < C::PS + C::P2; ++i) y[i] = rec[f++];
-}
-
-template <class S>
-__global__ __launch_bounds__(128) void kkt_fil_ws_kernel(const KktArgs a, double *__restrict__ scratch)
-{
-    using F = typename S::F;
-    using I = typename S::I;
-    using L = typename S::L;
-    using W = WsCfg<S>;
-    __shared__ double stg[3 * S::BUF];
-    __shared__ double shr[3 * 64 * W::SH];
-    __shared__ double fml[3 * 64 * W::FM];
-    const int N = a.N;                                          // ≥ 4 (host-checked)
-    const int64_t t0 = (int64_t)blockIdx.x * 64;
-    const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
-    Ctx<S> c;
-    c.lane = threadIdx.x & 63;
-    c.nlive = (int)(a.batch - t0 < 64 ? a.batch - t0 : 64);
-    c.live = c.lane < c.nlive;
-    c.bY = a.Y + t0 * a.sY;
-    c.by = a.y + t0 * a.sy;
-    c.bH = a.H + t0 * a.sH;
-    c.bg = a.g + t0 * a.sg;
-    c.bdz = a.dz + t0 * a.sg;
-    c.blam = a.lam + t0 * a.sl;
-    c.bS = scratch + (int64_t)blockIdx.x * N * S::SLOT * 64;
-    c.vS = 8u * c.lane;
-    c.vdz = (uint32_t)(c.lane * a.sg * 8);
-    c.vlam = (uint32_t)(c.lane * a.sl * 8);
-    if (producer) {
-        c.pY.init(a.sY, c.lane, c.nlive);
-        c.py.init(a.sy, c.lane, c.nlive);
-        c.pH.init(a.sH, c.lane, c.nlive);
-        c.pg.init(a.sg, c.lane, c.nlive);
-    }
-    auto shr_rec = [&](int k) { return shr + ((k % 3) * 64 + c.lane) * W::SH; };
-    auto fm_rec = [&](int k) { return fml + ((k % 3) * 64 + c.lane) * W::FM; };
-    int info = 0;
-
-    // ---------------- forward ----------------
-    if (producer) {
-        c.stage_any(a, 0, stg, true);
-        c.stage_any(a, 1, stg, true);
-    }
-    Carry<S> cy;
-#pragma unroll
-    for (int i = 0; i < S::NX; ++i) {
-        cy.lprev[i] = 0.0;
-#pragma unroll
-        for (int j = 0; j < S::NX; ++j) cy.Ua[i][j] = 0.0;
-    }
-    for (int s = 0; s <= N + 1; ++s) {
-        if (producer) {
-            if (s <= N - 1) {
-                // knot s landed: after its DMA (step s-2) came only the DMA of knot s+1
-                if (s + 1 <= N - 1) {
-                    if (s + 1 == N - 1) vm_wait<S::template Dmin<L>()>();
-                    else vm_wait<S::template Dmin<I>()>();
-                } else {
-                    vm_wait<0>();
-                }
-                if (s + 2 <= N - 1) c.stage_any(a, s + 2, stg, true);
-                Buf<S> b{stg + (s % 3) * S::BUF};
-                double *rec = shr_rec(s);
-                bool ok;
-                if (s == 0) {
-                    Shur<F> sh;
-                    ok = compute_shur<S, F>(sh, b.Y(c.lane, S::template LY<F>()), b.template H<S::template LH<F>()>(c.lane),
-                                            b.template g<S::template Lg<F>()>(c.lane));
-                    shur_put<F>(sh, b.template y<S::template Ly<F>()>(c.lane), rec);
-                } else if (s == N - 1) {
-                    Shur<L> sh;
-                    ok = compute_shur<S, L>(sh, b.Y(c.lane, S::template LY<L>()), b.template H<S::template LH<L>()>(c.lane),
-                                            b.template g<S::template Lg<L>()>(c.lane));
-                    shur_put<L>(sh, b.template y<S::template Ly<L>()>(c.lane), rec);
-                } else {
-                    Shur<I> sh;
-                    ok = compute_shur<S, I>(sh, b.Y(c.lane, S::template LY<I>()), b.template H<S::template LH<I>()>(c.lane),
-                                            b.template g<S::template Lg<I>()>(c.lane));
-                    shur_put<I>(sh, b.template y<S::template Ly<I>()>(c.lane), rec);
-                }
-                if (!ok && info == 0) info = -(s + 1);
-            }
-        } else if (s >= 2) {
-            const int k = s - 2;                                // factor knot k with Shur(k), Shur(k+1)
-            if (k == 0) {
-                Shur<F> sc; Shur<I> sn;
-                double yc[Z(F::PS + F::P2)], yn[Z(I::PS + I::P2)];
-                shur_get<F>(sc, yc, shr_rec(0));
-                shur_get<I>(sn, yn, shr_rec(1));
-                factor_knot<S, F, I>(0, sc, yc, sn, cy, c, info);
-            } else if (k == N - 1) {
-                Shur<L> sc; Shur<NoCls> sn;
-                double yc[Z(L::PS + L::P2)];
-                shur_get<L>(sc, yc, shr_rec(k));
-                factor_knot<S, L, NoCls>(k, sc, yc, sn, cy, c, info);
-            } else if (k == N - 2) {
-                Shur<I> sc; Shur<L> sn;
-                double yc[Z(I::PS + I::P2)], yn[Z(L::PS + L::P2)];
-                shur_get<I>(sc, yc, shr_rec(k));
-                shur_get<L>(sn, yn, shr_rec(k + 1));
-                factor_knot<S, I, L>(k, sc, yc, sn, cy, c, info);
-            } else {
-                Shur<I> sc, sn;
-                double yc[Z(I::PS + I::P2)], yn[Z(I::PS + I::P2)];
-                shur_get<I>(sc, yc, shr_rec(k));
-                shur_get<I>(sn, yn, shr_rec(k + 1));
-                factor_knot<S, I, I>(k, sc, yc, sn, cy, c, info);
-            }
-        }
-        __syncthreads();
-    }
-
-    // ---------------- backward + primal recovery ----------------
-    // (the chain wave's slab stores are its own: same-lane loads see them in order)
-    SlabV<I> vI, vpre;
-    SlabV<L> vL;
-    SlabV<F> v0;
-    auto fm_put = [&](int k, const double *mu, int ps, const double *la, int p2) {
-        double *r = fm_rec(k);
-        for (int i = 0; i < ps; ++i) r[i] = mu[i];
-        for (int i = 0; i < p2; ++i) r[ps + i] = la[i];
-    };
-    if (producer) {
-        vm_wait<0>();
-        c.stage_any(a, N - 1, stg, false);
-        c.stage_any(a, N - 2, stg, false);
-    } else {
-        vm_wait<0>();
-        slab_load<S, L>(vL, c, N - 1);
-        slab_load<S, I>(vI, c, N - 2);
-    }
-    for (int t = 0; t <= N + 1; ++t) {
-        if (!producer) {
-            const int j = N - 1 - t;
-            if (j == N - 1) {
-                SlabV<NoCls> vn;
-                bwd_knot<L, NoCls>(vL, vn);
-                store_lam<S, L>(c, j, vL);
-#pragma unroll
-                for (int i = 0; i < L::PS; ++i) fm_rec(j)[i] = vL.mu[i];
-            } else if (j == N - 2) {
-                if (N - 3 >= 1) slab_load<S, I>(vpre, c, N - 3);
-                bwd_knot<I, L>(vI, vL);
-                store_lam<S, I>(c, j, vI);
-#pragma unroll
-                for (int i = 0; i < I::PS; ++i) fm_rec(j)[i] = vI.mu[i];
-#pragma unroll
-                for (int i = 0; i < I::P2; ++i) fm_rec(j)[I::PS + i] = vI.la[i];
-            } else if (j >= 1) {
-                SlabV<I> v = vpre;
-                if (j - 1 >= 1) slab_load<S, I>(vpre, c, j - 1);
-                bwd_knot<I, I>(v, vI);
-                store_lam<S, I>(c, j, v);
-#pragma unroll
-                for (int i = 0; i < I::PS; ++i) fm_rec(j)[i] = v.mu[i];
-#pragma unroll
-                for (int i = 0; i < I::P2; ++i) fm_rec(j)[I::PS + i] = v.la[i];
-                vI = v;
-            } else if (j == 0) {
-                slab_load<S, F>(v0, c, 0);
-                bwd_knot<F, I>(v0, vI);
-                store_lam<S, F>(c, 0, v0);
-#pragma unroll
-                for (int i = 0; i < F::PS; ++i) fm_rec(0)[i] = v0.mu[i];
-#pragma unroll
-                for (int i = 0; i < F::P2; ++i) fm_rec(0)[F::PS + i] = v0.la[i];
-            }
-        } else if (t >= 2) {
-            const int q = N + 1 - t;                            // δz of knot q
-            // knot q landed: after its DMA (step t-2 or the prologue) came the DMA of knot q-1
-            // (≥ Dbwd of its class) — or nothing at q = 0
-            if (q >= 2) vm_wait<S::template Dbwd<I>()>();
-            else if (q == 1) vm_wait<S::template Dbwd<F>()>();
-            else vm_wait<0>();
-            if (q - 2 >= 0) c.stage_any(a, q - 2, stg, false);
-            Buf<S> b{stg + (q % 3) * S::BUF};
-            const double *rq = fm_rec(q);
-            if (q == N - 1) {
-                SlabV<L> v;
-#pragma unroll
-                for (int i = 0; i < L::PS; ++i) v.mu[i] = rq[i];
-                double lp[Z(L::P1)];
-#pragma unroll
-                for (int i = 0; i < L::P1; ++i) lp[i] = fm_rec(q - 1)[I::PS + i];
-                primal_knot<S, L, L::P1>(c, q, v, lp, b);
-            } else if (q >= 1) {
-                SlabV<I> v;
-#pragma unroll
-                for (int i = 0; i < I::PS; ++i) v.mu[i] = rq[i];
-#pragma unroll
-                for (int i = 0; i < I::P2; ++i) v.la[i] = rq[I::PS + i];
-                double lp[Z(I::P1)];
-                const int ps_prev = (q - 1 == 0) ? F::PS : I::PS;
-#pragma unroll
-                for (int i = 0; i < I::P1; ++i) lp[i] = fm_rec(q - 1)[ps_prev + i];
-                primal_knot<S, I, I::P1>(c, q, v, lp, b);
-            } else {
-                SlabV<F> v;
-#pragma unroll
-                for (int i = 0; i < F::PS; ++i) v.mu[i] = rq[i];
-#pragma unroll
-                for (int i = 0; i < F::P2; ++i) v.la[i] = rq[F::PS + i];
-                double none[1] = {0.0};
-                primal_knot<S, F, 0>(c, 0, v, none, b);
-            }
-        }
-        __syncthreads();
-    }
-    (void)fm_put;
-    // info: the producer saw H failures (−(k+1)), the chain wave Schur-pivot failures (k+1);
-    // H failures take precedence, as in the oracle (all H_k are factored before the Schur
-    // complement is formed)
-    __shared__ int infos[2][64];
-    infos[producer ? 0 : 1][c.lane] = info;
-    __syncthreads();
-    if (producer && a.info && c.live) {
-        const int ip = infos[0][c.lane], ic = infos[1][c.lane];
-        a.info[t0 + c.lane] = ip != 0 ? ip : ic;
-    }
-}
-
-template <class S>
-hipError_t launch_ws(const KktArgs &a, hipStream_t s)
-{
-    double *scratch = nullptr;
-    const size_t Bp = ((size_t)a.batch + 63) & ~(size_t)63;
-    const size_t bytes = Bp * (size_t)a.N * S::SLOT * sizeof(double);
-    hipError_t e = scratch_alloc((void **)&scratch, bytes, s);
-    if (e != hipSuccess) return e;
-    dim3 grid((unsigned)((a.batch + 63) / 64)), block(128);
-    hipLaunchKernelGGL((kkt_fil_ws_kernel<S>), grid, block, 0, s, a, scratch);
-    e = hipGetLastError();
-    hipError_t ef = scratch_free(scratch, s);
-    return e != hipSuccess ? e : ef;
-}
-
 template <class S>
 hipError_t launch(const KktArgs &a, hipStream_t s)
 {
@@ -1286,14 +1000,12 @@ hipError_t launch(const KktArgs &a, hipStream_t s)
     return e != hipSuccess ? e : ef;
 }
 
-// Explicit instantiations: clang drops the host stub of an implicitly instantiated kernel
-// template that is launched from both arms of a conditional alongside a second kernel.
+// Explicit instantiations of every dispatched shape: this compiler has dropped the host stub
+// of an implicitly instantiated kernel template launched from a conditional (link error).
 #define LQRX_FIL_INST(NX, M, A0, AK, AN)                                                                 \
     template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, true>>(const KktArgs, double *__restrict__);  \
     template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, false, true>>(const KktArgs, double *__restrict__); \
-    template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, false>>(const KktArgs, double *__restrict__); \
-    template __global__ void kkt_fil_ws_kernel<Shape<NX, M, A0, AK, AN, true, true>>(const KktArgs, double *__restrict__); \
-    template __global__ void kkt_fil_ws_kernel<Shape<NX, M, A0, AK, AN, true, false>>(const KktArgs, double *__restrict__);
+    template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, false>>(const KktArgs, double *__restrict__);
 LQRX_FIL_INST(3, 2, 3, 0, 3)
 #undef LQRX_FIL_INST
 
@@ -1311,17 +1023,14 @@ bool kkt_fil_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const
     for (int k = 1; k < N - 1; ++k)
         if (n1[k] != nx || n2[k] != nx || p[k] != PK || w[k] != nx + m) return false;
     const bool diag = a.h_mode == 2, ginv = a.ginv != 0;
-    // the warp-specialised variant is opt-in (LQRX_KKT_WS=1): measured slower on cfg3
-    // (0.53 vs 0.45 ms)
-    static const bool ws = [] { const char *v = std::getenv("LQRX_KKT_WS"); return v && *v == '1'; }();
 #define LQRX_FIL(NX, M, A0, AK, AN)                                                                      \
     if (nx == NX && m == M && P0 == A0 && PK == AK && PN == AN) {                                        \
         using SD = fil::Shape<NX, M, A0, AK, AN, true, true>;                                            \
         using SH = fil::Shape<NX, M, A0, AK, AN, false, true>;                                           \
         using SS = fil::Shape<NX, M, A0, AK, AN, true, false>;                                           \
-        if (diag && ginv) *err = ws ? fil::launch_ws<SD>(a, s) : fil::launch<SD>(a, s);                  \
-        else if (ginv) *err = fil::launch<SH>(a, s);   /* dense H: the WS rings exceed LDS */          \
-        else *err = ws ? fil::launch_ws<SS>(a, s) : fil::launch<SS>(a, s);                               \
+        if (diag && ginv) *err = fil::launch<SD>(a, s);                                                  \
+        else if (ginv) *err = fil::launch<SH>(a, s);                                                     \
+        else *err = fil::launch<SS>(a, s);                                                               \
         return true;                                                                                     \
     }
     LQRX_FIL(3, 2, 3, 0, 3)   // Dubins car (BASELINE cfg3), test/dubins.jl
