@@ -167,10 +167,13 @@ def main():
         pb = K.random_kkt(st, bt, seed=args.seed + rank, h_mode=K.H_DIAG)
         t = {k: torch.from_numpy(getattr(pb, k).ravel()).to(dev) for k in ("Y", "y", "H", "g")}
         t["batch"] = bt
-        out = K.kkt_solve_device(st, t, K.H_DIAG, 1, stream=sh)
+        # caller-owned workspace (lqrx_kkt_solve_ws): a step is the kernel alone, as a serving
+        # loop would run it (the pool path adds ~0.05 ms of stream-ordered alloc/free per call)
+        ws = torch.empty(K.workspace_size(st, bt, K.H_DIAG, 1), dtype=torch.uint8, device=dev)
+        out = K.kkt_solve_device(st, t, K.H_DIAG, 1, stream=sh, workspace=ws)
 
         def step():
-            K.kkt_solve_device(st, t, K.H_DIAG, 1, stream=sh, out=out)
+            K.kkt_solve_device(st, t, K.H_DIAG, 1, stream=sh, out=out, workspace=ws)
 
     for _ in range(args.warmup):
         step()

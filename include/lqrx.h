@@ -126,6 +126,15 @@ int lqrx_kkt_solve(const lqrx_kkt_desc *desc, const void *Y, const void *y, cons
                    const void *g, void *dz, void *lam, int32_t *info, void *stream);
 int lqrx_kkt_solve_host(const lqrx_kkt_desc *desc, const void *Y, const void *y,
                         const void *H, const void *g, void *dz, void *lam, int32_t *info);
+/* Caller-provided workspace (the factor slab): no allocation inside the call — the form a
+ * serving loop or a captured hipGraph wants.  lqrx_kkt_workspace_size gives the bytes this
+ * structure and batch need (0 for batch 0); lqrx_kkt_solve_ws returns -10 if
+ * workspace_bytes is smaller.  One workspace must not be shared by calls in flight on
+ * different streams (lqrx_kkt_solve draws stream-ordered scratch from a library pool). */
+int lqrx_kkt_workspace_size(const lqrx_kkt_desc *desc, size_t *bytes);
+int lqrx_kkt_solve_ws(const lqrx_kkt_desc *desc, const void *Y, const void *y, const void *H,
+                      const void *g, void *dz, void *lam, int32_t *info, void *workspace,
+                      size_t workspace_bytes, void *stream);
 /* sizes (elements per trajectory) of the packed KKT buffers, for allocation */
 int lqrx_kkt_sizes(const lqrx_kkt_desc *desc, int64_t *nY, int64_t *ny, int64_t *nH,
                    int64_t *ng, int64_t *nlam);

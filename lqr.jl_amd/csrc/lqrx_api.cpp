@@ -314,8 +314,63 @@ extern "C" int lqrx_kkt_sizes(const lqrx_kkt_desc *d, int64_t *nY, int64_t *ny, 
     return 0;
 }
 
+namespace {
+// kernel arguments of one KKT call (no device pointers yet)
+lqrx::KktArgs kkt_args(const lqrx_kkt_desc *d, const KktLayout &L)
+{
+    lqrx::KktArgs a{};
+    a.N = d->N; a.h_mode = d->h_mode; a.ginv = d->ginv; a.batch = d->batch;
+    a.sY = L.sY; a.sy = L.sy; a.sH = L.sH; a.sg = L.sg; a.sl = L.sy;
+    a.maxw = L.maxw; a.maxrows = L.maxrows;
+    a.max_p1 = L.max_p1; a.max_ps = L.max_ps; a.max_p2 = L.max_p2;
+    static const int force_lane = [] { const char *v = std::getenv("LQRX_KKT_FORCE_LANE"); return v && *v == '1'; }();
+    a.force_lane = force_lane;
+    return a;
+}
+// LQRX_KKT_GENERIC=1 forces the generic (runtime-shaped) kernel, for A/B checks
+bool kkt_force_generic()
+{
+    static const bool v = [] { const char *e = std::getenv("LQRX_KKT_GENERIC"); return e && *e == '1'; }();
+    return v;
+}
+size_t kkt_ws_bytes(const lqrx_kkt_desc *d, const lqrx::KktArgs &a)
+{
+    size_t b = 0;
+    if (!a.force_lane && !kkt_force_generic() && lqrx::kkt_fil_scratch_bytes(a, d->n1, d->p, d->n2, d->w, &b))
+        return b;
+    return lqrx::kkt_scratch_bytes(a);
+}
+int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const void *H, const void *g,
+                   void *dz, void *lam, int32_t *info, void *ws, size_t ws_bytes, void *stream);
+} // namespace
+
+extern "C" int lqrx_kkt_workspace_size(const lqrx_kkt_desc *d, size_t *bytes)
+{
+    KktLayout L;
+    int st = kkt_layout(d, L);
+    if (st) return st;
+    if (!bytes) return set_err(-2, "bytes is NULL");
+    *bytes = d->batch ? kkt_ws_bytes(d, kkt_args(d, L)) : 0;
+    return 0;
+}
+
 extern "C" int lqrx_kkt_solve(const lqrx_kkt_desc *d, const void *Y, const void *y, const void *H,
                               const void *g, void *dz, void *lam, int32_t *info, void *stream)
+{
+    return kkt_solve_impl(d, Y, y, H, g, dz, lam, info, nullptr, 0, stream);
+}
+
+extern "C" int lqrx_kkt_solve_ws(const lqrx_kkt_desc *d, const void *Y, const void *y, const void *H,
+                                 const void *g, void *dz, void *lam, int32_t *info, void *workspace,
+                                 size_t workspace_bytes, void *stream)
+{
+    if (!workspace) return set_err(-9, "workspace is NULL");
+    return kkt_solve_impl(d, Y, y, H, g, dz, lam, info, workspace, workspace_bytes, stream);
+}
+
+namespace {
+int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const void *H, const void *g,
+                   void *dz, void *lam, int32_t *info, void *ws, size_t ws_bytes, void *stream)
 {
     KktLayout L;
     int st = kkt_layout(d, L);
@@ -331,19 +386,18 @@ extern "C" int lqrx_kkt_solve(const lqrx_kkt_desc *d, const void *Y, const void 
     const int32_t *dmeta = nullptr;
     if ((st = device_meta(L.meta, &dmeta))) return st;
     hipError_t e;
-    lqrx::KktArgs a{};
+    lqrx::KktArgs a = kkt_args(d, L);
     a.Y = (const double *)Y; a.y = (const double *)y; a.H = (const double *)H; a.g = (const double *)g;
     a.dz = (double *)dz; a.lam = (double *)lam; a.info = info; a.meta = dmeta;
-    a.N = d->N; a.h_mode = d->h_mode; a.ginv = d->ginv; a.batch = d->batch;
-    a.sY = L.sY; a.sy = L.sy; a.sH = L.sH; a.sg = L.sg; a.sl = L.sy;
-    a.maxw = L.maxw; a.maxrows = L.maxrows;
-    a.max_p1 = L.max_p1; a.max_ps = L.max_ps; a.max_p2 = L.max_p2;
-    static const int force_lane = [] { const char *v = std::getenv("LQRX_KKT_FORCE_LANE"); return v && *v == '1'; }();
+    if (ws) {
+        const size_t need = kkt_ws_bytes(d, a);
+        if (ws_bytes < need)
+            return set_err(-10, "workspace of %zu bytes < %zu (lqrx_kkt_workspace_size)", ws_bytes, need);
+        a.ws = ws;
+        a.ws_bytes = ws_bytes;
+    }
     static const int debug_meta = [] { const char *v = std::getenv("LQRX_DEBUG_META"); return v && *v == '1'; }();
-    a.force_lane = force_lane;
-    // LQRX_KKT_GENERIC=1 forces the generic (runtime-shaped) kernel, for A/B checks
-    static const int force_generic = [] { const char *v = std::getenv("LQRX_KKT_GENERIC"); return v && *v == '1'; }();
-    if (force_lane || force_generic || !lqrx::kkt_fil_launch(a, d->n1, d->p, d->n2, d->w, s, &e))
+    if (a.force_lane || kkt_force_generic() || !lqrx::kkt_fil_launch(a, d->n1, d->p, d->n2, d->w, s, &e))
         e = lqrx::kkt_launch(a, s);
     if (debug_meta) {
         std::vector<int32_t> back(L.meta.size());
@@ -366,6 +420,7 @@ extern "C" int lqrx_kkt_solve(const lqrx_kkt_desc *d, const void *Y, const void 
     }
     return 0;
 }
+} // namespace
 
 extern "C" int lqrx_kkt_solve_host(const lqrx_kkt_desc *d, const void *Y, const void *y,
                                    const void *H, const void *g, void *dz, void *lam,

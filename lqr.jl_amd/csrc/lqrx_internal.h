@@ -33,6 +33,8 @@ struct KktArgs {
     int64_t sY, sy, sH, sg, sl; // per-trajectory strides (elements)
     int maxw, maxrows, max_p1, max_ps, max_p2;
     int force_lane; // debug: LQRX_KKT_FORCE_LANE=1 selects the register-only kernel
+    void *ws;         // caller's device workspace (lqrx_kkt_solve_ws) or NULL: library pool
+    size_t ws_bytes;
 };
 
 hipError_t kkt_launch(const KktArgs &a, hipStream_t s);
@@ -44,9 +46,30 @@ hipError_t kkt_launch(const KktArgs &a, hipStream_t s);
 // stream-ordered, never shared between calls.  (lqrx_api.cpp)
 hipError_t scratch_alloc(void **p, size_t bytes, hipStream_t s);
 hipError_t scratch_free(void *p, hipStream_t s);
+// a launch's slab: the caller's workspace when one was passed, else a pool block
+struct Scratch {
+    void *p = nullptr;
+    bool owned = false;
+    hipError_t get(const KktArgs &a, size_t bytes, hipStream_t s)
+    {
+        if (a.ws) {
+            if (a.ws_bytes < bytes) return hipErrorInvalidValue;
+            p = a.ws;
+            return hipSuccess;
+        }
+        owned = true;
+        return scratch_alloc(&p, bytes, s);
+    }
+    hipError_t release(hipStream_t s) { return owned ? scratch_free(p, s) : hipSuccess; }
+};
+// slab bytes the generic kernels need (mirrors kkt_launch's selection; 0 = unsupported)
+size_t kkt_scratch_bytes(const KktArgs &a);
 // compile-time-shaped kernel for first/interior/last structures (lqrx_kkt_fil.hip); returns
 // false (and launches nothing) when the structure has no instantiation
 bool kkt_fil_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
                     const int32_t *w, hipStream_t s, hipError_t *err);
+// slab bytes of the FIL kernel for this structure; false when no FIL shape serves it
+bool kkt_fil_scratch_bytes(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
+                           const int32_t *w, size_t *bytes);
 
 } // namespace lqrx

@@ -961,35 +961,51 @@ __global__ __launch_bounds__(64) void kkt_staged_kernel(const KktArgs a, const i
     if (a.info && live) a.info[t] = info;
 }
 
+template <int P1M, int PSM, int P2M>
+static size_t staged_bytes(const KktArgs &a)
+{
+    const size_t Bp = ((size_t)a.batch + 63) & ~(size_t)63;      // batch-fastest slab
+    return Bp * (size_t)a.N * Slab<P1M, PSM, P2M>::SIZE * sizeof(double);
+}
+template <int P1M, int PSM, int P2M>
+static size_t lane_bytes(const KktArgs &a)
+{
+    return (size_t)a.batch * (size_t)a.N * Slab<P1M, PSM, P2M>::SIZE * sizeof(double);
+}
+
 template <int P1M, int PSM, int P2M, int WM, int RM>
 static hipError_t launch_staged(const KktArgs &a, hipStream_t s)
 {
-    using SL = Slab<P1M, PSM, P2M>;
-    double *scratch = nullptr;
-    const size_t Bp = ((size_t)a.batch + 63) & ~(size_t)63;
-    size_t bytes = Bp * (size_t)a.N * SL::SIZE * sizeof(double);
-    hipError_t e = scratch_alloc((void **)&scratch, bytes, s);
+    Scratch sc;
+    hipError_t e = sc.get(a, staged_bytes<P1M, PSM, P2M>(a), s);
     if (e != hipSuccess) return e;
     dim3 grid((unsigned)((a.batch + 63) / 64)), block(64);
-    hipLaunchKernelGGL((kkt_staged_kernel<P1M, PSM, P2M, WM, RM>), grid, block, 0, s, a, a.meta, scratch);
+    hipLaunchKernelGGL((kkt_staged_kernel<P1M, PSM, P2M, WM, RM>), grid, block, 0, s, a, a.meta, (double *)sc.p);
     e = hipGetLastError();
-    hipError_t ef = scratch_free(scratch, s);
+    hipError_t ef = sc.release(s);
     return e != hipSuccess ? e : ef;
 }
 
 template <int P1M, int PSM, int P2M, int WM, int RM>
 static hipError_t launch_lane(const KktArgs &a, hipStream_t s)
 {
-    using SL = Slab<P1M, PSM, P2M>;
-    double *scratch = nullptr;
-    size_t bytes = (size_t)a.batch * (size_t)a.N * SL::SIZE * sizeof(double);
-    hipError_t e = scratch_alloc((void **)&scratch, bytes, s);
+    Scratch sc;
+    hipError_t e = sc.get(a, lane_bytes<P1M, PSM, P2M>(a), s);
     if (e != hipSuccess) return e;
     dim3 grid((unsigned)((a.batch + 63) / 64)), block(64);
-    hipLaunchKernelGGL((kkt_lane_kernel<P1M, PSM, P2M, WM, RM>), grid, block, 0, s, a, scratch);
+    hipLaunchKernelGGL((kkt_lane_kernel<P1M, PSM, P2M, WM, RM>), grid, block, 0, s, a, (double *)sc.p);
     e = hipGetLastError();
-    hipError_t ef = scratch_free(scratch, s);
+    hipError_t ef = sc.release(s);
     return e != hipSuccess ? e : ef;
+}
+
+size_t kkt_scratch_bytes(const KktArgs &a)
+{
+    const int P1 = a.max_p1, PS = a.max_ps, P2 = a.max_p2, W = a.maxw, R = a.maxrows;
+    if (!a.force_lane && P1 <= 3 && PS <= 3 && P2 <= 3 && W <= 5 && R <= 6) return staged_bytes<3, 3, 3>(a);
+    if (P1 <= 4 && PS <= 4 && P2 <= 4 && W <= 8 && R <= 8) return lane_bytes<4, 4, 4>(a);
+    if (P1 <= 8 && PS <= 8 && P2 <= 8 && W <= 12 && R <= 16) return lane_bytes<8, 8, 8>(a);
+    return 0;
 }
 
 hipError_t kkt_launch(const KktArgs &a, hipStream_t s)

@@ -985,18 +985,23 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     if (a.info && c.live) a.info[t0 + c.lane] = info;
 }
 
+template <class S> size_t slab_bytes(const KktArgs &a)
+{
+    const size_t Bp = ((size_t)a.batch + 63) & ~(size_t)63;   // wave-major slab, 64 lanes/wave
+    // (+1 KiB: the backward slab DMA of the last knot may read up to 512 B past its chunk)
+    return Bp * (size_t)a.N * S::SLOT * sizeof(double) + 1024;
+}
+
 template <class S>
 hipError_t launch(const KktArgs &a, hipStream_t s)
 {
-    double *scratch = nullptr;
-    const size_t Bp = ((size_t)a.batch + 63) & ~(size_t)63;   // wave-major slab, 64 lanes/wave
-    const size_t bytes = Bp * (size_t)a.N * S::SLOT * sizeof(double);
-    hipError_t e = scratch_alloc((void **)&scratch, bytes, s);
+    Scratch sc;
+    hipError_t e = sc.get(a, slab_bytes<S>(a), s);
     if (e != hipSuccess) return e;
     dim3 grid((unsigned)((a.batch + 63) / 64)), block(64);
-    hipLaunchKernelGGL((kkt_fil_kernel<S>), grid, block, 0, s, a, scratch);
+    hipLaunchKernelGGL((kkt_fil_kernel<S>), grid, block, 0, s, a, (double *)sc.p);
     e = hipGetLastError();
-    hipError_t ef = scratch_free(scratch, s);
+    hipError_t ef = sc.release(s);
     return e != hipSuccess ? e : ef;
 }
 
@@ -1013,8 +1018,10 @@ LQRX_FIL_INST(3, 2, 3, 0, 3)
 
 // Dispatch: the FIL kernel serves a structure iff every knot matches one of the
 // instantiated (n̄, m, P0, PK, PN) shapes; otherwise the generic kernel (lqrx_kkt.hip) runs.
-bool kkt_fil_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
-                    const int32_t *w, hipStream_t s, hipError_t *err)
+// F is called with the matching Shape (diag-H/Ginv, dense-H/Ginv, or SOC) as a value tag.
+template <class Fn>
+static bool fil_dispatch(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
+                         const int32_t *w, Fn &&fn)
 {
     const int N = a.N;
     if (N < 4) return false;
@@ -1025,17 +1032,26 @@ bool kkt_fil_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const
     const bool diag = a.h_mode == 2, ginv = a.ginv != 0;
 #define LQRX_FIL(NX, M, A0, AK, AN)                                                                      \
     if (nx == NX && m == M && P0 == A0 && PK == AK && PN == AN) {                                        \
-        using SD = fil::Shape<NX, M, A0, AK, AN, true, true>;                                            \
-        using SH = fil::Shape<NX, M, A0, AK, AN, false, true>;                                           \
-        using SS = fil::Shape<NX, M, A0, AK, AN, true, false>;                                           \
-        if (diag && ginv) *err = fil::launch<SD>(a, s);                                                  \
-        else if (ginv) *err = fil::launch<SH>(a, s);                                                     \
-        else *err = fil::launch<SS>(a, s);                                                               \
+        if (diag && ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true>{});                               \
+        else if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, false, true>{});                                 \
+        else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{});                                           \
         return true;                                                                                     \
     }
     LQRX_FIL(3, 2, 3, 0, 3)   // Dubins car (BASELINE cfg3), test/dubins.jl
 #undef LQRX_FIL
     return false;
+}
+
+bool kkt_fil_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
+                    const int32_t *w, hipStream_t s, hipError_t *err)
+{
+    return fil_dispatch(a, n1, p, n2, w, [&](auto shape) { *err = fil::launch<decltype(shape)>(a, s); });
+}
+
+bool kkt_fil_scratch_bytes(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
+                           const int32_t *w, size_t *bytes)
+{
+    return fil_dispatch(a, n1, p, n2, w, [&](auto shape) { *bytes = fil::slab_bytes<decltype(shape)>(a); });
 }
 
 } // namespace lqrx

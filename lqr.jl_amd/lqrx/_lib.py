@@ -50,6 +50,8 @@ _SIGS = {
     "lqrx_kkt_solve": (C.c_int, [C.POINTER(KktDesc)] + [_VP] * 7 + [_VP]),
     "lqrx_kkt_solve_host": (C.c_int, [C.POINTER(KktDesc)] + [_VP] * 7),
     "lqrx_kkt_sizes": (C.c_int, [C.POINTER(KktDesc)] + [C.POINTER(C.c_int64)] * 5),
+    "lqrx_kkt_workspace_size": (C.c_int, [C.POINTER(KktDesc), C.POINTER(C.c_size_t)]),
+    "lqrx_kkt_solve_ws": (C.c_int, [C.POINTER(KktDesc)] + [_VP] * 7 + [_VP, C.c_size_t, _VP]),
     "lqrx_make_random_dp": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_uint64,
                                       C.c_int32] + [_VP] * 6),
 }
@@ -66,6 +68,13 @@ def load() -> C.CDLL:
         raise RuntimeError(
             f"lqrx native library not built: {LIB_PATH} is missing "
             "(run `make -C lqr.jl_amd/csrc` or __graft_entry__.build())")
+    # One HIP runtime per process: torch ships its own libamdhip64 (same soname as
+    # /opt/rocm's, which liblqrx.so links).  Whichever loads first serves both, and torch
+    # finds no GPU on a runtime other than its own — so let torch's load first when present.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)

@@ -21,7 +21,7 @@ import numpy as np
 from . import _lib
 
 __all__ = ["KktStructure", "KktProblem", "ConstraintBlocks", "dubins_structure",
-           "double_integrator_structure", "random_kkt", "kkt_solve", "kkt_solve_device",
+           "double_integrator_structure", "random_kkt", "kkt_solve", "kkt_solve_device", "workspace_size",
            "second_order_correction"]
 
 H_DENSE, H_BLOCKDIAG, H_DIAG = 0, 1, 2
@@ -168,9 +168,19 @@ def second_order_correction(pb: KktProblem):
     return kkt_solve(pb, ginv=0)
 
 
+def workspace_size(st: KktStructure, batch: int, h_mode: int, ginv: int = 1) -> int:
+    """Bytes of device workspace lqrx_kkt_solve_ws needs (lqrx_kkt_workspace_size)."""
+    lib = _lib.load()
+    n = C.c_size_t(0)
+    _lib.check(lib.lqrx_kkt_workspace_size(C.byref(st.desc(batch, h_mode, ginv)), C.byref(n)))
+    return n.value
+
+
 def kkt_solve_device(st: KktStructure, t: dict, h_mode: int, ginv: int = 1,
-                     stream: int | None = None, out: dict | None = None) -> dict:
-    """Device-pointer entry on torch tensors (flat, ABI layout): t has Y, y, H, g, batch."""
+                     stream: int | None = None, out: dict | None = None, workspace=None) -> dict:
+    """Device-pointer entry on torch tensors (flat, ABI layout): t has Y, y, H, g, batch.
+    `workspace` (a device uint8 tensor of >= workspace_size() bytes) selects lqrx_kkt_solve_ws:
+    no allocation inside the call."""
     import torch
 
     lib = _lib.load()
@@ -183,8 +193,13 @@ def kkt_solve_device(st: KktStructure, t: dict, h_mode: int, ginv: int = 1,
                    info=torch.empty(bt, dtype=torch.int32, device=dev))
     d = st.desc(bt, h_mode, ginv)
     p = lambda x: C.c_void_p(x.data_ptr())
-    rc = lib.lqrx_kkt_solve(C.byref(d), p(t["Y"]), p(t["y"]), p(t["H"]), p(t["g"]), p(out["dz"]),
-                            p(out["lam"]), p(out["info"]), C.c_void_p(stream) if stream else None)
+    args = [C.byref(d), p(t["Y"]), p(t["y"]), p(t["H"]), p(t["g"]), p(out["dz"]), p(out["lam"]),
+            p(out["info"])]
+    sp = C.c_void_p(stream) if stream else None
+    if workspace is None:
+        rc = lib.lqrx_kkt_solve(*args, sp)
+    else:
+        rc = lib.lqrx_kkt_solve_ws(*args, p(workspace), workspace.numel() * workspace.element_size(), sp)
     _lib.check(rc)
     out["rc"] = rc
     return out

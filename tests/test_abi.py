@@ -83,6 +83,22 @@ def test_kkt_sizes(lqrx):
     assert sg == 101 * 3 + 100 * 2 and sy == 306        # NN = 503, P = (N+1)·n
 
 
+def test_kkt_workspace_size(lqrx):
+    """lqrx_kkt_workspace_size: the FIL slab (wave-major, batch padded to 64, +1 KiB DMA
+    overrun) for the Dubins structure; 0 for an empty batch; argument codes."""
+    import lqrx.kkt as K
+
+    st = K.dubins_structure(101)
+    n = K.workspace_size(st, 16384, K.H_DIAG, 1)
+    slot = 27                                            # first-knot slab: B̃ 6, C̃ 6, Ẽ 9, μ 3, λ 3
+    assert n == 16384 * 101 * slot * 8 + 1024
+    assert K.workspace_size(st, 100, K.H_DIAG, 1) == 128 * 101 * slot * 8 + 1024
+    assert K.workspace_size(st, 0, K.H_DIAG, 1) == 0
+    assert K.workspace_size(K.double_integrator_structure(3, 11), 64, K.H_DIAG, 1) > 0
+    d = st.desc(4, 2, 1)
+    assert lqrx.load().lqrx_kkt_workspace_size(C.byref(d), None) == -2
+
+
 def test_generator_deterministic_and_sharded(lqrx):
     a = lqrx.random_batch(6, 3, 10, 8, seed=99)
     b = lqrx.random_batch(6, 3, 10, 8, seed=99)

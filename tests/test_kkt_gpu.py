@@ -109,3 +109,25 @@ def test_kkt_fil_shapes(lqrx, gpu_ok, N, batch, h_mode, ginv):
     assert got["rc"] == 0 and (got["info"] == 0).all()
     assert rel(got["dz"], ref["dz"].reshape(batch, -1)) <= TOL
     assert rel(got["lam"], ref["lam"].reshape(batch, -1)) <= TOL
+
+
+def test_kkt_workspace_entry(lqrx, gpu_ok):
+    """lqrx_kkt_solve_ws (caller workspace, no allocation inside) equals lqrx_kkt_solve bit for
+    bit on the FIL and generic paths; a short workspace is rejected with -10."""
+    import ctypes as C
+    import torch
+    import lqrx.kkt as K
+
+    for st, bt in ((K.dubins_structure(101), 300), (K.double_integrator_structure(3, 11), 70)):
+        pb = K.random_kkt(st, bt, seed=5, h_mode=K.H_DIAG)
+        t = {k: torch.from_numpy(getattr(pb, k).ravel()).cuda() for k in ("Y", "y", "H", "g")}
+        t["batch"] = bt
+        a = K.kkt_solve_device(st, t, K.H_DIAG, 1)
+        nb = K.workspace_size(st, bt, K.H_DIAG, 1)
+        ws = torch.empty(nb, dtype=torch.uint8, device="cuda")
+        b = K.kkt_solve_device(st, t, K.H_DIAG, 1, workspace=ws)
+        torch.cuda.synchronize()
+        assert torch.equal(a["dz"], b["dz"]) and torch.equal(a["lam"], b["lam"])
+        with pytest.raises(lqrx.LqrxError) as e:
+            K.kkt_solve_device(st, t, K.H_DIAG, 1, workspace=ws[: nb - 8])
+        assert e.value.code == -10

@@ -8,7 +8,7 @@ OUT=gpurun_out/prof_${TAG:-x}
 mkdir -p $OUT
 nproc > $OUT/host.txt; lscpu | head -20 >> $OUT/host.txt
 for wl in ${WLS:-dp kkt cartpole}; do
-  CB="--no-cpu-baseline"; [ $wl = dp ] && CB="--cpu-seconds ${CPUS:-10}"
+  CB="--cpu-seconds ${CPUS:-10}"
   timeout -k 10 400 python bench.py --workload $wl --steps ${STEPS:-5} --warmup 1 $CB > $OUT/${wl}_bench.json 2> $OUT/${wl}_bench.err || { tail -20 $OUT/${wl}_bench.err; exit 2; }
   cat $OUT/${wl}_bench.json
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/${wl}_kt -o kt --output-format csv -- python bench.py --workload $wl --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline > $OUT/${wl}_kt.log 2>&1 || { tail -20 $OUT/${wl}_kt.log; exit 3; }
