@@ -140,6 +140,41 @@ int lqrx_kkt_sizes(const lqrx_kkt_desc *desc, int64_t *nY, int64_t *ny, int64_t 
                    int64_t *ng, int64_t *nlam);
 
 /* ------------------------------------------------------------------------------------
+ * Batched Dubins-car SQP around the KKT path: per trajectory,
+ * the outer loop of CholeskySolver.solve!/step! (/root/reference/src/cholesky_solver.jl:
+ * 109-153) with the KKT inputs assembled on the device (update!, :155-164: RK3 Dubins
+ * Jacobians, diagonal LQRObjective expansion), _solve! (:166-182), and the L1-merit
+ * backtracking line search with second-order correction of test/dubins_sqp.jl:58-97
+ * (SOC = second_order_correction!, cholesky_solver.jl:254-273).
+ *
+ * Model: RobotZoo.DubinsCar ẋ = [v cosθ, v sinθ, ω], RK3 (RobotDynamics) with step dt.
+ * Problem: min Σ_{k<N} ½(x_k−xf)ᵀQ(x_k−xf) + ½u_kᵀRu_k + ½(x_N−xf)ᵀQf(x_N−xf)
+ *          s.t. x_1 = x0, x_{k+1} = rk3(x_k, u_k), x_N = xf      (Q, R, Qf diagonal)
+ * Buffers (device; layout 0, batch slowest):
+ *   Z      (5N−2)·batch in/out: z = [x_1; u_1; …; x_{N−1}; u_{N−1}; x_N] (the KKT δz order)
+ *   x0, xf 3·batch
+ *   lam    3(N+1)·batch out: multipliers of the last accepted Newton step (KKT λ order)
+ *   iters  int32·batch out: accepted steps
+ *   status int32·batch out: 0 converged (‖c‖∞ < tol_p and ‖∇f+∇cᵀλ‖₂ < tol_d before a
+ *          step), 1 max_iters reached, 2 line search failed (iterate left unchanged)
+ * ------------------------------------------------------------------------------------ */
+typedef struct lqrx_dubins_sqp_desc {
+    int32_t N;              /* knots (>= 2)                                            */
+    int32_t max_iters;      /* CholeskySolver.solve!: 10                               */
+    int64_t batch;
+    double dt;              /* tf / (N−1)                                              */
+    double Q[3], R[2], Qf[3]; /* diagonal cost weights (> 0), shared by the batch       */
+    double mu;              /* L1 merit weight (dubins_sqp.jl:59 uses 1)               */
+    double tol_p, tol_d;    /* 1e-5, 1e-5 (cholesky_solver.jl:131-132)                 */
+} lqrx_dubins_sqp_desc;
+
+int lqrx_dubins_sqp_solve(const lqrx_dubins_sqp_desc *desc, double *Z, const double *x0,
+                          const double *xf, double *lam, int32_t *iters, int32_t *status,
+                          void *stream);
+int lqrx_dubins_sqp_solve_host(const lqrx_dubins_sqp_desc *desc, double *Z, const double *x0,
+                               const double *xf, double *lam, int32_t *iters, int32_t *status);
+
+/* ------------------------------------------------------------------------------------
  * Utilities
  * ------------------------------------------------------------------------------------ */
 int lqrx_abi_version(void);

@@ -341,7 +341,8 @@ size_t kkt_ws_bytes(const lqrx_kkt_desc *d, const lqrx::KktArgs &a)
     return lqrx::kkt_scratch_bytes(a);
 }
 int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const void *H, const void *g,
-                   void *dz, void *lam, int32_t *info, void *ws, size_t ws_bytes, void *stream);
+                   void *dz, void *lam, int32_t *info, void *ws, size_t ws_bytes, void *stream,
+                   bool null_sync = true);
 } // namespace
 
 extern "C" int lqrx_kkt_workspace_size(const lqrx_kkt_desc *d, size_t *bytes)
@@ -370,7 +371,7 @@ extern "C" int lqrx_kkt_solve_ws(const lqrx_kkt_desc *d, const void *Y, const vo
 
 namespace {
 int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const void *H, const void *g,
-                   void *dz, void *lam, int32_t *info, void *ws, size_t ws_bytes, void *stream)
+                   void *dz, void *lam, int32_t *info, void *ws, size_t ws_bytes, void *stream, bool null_sync)
 {
     KktLayout L;
     int st = kkt_layout(d, L);
@@ -407,7 +408,7 @@ int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const v
     }
     if (e == hipErrorNotSupported) return set_err(LQRX_ERR_UNSUPPORTED, "KKT kernel unavailable");
     if (e != hipSuccess) return hip_err(e, "kkt kernel launch");
-    if (stream == nullptr) {
+    if (stream == nullptr && null_sync) {
         e = hipStreamSynchronize(nullptr);
         if (e != hipSuccess) return hip_err(e, "kkt kernel");
         if (info) {
@@ -538,3 +539,128 @@ int lqrx_make_random_dp(int32_t n, int32_t m, int64_t batch, int64_t traj0, uint
 }
 
 } // extern "C"
+
+// ------------------------------------------------------------------ batched Dubins SQP
+namespace {
+int validate_sqp(const lqrx_dubins_sqp_desc *d)
+{
+    if (!d) return set_err(-1, "desc is NULL");
+    if (d->N < 2) return set_err(-1, "desc.N must be >= 2 (got %d)", d->N);
+    if (d->batch < 0) return set_err(-1, "desc.batch must be >= 0");
+    if (d->max_iters < 0) return set_err(-1, "desc.max_iters must be >= 0");
+    if (!(d->dt > 0)) return set_err(-1, "desc.dt must be > 0");
+    for (int i = 0; i < 3; ++i)
+        if (!(d->Q[i] > 0) || !(d->Qf[i] > 0)) return set_err(-1, "desc.Q / desc.Qf must be positive");
+    for (int i = 0; i < 2; ++i)
+        if (!(d->R[i] > 0)) return set_err(-1, "desc.R must be positive");
+    if (!(d->mu >= 0) || !(d->tol_p >= 0) || !(d->tol_d >= 0))
+        return set_err(-1, "desc.mu / tol_p / tol_d must be >= 0");
+    return 0;
+}
+
+struct SqpKkt {
+    lqrx_kkt_desc kd;
+    std::vector<int32_t> n1, p, n2, w;
+    const double *Y, *y, *H, *g;
+    double *lamn, *lams;
+    int32_t *info;
+    void *ws;
+    size_t ws_bytes;
+    hipStream_t s;
+};
+
+int sqp_kkt(void *ctx, int ginv, double *dz)
+{
+    SqpKkt &c = *(SqpKkt *)ctx;
+    c.kd.ginv = ginv;
+    return kkt_solve_impl(&c.kd, c.Y, c.y, c.H, c.g, dz, ginv ? c.lamn : c.lams, c.info, c.ws, c.ws_bytes, c.s,
+                          /*null_sync=*/false);
+}
+} // namespace
+
+extern "C" int lqrx_dubins_sqp_solve(const lqrx_dubins_sqp_desc *d, double *Z, const double *x0, const double *xf,
+                                     double *lam, int32_t *iters, int32_t *status, void *stream)
+{
+    int st = validate_sqp(d);
+    if (st) return st;
+    if (d->batch == 0) return 0;
+    if (!Z) return set_err(-2, "Z is NULL");
+    if (!x0) return set_err(-3, "x0 is NULL");
+    if (!xf) return set_err(-4, "xf is NULL");
+    if (!lam) return set_err(-5, "lam is NULL");
+    if (!iters) return set_err(-6, "iters is NULL");
+    if (!status) return set_err(-7, "status is NULL");
+    const int N = d->N;
+    const int64_t B = d->batch, NN = (int64_t)N * 3 + (int64_t)(N - 1) * 2, P = (int64_t)(N + 1) * 3;
+    hipStream_t s = (hipStream_t)stream;
+    SqpKkt c{};
+    lqrx::sqp_structure(N, c.n1, c.p, c.n2, c.w);
+    c.kd.N = N; c.kd.dtype = LQRX_F64; c.kd.batch = B;
+    c.kd.n1 = c.n1.data(); c.kd.p = c.p.data(); c.kd.n2 = c.n2.data(); c.kd.w = c.w.data();
+    c.kd.h_mode = 2; c.kd.ginv = 1; c.kd.layout = 0;
+    int64_t sY = 0, sy = 0, sH = 0, sg = 0;
+    if ((st = lqrx_kkt_sizes(&c.kd, &sY, &sy, &sH, &sg, nullptr))) return st;
+    size_t ws1 = 0, ws0 = 0;
+    if ((st = lqrx_kkt_workspace_size(&c.kd, &ws1))) return st;
+    c.kd.ginv = 0;
+    if ((st = lqrx_kkt_workspace_size(&c.kd, &ws0))) return st;
+    // one stream-ordered block, carved (256-B aligned pieces)
+    size_t off = 0;
+    auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+    const size_t oY = take(B * sY * 8), oy = take(B * sy * 8), oH = take(B * sH * 8), og = take(B * sg * 8),
+                 odz = take(B * NN * 8), olamn = take(B * P * 8), odzs = take(B * NN * 8), olams = take(B * P * 8),
+                 opart = take(B * N * 4 * 8), ophi = take(B * 8), odphi = take(B * 8), osoc = take(B * 4),
+                 oact = take(4), oinfo = take(B * 4), ows = take(std::max(ws0, ws1));
+    void *blk = nullptr;
+    hipError_t e = lqrx::scratch_alloc(&blk, off, s);
+    if (e != hipSuccess) return hip_err(e, "sqp scratch");
+    char *b = (char *)blk;
+    lqrx::SqpArgs A{};
+    A.N = N; A.B = B; A.dt = d->dt; A.mu = d->mu; A.tol_p = d->tol_p; A.tol_d = d->tol_d;
+    for (int i = 0; i < 3; ++i) A.Q[i] = d->Q[i], A.Qf[i] = d->Qf[i];
+    for (int i = 0; i < 2; ++i) A.R[i] = d->R[i];
+    A.x0 = x0; A.xf = xf; A.Z = Z; A.lam = lam; A.iters = iters; A.status = status;
+    A.Y = (double *)(b + oY); A.y = (double *)(b + oy); A.H = (double *)(b + oH); A.g = (double *)(b + og);
+    A.dz = (double *)(b + odz); A.lamn = (double *)(b + olamn); A.dzs = (double *)(b + odzs);
+    A.part = (double *)(b + opart); A.phi0 = (double *)(b + ophi); A.dphi = (double *)(b + odphi);
+    A.need_soc = (int32_t *)(b + osoc); A.n_active = (int32_t *)(b + oact);
+    c.Y = A.Y; c.y = A.y; c.H = A.H; c.g = A.g; c.lamn = A.lamn; c.lams = (double *)(b + olams);
+    c.info = (int32_t *)(b + oinfo); c.ws = b + ows; c.ws_bytes = std::max(ws0, ws1); c.s = s;
+    int kkt_rc = 0;
+    e = lqrx::sqp_run(A, d->max_iters, s, sqp_kkt, &c, &kkt_rc);
+    hipError_t ef = lqrx::scratch_free(blk, s);
+    if (kkt_rc < 0) return kkt_rc;
+    if (e != hipSuccess) return hip_err(e, "sqp");
+    if (ef != hipSuccess) return hip_err(ef, "sqp scratch free");
+    if (stream == nullptr && (e = hipStreamSynchronize(nullptr)) != hipSuccess) return hip_err(e, "sqp");
+    return 0;
+}
+
+extern "C" int lqrx_dubins_sqp_solve_host(const lqrx_dubins_sqp_desc *d, double *Z, const double *x0,
+                                          const double *xf, double *lam, int32_t *iters, int32_t *status)
+{
+    int st = validate_sqp(d);
+    if (st) return st;
+    if (d->batch == 0) return 0;
+    if (!Z || !x0 || !xf || !lam || !iters || !status) return set_err(-2, "NULL host pointer");
+    const int64_t B = d->batch, NN = (int64_t)d->N * 3 + (int64_t)(d->N - 1) * 2, P = (int64_t)(d->N + 1) * 3;
+    DevBuf dZ, dx0, dxf, dlam, dit, dst;
+    if ((st = dev_alloc(dZ, B * NN * 8, "Z")) || (st = dev_alloc(dx0, B * 24, "x0")) ||
+        (st = dev_alloc(dxf, B * 24, "xf")) || (st = dev_alloc(dlam, B * P * 8, "lam")) ||
+        (st = dev_alloc(dit, B * 4, "iters")) || (st = dev_alloc(dst, B * 4, "status")))
+        return st;
+    hipError_t e;
+    if ((e = hipMemcpy(dZ.p, Z, B * NN * 8, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(dx0.p, x0, B * 24, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(dxf.p, xf, B * 24, hipMemcpyHostToDevice)) != hipSuccess)
+        return hip_err(e, "sqp H2D");
+    if ((st = lqrx_dubins_sqp_solve(d, (double *)dZ.p, (const double *)dx0.p, (const double *)dxf.p,
+                                    (double *)dlam.p, (int32_t *)dit.p, (int32_t *)dst.p, nullptr)))
+        return st;
+    if ((e = hipMemcpy(Z, dZ.p, B * NN * 8, hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(lam, dlam.p, B * P * 8, hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(iters, dit.p, B * 4, hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(status, dst.p, B * 4, hipMemcpyDeviceToHost)) != hipSuccess)
+        return hip_err(e, "sqp D2H");
+    return 0;
+}

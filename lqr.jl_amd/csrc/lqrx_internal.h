@@ -1,6 +1,7 @@
 // lqrx_internal.h — kernel argument blocks shared by the launchers and the C ABI.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <vector>
 #include <stdint.h>
 
 namespace lqrx {
@@ -71,5 +72,27 @@ bool kkt_fil_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const
 // slab bytes of the FIL kernel for this structure; false when no FIL shape serves it
 bool kkt_fil_scratch_bytes(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
                            const int32_t *w, size_t *bytes);
+
+// ---- batched Dubins SQP (lqrx_sqp.hip) ----
+struct SqpArgs {
+    int N;
+    int64_t B;
+    double dt, mu, tol_p, tol_d;
+    double Q[3], R[2], Qf[3];
+    const double *x0, *xf;            // B×3
+    double *Z;                        // B×NN, in/out
+    double *lam;                      // B×P: multipliers of the last accepted Newton step
+    int32_t *iters, *status;          // B
+    double *Y, *y, *H, *g;            // KKT inputs, ABI layout (internal)
+    double *dz, *lamn, *dzs;          // Newton step + its multipliers, SOC step
+    double *part;                     // B×N×4 per-knot partials
+    double *phi0, *dphi;              // B
+    int32_t *need_soc;                // B
+    int32_t *n_active;                // 1
+};
+hipError_t sqp_run(const SqpArgs &A, int max_iters, hipStream_t s, int (*kkt)(void *ctx, int ginv, double *dz),
+                   void *ctx, int *kkt_rc);
+void sqp_structure(int N, std::vector<int32_t> &n1, std::vector<int32_t> &p, std::vector<int32_t> &n2,
+                   std::vector<int32_t> &w);
 
 } // namespace lqrx

@@ -39,6 +39,16 @@ class KktDesc(C.Structure):
     ]
 
 
+class SqpDesc(C.Structure):
+    """Mirror of ``lqrx_dubins_sqp_desc``."""
+
+    _fields_ = [
+        ("N", C.c_int32), ("max_iters", C.c_int32), ("batch", C.c_int64), ("dt", C.c_double),
+        ("Q", C.c_double * 3), ("R", C.c_double * 2), ("Qf", C.c_double * 3), ("mu", C.c_double),
+        ("tol_p", C.c_double), ("tol_d", C.c_double),
+    ]
+
+
 _VP = C.c_void_p
 _SIGS = {
     "lqrx_abi_version": (C.c_int, []),
@@ -52,6 +62,8 @@ _SIGS = {
     "lqrx_kkt_sizes": (C.c_int, [C.POINTER(KktDesc)] + [C.POINTER(C.c_int64)] * 5),
     "lqrx_kkt_workspace_size": (C.c_int, [C.POINTER(KktDesc), C.POINTER(C.c_size_t)]),
     "lqrx_kkt_solve_ws": (C.c_int, [C.POINTER(KktDesc)] + [_VP] * 7 + [_VP, C.c_size_t, _VP]),
+    "lqrx_dubins_sqp_solve": (C.c_int, [C.POINTER(SqpDesc)] + [_VP] * 6 + [_VP]),
+    "lqrx_dubins_sqp_solve_host": (C.c_int, [C.POINTER(SqpDesc)] + [_VP] * 6),
     "lqrx_make_random_dp": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_uint64,
                                       C.c_int32] + [_VP] * 6),
 }

@@ -1,0 +1,213 @@
+"""Dubins SQP oracle — TEST INFRASTRUCTURE ONLY (CPU restatement, numpy).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module;
+the product path (lqrx.sqp → liblqrx.so) never does.
+
+The reference's explicit SQP specification is /root/reference/test/dubins_sqp.jl:
+  objective f(Z)                             :37-42  (LQRObjective: Σ ½(x−xf)ᵀQ(x−xf) + ½uᵀRu,
+                                                      terminal ½(x−xf)ᵀQf(x−xf); Q, R, Qf diagonal)
+  constraints c(Z)                           :47-55  (x₁ − x0; discrete_dynamics(RK3, x_k, u_k) − x_{k+1})
+                                                      plus the goal x_N − xf that the cfg3 block
+                                                      structure carries (problems.jl:44-45 GoalConstraint)
+  merit ϕ = f + μ‖c‖₁, ϕ′ = ∇fᵀdx − μ‖c‖₁      :58-61
+  Newton KKT [∇²f ∇cᵀ; ∇c 0][dx; λ] = −[∇f; c]  :64-70, with ∇²f the cost Hessian (the
+                                                      CholeskySolver's expansion, cholesky_solver.jl:155-164)
+  backtracking line search + second-order correction  :74-97  (η = 1e-4, ρ = 0.5, 10 tries;
+                                                      dx̂ = −Aᵀ(AAᵀ)⁻¹c(x + dx), A = ∇c(x))
+and the outer loop of CholeskySolver.solve!/step! (cholesky_solver.jl:109-153): at most
+`iters` (10) steps; a trajectory stops when ‖c‖∞ < tol_p and ‖∇f + ∇cᵀλ‖₂ < tol_d, checked
+before its step with the λ of its previous Newton solve (zero at the start).  A line search
+that finds no acceptable step leaves the iterate unchanged and ends that trajectory
+(status 2; the script only warns, :96).
+
+Parity anchor: the reference's own functions above.  TrajOptCore / RobotZoo are absent, so the
+Dubins model (RobotZoo.DubinsCar: ẋ = [v cosθ, v sinθ, ω]) and RK3 (RobotDynamics:
+k1 = f(x)dt, k2 = f(x + k1/2)dt, k3 = f(x − k1 + 2k2)dt, x⁺ = x + (k1 + 4k2 + k3)/6) are
+restated from their published definitions; Jacobians here by complex-step differentiation
+(exact to rounding; the device path uses the analytic chain rule — an independent check).
+The merit weight μ is fixed (the script's μ = 1; TO.update_penalty! is absent).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+NX, NU = 3, 2
+ETA, RHO, LS_TRIES = 1e-4, 0.5, 10
+
+
+def dubins(x, u):
+    """RobotZoo.DubinsCar continuous dynamics."""
+    return np.array([u[0] * np.cos(x[2]), u[0] * np.sin(x[2]), u[1]], dtype=np.result_type(x, u))
+
+
+def rk3(x, u, dt):
+    k1 = dubins(x, u) * dt
+    k2 = dubins(x + k1 / 2, u) * dt
+    k3 = dubins(x - k1 + 2 * k2, u) * dt
+    return x + (k1 + 4 * k2 + k3) / 6
+
+
+def rk3_jac(x, u, dt, h=1e-30):
+    """[A B] = ∂rk3/∂[x u] by complex step."""
+    J = np.zeros((NX, NX + NU))
+    for i in range(NX + NU):
+        xc = x.astype(complex)
+        uc = u.astype(complex)
+        if i < NX:
+            xc[i] += 1j * h
+        else:
+            uc[i - NX] += 1j * h
+        J[:, i] = np.imag(rk3(xc, uc, dt)) / h
+    return J
+
+
+class DubinsSQP:
+    """One trajectory's NLP, variables in the reference's order z = [x₁; u₁; …; x_{N-1}; u_{N-1}; x_N]."""
+
+    def __init__(self, N, dt, Q, R, Qf, x0, xf, mu=1.0):
+        self.N, self.dt, self.mu = N, dt, mu
+        self.Q, self.R, self.Qf = (np.asarray(v, float) for v in (Q, R, Qf))
+        self.x0, self.xf = np.asarray(x0, float), np.asarray(xf, float)
+        self.NN = N * NX + (N - 1) * NU
+        self.P = (N + 1) * NX
+
+    def split(self, z):
+        w = NX + NU
+        X = [z[k * w:k * w + NX] for k in range(self.N - 1)] + [z[(self.N - 1) * w:]]
+        U = [z[k * w + NX:(k + 1) * w] for k in range(self.N - 1)]
+        return X, U
+
+    def f(self, z):
+        X, U = self.split(z)
+        J = 0.0
+        for k in range(self.N - 1):
+            e = X[k] - self.xf
+            J += 0.5 * e @ (self.Q * e) + 0.5 * U[k] @ (self.R * U[k])
+        e = X[-1] - self.xf
+        return J + 0.5 * e @ (self.Qf * e)
+
+    def grad(self, z):
+        X, U = self.split(z)
+        g = []
+        for k in range(self.N - 1):
+            g += [self.Q * (X[k] - self.xf), self.R * U[k]]
+        g.append(self.Qf * (X[-1] - self.xf))
+        return np.concatenate(g)
+
+    def hess_diag(self):
+        return np.concatenate([np.concatenate([self.Q, self.R])] * (self.N - 1) + [self.Qf])
+
+    def c(self, z):
+        X, U = self.split(z)
+        v = [X[0] - self.x0]
+        for k in range(self.N - 1):
+            v.append(rk3(X[k], U[k], self.dt) - X[k + 1])
+        v.append(X[-1] - self.xf)
+        return np.concatenate(v)
+
+    def jac(self, z):
+        X, U = self.split(z)
+        A = np.zeros((self.P, self.NN))
+        w = NX + NU
+        A[:NX, :NX] = np.eye(NX)
+        for k in range(self.N - 1):
+            r = NX * (k + 1)
+            A[r:r + NX, k * w:(k + 1) * w] = rk3_jac(X[k], U[k], self.dt)
+            A[r:r + NX, (k + 1) * w:(k + 1) * w + NX] = -np.eye(NX)
+        A[-NX:, (self.N - 1) * w:] = np.eye(NX)
+        return A
+
+    def phi(self, z):
+        return self.f(z) + self.mu * np.abs(self.c(z)).sum()
+
+    def newton(self, z):
+        """dubins_sqp.jl:64-70 with the cost Hessian: returns dz, λ."""
+        A, H = self.jac(z), self.hess_diag()
+        NN, P = self.NN, self.P
+        K = np.zeros((NN + P, NN + P))
+        K[:NN, :NN] = np.diag(H)
+        K[:NN, NN:] = A.T
+        K[NN:, :NN] = A
+        sol = np.linalg.solve(K, -np.concatenate([self.grad(z), self.c(z)]))
+        return sol[:NN], sol[NN:]
+
+    def soc(self, z, dz):
+        """dx̂ = −Aᵀ(AAᵀ)⁻¹c(x + dx) (dubins_sqp.jl:84-85; second_order_correction!)."""
+        A = self.jac(z)
+        return -A.T @ np.linalg.solve(A @ A.T, self.c(z + dz))
+
+    def line_search(self, z, dz):
+        """dubins_sqp.jl:74-97.  Returns (z_new, accepted, alpha, used_soc)."""
+        phi0 = self.phi(z)
+        dphi = self.grad(z) @ dz - self.mu * np.abs(self.c(z)).sum()
+        a = 1.0
+        for _ in range(LS_TRIES):
+            if self.phi(z + a * dz) <= phi0 + ETA * a * dphi:
+                return z + a * dz, True, a, False
+            if a == 1.0:
+                dzh = self.soc(z, dz)
+                if self.phi(z + dz + dzh) < phi0 + ETA * dphi:
+                    return z + dz + dzh, True, a, True
+            a *= RHO
+        return z, False, 0.0, False
+
+    def residuals(self, z, lam):
+        """max_violation and residual (cholesky_solver.jl:129-130, 238-252)."""
+        return np.abs(self.c(z)).max(), np.linalg.norm(self.grad(z) + self.jac(z).T @ lam)
+
+
+def solve(prob: DubinsSQP, z0, iters=10, tol_p=1e-5, tol_d=1e-5):
+    """CholeskySolver.solve! loop (cholesky_solver.jl:109-153).  Returns dict z, lam, iters
+    (steps taken), status (0 converged, 1 iteration limit, 2 line search failed), hist
+    (iterates), soc (per step: second-order correction used)."""
+    z, lam = np.array(z0, float), np.zeros(prob.P)
+    hist, socs = [z.copy()], []
+    for it in range(iters):
+        fp, fd = prob.residuals(z, lam)
+        if fp < tol_p and fd < tol_d:
+            return dict(z=z, lam=lam, iters=it, status=0, hist=hist, soc=socs)
+        dz, lam_n = prob.newton(z)
+        z_n, ok, _, used = prob.line_search(z, dz)
+        if not ok:
+            return dict(z=z, lam=lam, iters=it, status=2, hist=hist, soc=socs)
+        z, lam = z_n, lam_n
+        hist.append(z.copy())
+        socs.append(used)
+    return dict(z=z, lam=lam, iters=iters, status=1, hist=hist, soc=socs)
+
+
+def initial_guess(N, dt, x0, xf):
+    """States interpolated from x0 to xf, controls at the straight-line speed and turn rate:
+    violates the dynamics, so the SQP has work to do."""
+    x0, xf = np.asarray(x0, float), np.asarray(xf, float)
+    w = NX + NU
+    z = np.zeros(N * NX + (N - 1) * NU)
+    T = dt * (N - 1)
+    v = np.hypot(*(xf[:2] - x0[:2])) / T
+    om = (xf[2] - x0[2]) / T
+    for k in range(N):
+        s = k / (N - 1)
+        z[k * w:k * w + NX] = (1 - s) * x0 + s * xf
+        if k < N - 1:
+            z[k * w + NX:(k + 1) * w] = [v, om]
+    return z
+
+
+def assemble(prob: DubinsSQP, z):
+    """The Newton step's KKT inputs at z in the liblqrx ABI layout (h_mode 2): per knot
+    Y_k = [D2; C; D1] (column-major), y_k = [c; d], H_k (diagonal), g_k — the blocks
+    ConstraintBlocks / InvertedQuadratic hold (conblocks.jl:36-98, block_cholesky.jl:82-91,
+    126-132), cut from the dense ∇c, c, ∇²f, ∇f above.  Knot k's rows are the constraints
+    [λ_{k-1}; μ_k; λ_k] = c[mk : mk+6], mk = 0 (k = 0) or 3k; its columns are z_k."""
+    A, c, g, h = prob.jac(z), prob.c(z), prob.grad(z), prob.hess_diag()
+    N = prob.N
+    Y, y, H, G = [], [], [], []
+    for k in range(N):
+        w = NX + NU if k < N - 1 else NX
+        mk = 0 if k == 0 else 3 * k
+        Y.append(A[mk:mk + 6, 5 * k:5 * k + w].T.ravel())     # column-major
+        oy = 0 if k == 0 else 3 * k + 3
+        y.append(c[oy:oy + (6 if k == 0 else 3)])
+        H.append(h[5 * k:5 * k + w])
+        G.append(g[5 * k:5 * k + w])
+    return tuple(np.concatenate(v) for v in (Y, y, H, G))
