@@ -106,16 +106,17 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    ap.add_argument("--workload", choices=["dp", "cartpole", "kkt"], default="dp",
+    ap.add_argument("--workload", choices=["dp", "cartpole", "kkt", "sqp"], default="dp",
                     help="dp = random dense LQR (BASELINE configs[3], the headline); "
                          "cartpole = configs[1] (n=4 m=1 N=101 B=4096); "
-                         "kkt = Dubins block-tridiagonal KKT solve (configs[2], B=16384)")
+                         "kkt = Dubins block-tridiagonal KKT solve (configs[2], B=16384); "
+                         "sqp = Dubins SQP around the KKT solve (SURVEY §8(f) ranks 2-3, B=16384)")
     args = ap.parse_args()
     if args.workload == "cartpole":
         args.n, args.m, args.N = 4, 1, 101
         if args.batch == 65536:
             args.batch = 4096
-    if args.workload == "kkt":
+    if args.workload in ("kkt", "sqp"):
         args.n, args.m = 3, 2                       # Dubins car (test/dubins.jl)
         if args.batch == 65536:
             args.batch = 16384
@@ -161,6 +162,21 @@ def main():
 
         def step():
             lqrx.dp_solve_device(t, N, p_mode=0, stream=sh, out=out)
+    elif args.workload == "sqp":
+        import lqrx.sqp as Q
+        dt_, x0_, xf_, Z0_ = Q.random_dubins_batch(N, bt, seed=args.seed + rank)
+        sqp_prob = Q.DubinsSQP(N, dt_, mu=10.0)
+        z0 = torch.from_numpy(Z0_.ravel()).to(dev)
+        t = dict(Z=z0.clone(), x0=torch.from_numpy(x0_.ravel()).to(dev),
+                 xf=torch.from_numpy(xf_.ravel()).to(dev),
+                 lam=torch.empty(bt * Q.num_multipliers(N), dtype=torch.float64, device=dev),
+                 iters=torch.empty(bt, dtype=torch.int32, device=dev),
+                 status=torch.empty(bt, dtype=torch.int32, device=dev))
+        out = {"info": t["status"]}
+
+        def step():
+            t["Z"].copy_(z0)                                  # same problem every step
+            Q.dubins_sqp_solve_device(sqp_prob, t, stream=sh)
     else:
         import lqrx.kkt as K
         st = K.dubins_structure(N)
@@ -194,7 +210,8 @@ def main():
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps       # stream-timed launch duration
-    bad = int((out["info"] != 0).sum().item())
+    bad = int((out["info"] != 0).sum().item()) if args.workload != "sqp" else \
+        int((out["info"] == 2).sum().item())                  # SQP: line-search failures
 
     wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
     if world > 1:
@@ -205,7 +222,37 @@ def main():
     ms_per_step = wall / args.steps * 1e3
 
     if rank == 0:
-        if args.workload == "kkt":
+        if args.workload == "sqp":
+            import lqrx.kkt as K
+            import lqrx.sqp as Q
+            sY, sy, sH, sg = K.dubins_structure(N).sizes(K.H_DIAG)
+            it_max = int(t["iters"].max().item()) + 1                # loop passes (last = check only)
+            # algorithmic bytes per trajectory and loop pass: assembly (z, λ in; Y, y, H, g out),
+            # Newton KKT (41 KB class), SOC KKT (Y, y in; δẑ, λ out), line search (z, δz, g, δẑ, λ)
+            per_it = ((sg + sy) + (sY + sy + sH + sg)
+                      + (sY + sy + sH + sg + sg + sy) + (sY + sy + sg + sy)
+                      + (4 * sg + 2 * sy)) * 8
+            alg_bytes = per_it * it_max * bt
+            achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+                    "kernel": "whole SQP step (assembly + 2 KKT + line search per pass)",
+                    "kernel_ms": kern_ms, "alg_bytes_per_traj": alg_bytes / bt, "loop_passes": it_max}
+            metric = f"Dubins SQP solves/sec (n=3 m=2 N={N}, <=10 steps, L1-merit line search + SOC)"
+            workload = "Dubins SQP around the KKT solve (SURVEY.md 8(f) ranks 2-3)"
+            cpu = None
+            if not args.no_cpu_baseline and world == 1:
+                sys.path.insert(0, ROOT)
+                from oracle import sqp_oracle as S
+                nb = 4
+                t0c = time.perf_counter()
+                for b in range(nb):
+                    S.solve(S.DubinsSQP(N, dt_, sqp_prob.Q, sqp_prob.R, sqp_prob.Qf, x0_[b], xf_[b], mu=10.0), Z0_[b])
+                el = time.perf_counter() - t0c
+                cpu = {"value": nb / el, "unit": "trajectories/s", "cores": 1, "kind": "port",
+                       "sample": f"{nb} trajectories, oracle/sqp_oracle.py (numpy dense KKT restatement of "
+                                 f"test/dubins_sqp.jl), {el:.1f} s"}
+        elif args.workload == "kkt":
             import lqrx.kkt as K
             sY, sy, sH, sg = K.dubins_structure(N).sizes(K.H_DIAG)
             alg_bytes = (sY + sy + sH + sg + sg + sy) * 8 * bt     # inputs + dz + λ

@@ -609,7 +609,7 @@ extern "C" int lqrx_dubins_sqp_solve(const lqrx_dubins_sqp_desc *d, double *Z, c
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
     const size_t oY = take(B * sY * 8), oy = take(B * sy * 8), oH = take(B * sH * 8), og = take(B * sg * 8),
                  odz = take(B * NN * 8), olamn = take(B * P * 8), odzs = take(B * NN * 8), olams = take(B * P * 8),
-                 opart = take(B * N * 4 * 8), ophi = take(B * 8), odphi = take(B * 8), osoc = take(B * 4),
+                 ophi = take(B * 8), odphi = take(B * 8), osoc = take(B * 4),
                  oact = take(4), oinfo = take(B * 4), ows = take(std::max(ws0, ws1));
     void *blk = nullptr;
     hipError_t e = lqrx::scratch_alloc(&blk, off, s);
@@ -622,7 +622,7 @@ extern "C" int lqrx_dubins_sqp_solve(const lqrx_dubins_sqp_desc *d, double *Z, c
     A.x0 = x0; A.xf = xf; A.Z = Z; A.lam = lam; A.iters = iters; A.status = status;
     A.Y = (double *)(b + oY); A.y = (double *)(b + oy); A.H = (double *)(b + oH); A.g = (double *)(b + og);
     A.dz = (double *)(b + odz); A.lamn = (double *)(b + olamn); A.dzs = (double *)(b + odzs);
-    A.part = (double *)(b + opart); A.phi0 = (double *)(b + ophi); A.dphi = (double *)(b + odphi);
+    A.phi0 = (double *)(b + ophi); A.dphi = (double *)(b + odphi);
     A.need_soc = (int32_t *)(b + osoc); A.n_active = (int32_t *)(b + oact);
     c.Y = A.Y; c.y = A.y; c.H = A.H; c.g = A.g; c.lamn = A.lamn; c.lams = (double *)(b + olams);
     c.info = (int32_t *)(b + oinfo); c.ws = b + ows; c.ws_bytes = std::max(ws0, ws1); c.s = s;

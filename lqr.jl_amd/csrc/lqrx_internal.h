@@ -85,7 +85,6 @@ struct SqpArgs {
     int32_t *iters, *status;          // B
     double *Y, *y, *H, *g;            // KKT inputs, ABI layout (internal)
     double *dz, *lamn, *dzs;          // Newton step + its multipliers, SOC step
-    double *part;                     // B×N×4 per-knot partials
     double *phi0, *dphi;              // B
     int32_t *need_soc;                // B
     int32_t *n_active;                // 1

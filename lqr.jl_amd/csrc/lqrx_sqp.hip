@@ -14,9 +14,10 @@
 // Variables z = [x₁; u₁; …; x_{N-1}; u_{N-1}; x_N] per trajectory (the KKT δz ordering);
 // multipliers in the KKT λ ordering ([μ_init; λ₁] | λ_k | μ_goal).
 //
-// Work split: one thread per (trajectory, knot) for the assembly and the per-knot merit /
-// residual partials (coalesced over knots), one thread per trajectory for the scalar
-// line-search decisions (each walks its knots in order: deterministic sums).
+// Work split: one wave per trajectory, lanes over knots (k = lane, lane + 64, …) for the
+// assembly, the merit evaluations and the residual; wave reductions (fixed butterfly order,
+// lane 0's result broadcast) make every accept/reject decision wave-uniform and
+// deterministic.
 #include "lqrx_internal.h"
 
 #include <cmath>
@@ -139,30 +140,54 @@ __device__ __forceinline__ void knot_merit(const Args &A, int t, int k, const Kn
     }
 }
 
-__device__ double merit(const Args &A, int t, const KnotPt &p)
+// ---------------------------------------------------------------- wave-per-trajectory helpers
+// One wave per trajectory: lane l takes knots l, l+64, …; per-knot sums are reduced across
+// the wave and lane 0's value is broadcast, so every decision is wave-uniform.
+constexpr int TPB = 4;                                    // trajectories (waves) per workgroup
+
+__device__ __forceinline__ double wave_sum(double v)
+{
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return __shfl(v, 0, 64);
+}
+__device__ __forceinline__ double wave_max(double v)
+{
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return __shfl(v, 0, 64);
+}
+
+// ϕ = f + μ‖c‖₁ at the point p (dubins_sqp.jl:60)
+__device__ double merit(const Args &A, int t, const KnotPt &p, int lane)
 {
     double f = 0.0, c = 0.0;
-    for (int k = 0; k < A.N; ++k) {
+    for (int k = lane; k < A.N; k += 64) {
         double ck, c1;
         knot_merit(A, t, k, p, ck, c1);
         f += ck;
         c += c1;
     }
-    return f + A.mu * c;
+    return wave_sum(f) + A.mu * wave_sum(c);
 }
 
-// ---------------------------------------------------------------- assembly (update!)
-// Thread (t, k): Y_k, y_k, H_k, g_k of the Dubins structure (knot 0: (n1 0, p 3, n2 3, w 5),
-// interior (3, 0, 3, 5), last (3, 3, 0, 3)), and the knot's partials for the convergence
-// check: cost, Σ|c|, max|c|, ‖g_k + Y_kᵀ m_k‖² with m_k = [λ_{k-1}; μ_k; λ_k] the
-// multipliers of the last Newton step (calc_residual!, cholesky_solver.jl:201-236).
-__global__ __launch_bounds__(256) void sqp_expand_kernel(const Args A)
+// z ← p, λ ← λ of the Newton solve, one more accepted step (wave-cooperative, coalesced)
+__device__ void accept(const Args &A, int64_t t, const KnotPt &p, int lane)
 {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t NN = nn(A.N), P = np_(A.N);
+    double *z = A.Z + t * NN;
+    for (int64_t i = lane; i < NN; i += 64) z[i] = p.at(i);
+    for (int64_t i = lane; i < P; i += 64) A.lam[t * P + i] = A.lamn[t * P + i];
+    if (lane == 0) A.iters[t] += 1;
+}
+
+// ---------------------------------------------------------------- assembly (update!) + check
+// Knot k: Y_k, y_k, H_k, g_k of the Dubins structure (knot 0: (n1 0, p 3, n2 3, w 5),
+// interior (3, 0, 3, 5), last (3, 3, 0, 3)) and its share of the convergence check: cost,
+// Σ|c|, max|c|, ‖g_k + Y_kᵀ m_k‖² with m_k = [λ_{k-1}; μ_k; λ_k] the multipliers of the
+// last Newton step (calc_residual!, cholesky_solver.jl:201-236).  Then the wave's check:
+// ‖c‖∞ < tol_p and ‖∇f + ∇cᵀλ‖₂ < tol_d → converged (cholesky_solver.jl:129-137).
+__device__ void expand_knot(const Args &A, int t, int k, double &cost, double &c1, double &cinf, double &r2)
+{
     const int N = A.N;
-    if (idx >= A.B * N) return;
-    const int t = (int)(idx / N), k = (int)(idx - (int64_t)t * N);
-    if (A.status[t] != ACTIVE) return;
     const int64_t NN = nn(N), P = np_(N);
     const double *z = A.Z + t * NN + (int64_t)W * k;
     const double *xf = A.xf + (int64_t)t * NX;
@@ -173,7 +198,6 @@ __global__ __launch_bounds__(256) void sqp_expand_kernel(const Args A)
     const double *m = A.lam + t * P + om(k);
     double x[NX];
     for (int i = 0; i < NX; ++i) x[i] = z[i];
-    double cost = 0.0, c1 = 0.0, cinf = 0.0, r2 = 0.0;
     auto con = [&](double v, int i) {
         y[i] = v;
         c1 += fabs(v);
@@ -201,7 +225,7 @@ __global__ __launch_bounds__(256) void sqp_expand_kernel(const Args A)
             const double e = x[i] - xf[i];
             gk[i] = A.Q[i] * e;
             H[i] = A.Q[i];
-            cost += 0.5 * e * A.Q[i] * e;
+            cost += 0.5 * (x[i] - xf[i]) * A.Q[i] * (x[i] - xf[i]);
         }
         for (int i = 0; i < NU; ++i) {
             gk[NX + i] = A.R[i] * u[i];
@@ -210,9 +234,9 @@ __global__ __launch_bounds__(256) void sqp_expand_kernel(const Args A)
         }
         for (int j = 0; j < W; ++j) {
             g[j] = gk[j];
-            double s = gk[j];
-            for (int i = 0; i < 6; ++i) s += Yk[i][j] * m[i];
-            r2 += s * s;
+            double sres = gk[j];
+            for (int i = 0; i < 6; ++i) sres += Yk[i][j] * m[i];
+            r2 += sres * sres;
         }
     } else {
         // last knot: [D2 = −I; C = I (goal)], 6×3
@@ -226,73 +250,57 @@ __global__ __launch_bounds__(256) void sqp_expand_kernel(const Args A)
             const double e = x[i] - xf[i];
             g[i] = A.Qf[i] * e;
             H[i] = A.Qf[i];
-            cost += 0.5 * e * A.Qf[i] * e;
-            const double s = g[i] - m[i] + m[NX + i];
-            r2 += s * s;
+            cost += 0.5 * (x[i] - xf[i]) * A.Qf[i] * (x[i] - xf[i]);
+            const double sres = g[i] - m[i] + m[NX + i];
+            r2 += sres * sres;
         }
     }
-    double *pt = A.part + idx * 4;
-    pt[0] = cost;
-    pt[1] = c1;
-    pt[2] = cinf;
-    pt[3] = r2;
 }
 
-// ---------------------------------------------------------------- convergence check
-__global__ __launch_bounds__(256) void sqp_check_kernel(const Args A)
+__global__ __launch_bounds__(64 * TPB) void sqp_expand_kernel(const Args A)
 {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= A.B || A.status[t] != ACTIVE) return;
-    double f = 0.0, c1 = 0.0, cinf = 0.0, r2 = 0.0;
-    const double *pt = A.part + t * A.N * 4;
-    for (int k = 0; k < A.N; ++k) {
-        f += pt[4 * k];
-        c1 += pt[4 * k + 1];
-        cinf = fmax(cinf, pt[4 * k + 2]);
-        r2 += pt[4 * k + 3];
-    }
-    if (cinf < A.tol_p && sqrt(r2) < A.tol_d) {
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * TPB + (threadIdx.x >> 6);
+    if (t >= A.B || A.status[t] != ACTIVE) return;                 // wave-uniform
+    double cost = 0.0, c1 = 0.0, cinf = 0.0, r2 = 0.0;
+    for (int k = lane; k < A.N; k += 64) expand_knot(A, (int)t, k, cost, c1, cinf, r2);
+    const double f = wave_sum(cost), cs = wave_sum(c1), cm = wave_max(cinf), rs = wave_sum(r2);
+    if (lane != 0) return;
+    if (cm < A.tol_p && sqrt(rs) < A.tol_d) {
         A.status[t] = CONVERGED;
         return;
     }
-    A.phi0[t] = f + A.mu * c1;
-    A.dphi[t] = -A.mu * c1;          // + ∇fᵀdz once the step is known (sqp_ls1_kernel)
+    A.phi0[t] = f + A.mu * cs;
+    A.dphi[t] = -A.mu * cs;          // + ∇fᵀdz once the step is known (sqp_ls1_kernel)
     atomicAdd(A.n_active, 1);
-}
-
-__device__ __forceinline__ void accept(const Args &A, int64_t t, const KnotPt &p)
-{
-    const int64_t NN = nn(A.N), P = np_(A.N);
-    double *z = A.Z + t * NN;
-    for (int64_t i = 0; i < NN; ++i) z[i] = p.at(i);
-    for (int64_t i = 0; i < P; ++i) A.lam[t * P + i] = A.lamn[t * P + i];
-    A.iters[t] += 1;
 }
 
 // ---------------------------------------------------------------- line search, full step
 // ϕ′ = ∇fᵀdz − μ‖c‖₁ (dubins_sqp.jl:61); Armijo at α = 1 (:79); otherwise the constraint
 // values at z + dz go to y for the second-order-correction solve.
-__global__ __launch_bounds__(256) void sqp_ls1_kernel(const Args A)
+__global__ __launch_bounds__(64 * TPB) void sqp_ls1_kernel(const Args A)
 {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * TPB + (threadIdx.x >> 6);
     if (t >= A.B) return;
-    A.need_soc[t] = 0;
+    if (lane == 0) A.need_soc[t] = 0;
     if (A.status[t] != ACTIVE) return;
     const int N = A.N;
     const int64_t NN = nn(N), P = np_(N);
     const double *z = A.Z + t * NN, *dz = A.dz + t * NN, *g = A.g + t * NN;
     double gd = 0.0;
-    for (int64_t i = 0; i < NN; ++i) gd += g[i] * dz[i];
-    const double dphi = gd + A.dphi[t];
-    A.dphi[t] = dphi;
+    for (int64_t i = lane; i < NN; i += 64) gd += g[i] * dz[i];
+    const double dphi = wave_sum(gd) + A.dphi[t];
     const KnotPt p1{z, dz, nullptr, 1.0, 0.0};
-    if (merit(A, (int)t, p1) <= A.phi0[t] + ETA * dphi) {
-        accept(A, t, p1);
+    const double phi1 = merit(A, (int)t, p1, lane);
+    if (lane == 0) A.dphi[t] = dphi;
+    if (phi1 <= A.phi0[t] + ETA * dphi) {
+        accept(A, t, p1, lane);
         return;
     }
-    A.need_soc[t] = 1;
+    if (lane == 0) A.need_soc[t] = 1;
     double *y = A.y + t * P;
-    for (int k = 0; k < N; ++k) {
+    for (int k = lane; k < N; k += 64) {
         const int64_t o = (int64_t)W * k;
         double x[NX];
         for (int i = 0; i < NX; ++i) x[i] = p1.at(o + i);
@@ -313,27 +321,28 @@ __global__ __launch_bounds__(256) void sqp_ls1_kernel(const Args A)
 
 // ---------------------------------------------------------------- line search, SOC + backtracking
 // dubins_sqp.jl:82-94: z + dz + dẑ accepted on strict decrease below ϕ + ηϕ′; else α = ρ, ρ², …
-__global__ __launch_bounds__(256) void sqp_ls2_kernel(const Args A)
+__global__ __launch_bounds__(64 * TPB) void sqp_ls2_kernel(const Args A)
 {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * TPB + (threadIdx.x >> 6);
     if (t >= A.B || !A.need_soc[t]) return;
     const int64_t NN = nn(A.N);
     const double *z = A.Z + t * NN, *dz = A.dz + t * NN, *ds = A.dzs + t * NN;
     const double phi0 = A.phi0[t], dphi = A.dphi[t];
     const KnotPt ps{z, dz, ds, 1.0, 1.0};
-    if (merit(A, (int)t, ps) < phi0 + ETA * dphi) {
-        accept(A, t, ps);
+    if (merit(A, (int)t, ps, lane) < phi0 + ETA * dphi) {
+        accept(A, t, ps, lane);
         return;
     }
     double a = RHO;
     for (int i = 1; i < LS_TRIES; ++i, a *= RHO) {
         const KnotPt pa{z, dz, nullptr, a, 0.0};
-        if (merit(A, (int)t, pa) <= phi0 + ETA * a * dphi) {
-            accept(A, t, pa);
+        if (merit(A, (int)t, pa, lane) <= phi0 + ETA * a * dphi) {
+            accept(A, t, pa, lane);
             return;
         }
     }
-    A.status[t] = LS_FAILED;
+    if (lane == 0) A.status[t] = LS_FAILED;
 }
 
 __global__ __launch_bounds__(256) void sqp_init_kernel(const Args A)
@@ -386,16 +395,16 @@ hipError_t sqp_run(const SqpArgs &A0, int max_iters, hipStream_t s, int (*kkt)(v
     for (int it = 0; it < max_iters; ++it) {
         hipError_t e = hipMemsetAsync(A.n_active, 0, sizeof(int32_t), s);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(sqp_expand_kernel, grid_for(A.B * A.N), dim3(256), 0, s, A);
-        hipLaunchKernelGGL(sqp_check_kernel, grid_for(A.B), dim3(256), 0, s, A);
+        const dim3 gw((unsigned)((A.B + TPB - 1) / TPB)), bw(64 * TPB);
+        hipLaunchKernelGGL(sqp_expand_kernel, gw, bw, 0, s, A);
         if ((e = hipMemcpyAsync(&h_active, A.n_active, sizeof(int32_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
             (e = hipStreamSynchronize(s)) != hipSuccess)
             return e;
         if (h_active == 0) break;
         if ((*kkt_rc = kkt(ctx, 1, A.dz)) < 0) return hipSuccess;
-        hipLaunchKernelGGL(sqp_ls1_kernel, grid_for(A.B), dim3(256), 0, s, A);
+        hipLaunchKernelGGL(sqp_ls1_kernel, gw, bw, 0, s, A);
         if ((*kkt_rc = kkt(ctx, 0, A.dzs)) < 0) return hipSuccess;
-        hipLaunchKernelGGL(sqp_ls2_kernel, grid_for(A.B), dim3(256), 0, s, A);
+        hipLaunchKernelGGL(sqp_ls2_kernel, gw, bw, 0, s, A);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(sqp_finish_kernel, grid_for(A.B), dim3(256), 0, s, A);

@@ -82,3 +82,31 @@ def dubins_sqp_solve_device(prob: DubinsSQP, t: dict, stream: int | None = None)
                                          p(t["lam"]), p(t["iters"]), p(t["status"]),
                                          C.c_void_p(stream) if stream else None))
     return t
+
+
+def initial_guess(N: int, dt: float, x0, xf) -> np.ndarray:
+    """States interpolated from x0 to xf, controls at the straight-line speed and turn rate
+    (a guess that violates the dynamics; the SQP removes the violation)."""
+    x0, xf = np.asarray(x0, float), np.asarray(xf, float)
+    z = np.zeros(num_vars(N))
+    T = dt * (N - 1)
+    v = np.hypot(*(xf[:2] - x0[:2])) / T
+    om = (xf[2] - x0[2]) / T
+    for k in range(N):
+        s = k / (N - 1)
+        z[5 * k:5 * k + 3] = (1 - s) * x0 + s * xf
+        if k < N - 1:
+            z[5 * k + 3:5 * k + 5] = [v, om]
+    return z
+
+
+def random_dubins_batch(N: int, batch: int, seed: int, tf: float = 3.0):
+    """Synthetic cfg3-shaped SQP batch: x0 ~ N(0, 0.1²), goals uniform in [−4, 4]² × [−3, 3],
+    perturbed straight-line guesses.  Returns dt, x0, xf, Z0 (numpy, batch-major)."""
+    rng = np.random.default_rng(seed)
+    dt = tf / (N - 1)
+    x0 = 0.1 * rng.standard_normal((batch, 3))
+    xf = np.stack([rng.uniform(-4, 4, batch), rng.uniform(-4, 4, batch), rng.uniform(-3, 3, batch)], 1)
+    Z0 = np.stack([initial_guess(N, dt, x0[b], xf[b]) for b in range(batch)])
+    Z0 += 0.3 * rng.standard_normal(Z0.shape)
+    return dt, x0, xf, Z0
