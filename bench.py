@@ -291,11 +291,19 @@ def main():
                     "kernel_ms": kern_ms,
                     "flops_per_traj": dp_flops_per_traj(n, m, N),
                     "alg_bytes_per_launch": dp_bytes_per_traj(n, m, N, 8 if f64 else 4) * bt}
-            metric = METRIC if args.workload == "dp" else \
-                "LQR trajectories/sec (Riccati bwd+fwd), cartpole n=4 m=1 N=101 B=4096"
-            workload = ("random dense time-invariant LQR, Riccati backward pass + forward "
-                        "rollout (BASELINE.json configs[3])") if args.workload == "dp" else \
-                "cartpole LQR, RK3-linearised (BASELINE.json configs[1])"
+            headline = (n, m, N, bt, args.dtype) == (32, 16, 256, 65536, "f64")
+            if args.workload == "cartpole":
+                metric = f"LQR trajectories/sec (Riccati bwd+fwd), cartpole n=4 m=1 N={N} B={bt}"
+                workload = "cartpole LQR, RK3-linearised (BASELINE.json configs[1])"
+            elif headline:
+                metric = METRIC
+                workload = ("random dense time-invariant LQR, Riccati backward pass + forward "
+                            "rollout (BASELINE.json configs[3])")
+            else:
+                metric = f"LQR trajectories/sec (Riccati bwd+fwd), n={n} m={m} N={N} B={bt} {args.dtype}"
+                cfg5 = (n, m, N, args.dtype) == (64, 32, 512, "f32")
+                workload = ("random dense time-invariant LQR, Riccati backward pass + forward rollout"
+                            + (" (BASELINE.json configs[4], per GPU)" if cfg5 else " (non-baseline shape)"))
             cpu = cpu_baseline(n, m, N, target_s=args.cpu_seconds) \
                 if not args.no_cpu_baseline and world == 1 else None
         line = {
