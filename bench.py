@@ -37,9 +37,11 @@ def dp_flops_per_traj(n, m, N):
         + (N - 1) * (2 * n**2 + 4 * n * m)
 
 
-def dp_bytes_per_traj(n, m, N, s=8):
-    """SURVEY.md §8(d), time-invariant: read (3n²+nm+m²+n)s, write ((N−1)mn+Nn+(N−1)m+n²)s."""
-    return (3 * n * n + n * m + m * m + n) * s + ((N - 1) * m * n + N * n + (N - 1) * m + n * n) * s
+def dp_bytes_per_traj(n, m, N, s=8, tv=False):
+    """SURVEY.md §8(d), time-invariant: read (3n²+nm+m²+n)s, write ((N−1)mn+Nn+(N−1)m+n²)s;
+    time-varying: A, B, Q, R read once per knot (×(N−1))."""
+    rd = (2 * n * n + n * m + m * m) * ((N - 1) if tv else 1) + n * n + n
+    return rd * s + ((N - 1) * m * n + N * n + (N - 1) * m + n * n) * s
 
 
 def cpu_baseline(n, m, N, target_s=12.0, threads=None):
@@ -104,6 +106,9 @@ def main():
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     ap.add_argument("--seed", type=int, default=20260104)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--tv", action="store_true",
+                    help="dp: time-varying problem (per-knot A_k, B_k, Q_k, R_k; knot_stride 1, "
+                         "SURVEY §8(f) rank 1); default batch 16384 (65536 would need 376 GB)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     ap.add_argument("--workload", choices=["dp", "cartpole", "kkt", "sqp"], default="dp",
@@ -112,6 +117,8 @@ def main():
                          "kkt = Dubins block-tridiagonal KKT solve (configs[2], B=16384); "
                          "sqp = Dubins SQP around the KKT solve (SURVEY §8(f) ranks 2-3, B=16384)")
     args = ap.parse_args()
+    if args.tv and args.batch == 65536:
+        args.batch = 16384
     if args.workload == "cartpole":
         args.n, args.m, args.N = 4, 1, 101
         if args.batch == 65536:
@@ -161,6 +168,13 @@ def main():
         t = {k: torch.from_numpy(host[k]).to(dev) for k in ("A", "B", "Q", "R", "Qf", "x0")}
         t.update(n=n, m=m, batch=bt)
         del host
+        if args.tv:
+            # per-knot fields: every knot's block is its own copy in HBM (the kernel streams
+            # all N−1 of them), values = the time-invariant draw
+            for k in ("A", "B", "Q", "R"):
+                v = t[k].view(bt, 1, -1)
+                t[k] = v.expand(bt, N - 1, v.shape[-1]).contiguous().view(-1)
+            t.update(tv_AB=1, tv_QR=1)
         out = lqrx.dp_solve_device(t, N, p_mode=0, stream=sh)   # allocates outputs once
 
         def step():
@@ -293,8 +307,8 @@ def main():
                     "kernel": "dp_lane_kernel" if (n <= 4 and m <= 4) else "dp_riccati_kernel",
                     "kernel_ms": kern_ms,
                     "flops_per_traj": dp_flops_per_traj(n, m, N),
-                    "alg_bytes_per_launch": dp_bytes_per_traj(n, m, N, 8 if f64 else 4) * bt}
-            headline = (n, m, N, bt, args.dtype) == (32, 16, 256, 65536, "f64")
+                    "alg_bytes_per_launch": dp_bytes_per_traj(n, m, N, 8 if f64 else 4, args.tv) * bt}
+            headline = (n, m, N, bt, args.dtype) == (32, 16, 256, 65536, "f64") and not args.tv
             if args.workload == "cartpole":
                 metric = f"LQR trajectories/sec (Riccati bwd+fwd), cartpole n=4 m=1 N={N} B={bt}"
                 workload = "cartpole LQR, RK3-linearised (BASELINE.json configs[1])"
@@ -303,9 +317,11 @@ def main():
                 workload = ("random dense time-invariant LQR, Riccati backward pass + forward "
                             "rollout (BASELINE.json configs[3])")
             else:
-                metric = f"LQR trajectories/sec (Riccati bwd+fwd), n={n} m={m} N={N} B={bt} {args.dtype}"
+                metric = (f"LQR trajectories/sec (Riccati bwd+fwd), n={n} m={m} N={N} B={bt} {args.dtype}"
+                          + (", time-varying A_k B_k Q_k R_k" if args.tv else ""))
                 cfg5 = (n, m, N, args.dtype) == (64, 32, 512, "f32")
-                workload = ("random dense time-invariant LQR, Riccati backward pass + forward rollout"
+                workload = (("random dense time-varying LQR (SURVEY §8(f) rank 1)" if args.tv else
+                             "random dense time-invariant LQR") + ", Riccati backward pass + forward rollout"
                             + (" (BASELINE.json configs[4], per GPU)" if cfg5 else " (non-baseline shape)"))
             cpu = cpu_baseline(n, m, N, target_s=args.cpu_seconds) \
                 if not args.no_cpu_baseline and world == 1 else None
