@@ -175,6 +175,38 @@ int lqrx_dubins_sqp_solve_host(const lqrx_dubins_sqp_desc *desc, double *Z, cons
                                const double *xf, double *lam, int32_t *iters, int32_t *status);
 
 /* ------------------------------------------------------------------------------------
+ * Condensed least-squares LQR: replaces
+ * solve!(sol, ::LeastSquaresSolver, prob) (/root/reference/src/least_squares.jl:158-192)
+ * with opts :solve_type => :cholesky — Ā/b̄ as buildAb! builds them (:58-103),
+ * H = ĀᵀĀ + Hu, y = −Āᵀb̄ (:171-173), potrf/potrs 'U' (:181-182), rollout! (:197-202).
+ * One workgroup per trajectory with the whole problem in LDS: requires
+ * lqrx_ls_lds_bytes(n, m, N) <= 163840 (e.g. n=4, m=1, N ≤ 121; n=6, m=3, N ≤ 41).
+ *   hu_mode 0: Hu = 0 — a fresh LeastSquaresSolver (:44), the reference default; the
+ *              solve then carries no control cost
+ *           1: Hu = blkdiag(chol(R).U) — what build_least_squares! leaves (:121)
+ *           2: Hu = blkdiag(R) — the LQR cost; U then equals the DP rollout (extension)
+ * Inputs (device, layout 0, batch slowest, time-invariant): A n×n, B n×m, Q n×n, R m×m,
+ * Qf n×n, x0 n.  Outputs: U (N−1)·m per trajectory (sol.U_), X N·n (sol.X);
+ * Abar (N·n)×((N−1)·m) col-major and bbar N·n per trajectory when non-NULL (buildAb!'s Ā,
+ * b̄, for checks).  info[b]: 0 ok, j > 0 = potrf pivot j of H not positive, −1 = Q, Qf
+ * (or R for hu_mode 1) not positive definite (cholesky() throws there, :50-52).
+ * Return: 0 ok, 1 some info ≠ 0 (synchronous calls only), < 0 as above.
+ * ------------------------------------------------------------------------------------ */
+typedef struct lqrx_ls_desc {
+    int32_t n, m, N;
+    int32_t hu_mode;
+    int64_t batch;
+} lqrx_ls_desc;
+
+size_t lqrx_ls_lds_bytes(int32_t n, int32_t m, int32_t N);
+int lqrx_ls_solve(const lqrx_ls_desc *desc, const double *A, const double *B, const double *Q,
+                  const double *R, const double *Qf, const double *x0, double *U, double *X,
+                  int32_t *info, double *Abar, double *bbar, void *stream);
+int lqrx_ls_solve_host(const lqrx_ls_desc *desc, const double *A, const double *B,
+                       const double *Q, const double *R, const double *Qf, const double *x0,
+                       double *U, double *X, int32_t *info);
+
+/* ------------------------------------------------------------------------------------
  * Utilities
  * ------------------------------------------------------------------------------------ */
 int lqrx_abi_version(void);

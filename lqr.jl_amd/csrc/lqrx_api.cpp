@@ -664,3 +664,95 @@ extern "C" int lqrx_dubins_sqp_solve_host(const lqrx_dubins_sqp_desc *d, double 
         return hip_err(e, "sqp D2H");
     return 0;
 }
+
+
+// ------------------------------------------------------------------ condensed least squares
+namespace {
+constexpr size_t LS_LDS_MAX = 163840;
+
+int validate_ls(const lqrx_ls_desc *d)
+{
+    if (!d) return set_err(-1, "desc is NULL");
+    if (d->n < 1 || d->m < 1) return set_err(-1, "desc.n, desc.m must be >= 1 (got %d, %d)", d->n, d->m);
+    if (d->N < 2) return set_err(-1, "desc.N must be >= 2 (got %d)", d->N);
+    if (d->hu_mode < 0 || d->hu_mode > 2) return set_err(-1, "desc.hu_mode must be 0, 1 or 2");
+    if (d->batch < 0 || d->batch > 0x7fffffff) return set_err(-1, "desc.batch must be in [0, 2^31)");
+    const size_t lds = lqrx::ls_lds_bytes(d->n, d->m, d->N);
+    if (lds > LS_LDS_MAX)
+        return set_err(LQRX_ERR_UNSUPPORTED, "n=%d m=%d N=%d needs %zu B of LDS (> %zu)", d->n, d->m, d->N, lds,
+                       LS_LDS_MAX);
+    return 0;
+}
+} // namespace
+
+extern "C" size_t lqrx_ls_lds_bytes(int32_t n, int32_t m, int32_t N)
+{
+    if (n < 1 || m < 1 || N < 2) return 0;
+    return lqrx::ls_lds_bytes(n, m, N);
+}
+
+extern "C" int lqrx_ls_solve(const lqrx_ls_desc *d, const double *A, const double *B, const double *Q,
+                             const double *R, const double *Qf, const double *x0, double *U, double *X,
+                             int32_t *info, double *Abar, double *bbar, void *stream)
+{
+    int st = validate_ls(d);
+    if (st) return st;
+    if (d->batch == 0) return 0;
+    const double *in[6] = {A, B, Q, R, Qf, x0};
+    for (int i = 0; i < 6; ++i)
+        if (!in[i]) return set_err(-(i + 2), "input pointer %d is NULL", i + 2);
+    if (!U) return set_err(-8, "U is NULL");
+    if (!X) return set_err(-9, "X is NULL");
+    lqrx::LsArgs a{};
+    a.A = A; a.B = B; a.Q = Q; a.R = R; a.Qf = Qf; a.x0 = x0;
+    a.U = U; a.X = X; a.info = info; a.Ab = Abar; a.bb = bbar;
+    a.n = d->n; a.m = d->m; a.N = d->N; a.hu_mode = d->hu_mode; a.batch = d->batch;
+    hipError_t e = lqrx::ls_launch(a, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_err(e, "ls kernel launch");
+    if (stream == nullptr) {
+        if ((e = hipStreamSynchronize(nullptr)) != hipSuccess) return hip_err(e, "ls kernel");
+        if (info) {
+            std::vector<int32_t> h((size_t)d->batch);
+            if ((e = hipMemcpy(h.data(), info, h.size() * 4, hipMemcpyDeviceToHost)) != hipSuccess)
+                return hip_err(e, "info D2H");
+            for (int32_t v : h)
+                if (v) return 1;
+        }
+    }
+    return 0;
+}
+
+extern "C" int lqrx_ls_solve_host(const lqrx_ls_desc *d, const double *A, const double *B, const double *Q,
+                                  const double *R, const double *Qf, const double *x0, double *U, double *X,
+                                  int32_t *info)
+{
+    int st = validate_ls(d);
+    if (st) return st;
+    if (d->batch == 0) return 0;
+    const size_t bt = (size_t)d->batch, n = d->n, m = d->m, N = d->N;
+    const size_t szin[6] = {n * n, n * m, n * n, m * m, n * n, n};
+    const double *hin[6] = {A, B, Q, R, Qf, x0};
+    DevBuf din[6], dU, dX, dinfo;
+    for (int i = 0; i < 6; ++i) {
+        if (!hin[i]) return set_err(-(i + 2), "input pointer %d is NULL", i + 2);
+        if ((st = dev_alloc(din[i], szin[i] * 8 * bt, "hipMalloc input"))) return st;
+        hipError_t e = hipMemcpy(din[i].p, hin[i], szin[i] * 8 * bt, hipMemcpyHostToDevice);
+        if (e != hipSuccess) return hip_err(e, "H2D");
+    }
+    if (!U) return set_err(-8, "U is NULL");
+    if (!X) return set_err(-9, "X is NULL");
+    if ((st = dev_alloc(dU, (N - 1) * m * 8 * bt, "hipMalloc U"))) return st;
+    if ((st = dev_alloc(dX, N * n * 8 * bt, "hipMalloc X"))) return st;
+    if ((st = dev_alloc(dinfo, 4 * bt, "hipMalloc info"))) return st;
+    st = lqrx_ls_solve(d, (const double *)din[0].p, (const double *)din[1].p, (const double *)din[2].p,
+                       (const double *)din[3].p, (const double *)din[4].p, (const double *)din[5].p,
+                       (double *)dU.p, (double *)dX.p, (int32_t *)dinfo.p, nullptr, nullptr, nullptr);
+    if (st < 0) return st;
+    hipError_t e;
+    if ((e = hipMemcpy(U, dU.p, (N - 1) * m * 8 * bt, hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(X, dX.p, N * n * 8 * bt, hipMemcpyDeviceToHost)) != hipSuccess)
+        return hip_err(e, "D2H");
+    if (info && (e = hipMemcpy(info, dinfo.p, 4 * bt, hipMemcpyDeviceToHost)) != hipSuccess)
+        return hip_err(e, "D2H info");
+    return st;
+}

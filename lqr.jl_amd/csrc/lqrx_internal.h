@@ -94,4 +94,15 @@ hipError_t sqp_run(const SqpArgs &A, int max_iters, hipStream_t s, int (*kkt)(vo
 void sqp_structure(int N, std::vector<int32_t> &n1, std::vector<int32_t> &p, std::vector<int32_t> &n2,
                    std::vector<int32_t> &w);
 
+// ---- condensed least-squares LQR (lqrx_ls.hip) ----
+struct LsArgs {
+    const double *A, *B, *Q, *R, *Qf, *x0;
+    double *U, *X, *Ab, *bb;
+    int32_t *info;
+    int n, m, N, hu_mode;
+    int64_t batch;
+};
+size_t ls_lds_bytes(int n, int m, int N);
+hipError_t ls_launch(const LsArgs &a, hipStream_t s);
+
 } // namespace lqrx

@@ -49,6 +49,13 @@ class SqpDesc(C.Structure):
     ]
 
 
+class LsDesc(C.Structure):
+    """Mirror of ``lqrx_ls_desc``."""
+
+    _fields_ = [("n", C.c_int32), ("m", C.c_int32), ("N", C.c_int32), ("hu_mode", C.c_int32),
+                ("batch", C.c_int64)]
+
+
 _VP = C.c_void_p
 _SIGS = {
     "lqrx_abi_version": (C.c_int, []),
@@ -64,6 +71,9 @@ _SIGS = {
     "lqrx_kkt_solve_ws": (C.c_int, [C.POINTER(KktDesc)] + [_VP] * 7 + [_VP, C.c_size_t, _VP]),
     "lqrx_dubins_sqp_solve": (C.c_int, [C.POINTER(SqpDesc)] + [_VP] * 6 + [_VP]),
     "lqrx_dubins_sqp_solve_host": (C.c_int, [C.POINTER(SqpDesc)] + [_VP] * 6),
+    "lqrx_ls_lds_bytes": (C.c_size_t, [C.c_int32, C.c_int32, C.c_int32]),
+    "lqrx_ls_solve": (C.c_int, [C.POINTER(LsDesc)] + [_VP] * 11 + [_VP]),
+    "lqrx_ls_solve_host": (C.c_int, [C.POINTER(LsDesc)] + [_VP] * 9),
     "lqrx_make_random_dp": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_uint64,
                                       C.c_int32] + [_VP] * 6),
 }
@@ -99,7 +109,7 @@ def load() -> C.CDLL:
 def header_functions() -> list[str]:
     """Names of every function declared in include/lqrx.h."""
     src = open(HEADER_PATH).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(lqrx_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char \*)\s*(lqrx_\w+)\s*\(", src, re.M)))
 
 
 class LqrxError(RuntimeError):

@@ -22,7 +22,7 @@ from . import _lib
 
 __all__ = ["KktStructure", "KktProblem", "ConstraintBlocks", "dubins_structure",
            "double_integrator_structure", "random_kkt", "kkt_solve", "kkt_solve_device", "workspace_size",
-           "second_order_correction"]
+           "second_order_correction", "SparseSolver"]
 
 H_DENSE, H_BLOCKDIAG, H_DIAG = 0, 1, 2
 
@@ -203,3 +203,65 @@ def kkt_solve_device(st: KktStructure, t: dict, h_mode: int, ginv: int = 1,
     _lib.check(rc)
     out["rc"] = rc
     return out
+
+
+# ------------------------------------------------------------------ sparse formulation
+class SparseSolver:
+    """The SparseSolver formulation (/root/reference/src/sparse_solver.jl:120-246): one
+    global sparse constraint Jacobian D (P×NN, SparseConstraintSet :17-43), violation d,
+    block-diagonal cost Hessian G and gradient g over z = [x_1; u_1; …; x_N].  Its
+    `_solve!` (:267-292: HD = G⁻¹Dᵀ, S = D·HD, λ = S⁻¹(d − D G⁻¹g), δZ = −HD·λ − G⁻¹g) is
+    the same KKT system the block solver factors, so the device path gathers the per-knot
+    blocks — Dblocks[k] = D[off_k + (1:rows_k), zinds[k]] (:156-160), G's diagonal blocks
+    (Gblocks, :164) — into the packed layout and runs lqrx_kkt_solve.  Batched: D, d, G, g
+    are lists (one per trajectory) sharing `st`'s structure."""
+
+    def __init__(self, st: KktStructure, h_mode: int = H_DENSE):
+        self.st, self.h_mode = st, h_mode
+
+    def blocks(self, D, d, G, g) -> KktProblem:
+        """Global (D, d, G, g) of each trajectory → packed Y, y, H, g (batch axis first)."""
+        st, h_mode = self.st, self.h_mode
+        Ds, ds, Gs, gs = (x if isinstance(x, (list, tuple)) else [x] for x in (D, d, G, g))
+        bt = len(Ds)
+        sY, sy, sH, sg = st.sizes(h_mode)
+        Y = np.zeros((bt, sY)); y = np.zeros((bt, sy)); H = np.zeros((bt, sH)); gg = np.zeros((bt, sg))
+        for b in range(bt):
+            Db = Ds[b].tocsr() if hasattr(Ds[b], "tocsr") else np.asarray(Ds[b])
+            Gb = Gs[b].tocsr() if hasattr(Gs[b], "tocsr") else np.asarray(Gs[b])
+            dense = lambda M, r0, r1, c0, c1: (M[r0:r1, c0:c1].toarray() if hasattr(M, "toarray")
+                                               else np.asarray(M[r0:r1, c0:c1]))
+            oY = oy = oH = 0
+            off1 = off2 = 0
+            for k in range(st.N):
+                n1, p, n2, w = int(st.n1[k]), int(st.p[k]), int(st.n2[k]), int(st.w[k])
+                rows = n1 + p + n2
+                Y[b, oY:oY + rows * w] = dense(Db, off1, off1 + rows, off2, off2 + w).T.reshape(-1)
+                y[b, oy:oy + p + n2] = np.asarray(ds[b])[off1 + n1:off1 + rows]
+                Gk = dense(Gb, off2, off2 + w, off2, off2 + w)
+                if h_mode == H_DIAG:
+                    H[b, oH:oH + w] = np.diag(Gk)
+                    oH += w
+                else:
+                    H[b, oH:oH + w * w] = Gk.T.reshape(-1)
+                    oH += w * w
+                gg[b, off2:off2 + w] = np.asarray(gs[b])[off2:off2 + w]
+                oY += rows * w
+                oy += p + n2
+                off1 += n1 + p
+                off2 += w
+        return KktProblem(st, bt, h_mode, Y, y, H, gg)
+
+    def solve(self, D, d, G, g) -> dict:
+        """_solve!(::SparseSolver) (sparse_solver.jl:267-292) on the device: δZ, λ."""
+        return kkt_solve(self.blocks(D, d, G, g), ginv=1)
+
+    def second_order_correction(self, D, d) -> dict:
+        """second_order_correction!(::SparseSolver) (sparse_solver.jl:385-401):
+        δx̂ = −Dᵀ(DDᵀ)⁻¹d — the block solver's Ginv = false variant."""
+        st = self.st
+        NN = int(np.sum(st.w))
+        Ds = D if isinstance(D, (list, tuple)) else [D]
+        eye = [np.eye(NN)] * len(Ds)
+        zero = [np.zeros(NN)] * len(Ds)
+        return kkt_solve(self.blocks(D, d, eye, zero), ginv=0)
