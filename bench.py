@@ -111,15 +111,16 @@ def main():
                          "SURVEY §8(f) rank 1); default batch 16384 (65536 would need 376 GB)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    ap.add_argument("--workload", choices=["dp", "cartpole", "kkt", "sqp"], default="dp",
+    ap.add_argument("--workload", choices=["dp", "cartpole", "kkt", "sqp", "ls"], default="dp",
                     help="dp = random dense LQR (BASELINE configs[3], the headline); "
                          "cartpole = configs[1] (n=4 m=1 N=101 B=4096); "
                          "kkt = Dubins block-tridiagonal KKT solve (configs[2], B=16384); "
-                         "sqp = Dubins SQP around the KKT solve (SURVEY §8(f) ranks 2-3, B=16384)")
+                         "sqp = Dubins SQP around the KKT solve (SURVEY §8(f) ranks 2-3, B=16384); "
+                         "ls = condensed least-squares LQR on cartpole (SURVEY §8(f) rank 4, B=4096)")
     args = ap.parse_args()
     if args.tv and args.batch == 65536:
         args.batch = 16384
-    if args.workload == "cartpole":
+    if args.workload in ("cartpole", "ls"):
         args.n, args.m, args.N = 4, 1, 101
         if args.batch == 65536:
             args.batch = 4096
@@ -152,7 +153,19 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
-    if args.workload in ("dp", "cartpole"):
+    if args.workload == "ls":
+        from lqrx import ls as LS
+        from lqrx.models import cartpole_batch
+        from lqrx.dp import to_abi
+        cb = cartpole_batch(bt, N, seed=args.seed + rank)
+        t = {k: torch.from_numpy(to_abi(getattr(cb, k)).ravel()).to(dev) for k in ("A", "B", "Q", "R", "Qf")}
+        t["x0"] = torch.from_numpy(cb.x0.ravel()).to(dev)
+        t.update(n=n, m=m, batch=bt)
+        out = LS.ls_solve_device(t, N, hu_mode=LS.HU_ZERO, stream=sh)
+
+        def step():
+            LS.ls_solve_device(t, N, hu_mode=LS.HU_ZERO, stream=sh, out=out)
+    elif args.workload in ("dp", "cartpole"):
         tdt = torch.float64 if f64 else torch.float32
         if args.workload == "dp":
             host = lqrx.random_batch(n, m, N, bt, seed=args.seed, traj0=rank * bt,
@@ -269,6 +282,29 @@ def main():
                 cpu = {"value": nb / el, "unit": "trajectories/s", "cores": 1, "kind": "port",
                        "sample": f"{nb} trajectories, oracle/sqp_oracle.py (numpy dense KKT restatement of "
                                  f"test/dubins_sqp.jl), {el:.1f} s"}
+        elif args.workload == "ls":
+            Nm, Nn = (N - 1) * m, N * n
+            # reference op count (least_squares.jl:171-182): ĀᵀĀ as a dense gemm, Āᵀb̄, potrf, potrs
+            fl = 2.0 * Nn * Nm * Nm + 2.0 * Nn * Nm + Nm ** 3 / 3.0 + 2.0 * Nm * Nm
+            achieved = fl * bt / (kern_ms * 1e-3) / 1e12
+            roof = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                    "frac": achieved / PEAK_FP64_TFLOPS, "traffic": None,
+                    "kernel": "ls_condensed_kernel (fp64 VALU, LDS-resident H)", "kernel_ms": kern_ms,
+                    "flops_per_traj": fl}
+            metric = f"condensed least-squares LQR solves/sec (cartpole n=4 m=1 N={N} B={bt}, Hu=0 as a fresh solver)"
+            workload = "LeastSquaresSolver solve! on cartpole (SURVEY.md 8(f) rank 4)"
+            cpu = None
+            if not args.no_cpu_baseline and world == 1:
+                sys.path.insert(0, ROOT)
+                from oracle import ls_oracle as LO
+                nb, t0c = 0, time.perf_counter()
+                while time.perf_counter() - t0c < min(args.cpu_seconds, 5.0) and nb < bt:
+                    LO.ls_solve(cb.A[nb], cb.B[nb], cb.Q[nb], cb.R[nb], cb.Qf[nb], cb.x0[nb], N)
+                    nb += 1
+                el = time.perf_counter() - t0c
+                cpu = {"value": nb / el, "unit": "trajectories/s", "cores": 1, "kind": "port",
+                       "sample": f"{nb} cartpole trajectories, oracle/ls_oracle.py (numpy restatement of "
+                                 f"least_squares.jl solve!, OpenBLAS), {el:.1f} s"}
         elif args.workload == "kkt":
             import lqrx.kkt as K
             sY, sy, sH, sg = K.dubins_structure(N).sizes(K.H_DIAG)

@@ -14,10 +14,10 @@
 // (l ≤ K−1), K = N−1 controls,
 //   H[(c1,a),(c2,b)] = Σ_{r=max(c1,c2)+1}^{K−1} (V_q[r−1−c1]ᵀ V_q[r−1−c2])_{ab}
 //                      + (V_f[K−1−c1]ᵀ V_f[K−1−c2])_{ab}
-// which is ĀᵀĀ summed by row blocks, one element of H's upper triangle per thread-iteration;
-// the Cholesky is right-looking over LDS columns, the triangular solves one column per
-// barrier.  Bound: LDS bandwidth of the
-// O(K³n m²/3) ĀᵀĀ sum; one workgroup per CU when H is large.  Ā and b̄ can be written out
+// which is ĀᵀĀ summed by row blocks (a prefix sum along each block diagonal, below);
+// H is stored packed (upper triangle); the Cholesky is right-looking over LDS columns, the triangular solves one column per
+// barrier.  Bound: the Nm-step
+// Cholesky / substitution barrier chain; one workgroup per CU when H is large.  Ā and b̄ can be written out
 // (optional) for a direct buildAb! parity check.
 #include "lqrx_internal.h"
 #include <math.h>
@@ -27,6 +27,38 @@ namespace lqrx {
 namespace {
 
 constexpr int LS_THREADS = 256;
+constexpr int LS_MAX_NM = 192; // (N−1)·m; LDS binds first (H is Nm² doubles: Nm ≤ 143)
+
+// order one wave's LDS accesses across lanes (a wave executes LDS ops in order; this stops
+// the compiler from moving them across and waits for the writes)
+__device__ inline void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// element j of a wave-distributed vector (lane l, slot s ↔ index l + 64 s), j wave-uniform.
+// Every slot is read out by readlane and the scalar results selected: selecting the slot
+// first made the compiler index the array dynamically (through scratch).
+__device__ inline double readlane_d(double v, int lane)
+{
+    const long long bits = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)bits, lane);
+    const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int S>
+__device__ inline double bcast_slot(const double (&v)[S], int j)
+{
+    double sel = readlane_d(v[0], j & 63);
+#pragma unroll
+    for (int s = 1; s < S; ++s) {
+        const double r = readlane_d(v[s], j & 63);
+        sel = (j >> 6) == s ? r : sel;
+    }
+    return sel;
+}
 
 struct LsLayout {
     int n, m, N, K, Nm, Nn;
@@ -49,14 +81,18 @@ __host__ __device__ inline LsLayout ls_layout(int n, int m, int N)
     L.oVq = o; o += (L.K > 1 ? L.K - 1 : 1) * n * m;
     L.oVf = o; o += L.K * n * m;
     L.obb = o; o += N * n;
+    L.oX = L.obb;   // X (rollout) reuses b̄'s space: b̄ is dead once y = −Āᵀb̄ is formed
     L.oH = o;  // also stages Q, Qf, R for the small factorisations
-    o += L.Nm * L.Nm > 2 * n * n + m * m ? L.Nm * L.Nm : 2 * n * n + m * m;
+    const int hp = L.Nm * (L.Nm + 1) / 2;   // packed upper triangle, column-major
+    o += hp > 2 * n * n + m * m ? hp : 2 * n * n + m * m;
     L.oy = o; o += L.Nm;
-    L.oX = o; o += N * n;
     L.oFlag = o; o += 1;
     L.total = o;
     return L;
 }
+
+// packed upper-triangular index of (i, k), i ≤ k: columns stored contiguously
+__device__ inline int up(int i, int k) { return (k * (k + 1) >> 1) + i; }
 
 // upper Cholesky of a small s×s column-major matrix in LDS (thread 0 only); returns false
 // when a pivot is not positive (cholesky() throws PosDefException there, :50-52)
@@ -121,37 +157,41 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
     }
 
     // ---- buildAb! :70-101: powers P_l = A^l B, w_r = A^r x0; V_q, V_f and b̄ = S_r w_r
-    for (int i = tid; i < nm; i += LS_THREADS) Pl[i] = B[i];
-    __syncthreads();
-    for (int l = 0; l <= K; ++l) {
-        const double *P = Pl + (l & 1) * nm, *w = W + (l & 1) * n;
-        double *Pn = Pl + ((l + 1) & 1) * nm, *wn = W + ((l + 1) & 1) * n;
-        // b̄ row block l: S_l·A^l·x0 (S = Sf for the last block, :71-75)
-        const double *S = l < K ? Sq : Sf;
-        for (int i = tid; i < n; i += LS_THREADS) {
-            double v = 0.0;
-            for (int j = i; j < n; ++j) v = fma(S[i + j * n], w[j], v);
-            bb[l * n + i] = v;
+    // a serial chain of K+1 tiny steps: wave 0 alone, wave-level ordering instead of barriers
+    if (tid < 64) {
+        for (int i = tid; i < nm; i += 64) Pl[i] = B[i];
+        wave_sync();
+        for (int l = 0; l <= K; ++l) {
+            const double *P = Pl + (l & 1) * nm, *w = W + (l & 1) * n;
+            double *Pn = Pl + ((l + 1) & 1) * nm, *wn = W + ((l + 1) & 1) * n;
+            // b̄ row block l: S_l·A^l·x0 (S = Sf for the last block, :71-75)
+            const double *S = l < K ? Sq : Sf;
+            for (int i = tid; i < n; i += 64) {
+                double v = 0.0;
+                for (int j = i; j < n; ++j) v = fma(S[i + j * n], w[j], v);
+                bb[l * n + i] = v;
+            }
+            for (int e = tid; e < 2 * nm; e += 64) {
+                const int which = e / nm, ea = e - which * nm, i = ea % n, a = ea / n;
+                if (l >= K || (which == 0 && l >= K - 1)) continue;
+                const double *S2 = which ? Sf : Sq;
+                double v = 0.0;
+                for (int j = i; j < n; ++j) v = fma(S2[i + j * n], P[j + a * n], v);
+                (which ? Vf : Vq)[l * nm + ea] = v;
+            }
+            // next powers (:101): P_{l+1} = A·P_l, w_{l+1} = A·w_l
+            for (int e = tid; e < nm + n; e += 64) {
+                const bool isw = e >= nm;
+                const int ea = isw ? e - nm : e, i = ea % n, a = ea / n;
+                const double *src = isw ? w : P + a * n;
+                double v = 0.0;
+                for (int j = 0; j < n; ++j) v = fma(A[i + j * n], src[j], v);
+                if (isw) wn[i] = v; else Pn[ea] = v;
+            }
+            wave_sync();
         }
-        for (int e = tid; e < 2 * nm; e += LS_THREADS) {
-            const int which = e / nm, ea = e - which * nm, i = ea % n, a = ea / n;
-            if (l >= K || (which == 0 && l >= K - 1)) continue;
-            const double *S2 = which ? Sf : Sq;
-            double v = 0.0;
-            for (int j = i; j < n; ++j) v = fma(S2[i + j * n], P[j + a * n], v);
-            (which ? Vf : Vq)[l * nm + ea] = v;
-        }
-        // next powers (:101): P_{l+1} = A·P_l, w_{l+1} = A·w_l
-        for (int e = tid; e < nm + n; e += LS_THREADS) {
-            const bool isw = e >= nm;
-            const int ea = isw ? e - nm : e, i = ea % n, a = ea / n;
-            const double *src = isw ? w : P + a * n;
-            double v = 0.0;
-            for (int j = 0; j < n; ++j) v = fma(A[i + j * n], src[j], v);
-            if (isw) wn[i] = v; else Pn[ea] = v;
-        }
-        __syncthreads();
     }
+    __syncthreads();
 
     // optional outputs: Ā (Nn×Nm col-major) and b̄, as buildAb! leaves them
     if (gAb) {
@@ -171,27 +211,29 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
     if (gbb)
         for (int e = tid; e < L.Nn; e += LS_THREADS) gbb[b * L.Nn + e] = bb[e];
 
-    // ---- H = ĀᵀĀ + Hu (:171-172), upper triangle (potrf 'U' reads no other), one element
-    // per thread-iteration, consecutive threads down a column
-    const int ntri = Nm * (Nm + 1) / 2;
-    for (int t = tid; t < ntri; t += LS_THREADS) {
-        int q = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-        while (q * (q + 1) / 2 > t) --q;
-        while ((q + 1) * (q + 2) / 2 <= t) ++q;
-        const int p = t - q * (q + 1) / 2;
-        const int c1 = p / m, a1 = p - c1 * m, c2 = q / m, a2 = q - c2 * m;
-        const int r0 = (c1 > c2 ? c1 : c2) + 1;
-        double v = 0.0;
-        for (int r = r0; r < K; ++r) {
-            const double *v1 = Vq + (r - 1 - c1) * nm + a1 * n;
-            const double *v2 = Vq + (r - 1 - c2) * nm + a2 * n;
-            for (int i = 0; i < n; ++i) v = fma(v1[i], v2[i], v);
+    // ---- H = ĀᵀĀ + Hu (:171-172), upper triangle (potrf 'U' reads no other).  Along a block
+    // diagonal d = c2 − c1 the Q-rows part is a prefix sum: with s = r−1−c2,
+    //   H_q(c1, c2) = Σ_{s=0}^{K−2−c2} V_q[s+d]ᵀ V_q[s]
+    // so one thread per (d, a1, a2) scans s upward and emits H(c2−d, c2) for c2 = K−2−s —
+    // O(K²nm²) instead of the O(K³nm²) of a dense ĀᵀĀ (same sum, accumulated in s order).
+    for (int e = tid; e < K * mm; e += LS_THREADS) {
+        const int d = e / mm, a12 = e - d * mm, a1 = a12 % m, a2 = a12 / m;
+        if (d == 0 && a1 > a2) continue;
+        const double hu = d == 0 ? Hu[a1 + a2 * m] : 0.0;
+        auto emit = [&](int c2, double q) {
+            const int c1 = c2 - d;
+            const double *f1 = Vf + (K - 1 - c1) * nm + a1 * n, *f2 = Vf + (K - 1 - c2) * nm + a2 * n;
+            double v = q;
+            for (int i = 0; i < n; ++i) v = fma(f1[i], f2[i], v);
+            H[up(c1 * m + a1, c2 * m + a2)] = v + hu;
+        };
+        if (K - 1 - d >= 0) emit(K - 1, 0.0);          // last control: Qf row only
+        double acc = 0.0;
+        for (int s2 = 0; s2 <= K - 2 - d; ++s2) {
+            const double *v1 = Vq + (s2 + d) * nm + a1 * n, *v2 = Vq + s2 * nm + a2 * n;
+            for (int i = 0; i < n; ++i) acc = fma(v1[i], v2[i], acc);
+            emit(K - 2 - s2, acc);
         }
-        const double *f1 = Vf + (K - 1 - c1) * nm + a1 * n;
-        const double *f2 = Vf + (K - 1 - c2) * nm + a2 * n;
-        for (int i = 0; i < n; ++i) v = fma(f1[i], f2[i], v);
-        if (c1 == c2) v += Hu[a1 + a2 * m];
-        H[p + q * Nm] = v;
     }
     // y = −Āᵀb̄ (:173): y[(c,a)] = −Σ_{r>c} (S_r A^{r−1−c} B)ᵀ_a · b̄_r
     for (int pidx = tid; pidx < Nm; pidx += LS_THREADS) {
@@ -207,49 +249,85 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
     if (tid == 0) *flag = 0;
     __syncthreads();
 
-    // ---- potrf 'U' (:181): right-looking over columns; info = first non-positive pivot
+    // ---- potrf 'U' (:181): right-looking, one barrier per pivot.  Step j updates the trailing
+    // upper triangle with the unscaled row j (H[i,k] −= H[j,i]·H[j,k]/d_j) and scales row j−1
+    // (read by nobody in step j); info = first non-positive pivot.  Waves own columns, lanes
+    // rows (contiguous LDS within a column).
+    const int wave = tid >> 6, lane = tid & 63;
+    double dprev = 1.0;
     for (int j = 0; j < Nm; ++j) {
-        const double d = H[j + j * Nm];
+        const double d = H[up(j, j)];
         if (!(d > 0.0)) {   // uniform: every thread reads the same LDS word
             if (tid == 0 && ginfo) ginfo[b] = j + 1;
             return;
         }
-        const double rd = 1.0 / sqrt(d);
-        // scale row j right of the diagonal, then the trailing update of the upper triangle
-        for (int k = j + 1 + tid; k < Nm; k += LS_THREADS) H[j + k * Nm] *= rd;
-        __syncthreads();
-        if (tid == 0) H[j + j * Nm] = d * rd;
-        const int tr = Nm - j - 1, ntr = tr * (tr + 1) / 2;
-        for (int t = tid; t < ntr; t += LS_THREADS) {
-            int kk = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-            while (kk * (kk + 1) / 2 > t) --kk;
-            while ((kk + 1) * (kk + 2) / 2 <= t) ++kk;
-            const int ii = t - kk * (kk + 1) / 2;
-            const int i = j + 1 + ii, k = j + 1 + kk;
-            H[i + k * Nm] = fma(-H[j + i * Nm], H[j + k * Nm], H[i + k * Nm]);
+        const double rinv = 1.0 / d;
+        if (j > 0) {
+            const double rdp = 1.0 / sqrt(dprev);
+            for (int k = j + tid; k < Nm; k += LS_THREADS) H[up(j - 1, k)] *= rdp;
+            if (tid == 0) H[up(j - 1, j - 1)] = dprev * rdp;
         }
+        // 4 columns per wave pass: the 4 independent LDS read-modify-writes per lane overlap
+        for (int k0 = j + 1 + 4 * wave; k0 < Nm; k0 += 4 * (LS_THREADS / 64)) {
+            double hk[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) hk[u] = k0 + u < Nm ? H[up(j, k0 + u)] * rinv : 0.0;
+            const int kmax = k0 + 3 < Nm ? k0 + 3 : Nm - 1;
+            for (int i = j + 1 + lane; i <= kmax; i += 64) {
+                const double hji = H[up(j, i)];
+                double h[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (i <= k0 + u && k0 + u < Nm) h[u] = H[up(i, k0 + u)];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (i <= k0 + u && k0 + u < Nm) H[up(i, k0 + u)] = fma(-hji, hk[u], h[u]);
+            }
+        }
+        dprev = d;
         __syncthreads();
     }
-    // ---- potrs 'U' (:182): Uᵀz = y, then U x = z
-    for (int j = 0; j < Nm; ++j) {
-        const double zj = y[j] / H[j + j * Nm];
-        for (int k = j + 1 + tid; k < Nm; k += LS_THREADS) y[k] = fma(-H[j + k * Nm], zj, y[k]);
-        __syncthreads();
-        if (tid == 0) y[j] = zj;
-    }
+    if (tid == 0) H[up(Nm - 1, Nm - 1)] = sqrt(dprev);
     __syncthreads();
-    for (int j = Nm - 1; j >= 0; --j) {
-        const double xj = y[j] / H[j + j * Nm];
-        for (int i = tid; i < j; i += LS_THREADS) y[i] = fma(-H[i + j * Nm], xj, y[i]);
-        __syncthreads();
-        if (tid == 0) y[j] = xj;
+    // ---- potrs 'U' (:182): Uᵀz = y, then U x = z — wave 0, y held in registers (lane l owns
+    // y[l + 64 s]), the pivot broadcast by readlane: no barriers in the 2·Nm-step chain
+    if (tid < 64) {
+        constexpr int S = LS_MAX_NM / 64;
+        double yr[S];
+#pragma unroll
+        for (int s2 = 0; s2 < S; ++s2) {
+            const int idx = lane + 64 * s2;
+            yr[s2] = idx < Nm ? y[idx] : 0.0;
+        }
+        for (int j = 0; j < Nm; ++j) {
+            const double zj = bcast_slot<S>(yr, j) / H[up(j, j)];
+#pragma unroll
+            for (int s2 = 0; s2 < S; ++s2) {
+                const int idx = lane + 64 * s2;
+                if (idx > j && idx < Nm) yr[s2] = fma(-H[up(j, idx)], zj, yr[s2]);
+                else if (idx == j) yr[s2] = zj;
+            }
+        }
+        for (int j = Nm - 1; j >= 0; --j) {
+            const double xj = bcast_slot<S>(yr, j) / H[up(j, j)];
+#pragma unroll
+            for (int s2 = 0; s2 < S; ++s2) {
+                const int idx = lane + 64 * s2;
+                if (idx < j) yr[s2] = fma(-H[up(idx, j)], xj, yr[s2]);
+                else if (idx == j) yr[s2] = xj;
+            }
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < S; ++s2) {
+            const int idx = lane + 64 * s2;
+            if (idx < Nm) y[idx] = yr[s2];
+        }
+        wave_sync();
     }
-    __syncthreads();
     // ---- rollout! (:197-202), one wave (n ≤ 64 lanes per row sweep)
     if (tid < 64) {
         for (int i = tid; i < n; i += 64) X[i] = gx0[b * n + i];
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        wave_sync();
         for (int k = 0; k < K; ++k) {
             const double *xk = X + k * n, *uk = y + k * m;
             for (int i = tid; i < n; i += 64) {
@@ -258,9 +336,7 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
                 for (int a = 0; a < m; ++a) v = fma(B[i + a * n], uk[a], v);
                 X[(k + 1) * n + i] = v;
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            wave_sync();
         }
     }
     __syncthreads();

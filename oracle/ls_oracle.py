@@ -122,8 +122,11 @@ def ls_solve(A, B, Q, R, Qf, x0, N, hu=HU_ZERO, matbuild="Ab"):
     H = Ab.T @ Ab + Hu                             # :171-172
     y = -(Ab.T @ bb)                               # :173
     info = 0
+    # potrf 'U' reads only the upper triangle of H (:181); with Hu = chol(R).U the matrix
+    # H .+= Hu is not symmetric, so symmetrise from the upper triangle as LAPACK sees it
+    Hs = np.triu(H) + np.triu(H, 1).T
     try:                                           # :177-183 potrf 'U' / potrs 'U'
-        Uc = np.linalg.cholesky(H).T
+        Uc = np.linalg.cholesky(Hs).T
         z = np.linalg.solve(Uc.T, y)
         u = np.linalg.solve(Uc, z)
     except np.linalg.LinAlgError:
