@@ -129,6 +129,35 @@ function kkt_solve!(dz::Matrix{Float64}, lam::Matrix{Float64}, info::Vector{Int3
     return check(rc)
 end
 
-export LQRProblem, LQRSolution, LQRBatch, DPSolver, solve!, kkt_solve!
+# ---- condensed least squares: lqrx_ls_desc ----
+struct LsDesc
+    n::Int32; m::Int32; N::Int32; hu_mode::Int32
+    batch::Int64
+end
+
+"""
+    ls_solve!(U, X, info, A, B, Q, R, Qf, x0, N; hu_mode=0)
+
+solve!(sol, ::LeastSquaresSolver, prob) (src/least_squares.jl:158-192) for a batch:
+A (n,n,batch), B (n,m,batch), Q, R, Qf, x0 (n,batch) → U ((N-1)m, batch) = sol.U_,
+X (nN, batch).  hu_mode 0 = a fresh solver (Hu = 0, :44), 1 = after build_least_squares!
+(Hu = chol(R).U blocks, :121), 2 = R blocks (the LQR cost).
+"""
+function ls_solve!(U::Matrix{Float64}, X::Matrix{Float64}, info::Vector{Int32},
+                   A::Array{Float64,3}, B::Array{Float64,3}, Q::Array{Float64,3},
+                   R::Array{Float64,3}, Qf::Array{Float64,3}, x0::Matrix{Float64}, N::Integer;
+                   hu_mode::Integer=0)
+    n, m, batch = size(B)
+    d = Ref(LsDesc(n, m, N, hu_mode, batch))
+    GC.@preserve A B Q R Qf x0 U X info begin
+        rc = ccall((:lqrx_ls_solve_host, liblqrx), Cint,
+                   (Ref{LsDesc}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                    Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}),
+                   d, A, B, Q, R, Qf, x0, U, X, info)
+    end
+    return check(rc)
+end
+
+export LQRProblem, LQRSolution, LQRBatch, DPSolver, solve!, kkt_solve!, ls_solve!
 
 end # module
