@@ -44,6 +44,15 @@ def dp_bytes_per_traj(n, m, N, s=8, tv=False):
     return rd * s + ((N - 1) * m * n + N * n + (N - 1) * m + n * n) * s
 
 
+def _dp_kernel_name(n, m, bt, tv):
+    """Which DP kernel lqrx_dp_solve dispatches to (mirrors dp_launch / dp_lane_launch)."""
+    if n <= 4 and m <= 4:
+        small = os.environ.get("LQRX_DP_SMALL", "")
+        quad = n >= 3 and not tv and (small.startswith("q") or (not small.startswith("l") and bt <= 16384))
+        return "dp_quad_kernel" if quad else "dp_lane_kernel"
+    return "dp_riccati_kernel"
+
+
 def cpu_baseline(n, m, N, target_s=12.0, threads=None):
     """Time the CPU oracle (C restatement of dynamic_programming.jl, OpenMP over the batch)
     on a bounded sample of the same workload; returns traj/s and the sample description."""
@@ -340,7 +349,7 @@ def main():
                     traffic = None
             roof = {"bound": "mfma", "achieved": achieved, "peak": peak,
                     "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
-                    "kernel": "dp_lane_kernel" if (n <= 4 and m <= 4) else "dp_riccati_kernel",
+                    "kernel": _dp_kernel_name(n, m, bt, args.tv),
                     "kernel_ms": kern_ms,
                     "flops_per_traj": dp_flops_per_traj(n, m, N),
                     "alg_bytes_per_launch": dp_bytes_per_traj(n, m, N, 8 if f64 else 4, args.tv) * bt}

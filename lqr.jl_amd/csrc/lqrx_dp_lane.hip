@@ -18,6 +18,7 @@
 // matrices instead of keeping them in registers.
 #include "lqrx_internal.h"
 #include "lqrx_tile.h"
+#include <cstdlib>
 
 namespace lqrx {
 
@@ -299,6 +300,242 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// dp_quad_kernel: FOUR LANES PER TRAJECTORY (a DPP quad), n ∈ {3, 4}, time-invariant.
+// With one lane per trajectory a B = 4096 batch is 64 waves — one per CU on a quarter of
+// the chip, each a serial ~160-FMA-per-knot chain.  Here lane q of the quad owns column q
+// of everything that splits by columns and the small m-sized work is replicated:
+//   replicated: PB = P·B, E = R + BᵀPB, G = PBᵀA (= BᵀPA for symmetric P), potrf of E
+//   column q:   PA[:,q] = P·A[:,q]; Kq = E⁻¹G[:,q]; P_[:,q] = Q[:,q] + Aᵀ·PA[:,q] − Gᵀ·Kq
+// then P_ is re-replicated by four DPP quad broadcasts of the lower-triangle columns (lane r
+// supplies column r).  Rollout: x replicated, lane q computes x_{k+1}[q] = A[q,:]x + B[q,:]u
+// and the quad broadcasts re-assemble x.  Same reference lines as dp_lane_kernel.
+template <int CTRL>
+__device__ __forceinline__ double qbcast(double v)
+{
+    const long long x = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(x >> 32), CTRL, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int CTRL>
+__device__ __forceinline__ float qbcast(float v)
+{
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+// quad_perm [r,r,r,r]: every lane of the quad reads lane r
+template <int R, typename T>
+__device__ __forceinline__ T qfrom(T v) { return qbcast<R | (R << 2) | (R << 4) | (R << 6)>(v); }
+
+template <typename T, int MP>
+__global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
+{
+    constexpr int NP = 4;
+    const int64_t b = ((int64_t)blockIdx.x * 64 + threadIdx.x) >> 2;
+    const int q = threadIdx.x & 3;
+    if (b >= a.batch) return;   // whole quads retire together; DPP stays inside the quad
+    const int n = a.n, m = a.m, N = a.N;
+    const int64_t nn = (int64_t)n * n, nm = (int64_t)n * m, mm = (int64_t)m * m;
+    const T *Ag = (const T *)a.A + b * nn, *Bg = (const T *)a.B + b * nm;
+    const T *Qg = (const T *)a.Q + b * nn, *Rg = (const T *)a.R + b * mm;
+
+    T A[NP][NP], B[NP][MP], R[MP][MP], P[NP][NP];
+    lane_load<T, NP, NP>(P, (const T *)a.Qf + b * nn, n, n, (T)0);   // :58 P = Qf
+    lane_load<T, NP, NP>(A, Ag, n, n, (T)0);
+    lane_load<T, NP, MP>(B, Bg, n, m, (T)0);
+    lane_load<T, MP, MP>(R, Rg, m, m, (T)1);
+    // this lane's column of A and Q, row of A and B (dynamic q → loaded, not indexed)
+    T Acol[NP], Qcol[NP], Arow[NP], Brow[MP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const bool ok = i < n && q < n;
+        Acol[i] = ok ? Ag[i + q * n] : (T)0;
+        Qcol[i] = ok ? Qg[i + q * n] : (T)0;
+        Arow[i] = ok ? Ag[q + i * n] : (T)0;
+    }
+#pragma unroll
+    for (int c = 0; c < MP; ++c) Brow[c] = (q < n && c < m) ? Bg[q + c * n] : (T)0;
+
+    T *Kb = (T *)a.K + b * (int64_t)(N - 1) * nm;
+    T *Pall = a.p_all ? (T *)a.P + b * nn * N : nullptr;
+#define PS(i, j) ((i) >= (j) ? P[i][j] : P[j][i])
+    auto store_Pcol = [&](T *dst) {   // lane q writes column q
+        if (q >= n) return;
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            T v = P[i][0];
+#pragma unroll
+            for (int r = 1; r < NP; ++r) v = q == r ? PS(i, r) : v;
+            if (q == 0) v = PS(i, 0);
+            if (i < n) dst[i + q * n] = v;
+        }
+    };
+    if (Pall) store_Pcol(Pall + (int64_t)(N - 1) * nn);
+    int info = 0;
+    for (int k = N - 1; k >= 1; --k) {   // :61
+        T PB[NP][MP];
+#pragma unroll
+        for (int i = 0; i < NP; ++i)
+#pragma unroll
+            for (int c = 0; c < MP; ++c) {                       // :38 PB = P B
+                T s = (T)0;
+#pragma unroll
+                for (int l = 0; l < NP; ++l) s = fma(PS(i, l), B[l][c], s);
+                PB[i][c] = s;
+            }
+        T PAc[NP];
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {                           // :40 PA[:,q] = P A[:,q]
+            T s = (T)0;
+#pragma unroll
+            for (int l = 0; l < NP; ++l) s = fma(PS(i, l), Acol[l], s);
+            PAc[i] = s;
+        }
+        T E[MP][MP], G[MP][NP], Gq[MP];
+#pragma unroll
+        for (int c = 0; c < MP; ++c) {
+#pragma unroll
+            for (int d = 0; d <= c; ++d) {                       // :39 E = R + BᵀPB (lower)
+                T s = R[c][d];
+#pragma unroll
+                for (int i = 0; i < NP; ++i) s = fma(B[i][c], PB[i][d], s);
+                E[c][d] = s;
+            }
+#pragma unroll
+            for (int j = 0; j < NP; ++j) {                       // :41 G = BᵀPA = PBᵀA
+                T s = (T)0;
+#pragma unroll
+                for (int l = 0; l < NP; ++l) s = fma(PB[l][c], A[l][j], s);
+                G[c][j] = s;
+            }
+            T s = (T)0;
+#pragma unroll
+            for (int l = 0; l < NP; ++l) s = fma(PB[l][c], Acol[l], s);
+            Gq[c] = s;
+        }
+        // :29 potrf 'U' of E (replicated), :30 potrs for this lane's column Kq = E⁻¹G[:,q]
+        T L[MP][MP], Linv[MP];
+#pragma unroll
+        for (int j = 0; j < MP; ++j) {
+            T d = E[j][j];
+#pragma unroll
+            for (int p = 0; p < j; ++p) d = fma(-L[j][p], L[j][p], d);
+            if (!(d > (T)0) && info == 0) info = k;
+            const T ri = lane_rsqrt<T>(d);
+            Linv[j] = ri;
+#pragma unroll
+            for (int i = j + 1; i < MP; ++i) {
+                T s = E[i][j];
+#pragma unroll
+                for (int p = 0; p < j; ++p) s = fma(-L[i][p], L[j][p], s);
+                L[i][j] = s * ri;
+            }
+            L[j][j] = d * ri;
+        }
+        T y[MP], Kq[MP];
+#pragma unroll
+        for (int i = 0; i < MP; ++i) {
+            T s = Gq[i];
+#pragma unroll
+            for (int p = 0; p < i; ++p) s = fma(-L[i][p], y[p], s);
+            y[i] = s * Linv[i];
+        }
+#pragma unroll
+        for (int i = MP - 1; i >= 0; --i) {
+            T s = y[i];
+#pragma unroll
+            for (int p = i + 1; p < MP; ++p) s = fma(-L[p][i], Kq[p], s);
+            Kq[i] = s * Linv[i];
+        }
+        if (q < n) {
+            T *Kk = Kb + (int64_t)(k - 1) * nm + q * m;           // sol.K[k] column q
+#pragma unroll
+            for (int c = 0; c < MP; ++c)
+                if (c < m) Kk[c] = Kq[c];
+        }
+        // :51 P_[:,q] = Q[:,q] + Aᵀ PA[:,q] − Gᵀ Kq
+        T Pn[NP];
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            T s = Qcol[i];
+#pragma unroll
+            for (int l = 0; l < NP; ++l) s = fma(A[l][i], PAc[l], s);
+#pragma unroll
+            for (int c = 0; c < MP; ++c) s = fma(-G[c][i], Kq[c], s);
+            Pn[i] = s;
+        }
+        // re-replicate the lower triangle: P[i][r] (i ≥ r) from lane r
+#pragma unroll
+        for (int i = 0; i < NP; ++i) P[i][0] = qfrom<0>(Pn[i]);
+#pragma unroll
+        for (int i = 1; i < NP; ++i) P[i][1] = qfrom<1>(Pn[i]);
+#pragma unroll
+        for (int i = 2; i < NP; ++i) P[i][2] = qfrom<2>(Pn[i]);
+        P[3][3] = qfrom<3>(Pn[3]);
+        if (Pall) store_Pcol(Pall + (int64_t)(k - 1) * nn);
+    }
+    if (!a.p_all) store_Pcol((T *)a.P + b * nn);
+    if (a.info && q == 0) a.info[b] = info;
+
+    // forward rollout :66-70 — x replicated; lane q forms x_{k+1}[q]
+    T *Xb = (T *)a.X + b * (int64_t)N * n, *Ub = (T *)a.U + b * (int64_t)(N - 1) * m;
+    const T *x0 = (const T *)a.x0 + b * n;
+    T x[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) x[i] = i < n ? x0[i] : (T)0;
+    if (q < n) Xb[q] = q == 0 ? x[0] : (q == 1 ? x[1] : (q == 2 ? x[2] : x[3]));
+    constexpr int RD = 8;
+    T ring[RD][MP][NP];
+    auto fetch = [&](int k, T (&d)[MP][NP]) {
+        if (k > N - 1) return;
+        const T *Kk = Kb + (int64_t)(k - 1) * nm;
+#pragma unroll
+        for (int j = 0; j < NP; ++j)
+#pragma unroll
+            for (int i = 0; i < MP; ++i) d[i][j] = (i < m && j < n) ? Kk[i + j * m] : (T)0;
+    };
+    // K_k was written by this quad's own lanes above; make those stores visible to the
+    // quad's loads (other lanes' stores: complete them and drop any stale L1 line, once)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#pragma unroll
+    for (int d = 0; d < RD; ++d) fetch(1 + d, ring[d]);
+    for (int k0 = 1; k0 <= N - 1; k0 += RD) {
+#pragma unroll
+        for (int d = 0; d < RD; ++d) {
+            const int k = k0 + d;
+            if (k > N - 1) break;
+            T Kc[MP][NP];
+#pragma unroll
+            for (int j = 0; j < NP; ++j)
+#pragma unroll
+                for (int i = 0; i < MP; ++i) Kc[i][j] = ring[d][i][j];
+            fetch(k + RD, ring[d]);
+            T u[MP];
+#pragma unroll
+            for (int i = 0; i < MP; ++i) {
+                T s = (T)0;
+#pragma unroll
+                for (int j = 0; j < NP; ++j) s = fma(Kc[i][j], x[j], s);
+                u[i] = -s;
+                if (q == 0 && i < m) Ub[(int64_t)(k - 1) * m + i] = u[i];
+            }
+            T s = (T)0;
+#pragma unroll
+            for (int j = 0; j < NP; ++j) s = fma(Arow[j], x[j], s);
+#pragma unroll
+            for (int c = 0; c < MP; ++c) s = fma(Brow[c], u[c], s);
+            if (q < n) Xb[(int64_t)k * n + q] = s;
+            x[0] = qfrom<0>(s);
+            x[1] = qfrom<1>(s);
+            x[2] = qfrom<2>(s);
+            x[3] = qfrom<3>(s);
+        }
+    }
+#undef PS
+}
+
 template <typename T, int NP, int MP>
 static hipError_t launch_lane(const DpArgs &a, hipStream_t s)
 {
@@ -312,9 +549,38 @@ static hipError_t launch_lane(const DpArgs &a, hipStream_t s)
 
 bool dp_lane_supported(int n, int m) { return n >= 1 && m >= 1 && n <= 4 && m <= 4; }
 
+// quad kernel for small batches: 4·batch lanes still fit ≤ 4 waves per CU, where the
+// lane kernel would leave most CUs idle.  LQRX_DP_SMALL=lane|quad overrides (tests).
+static bool use_quad(const DpArgs &a)
+{
+    if (a.tv_AB || a.tv_QR || a.n < 3 || a.n > 4) return false;
+    const char *e = std::getenv("LQRX_DP_SMALL");
+    if (e && e[0] == 'l') return false;
+    if (e && e[0] == 'q') return true;
+    return a.batch <= 16384;
+}
+
+template <typename T, int MP>
+static hipError_t launch_quad(const DpArgs &a, hipStream_t s)
+{
+    dim3 grid((unsigned)((a.batch * 4 + 63) / 64)), block(64);
+    hipLaunchKernelGGL((dp_quad_kernel<T, MP>), grid, block, 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t dp_lane_launch(const DpArgs &a, hipStream_t s)
 {
     const int np = a.n <= 2 ? 2 : 4, mp = a.m <= 1 ? 1 : (a.m <= 2 ? 2 : 4);
+    if (use_quad(a)) {
+        if (a.dtype == 0) {
+            if (mp == 1) return launch_quad<double, 1>(a, s);
+            if (mp == 2) return launch_quad<double, 2>(a, s);
+            return launch_quad<double, 4>(a, s);
+        }
+        if (mp == 1) return launch_quad<float, 1>(a, s);
+        if (mp == 2) return launch_quad<float, 2>(a, s);
+        return launch_quad<float, 4>(a, s);
+    }
     if (a.dtype == 0) {
         if (np == 2 && mp == 1) return launch_lane<double, 2, 1>(a, s);
         if (np == 2 && mp == 2) return launch_lane<double, 2, 2>(a, s);

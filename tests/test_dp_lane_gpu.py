@@ -162,3 +162,24 @@ def test_time_varying_parity(lqrx, oracle, gpu_ok, n, m, tv_ab, tv_qr, N, bt):
     assert relerr_per_knot(got["P"], from_abi(ref["P"], (bt, N, n, n))) <= TOL64
     refX = ref["X"].reshape(bt, N, n)
     assert np.abs(got["X"] - refX).max() <= TOL64 * max(1.0, np.abs(refX).max())
+
+
+@pytest.mark.parametrize("mode", ["lane", "quad"])
+@pytest.mark.parametrize("n,m,N,batch", [(4, 1, 101, 300), (3, 2, 60, 130), (4, 4, 20, 33),
+                                         (4, 2, 30, 70)])
+def test_small_kernel_modes(lqrx, oracle, gpu_ok, monkeypatch, mode, n, m, N, batch):
+    """Both small-n kernels — one lane per trajectory (dp_lane_kernel) and one quad per
+    trajectory (dp_quad_kernel, the default for batch ≤ 16384 at n ∈ {3, 4}) — against the
+    oracle; LQRX_DP_SMALL selects the kernel per call."""
+    monkeypatch.setenv("LQRX_DP_SMALL", mode)
+    seed = 700 + 11 * n + m
+    got, ref = run_pair(lqrx, oracle, n, m, N, batch, seed=seed, all_P=True)
+    assert got["rc"] == 0 and (got["info"] == 0).all()
+    assert_parity(got, ref, lqrx.random_batch(n, m, N, batch, seed), N)
+
+
+def test_small_kernel_auto_large_batch(lqrx, oracle, gpu_ok):
+    """batch > 16384 at n = 4 selects the lane kernel (auto)."""
+    got, ref = run_pair(lqrx, oracle, 4, 1, 12, 16384 + 70, seed=77)
+    assert got["rc"] == 0
+    assert_parity(got, ref, lqrx.random_batch(4, 1, 12, 16384 + 70, 77), 12)
