@@ -119,6 +119,8 @@ def main():
                     help="dp: time-varying problem (per-knot A_k, B_k, Q_k, R_k; knot_stride 1, "
                          "SURVEY §8(f) rank 1); default batch 16384 (65536 would need 376 GB)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-gather", action="store_true",
+                    help="skip the final info + P_1 gather to rank 0 (N > 1)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     ap.add_argument("--workload", choices=["dp", "cartpole", "kkt", "sqp", "ls"], default="dp",
                     help="dp = random dense LQR (BASELINE configs[3], the headline); "
@@ -252,6 +254,29 @@ def main():
     bad = int((out["info"] != 0).sum().item()) if args.workload != "sqp" else \
         int((out["info"] == 2).sum().item())                  # SQP: line-search failures
 
+    # final gather, timed separately from the solve: info + P_1 of every
+    # shard to rank 0 over RCCL (grouped send/recv); K stays sharded
+    gather = None
+    if world > 1 and args.workload in ("dp", "cartpole") and not args.no_gather:
+        from lqrx.shard import gather_to_root
+        fields = {"info": out["info"], "P": out["P"]}
+        try:
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            tg0 = time.perf_counter()
+            got = gather_to_root(fields, bt * world)
+            torch.cuda.synchronize(dev)
+            tg = torch.tensor([time.perf_counter() - tg0], dtype=torch.float64, device=dev)
+            dist.all_reduce(tg, op=dist.ReduceOp.MAX)
+            gbytes = sum(f.numel() * f.element_size() for f in fields.values()) * (world - 1)
+            gather = {"ms": float(tg.item()) * 1e3, "bytes_to_root": gbytes,
+                      "what": "info + P_1 of every shard to rank 0 (torch.distributed.gather = RCCL "
+                              "send/recv); K stays sharded",
+                      "root_info_nonzero": int((got["info"] != 0).sum().item()) if got is not None else None}
+            del got
+        except Exception as e:  # the solve measurement stands without the gather
+            gather = {"error": f"{type(e).__name__}: {e}"}
+
     wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
@@ -381,7 +406,10 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "nonfinite_or_info": bad,
+            "gather": gather,
         }
+        if gather is not None and "ms" in gather:
+            line["value_solve_plus_gather"] = total / (wall + gather["ms"] * 1e-3)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -61,3 +61,59 @@ def test_two_rank_sharding_gloo(lqrx):
     assert np.array_equal(np.concatenate([res[0][1], res[1][1]]), full["A"])
     assert np.array_equal(np.concatenate([res[0][2], res[1][2]]), ref["K"])
     assert res[0][3] == pytest.approx(0.2) and res[1][3] == pytest.approx(0.2)
+
+
+def _gather_worker(rank, world, port, root, batch, q):
+    import sys
+
+    sys.path[:0] = [os.path.join(root, "lqr.jl_amd"), root]
+    import torch
+    import lqrx
+    from lqrx.shard import gather_to_root, shard_range
+    from oracle import oracle as orc
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n, m, N = 4, 2, 9
+    first, cnt = shard_range(batch, rank, world)
+    if cnt:
+        d = lqrx.random_batch(n, m, N, cnt, seed=31, traj0=first)
+        o = orc.dp_solve_abi(d, N)
+        fields = {"info": torch.from_numpy(o["info"]), "P": torch.from_numpy(o["P"]),
+                  "U": torch.from_numpy(o["U"])}
+    else:
+        fields = {"info": torch.zeros(0, dtype=torch.int32), "P": torch.zeros(0, dtype=torch.float64),
+                  "U": torch.zeros(0, dtype=torch.float64)}
+    got = gather_to_root(fields, batch)
+    q.put((rank, None if got is None else {k: v.numpy() for k, v in got.items()}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,batch", [(2, 11), (3, 7), (3, 2)])
+def test_gather_to_root_gloo(lqrx, world, batch):
+    """Final gather: ragged contiguous shards (shard_range), info + P_1 + U of
+    every shard reach rank 0 in trajectory order and equal the single-process solve; other
+    ranks receive nothing.  (3, 2) has an empty shard."""
+    import lqrx as L
+    from lqrx.shard import shard_range
+    from oracle import oracle as orc
+
+    spans = [shard_range(batch, r, world) for r in range(world)]
+    assert spans[0][0] == 0 and sum(c for _, c in spans) == batch
+    assert all(spans[r][0] + spans[r][1] == spans[r + 1][0] for r in range(world - 1))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, root, batch, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(res[r] is None for r in range(1, world))
+    ref = orc.dp_solve_abi(L.random_batch(4, 2, 9, batch, seed=31), 9)
+    for k in ("info", "P", "U"):
+        assert np.array_equal(res[0][k], ref[k]), k
