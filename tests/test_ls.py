@@ -138,7 +138,7 @@ def _batch(rng, n, m, bt):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,m,N,bt", [(4, 1, 101, 37), (3, 2, 40, 64), (6, 3, 12, 5), (2, 1, 2, 3),
-                                      (8, 4, 16, 9)])
+                                      (8, 4, 16, 9), (16, 4, 8, 5)])   # last: n·m + n > 64, LDS path
 @pytest.mark.parametrize("hu", [0, 1, 2])
 def test_ls_gpu_parity(lqrx, gpu_ok, n, m, N, bt, hu):
     from lqrx import ls
