@@ -125,3 +125,38 @@ def test_get_last_error_copies(lqrx):
     assert n == len(full) and buf.value == full[:7]
     big = C.create_string_buffer(1024)
     assert lib.lqrx_get_last_error(big, 1024) == len(full) and big.value == full
+
+
+def test_ls_validation(lqrx):
+    """lqrx_ls_solve argument checks (no compute): bad desc fields, NULL pointers, LDS limit."""
+    import ctypes as C
+
+    from lqrx import _lib
+
+    lib = _lib.load()
+    buf = (C.c_double * 4)()
+    ptrs = [C.cast(buf, C.c_void_p)] * 9
+    ok = dict(n=4, m=1, N=101, hu_mode=0, batch=2)
+    for field, val, code in [("n", 0, -1), ("N", 1, -1), ("hu_mode", 3, -1), ("batch", -1, -1),
+                             ("N", 400, _lib.ERR_UNSUPPORTED)]:
+        d = _lib.LsDesc(**{**ok, field: val})
+        assert lib.lqrx_ls_solve(C.byref(d), *ptrs, None, None, None) == code, (field, val)
+    d = _lib.LsDesc(**ok)
+    assert lib.lqrx_ls_solve(C.byref(d), None, *ptrs[1:], None, None, None) == -2
+    assert lib.lqrx_ls_solve(C.byref(d), *ptrs[:6], None, ptrs[7], ptrs[8], None, None, None) == -8
+    assert lib.lqrx_ls_solve(C.byref(_lib.LsDesc(**{**ok, "batch": 0})), *ptrs, None, None, None) == 0
+    assert lib.lqrx_ls_lds_bytes(4, 1, 101) > 0 and lib.lqrx_ls_lds_bytes(0, 1, 5) == 0
+
+
+def test_constraint_block_dims(lqrx):
+    """test/constraint_blocks.jl:25-32 — with dynamics on 1:N-1, an initial-condition
+    constraint at knot 1 and a goal at N, block 1 is 2n×(n+m), interior blocks n̄+p+n̄ rows,
+    block N is 2n×n (conblocks.jl:79-93 sizing)."""
+    import lqrx.kkt as K
+
+    for st in (K.double_integrator_structure(3, 101), K.dubins_structure(11)):
+        n, m, N = st.n, st.m, st.N
+        rows, w = st.rows, st.w
+        assert (rows[0], w[0]) == (2 * n, n + m)
+        assert (rows[-1], w[-1]) == (2 * n, n)
+        assert all(rows[k] == 2 * n + st.p[k] and w[k] == n + m for k in range(1, N - 1))
