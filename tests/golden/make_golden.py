@@ -39,6 +39,17 @@ def kkt_fixture(name, st, pb, ginv=1):
                         g=pb.g, dz=out["dz"], lam=out["lam"], info=out["info"])
 
 
+def ls_fixture(name, cb, N, hu):
+    """Condensed least squares (oracle/ls_oracle.py, least_squares.jl:158-202)."""
+    from oracle import ls_oracle as LO
+
+    outs = [LO.ls_solve(cb.A[b], cb.B[b], cb.Q[b], cb.R[b], cb.Qf[b], cb.x0[b], N, hu=hu)
+            for b in range(cb.A.shape[0])]
+    np.savez_compressed(os.path.join(HERE, name), N=N, hu=hu, A=cb.A, B=cb.B, Q=cb.Q, R=cb.R,
+                        Qf=cb.Qf, x0=cb.x0, U=np.stack([o["U"] for o in outs]),
+                        X=np.stack([o["X"] for o in outs]))
+
+
 def main():
     cb = cartpole_batch(4, 101, seed=1)
     d = {k: to_abi(getattr(cb, k)).ravel() for k in ("A", "B", "Q", "R", "Qf")}
@@ -53,6 +64,9 @@ def main():
     kkt_fixture("kkt_dubins_N11_soc.npz", st, K.random_kkt(st, 4, seed=8, h_mode=K.H_DIAG), ginv=0)
     st = K.double_integrator_structure(2, 12)
     kkt_fixture("kkt_di2_N12_dense.npz", st, K.random_kkt(st, 3, seed=9, h_mode=K.H_DENSE))
+    cb = cartpole_batch(3, 41, seed=3)
+    for hu in (0, 1, 2):
+        ls_fixture(f"ls_cartpole_N41_hu{hu}.npz", cb, 41, hu)
 
 
 if __name__ == "__main__":

@@ -80,3 +80,34 @@ def test_kkt_fixture_gpu(lqrx, gpu_ok, path):
     got = K.kkt_solve(pb, ginv=int(f["ginv"]))
     assert _rel(got["dz"], f["dz"].reshape(bt, -1)) <= 1e-10
     assert _rel(got["lam"], f["lam"].reshape(bt, -1)) <= 1e-10
+
+
+LS = sorted(glob.glob(os.path.join(HERE, "ls_*.npz")))
+
+
+@pytest.mark.parametrize("path", LS, ids=os.path.basename)
+def test_ls_fixture_oracle(lqrx, path):
+    """The condensed least-squares restatement reproduces its fixtures (numpy/OpenBLAS: to
+    rounding, not bit-exact — BLAS summation order is not pinned)."""
+    from oracle import ls_oracle as LO
+
+    f = np.load(path)
+    for b in range(f["A"].shape[0]):
+        o = LO.ls_solve(f["A"][b], f["B"][b], f["Q"][b], f["R"][b], f["Qf"][b], f["x0"][b],
+                        int(f["N"]), hu=int(f["hu"]))
+        assert _rel(o["U"], f["U"][b]) <= 1e-12 and _rel(o["X"], f["X"][b]) <= 1e-12
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", LS, ids=os.path.basename)
+def test_ls_fixture_gpu(lqrx, gpu_ok, path):
+    """ls_condensed_kernel on the fixture inputs: U, X within 1e-9 relative (cond(H) of the
+    cartpole N=41 fixtures ≤ 2e6; two Cholesky solves of the same normal equations)."""
+    from lqrx import ls
+    from lqrx.dp import LQRBatch
+
+    f = np.load(path)
+    out = ls.ls_solve_batch(LQRBatch(f["A"], f["B"], f["Q"], f["R"], f["Qf"], f["x0"], int(f["N"])),
+                            hu_mode=int(f["hu"]))
+    assert out["rc"] == 0
+    assert _rel(out["U"], f["U"]) <= 1e-9 and _rel(out["X"], f["X"]) <= 1e-9
