@@ -92,8 +92,10 @@ __host__ __device__ inline LsLayout ls_layout(int n, int m, int N)
     return L;
 }
 
-// packed upper-triangular index of (i, k), i ≤ k: columns stored contiguously
-__device__ inline int up(int i, int k) { return (k * (k + 1) >> 1) + i; }
+// packed upper-triangular index of (i, k), i ≤ k, rows stored contiguously (row i holds
+// columns i..Nm−1 and starts at Σ_{r<i} (Nm − r))
+__device__ inline int rbase(int i, int Nm) { return i * Nm - ((i * (i - 1)) >> 1) - i; }  // + k
+__device__ inline int up(int i, int k, int Nm) { return rbase(i, Nm) + k; }
 
 // upper Cholesky of a small s×s column-major matrix in LDS (thread 0 only); returns false
 // when a pivot is not positive (cholesky() throws PosDefException there, :50-52)
@@ -262,7 +264,7 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
             const double *f1 = Vf + (K - 1 - c1) * nm + a1 * n, *f2 = Vf + (K - 1 - c2) * nm + a2 * n;
             double v = q;
             for (int i = 0; i < n; ++i) v = fma(f1[i], f2[i], v);
-            H[up(c1 * m + a1, c2 * m + a2)] = v + hu;
+            H[up(c1 * m + a1, c2 * m + a2, Nm)] = v + hu;
         };
         if (K - 1 - d >= 0) emit(K - 1, 0.0);          // last control: Qf row only
         double acc = 0.0;
@@ -288,12 +290,12 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
 
     // ---- potrf 'U' (:181): right-looking, one barrier per pivot.  Step j updates the trailing
     // upper triangle with the unscaled row j (H[i,k] −= H[j,i]·H[j,k]/d_j) and scales row j−1
-    // (read by nobody in step j); info = first non-positive pivot.  Waves own columns, lanes
-    // rows (contiguous LDS within a column).
+    // (read by nobody in step j); info = first non-positive pivot.  Waves own rows (4 per
+    // pass, sharing each loaded H[j,k]), lanes columns: every LDS access is row-contiguous.
     const int wave = tid >> 6, lane = tid & 63;
     double dprev = 1.0;
     for (int j = 0; j < Nm; ++j) {
-        const double d = H[up(j, j)];
+        const double d = H[up(j, j, Nm)];
         if (!(d > 0.0)) {   // uniform: every thread reads the same LDS word
             if (tid == 0 && ginfo) ginfo[b] = j + 1;
             return;
@@ -301,30 +303,35 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
         const double rinv = 1.0 / d;
         if (j > 0) {
             const double rdp = 1.0 / sqrt(dprev);
-            for (int k = j + tid; k < Nm; k += LS_THREADS) H[up(j - 1, k)] *= rdp;
-            if (tid == 0) H[up(j - 1, j - 1)] = dprev * rdp;
+            const int rb = rbase(j - 1, Nm);
+            for (int k = j + tid; k < Nm; k += LS_THREADS) H[rb + k] *= rdp;
+            if (tid == 0) H[rb + j - 1] = dprev * rdp;
         }
-        // 4 columns per wave pass: the 4 independent LDS read-modify-writes per lane overlap
-        for (int k0 = j + 1 + 4 * wave; k0 < Nm; k0 += 4 * (LS_THREADS / 64)) {
-            double hk[4];
+        const int rj = rbase(j, Nm);
+        for (int i0 = j + 1 + 4 * wave; i0 < Nm; i0 += 4 * (LS_THREADS / 64)) {
+            double hi[4];
+            int rb[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) hk[u] = k0 + u < Nm ? H[up(j, k0 + u)] * rinv : 0.0;
-            const int kmax = k0 + 3 < Nm ? k0 + 3 : Nm - 1;
-            for (int i = j + 1 + lane; i <= kmax; i += 64) {
-                const double hji = H[up(j, i)];
+            for (int u = 0; u < 4; ++u) {
+                const bool ok = i0 + u < Nm;
+                hi[u] = ok ? H[rj + i0 + u] * rinv : 0.0;
+                rb[u] = ok ? rbase(i0 + u, Nm) : 0;
+            }
+            for (int k = i0 + lane; k < Nm; k += 64) {
+                const double hjk = H[rj + k];
                 double h[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
-                    if (i <= k0 + u && k0 + u < Nm) h[u] = H[up(i, k0 + u)];
+                    if (i0 + u <= k) h[u] = H[rb[u] + k];
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
-                    if (i <= k0 + u && k0 + u < Nm) H[up(i, k0 + u)] = fma(-hji, hk[u], h[u]);
+                    if (i0 + u <= k) H[rb[u] + k] = fma(-hi[u], hjk, h[u]);
             }
         }
         dprev = d;
         __syncthreads();
     }
-    if (tid == 0) H[up(Nm - 1, Nm - 1)] = sqrt(dprev);
+    if (tid == 0) H[up(Nm - 1, Nm - 1, Nm)] = sqrt(dprev);
     __syncthreads();
     // ---- potrs 'U' (:182): Uᵀz = y, then U x = z — wave 0, y held in registers (lane l owns
     // y[l + 64 s]), the pivot broadcast by readlane: no barriers in the 2·Nm-step chain
@@ -337,20 +344,20 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
             yr[s2] = idx < Nm ? y[idx] : 0.0;
         }
         for (int j = 0; j < Nm; ++j) {
-            const double zj = bcast_slot<S>(yr, j) / H[up(j, j)];
+            const double zj = bcast_slot<S>(yr, j) / H[up(j, j, Nm)];
 #pragma unroll
             for (int s2 = 0; s2 < S; ++s2) {
                 const int idx = lane + 64 * s2;
-                if (idx > j && idx < Nm) yr[s2] = fma(-H[up(j, idx)], zj, yr[s2]);
+                if (idx > j && idx < Nm) yr[s2] = fma(-H[up(j, idx, Nm)], zj, yr[s2]);
                 else if (idx == j) yr[s2] = zj;
             }
         }
         for (int j = Nm - 1; j >= 0; --j) {
-            const double xj = bcast_slot<S>(yr, j) / H[up(j, j)];
+            const double xj = bcast_slot<S>(yr, j) / H[up(j, j, Nm)];
 #pragma unroll
             for (int s2 = 0; s2 < S; ++s2) {
                 const int idx = lane + 64 * s2;
-                if (idx < j) yr[s2] = fma(-H[up(idx, j)], xj, yr[s2]);
+                if (idx < j) yr[s2] = fma(-H[up(idx, j, Nm)], xj, yr[s2]);
                 else if (idx == j) yr[s2] = xj;
             }
         }

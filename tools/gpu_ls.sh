@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out/ls_${TAG:-x}
 mkdir -p $OUT
-timeout -k 10 300 python -u -m pytest tests/test_ls.py -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1; rc=$?
+timeout -k 10 300 python -u -m pytest tests/test_ls.py tests/test_golden.py -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1; rc=$?
 tail -8 $OUT/tests.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python bench.py --workload ls --steps 10 --warmup 3 --cpu-seconds 4 > $OUT/ls.json 2> $OUT/ls.err || { tail -20 $OUT/ls.err; exit 3; }
