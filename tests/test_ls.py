@@ -234,11 +234,14 @@ def test_ls_gpu_solver_surface(lqrx, gpu_ok):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,h_mode", [("dubins", 2), ("dubins", 0), ("di_small", 1)])
+@pytest.mark.parametrize("name,h_mode", [("dubins", 2), ("dubins", 0), ("di_small", 1), ("di", 2)])
 def test_sparse_solver_gpu(lqrx, gpu_ok, name, h_mode):
+    """("di", 2) is test/sparse_solver.jl's own problem structure, DoubleIntegrator(3, 101)
+    with diagonal costs (dense_cost=false)."""
     import lqrx.kkt as K
 
-    st = {"dubins": K.dubins_structure(31), "di_small": K.double_integrator_structure(2, 12)}[name]
+    st = {"dubins": K.dubins_structure(31), "di_small": K.double_integrator_structure(2, 12),
+          "di": K.double_integrator_structure(3, 101)}[name]
     bt = 4
     pb = K.random_kkt(st, bt, seed=21, h_mode=h_mode)
     glob = [LO.blocks_to_global(st, pb.Y[b], pb.y[b], pb.H[b], pb.g[b], h_mode) for b in range(bt)]
