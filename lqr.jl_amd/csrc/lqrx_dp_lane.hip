@@ -305,8 +305,9 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
 // With one lane per trajectory a B = 4096 batch is 64 waves — one per CU on a quarter of
 // the chip, each a serial ~160-FMA-per-knot chain.  Here lane q of the quad owns column q
 // of everything that splits by columns and the small m-sized work is replicated:
-//   replicated: PB = P·B, E = R + BᵀPB, G = PBᵀA (= BᵀPA for symmetric P), potrf of E
-//   column q:   PA[:,q] = P·A[:,q]; Kq = E⁻¹G[:,q]; P_[:,q] = Q[:,q] + Aᵀ·PA[:,q] − Gᵀ·Kq
+//   replicated: PB = P·B, E = R + BᵀPB, potrf of E
+//   column q:   PA[:,q] = P·A[:,q]; G[:,q] = PBᵀA[:,q] (= BᵀPA for symmetric P);
+//               Kq = E⁻¹G[:,q]; P_[:,q] = Q[:,q] + Aᵀ(PA[:,q] − PB·Kq)  (= AᵀPA − GᵀK)
 // then P_ is re-replicated by four DPP quad broadcasts of the lower-triangle columns (lane r
 // supplies column r).  Rollout: x replicated, lane q computes x_{k+1}[q] = A[q,:]x + B[q,:]u
 // and the quad broadcasts re-assemble x.  Same reference lines as dp_lane_kernel.
@@ -391,7 +392,7 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
             for (int l = 0; l < NP; ++l) s = fma(PS(i, l), Acol[l], s);
             PAc[i] = s;
         }
-        T E[MP][MP], G[MP][NP], Gq[MP];
+        T E[MP][MP], Gq[MP];
 #pragma unroll
         for (int c = 0; c < MP; ++c) {
 #pragma unroll
@@ -401,14 +402,7 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
                 for (int i = 0; i < NP; ++i) s = fma(B[i][c], PB[i][d], s);
                 E[c][d] = s;
             }
-#pragma unroll
-            for (int j = 0; j < NP; ++j) {                       // :41 G = BᵀPA = PBᵀA
-                T s = (T)0;
-#pragma unroll
-                for (int l = 0; l < NP; ++l) s = fma(PB[l][c], A[l][j], s);
-                G[c][j] = s;
-            }
-            T s = (T)0;
+            T s = (T)0;                                          // :41 G[:,q] = PBᵀA[:,q]
 #pragma unroll
             for (int l = 0; l < NP; ++l) s = fma(PB[l][c], Acol[l], s);
             Gq[c] = s;
@@ -453,15 +447,21 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
             for (int c = 0; c < MP; ++c)
                 if (c < m) Kk[c] = Kq[c];
         }
-        // :51 P_[:,q] = Q[:,q] + Aᵀ PA[:,q] − Gᵀ Kq
-        T Pn[NP];
+        // :51 P_[:,q] = Q[:,q] + AᵀPA[:,q] − Gᵀ Kq = Q[:,q] + Aᵀ(PA[:,q] − PB·Kq)
+        // (G = PBᵀA, so GᵀKq = Aᵀ(PB Kq): no full G)
+        T wv[NP], Pn[NP];
+#pragma unroll
+        for (int l = 0; l < NP; ++l) {
+            T s = PAc[l];
+#pragma unroll
+            for (int c = 0; c < MP; ++c) s = fma(-PB[l][c], Kq[c], s);
+            wv[l] = s;
+        }
 #pragma unroll
         for (int i = 0; i < NP; ++i) {
             T s = Qcol[i];
 #pragma unroll
-            for (int l = 0; l < NP; ++l) s = fma(A[l][i], PAc[l], s);
-#pragma unroll
-            for (int c = 0; c < MP; ++c) s = fma(-G[c][i], Kq[c], s);
+            for (int l = 0; l < NP; ++l) s = fma(A[l][i], wv[l], s);
             Pn[i] = s;
         }
         // re-replicate the lower triangle: P[i][r] (i ≥ r) from lane r
