@@ -181,7 +181,7 @@ int lqrx_dubins_sqp_solve_host(const lqrx_dubins_sqp_desc *desc, double *Z, cons
  * H = ĀᵀĀ + Hu, y = −Āᵀb̄ (:171-173), potrf/potrs 'U' (:181-182), rollout! (:197-202).
  * One workgroup per trajectory with the whole problem in LDS: requires
  * lqrx_ls_lds_bytes(n, m, N) <= 163840 and (N−1)·m <= 192 (e.g. n=4, m=1: N ≤ 189;
- * n=3, m=2: N ≤ 97; n=6, m=3: N ≤ 63).
+ * n=3, m=2: N ≤ 97; n=6, m=3: N ≤ 62).
  *   hu_mode 0: Hu = 0 — a fresh LeastSquaresSolver (:44), the reference default; the
  *              solve then carries no control cost
  *           1: Hu = blkdiag(chol(R).U) — what build_least_squares! leaves (:121)

@@ -20,6 +20,7 @@
 // Cholesky / substitution barrier chain; one workgroup per CU when H is large.  Ā and b̄ can be written out
 // (optional) for a direct buildAb! parity check.
 #include "lqrx_internal.h"
+#include "lqrx_tile.h"
 #include <math.h>
 
 namespace lqrx {
@@ -64,7 +65,7 @@ __device__ inline double bcast_slot(const double (&v)[S], int j)
 struct LsLayout {
     int n, m, N, K, Nm, Nn;
     // LDS offsets in doubles
-    int oSq, oSf, oHu, oA, oB, oPl, oW, oVq, oVf, obb, oH, oy, oX, oFlag, total;
+    int oSq, oSf, oHu, oA, oB, oPl, oW, oVq, oVf, obb, oH, oy, odi, oX, oFlag, total;
 };
 
 __host__ __device__ inline LsLayout ls_layout(int n, int m, int N)
@@ -87,6 +88,7 @@ __host__ __device__ inline LsLayout ls_layout(int n, int m, int N)
     const int hp = L.Nm * (L.Nm + 1) / 2;   // packed upper triangle, column-major
     o += hp > 2 * n * n + m * m ? hp : 2 * n * n + m * m;
     L.oy = o; o += L.Nm;
+    L.odi = o; o += L.Nm;   // 1/U_jj of the factor (potrs multiplies instead of dividing)
     L.oFlag = o; o += 1;
     L.total = o;
     return L;
@@ -130,7 +132,7 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
     const int64_t b = blockIdx.x;
     double *Sq = lds + L.oSq, *Sf = lds + L.oSf, *Hu = lds + L.oHu, *A = lds + L.oA, *B = lds + L.oB;
     double *Pl = lds + L.oPl, *W = lds + L.oW, *Vq = lds + L.oVq, *Vf = lds + L.oVf, *bb = lds + L.obb;
-    double *H = lds + L.oH, *y = lds + L.oy, *X = lds + L.oX;
+    double *H = lds + L.oH, *y = lds + L.oy, *X = lds + L.oX, *dinv = lds + L.odi;
     int *flag = (int *)(lds + L.oFlag);
     const int nn = n * n, nm = n * m, mm = m * m;
 
@@ -300,12 +302,15 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
             if (tid == 0 && ginfo) ginfo[b] = j + 1;
             return;
         }
-        const double rinv = 1.0 / d;
+        const double rinv = rcp_nr2(d);
         if (j > 0) {
-            const double rdp = 1.0 / sqrt(dprev);
+            const double rdp = rsqrt_nr(dprev);
             const int rb = rbase(j - 1, Nm);
             for (int k = j + tid; k < Nm; k += LS_THREADS) H[rb + k] *= rdp;
-            if (tid == 0) H[rb + j - 1] = dprev * rdp;
+            if (tid == 0) {
+                H[rb + j - 1] = dprev * rdp;
+                dinv[j - 1] = rdp;
+            }
         }
         const int rj = rbase(j, Nm);
         for (int i0 = j + 1 + 4 * wave; i0 < Nm; i0 += 4 * (LS_THREADS / 64)) {
@@ -331,7 +336,11 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
         dprev = d;
         __syncthreads();
     }
-    if (tid == 0) H[up(Nm - 1, Nm - 1, Nm)] = sqrt(dprev);
+    if (tid == 0) {
+        const double rdp = rsqrt_nr(dprev);
+        H[up(Nm - 1, Nm - 1, Nm)] = dprev * rdp;
+        dinv[Nm - 1] = rdp;
+    }
     __syncthreads();
     // ---- potrs 'U' (:182): Uᵀz = y, then U x = z — wave 0, y held in registers (lane l owns
     // y[l + 64 s]), the pivot broadcast by readlane: no barriers in the 2·Nm-step chain
@@ -344,7 +353,7 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
             yr[s2] = idx < Nm ? y[idx] : 0.0;
         }
         for (int j = 0; j < Nm; ++j) {
-            const double zj = bcast_slot<S>(yr, j) / H[up(j, j, Nm)];
+            const double zj = bcast_slot<S>(yr, j) * dinv[j];
 #pragma unroll
             for (int s2 = 0; s2 < S; ++s2) {
                 const int idx = lane + 64 * s2;
@@ -353,7 +362,7 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
             }
         }
         for (int j = Nm - 1; j >= 0; --j) {
-            const double xj = bcast_slot<S>(yr, j) / H[up(j, j, Nm)];
+            const double xj = bcast_slot<S>(yr, j) * dinv[j];
 #pragma unroll
             for (int s2 = 0; s2 < S; ++s2) {
                 const int idx = lane + 64 * s2;
