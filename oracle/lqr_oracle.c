@@ -307,17 +307,28 @@ static void hinv_apply(int hm, int w, const double *Hf, double *X, int nc)
     }
 }
 
-int oracle_kkt_solve_one(int N, const int *n1, const int *p, const int *n2, const int *w,
-                         const double *Y, const double *y, int h_mode, const double *H,
-                         const double *g, int ginv, double *dz, double *lam, double *Sd,
-                         double *Ud, double *rd)
+/* Shared by the upper solve and the lower-variant factor: per-knot offsets into the
+ * packed inputs, the H_k factors and the Schur pieces r_k. */
+typedef struct {
+    size_t *oY, *oy, *oH, *og;
+    double *Hf;
+    double **rk;
+} kkt_work;
+
+static void kkt_work_free(int N, kkt_work *wk)
+{
+    for (int k = 0; k < N; ++k) free(wk->rk[k]);
+    free(wk->rk); free(wk->Hf); free(wk->oY); free(wk->oy); free(wk->oH); free(wk->og);
+}
+
+/* H_k factors (block_cholesky.jl:55-91,145-153) and calculate_shur_factors!
+ * (jacobian_blocks.jl:220-286) into F, stored as copy_shur!(::BlockUpperTriangular3)
+ * writes it (:271-286).  Returns −(k+1) for the first H_k that is not SPD, else 0. */
+static int kkt_schur(int N, const int *n1, const int *p, const int *n2, const int *w,
+                     const double *Y, const double *y, int h_mode, const double *H,
+                     const double *g, int ginv, oblk *F, kkt_work *wkp)
 {
     int info = 0;
-    oblk *F = calloc((size_t)N, sizeof(oblk)), *U = calloc((size_t)N, sizeof(oblk));
-    alloc_blocks(N, n1, p, n2, F);
-    alloc_blocks(N, n1, p, n2, U);
-
-    /* per-knot offsets into the packed inputs */
     size_t *oY = malloc(N * sizeof(size_t)), *oy = malloc(N * sizeof(size_t));
     size_t *oH = malloc(N * sizeof(size_t)), *og = malloc(N * sizeof(size_t));
     size_t aY = 0, ay = 0, aH = 0, ag = 0;
@@ -381,6 +392,22 @@ int oracle_kkt_solve_one(int N, const int *n1, const int *p, const int *n2, cons
             for (int i = 0; i < F[k - 1].p2; ++i) F[k - 1].d[i] += rk[k][i];
         free(JYt); free(YYt);
     }
+    wkp->oY = oY; wkp->oy = oy; wkp->oH = oH; wkp->og = og; wkp->Hf = Hf; wkp->rk = rk;
+    return info;
+}
+
+int oracle_kkt_solve_one(int N, const int *n1, const int *p, const int *n2, const int *w,
+                         const double *Y, const double *y, int h_mode, const double *H,
+                         const double *g, int ginv, double *dz, double *lam, double *Sd,
+                         double *Ud, double *rd)
+{
+    oblk *F = calloc((size_t)N, sizeof(oblk)), *U = calloc((size_t)N, sizeof(oblk));
+    alloc_blocks(N, n1, p, n2, F);
+    alloc_blocks(N, n1, p, n2, U);
+    kkt_work kw;
+    int info = kkt_schur(N, n1, p, n2, w, Y, y, h_mode, H, g, ginv, F, &kw);
+    const size_t *oY = kw.oY, *oH = kw.oH, *og = kw.og;
+    const double *Hf = kw.Hf;
 
     /* dense S and r (copy_shur_factors!, jacobian_blocks.jl:173-211) */
     size_t Ptot = 0;
@@ -523,9 +550,208 @@ int oracle_kkt_solve_one(int N, const int *n1, const int *p, const int *n2, cons
         oz += (size_t)wk;
     }
 
-    for (int k = 0; k < N; ++k) free(rk[k]);
-    free(rk); free(Hf); free(oY); free(oy); free(oH); free(og);
+    kkt_work_free(N, &kw);
     free_blocks(N, F); free_blocks(N, U); free(F); free(U);
+    return info;
+}
+
+/* ------------------------------------------------ KKT-12: lower-storage block Cholesky */
+
+/* Lower Cholesky A = L Lᵀ in place (Julia cholesky(A).L), strict upper part zeroed.
+ * Returns LAPACK-style info (cholesky() throws PosDefException there). */
+static int potrf_lower(int n, double *A, int lda)
+{
+    for (int j = 0; j < n; ++j) {
+        double d = A[IDX(j, j, lda)];
+        for (int q = 0; q < j; ++q) d -= A[IDX(j, q, lda)] * A[IDX(j, q, lda)];
+        if (!(d > 0.0)) return j + 1;
+        d = sqrt(d);
+        A[IDX(j, j, lda)] = d;
+        for (int i = j + 1; i < n; ++i) {
+            double s = A[IDX(i, j, lda)];
+            for (int q = 0; q < j; ++q) s -= A[IDX(i, q, lda)] * A[IDX(j, q, lda)];
+            A[IDX(i, j, lda)] = s / d;
+        }
+        for (int i = 0; i < j; ++i) A[IDX(i, j, lda)] = 0.0;
+    }
+    return 0;
+}
+
+/* X ← X / Lᵀ  (Julia X / chol.U with chol.U = Lᵀ): X is r×c, L lower c×c. */
+static void rdiv_lt(int r, int c, double *X, int ldx, const double *L, int ldl)
+{
+    for (int i = 0; i < r; ++i)
+        for (int j = 0; j < c; ++j) {
+            double s = X[IDX(i, j, ldx)];
+            for (int q = 0; q < j; ++q) s -= X[IDX(i, q, ldx)] * L[IDX(j, q, ldl)];
+            X[IDX(i, j, ldx)] = s / L[IDX(j, j, ldl)];
+        }
+}
+
+/* x ← L⁻¹ x (trans = 0) or L⁻ᵀ x (trans = 1), L lower n×n */
+static void trsv_l(int n, const double *L, int ldl, double *x, int trans)
+{
+    if (!trans) {
+        for (int i = 0; i < n; ++i) {
+            double s = x[i];
+            for (int q = 0; q < i; ++q) s -= L[IDX(i, q, ldl)] * x[q];
+            x[i] = s / L[IDX(i, i, ldl)];
+        }
+    } else {
+        for (int i = n - 1; i >= 0; --i) {
+            double s = x[i];
+            for (int q = i + 1; q < n; ++q) s -= L[IDX(q, i, ldl)] * x[q];
+            x[i] = s / L[IDX(i, i, ldl)];
+        }
+    }
+}
+
+/*
+ * KKT-12: the reference's lower-storage variant, used only as a cross-check
+ * of the upper factor (test/constraint_blocks.jl:96-133).
+ *   Schur blocks in BlockLowerTriangular3 storage (copy_shur!(::BlockTriangular3),
+ *     jacobian_blocks.jl:254-269: D = YYt[ps,p1], E = YYt[p2,ps], F = YYt[p2,p1]),
+ *   cholesky!(L, F)  cholesky_solve.jl:5-26 (A = previous C factor, D/A.U, B = chol(.).L,
+ *     F/A.U, E = (F.E − L.F L.Dᵀ)/B.U, C = chol(.).L),
+ *   the lower forward/backward substitutions kept (commented out) at cholesky_solve.jl:
+ *     146-168 — in the reference the live forward_substitution! has no method for lower
+ *     blocks, so these follow the commented text: y = L⁻¹h, then x = L⁻ᵀy = S⁻¹h with
+ *     h = [c; d] (= r, the Schur residual).
+ * Outputs (P = Σ p_k + n2_k; NULL to skip): Ld (P×P, copy_block! placement :181-195),
+ * yv (P, after the forward sweep), xv (P, after the backward sweep).  Returns the
+ * 1-based block whose B or C factor failed (cholesky() throws), −(k+1) for a non-SPD
+ * H_k, else 0.
+ */
+int oracle_kkt_lower_one(int N, const int *n1, const int *p, const int *n2, const int *w,
+                         const double *Y, const double *y, int h_mode, const double *H,
+                         const double *g, int ginv, double *Ld, double *yv, double *xv)
+{
+    oblk *F = calloc((size_t)N, sizeof(oblk)), *L = calloc((size_t)N, sizeof(oblk));
+    alloc_blocks(N, n1, p, n2, F);
+    alloc_blocks(N, n1, p, n2, L);   /* D/E/F buffers hold the transposed shapes */
+    kkt_work kw;
+    int info = kkt_schur(N, n1, p, n2, w, Y, y, h_mode, H, g, ginv, F, &kw);
+    size_t Ptot = 0;
+    for (int k = 0; k < N; ++k) Ptot += (size_t)p[k] + n2[k];
+
+    /* cholesky!(L, F)  :5-26;  `A` = the previous block's C factor (0×0 at k = 1, :7) */
+    for (int k = 0; k < N; ++k) {
+        oblk *l = &L[k], *f = &F[k];
+        int p1 = l->p1, ps = l->ps, p2 = l->p2;
+        const double *Af = k ? L[k - 1].C : NULL;
+        for (int j = 0; j < p1; ++j)                                      /* :16 D = F.D/A.U */
+            for (int i = 0; i < ps; ++i) l->D[IDX(i, j, ps)] = f->D[IDX(j, i, p1)];
+        if (p1) rdiv_lt(ps, p1, l->D, ps, Af, p1);
+        for (int j = 0; j < ps; ++j)                                      /* :17 B − D Dᵀ */
+            for (int i = 0; i < ps; ++i) {
+                double s = f->B[IDX(i, j, ps)];
+                for (int q = 0; q < p1; ++q) s -= l->D[IDX(i, q, ps)] * l->D[IDX(j, q, ps)];
+                l->B[IDX(i, j, ps)] = s;
+            }
+        if (ps) { int st = potrf_lower(ps, l->B, ps); if (st && !info) info = k + 1; } /* :17-18 */
+        for (int j = 0; j < p1; ++j)                                      /* :19 F = F.F/A.U */
+            for (int i = 0; i < p2; ++i) l->F[IDX(i, j, p2)] = f->F[IDX(j, i, p1)];
+        if (p1) rdiv_lt(p2, p1, l->F, p2, Af, p1);
+        for (int j = 0; j < ps; ++j)                                      /* :20 (E − F Dᵀ)/B.U */
+            for (int i = 0; i < p2; ++i) {
+                double s = f->E[IDX(j, i, ps)];
+                for (int q = 0; q < p1; ++q) s -= l->F[IDX(i, q, p2)] * l->D[IDX(j, q, ps)];
+                l->E[IDX(i, j, p2)] = s;
+            }
+        if (ps) rdiv_lt(p2, ps, l->E, p2, l->B, ps);
+        for (int j = 0; j < p2; ++j)                                      /* :21 C − FFᵀ − EEᵀ */
+            for (int i = 0; i < p2; ++i) {
+                double s = f->C[IDX(i, j, p2)];
+                for (int q = 0; q < p1; ++q) s -= l->F[IDX(i, q, p2)] * l->F[IDX(j, q, p2)];
+                for (int q = 0; q < ps; ++q) s -= l->E[IDX(i, q, p2)] * l->E[IDX(j, q, p2)];
+                l->C[IDX(i, j, p2)] = s;
+            }
+        if (p2) { int st = potrf_lower(p2, l->C, p2); if (st && !info) info = k + 1; } /* :21-22 */
+        memcpy(l->c, f->c, (size_t)ps * sizeof(double));                 /* :23-24 */
+        memcpy(l->d, f->d, (size_t)p2 * sizeof(double));
+    }
+
+    /* forward substitution, lower blocks (commented text :146-156) */
+    for (int k = 0; k < N; ++k) {
+        oblk *l = &L[k];
+        int p1 = l->p1, ps = l->ps, p2 = l->p2;
+        const double *lp = k ? L[k - 1].lam : NULL;
+        for (int i = 0; i < ps; ++i) {                                    /* μ = B\(c − Dλ) */
+            double s = l->c[i];
+            for (int q = 0; q < p1 && k; ++q) s -= l->D[IDX(i, q, ps)] * lp[q];
+            l->mu[i] = s;
+        }
+        if (ps) trsv_l(ps, l->B, ps, l->mu, 0);
+        for (int i = 0; i < p2; ++i) {                                    /* λ = C\(d − Fλ − Eμ) */
+            double s = l->d[i];
+            for (int q = 0; q < p1 && k; ++q) s -= l->F[IDX(i, q, p2)] * lp[q];
+            for (int q = 0; q < ps; ++q) s -= l->E[IDX(i, q, p2)] * l->mu[q];
+            l->lam[i] = s;
+        }
+        if (p2) trsv_l(p2, l->C, p2, l->lam, 0);
+    }
+    size_t ol = 0;
+    for (int k = 0; k < N; ++k) {
+        if (yv) {
+            for (int i = 0; i < L[k].ps; ++i) yv[ol + i] = L[k].mu[i];
+            for (int i = 0; i < L[k].p2; ++i) yv[ol + L[k].ps + i] = L[k].lam[i];
+        }
+        ol += (size_t)L[k].ps + L[k].p2;
+    }
+    /* backward substitution, lower blocks (commented text :158-168) */
+    for (int k = N - 1; k >= 0; --k) {
+        oblk *l = &L[k];
+        int ps = l->ps, p2 = l->p2;
+        if (k < N - 1) {
+            oblk *nx = &L[k + 1];                                         /* Lprev = L[k+1] */
+            for (int i = 0; i < p2; ++i) {                                /* λ −= D'μ' + F'λ' */
+                double s = l->lam[i];
+                for (int q = 0; q < nx->ps; ++q) s -= nx->D[IDX(q, i, nx->ps)] * nx->mu[q];
+                for (int q = 0; q < nx->p2; ++q) s -= nx->F[IDX(q, i, nx->p2)] * nx->lam[q];
+                l->lam[i] = s;
+            }
+            if (p2) trsv_l(p2, l->C, p2, l->lam, 1);
+            for (int i = 0; i < ps; ++i) {                                /* μ −= E'λ */
+                double s = l->mu[i];
+                for (int q = 0; q < p2; ++q) s -= l->E[IDX(q, i, p2)] * l->lam[q];
+                l->mu[i] = s;
+            }
+        } else if (p2) {
+            trsv_l(p2, l->C, p2, l->lam, 1);       /* a terminal p2 > 0 (not a reference shape) */
+            for (int i = 0; i < ps; ++i) {
+                double s = l->mu[i];
+                for (int q = 0; q < p2; ++q) s -= l->E[IDX(q, i, p2)] * l->lam[q];
+                l->mu[i] = s;
+            }
+        }
+        if (ps) trsv_l(ps, l->B, ps, l->mu, 1);
+    }
+
+    /* dense L and x (copy_block!, lower storage :181-195) */
+    if (Ld) memset(Ld, 0, Ptot * Ptot * sizeof(double));
+    size_t off = 0;
+    ol = 0;
+    for (int k = 0; k < N; ++k) {
+        oblk *l = &L[k];
+        int p1 = l->p1, ps = l->ps, p2 = l->p2;
+        size_t b1 = off, bs = off + p1, b2 = off + p1 + ps;
+        if (Ld) {
+#define PUTL(blk, r0, c0, nr, nc)                                                        \
+    for (int j = 0; j < (nc); ++j)                                                      \
+        for (int i = 0; i < (nr); ++i) Ld[IDX((r0) + i, (c0) + j, Ptot)] = (blk)[IDX(i, j, (nr))];
+            PUTL(l->B, bs, bs, ps, ps); PUTL(l->C, b2, b2, p2, p2);
+            PUTL(l->D, bs, b1, ps, p1); PUTL(l->E, b2, bs, p2, ps); PUTL(l->F, b2, b1, p2, p1);
+#undef PUTL
+        }
+        if (xv) {
+            for (int i = 0; i < ps; ++i) xv[ol + i] = l->mu[i];
+            for (int i = 0; i < p2; ++i) xv[ol + ps + i] = l->lam[i];
+        }
+        ol += (size_t)ps + p2;
+        off += (size_t)p1 + ps;
+    }
+    kkt_work_free(N, &kw);
+    free_blocks(N, F); free_blocks(N, L); free(F); free(L);
     return info;
 }
 

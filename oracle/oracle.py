@@ -49,6 +49,9 @@ def load():
         lib.oracle_kkt_solve_batch.restype = i64
         lib.oracle_kkt_solve_batch.argtypes = [i32, vp, vp, vp, vp, i64, vp, vp, i32, vp, vp,
                                                i32, vp, vp, vp, i32]
+        lib.oracle_kkt_lower_one.restype = i32
+        lib.oracle_kkt_lower_one.argtypes = [i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, i32, vp,
+                                             vp, vp]
         lib.oracle_num_threads_max.restype = i32
         _lib = lib
     return _lib
@@ -145,6 +148,22 @@ def kkt_solve_one(st: KktStructure, Y, y, H, g, h_mode=2, ginv=1, debug=False):
     if debug:
         out.update(S=S.reshape(st.P, st.P, order="F"), U=U.reshape(st.P, st.P, order="F"), r=r)
     return out
+
+
+def kkt_lower_one(st: KktStructure, Y, y, H, g, h_mode=2, ginv=1):
+    """KKT-12: the lower-storage block Cholesky (cholesky_solve.jl:5-26) and the lower
+    forward/backward substitutions (the commented text :146-168).  Returns the dense lower
+    factor L (P×P), yv = L⁻¹r after the forward sweep, xv = S⁻¹r after the backward sweep,
+    and info."""
+    lib = load()
+    L = np.zeros(st.P * st.P)
+    yv = np.zeros(st.P)
+    xv = np.zeros(st.P)
+    f = lambda a: np.ascontiguousarray(a, dtype=np.float64)
+    Y, y, H, g = f(Y), f(y), f(H), f(g)
+    info = lib.oracle_kkt_lower_one(st.N, _p(st.n1), _p(st.p), _p(st.n2), _p(st.w), _p(Y), _p(y),
+                                    h_mode, _p(H), _p(g), ginv, _p(L), _p(yv), _p(xv))
+    return dict(L=L.reshape(st.P, st.P, order="F"), y=yv, x=xv, info=info)
 
 
 def kkt_solve_batch(st: KktStructure, bt, Y, y, H, g, h_mode=2, ginv=1, nthreads=1):

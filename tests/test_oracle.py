@@ -87,6 +87,56 @@ def test_kkt_oracle_soc(lqrx, name):
     assert np.allclose(out["dz"], ref, rtol=1e-9, atol=1e-11)
 
 
+@pytest.mark.parametrize("name", ["di", "dubins", "di_small"])
+@pytest.mark.parametrize("h_mode", [0, 2])
+def test_kkt12_lower_variant(lqrx, name, h_mode):
+    """KKT-12: the lower-storage block Cholesky (cholesky_solve.jl:5-26) cross-checks the
+    upper one, as test/constraint_blocks.jl:103-133 does:
+      :122  L_ ≈ U_'          :123  L_ ≈ cholesky(S0).L     :124  U_ ≈ cholesky(S0).U
+      :125  cholesky(S0).L\\d ≈ λ  (after the forward sweep)
+      :133  cholesky(S0)\\d ≈ λ    (after the backward sweep)
+    with d = the stacked [c; d] right-hand side r of the Schur system; the upper solve
+    returns −S⁻¹r (its backward sweep negates, :135-136), the lower one +S⁻¹r."""
+    import lqrx.kkt as K
+
+    st = _struct(name)
+    pb = K.random_kkt(st, 1, seed=41 + h_mode, h_mode=h_mode)
+    os_ = _oracle_struct(st)
+    up = orc.kkt_solve_one(os_, pb.Y[0], pb.y[0], pb.H[0], pb.g[0], h_mode=h_mode, debug=True)
+    lo = orc.kkt_lower_one(os_, pb.Y[0], pb.y[0], pb.H[0], pb.g[0], h_mode=h_mode)
+    assert up["info"] == 0 and lo["info"] == 0
+    dn = orc.kkt_dense(os_, pb.Y[0], pb.y[0], pb.H[0], pb.g[0], h_mode=h_mode)
+    S0 = dn["S"]
+    S0 = 0.5 * (S0 + S0.T)
+    Lref = np.linalg.cholesky(S0)
+    L, U = lo["L"], np.triu(up["U"])
+    sc = np.abs(Lref).max()
+    assert np.array_equal(L, np.tril(L))                       # lower storage only
+    assert np.abs(L - U.T).max() <= 1e-12 * sc                  # :122
+    assert np.abs(L - Lref).max() <= 1e-9 * sc                  # :123
+    assert np.abs(U - Lref.T).max() <= 1e-9 * sc                # :124
+    r = up["r"]
+    y_ref = sla.solve_triangular(Lref, r, lower=True)
+    assert np.allclose(lo["y"], y_ref, rtol=1e-8, atol=1e-10 * np.abs(y_ref).max())   # :125
+    x_ref = np.linalg.solve(S0, r)
+    assert np.allclose(lo["x"], x_ref, rtol=1e-8, atol=1e-10 * np.abs(x_ref).max())   # :133
+    assert np.allclose(lo["x"], -up["lam"], rtol=1e-10, atol=1e-12 * np.abs(x_ref).max())
+
+
+def test_kkt12_lower_variant_throws_on_indefinite(lqrx):
+    """cholesky() in the lower variant throws PosDefException (cholesky_solve.jl:17,21);
+    the oracle reports the failing block."""
+    import lqrx.kkt as K
+
+    st = K.dubins_structure(11)
+    pb = K.random_kkt(st, 1, seed=3, h_mode=2)
+    h = pb.H.shape[1]
+    pb.H[0, h // 2:] = -np.abs(pb.H[0, h // 2:])              # later knots: negative cost
+    lo = orc.kkt_lower_one(_oracle_struct(st), pb.Y[0], pb.y[0], pb.H[0], pb.g[0], h_mode=2)
+    up = orc.kkt_solve_one(_oracle_struct(st), pb.Y[0], pb.y[0], pb.H[0], pb.g[0], h_mode=2)
+    assert lo["info"] > 0 and lo["info"] == up["info"]
+
+
 def test_kkt_oracle_non_spd_info(lqrx):
     """A negative cost Hessian entry must be reported (the reference discards potrf info)."""
     import lqrx.kkt as K
