@@ -103,6 +103,72 @@ def cpu_baseline_kkt(N, target_s=12.0, threads=None):
                        f"of _solve!), OpenMP {threads} threads, {dt:.1f} s")
 
 
+def _sample_index(batch, k=64):
+    import numpy as np
+    return np.unique(np.linspace(0, batch - 1, k).round().astype(np.int64))
+
+
+def check_dp_sample(out, sub, idx, n, m, N, bt, tol, threads):
+    """Checker (outside the timed region): the timed launch's K, P₁, X, U for a strided
+    sample of trajectories (first and last included) against the CPU oracle on the same
+    inputs — K/P per knot relative, X/U on the trajectory's scale."""
+    import numpy as np
+    import torch
+    from lqrx.dp import from_abi
+    from oracle import oracle as orc
+
+    ti = torch.from_numpy(idx).to(out["K"].device)
+    pick = lambda x, w: x.view(bt, w).index_select(0, ti).cpu().numpy().astype(np.float64)
+    s = len(idx)
+    ref = orc.dp_solve_abi(dict(sub, n=n, m=m, N=N, batch=s), N, nthreads=threads)
+
+    def knot_err(a, b):
+        a, b = a.reshape(s, a.shape[1], -1), b.reshape(s, b.shape[1], -1)
+        den = np.abs(b).max(axis=2)
+        den[den == 0] = 1.0
+        return float((np.abs(a - b).max(axis=2) / den).max())
+
+    def traj_err(a, b):
+        a, b = a.reshape(s, -1), b.reshape(s, -1)
+        return float((np.abs(a - b).max(axis=1) / np.maximum(1.0, np.abs(b).max(axis=1))).max())
+
+    e = dict(K=knot_err(from_abi(pick(out["K"], (N - 1) * m * n), (s, N - 1, m, n)),
+                        from_abi(ref["K"], (s, N - 1, m, n))),
+             P=knot_err(pick(out["P"], n * n)[:, None], ref["P"].reshape(s, 1, n * n)),
+             X=traj_err(pick(out["X"], N * n), ref["X"]),
+             U=traj_err(pick(out["U"], (N - 1) * m), ref["U"]))
+    return {"trajectories": s, "last_index": int(idx[-1]), "max_rel_err": e, "tol": tol,
+            "pass": bool(max(e.values()) <= tol),
+            "oracle": "oracle/lqr_oracle.c (restatement of dynamic_programming.jl:54-72)"}
+
+
+def check_kkt_sample(out, pb, st, idx, bt, threads):
+    """Checker: the timed launch's δz, λ for a strided sample against the C oracle of
+    cholesky_solver.jl _solve! (1e-10 relative)."""
+    import numpy as np
+    import torch
+    from oracle import oracle as orc
+
+    ti = torch.from_numpy(idx).to(out["dz"].device)
+    s = len(idx)
+    dz = out["dz"].view(bt, -1).index_select(0, ti).cpu().numpy()
+    lam = out["lam"].view(bt, -1).index_select(0, ti).cpu().numpy()
+    ref = orc.kkt_solve_batch(orc.KktStructure(st.n, st.m, st.N, st.p), s, pb.Y[idx], pb.y[idx],
+                              pb.H[idx], pb.g[idx], h_mode=2, nthreads=threads)
+    rel = lambda a, b: float((np.abs(a - b.reshape(a.shape)).max(axis=1)
+                              / np.maximum(1e-300, np.abs(b.reshape(a.shape)).max(axis=1))).max())
+    e = dict(dz=rel(dz, ref["dz"]), lam=rel(lam, ref["lam"]))
+    return {"trajectories": s, "last_index": int(idx[-1]), "max_rel_err": e, "tol": 1e-10,
+            "pass": bool(max(e.values()) <= 1e-10),
+            "oracle": "oracle/lqr_oracle.c (restatement of cholesky_solver.jl _solve!)"}
+
+
+def nonfinite_count(out, keys):
+    """Whole-batch scan of the timed launch's outputs on the device."""
+    import torch
+    return int(sum(int((~torch.isfinite(out[k])).sum().item()) for k in keys if k in out))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -143,15 +209,13 @@ def main():
             args.N = 101
 
     import torch
-    import torch.distributed as dist
     import lqrx
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from lqrx import shard as SH
+
+    rank, world, local = SH.dist_env()
     torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    SH.init_ranks("nccl", torch.device("cuda", local))
     lib = lqrx.load()
     if lib.lqrx_device_available() != 1:
         raise RuntimeError("liblqrx.so sees no gfx950 device")
@@ -191,6 +255,10 @@ def main():
             host["x0"] = cb.x0.astype(npdt).ravel()
         t = {k: torch.from_numpy(host[k]).to(dev) for k in ("A", "B", "Q", "R", "Qf", "x0")}
         t.update(n=n, m=m, batch=bt)
+        chk_idx = _sample_index(bt)
+        widths = dict(A=n * n, B=n * m, Q=n * n, R=m * m, Qf=n * n, x0=n)
+        chk_sub = {k: host[k].reshape(bt, w)[chk_idx].astype("float64").ravel()
+                   for k, w in widths.items()}
         del host
         if args.tv:
             # per-knot fields: every knot's block is its own copy in HBM (the kernel streams
@@ -232,55 +300,43 @@ def main():
         def step():
             K.kkt_solve_device(st, t, K.H_DIAG, 1, stream=sh, out=out, workspace=ws)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
+    sync = lambda: torch.cuda.synchronize(dev)
+    wall = SH.timed_steps(step, args.steps, args.warmup, sync, world,
+                          on_start=lambda: ev0.record(stream), on_stop=lambda: ev1.record(stream))
     kern_ms = ev0.elapsed_time(ev1) / args.steps       # stream-timed launch duration
     bad = int((out["info"] != 0).sum().item()) if args.workload != "sqp" else \
         int((out["info"] == 2).sum().item())                  # SQP: line-search failures
+    # output checks, outside the timed region: the whole batch scanned on the device for
+    # non-finite values; a strided sample compared with the CPU oracle (rank 0)
+    nonfinite = nonfinite_count(out if args.workload != "sqp" else t,
+                                ("K", "P", "X", "U", "dz", "lam", "Z"))
+    nonfinite, bad = SH.sum_over_ranks([nonfinite, bad], world, dev)
+    sampled = None
+    if rank == 0 and args.workload in ("dp", "cartpole", "kkt"):
+        thr = max(1, min(16, os.cpu_count() or 1))
+        if args.workload == "kkt":
+            sampled = check_kkt_sample(out, pb, st, _sample_index(bt), bt, thr)
+        else:   # (a --tv run repeats the time-invariant draw per knot: same oracle problem)
+            sampled = check_dp_sample(out, chk_sub, chk_idx, n, m, N, bt,
+                                      1e-10 if f64 else 1e-4, thr)
 
     # final gather, timed separately from the solve: info + P_1 of every
     # shard to rank 0 over RCCL (grouped send/recv); K stays sharded
     gather = None
     if world > 1 and args.workload in ("dp", "cartpole") and not args.no_gather:
-        from lqrx.shard import gather_to_root
-        fields = {"info": out["info"], "P": out["P"]}
         try:
-            torch.cuda.synchronize(dev)
-            dist.barrier()
-            tg0 = time.perf_counter()
-            got = gather_to_root(fields, bt * world)
-            torch.cuda.synchronize(dev)
-            tg = torch.tensor([time.perf_counter() - tg0], dtype=torch.float64, device=dev)
-            dist.all_reduce(tg, op=dist.ReduceOp.MAX)
-            gbytes = sum(f.numel() * f.element_size() for f in fields.values()) * (world - 1)
-            gather = {"ms": float(tg.item()) * 1e3, "bytes_to_root": gbytes,
-                      "what": "info + P_1 of every shard to rank 0 (torch.distributed.gather = RCCL "
-                              "send/recv); K stays sharded",
-                      "root_info_nonzero": int((got["info"] != 0).sum().item()) if got is not None else None}
+            g = SH.timed_gather({"info": out["info"], "P": out["P"]}, bt * world, world, sync, dev)
+            got = g.pop("got")
+            gather = dict(g, what="info + P_1 of every shard to rank 0 (torch.distributed.gather "
+                                  "= RCCL send/recv); K stays sharded",
+                          root_info_nonzero=int((got["info"] != 0).sum().item()) if got is not None else None)
             del got
         except Exception as e:  # the solve measurement stands without the gather
             gather = {"error": f"{type(e).__name__}: {e}"}
 
-    wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
-    wall = float(wall_t.item())
+    wall = SH.max_over_ranks(wall, world, dev)
     total = bt * world * args.steps
     value = total / wall
     ms_per_step = wall / args.steps * 1e3
@@ -405,15 +461,13 @@ def main():
                        "global_batch": bt * world, "parallelism": f"batch-sharded x{world}"},
             "roofline": roof,
             "cpu_baseline": cpu,
-            "nonfinite_or_info": bad,
+            "check": {"nonfinite": nonfinite, "info_nonzero": bad, "sampled_parity": sampled},
             "gather": gather,
         }
         if gather is not None and "ms" in gather:
             line["value_solve_plus_gather"] = total / (wall + gather["ms"] * 1e-3)
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    SH.finish_ranks(world)
 
 
 if __name__ == "__main__":

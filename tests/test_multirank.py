@@ -117,3 +117,75 @@ def test_gather_to_root_gloo(lqrx, world, batch):
     ref = orc.dp_solve_abi(L.random_batch(4, 2, 9, batch, seed=31), 9)
     for k in ("info", "P", "U"):
         assert np.array_equal(res[0][k], ref[k]), k
+
+
+def _bench_scaffold_worker(rank, world, port, root, per, q):
+    """bench.py's rank logic (lqrx.shard: init_ranks, timed_steps, sum/max_over_ranks,
+    timed_gather, finish_ranks) with the oracle as the per-rank solver."""
+    import sys
+    import time
+
+    sys.path[:0] = [os.path.join(root, "lqr.jl_amd"), root]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch
+    import lqrx
+    from lqrx import shard as SH
+    from oracle import oracle as orc
+
+    r, w, local = SH.init_ranks("gloo")
+    assert (r, w, local) == (rank, world, rank)
+    n, m, N = 4, 2, 10
+    d = lqrx.random_batch(n, m, N, per, seed=91, traj0=rank * per)    # bench's weak sharding
+    calls = []
+    res = {}
+
+    def step():
+        calls.append(1)
+        res.update(orc.dp_solve_abi(d, N))
+        time.sleep(0.02 * (rank + 1))                                  # ranks finish unevenly
+
+    wall = SH.timed_steps(step, steps=3, warmup=2, world=w)
+    nonfinite = int(sum((~np.isfinite(res[k])).sum() for k in ("K", "X", "U")))
+    bad = int((res["info"] != 0).sum())
+    nf, nb = SH.sum_over_ranks([nonfinite, bad + rank], w)
+    job = SH.max_over_ranks(wall, w)
+    g = SH.timed_gather({"info": torch.from_numpy(res["info"]), "P": torch.from_numpy(res["P"])},
+                        per * w, w)
+    got = g["got"]
+    q.put((rank, len(calls), wall, job, nf, nb, g["ms"], g["bytes_to_root"],
+           None if got is None else {k: v.numpy() for k, v in got.items()}))
+    SH.finish_ranks(w)
+
+
+def test_bench_rank_scaffolding_gloo(lqrx):
+    """The multi-GPU bench path minus the GPU: warmup + exactly `steps` timed steps per rank,
+    job time = MAX over ranks (≥ the slowest rank's own wall), counters summed over ranks,
+    the timed final gather delivers rank-ordered info + P₁ equal to a one-process solve."""
+    import lqrx as L
+    from oracle import oracle as orc
+
+    world, per = 2, 3
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_scaffold_worker, args=(r, world, port, root, per, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r[0]: r for r in (q.get(timeout=180) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        _, ncalls, wall, job, nf, nb, gms, gbytes, got = res[r]
+        assert ncalls == 5                                   # 2 warmup + 3 timed
+        assert job >= max(res[k][2] for k in range(world)) - 1e-9
+        assert job >= 3 * 0.02 * world                       # slowest rank's sleeps
+        assert nf == 0 and nb == sum(range(world))           # SUM over ranks
+        assert gms > 0 and gbytes == per * (4 + 4 * 4 * 8) * (world - 1)
+        assert (got is None) == (r != 0)
+    ref = orc.dp_solve_abi(L.random_batch(4, 2, 10, per * world, seed=91), 10)
+    assert np.array_equal(res[0][8]["info"], ref["info"])
+    assert np.array_equal(res[0][8]["P"], ref["P"])
