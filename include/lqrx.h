@@ -18,7 +18,15 @@
  *     of the calling thread;
  *   - `stream` is a hipStream_t: NULL = synchronous (like the reference's solve!), else the
  *     work is enqueued and the call returns immediately (check info[] after syncing);
- *   - reentrant; no mutable global state besides the thread-local error string.
+ *   - reentrant and thread-safe.  Mutable library state, all of it process-wide and
+ *     mutex-guarded: the calling thread's last-error string (thread-local); one HIP
+ *     memory pool per device for stream-ordered scratch (created on first use, blocks kept
+ *     mapped); a cache of uploaded KKT block-structure tables (≤ 4096 distinct structures,
+ *     never evicted — each is uploaded once, with a blocking copy, on its first use; calls
+ *     with further structures upload a per-call table on their own stream and wait for that
+ *     stream only); environment switches read once.  All of it is keyed on the device of
+ *     the call's `stream`, not on the thread's current device.  No call synchronises the
+ *     whole device.
  */
 #ifndef LQRX_H
 #define LQRX_H

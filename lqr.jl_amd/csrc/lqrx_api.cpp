@@ -82,12 +82,27 @@ int validate_dp(const lqrx_dp_desc *d)
 } // namespace
 
 namespace lqrx {
+// The device a stream belongs to (the null stream: the calling thread's current device).
+// Library state below is keyed on it, not on hipGetDevice(), so a call on a stream of
+// device d works whatever device the calling thread has current.
+hipError_t stream_device(hipStream_t s, int *dev)
+{
+    if (!s) return hipGetDevice(dev);
+    hipDevice_t d = 0;
+    hipError_t e = hipStreamGetDevice(s, &d);
+    if (e == hipSuccess) *dev = (int)d;
+    return e;
+}
+
+// Process-wide state (mutex-guarded, created on first use): one memory pool per device for
+// stream-ordered scratch; freed blocks stay mapped (release threshold ∞), so steady-state
+// calls allocate nothing from the driver.
 hipError_t scratch_alloc(void **p, size_t bytes, hipStream_t s)
 {
     static std::mutex mu;
     static std::map<int, hipMemPool_t> pools;
     int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
+    hipError_t e = stream_device(s, &dev);
     if (e != hipSuccess) return e;
     hipMemPool_t pool = nullptr;
     {
@@ -264,17 +279,28 @@ int kkt_layout(const lqrx_kkt_desc *d, KktLayout &L)
     if (L.sY > INT32_MAX) return set_err(LQRX_ERR_UNSUPPORTED, "trajectory too large");
     return 0;
 }
-// Per-device cache of uploaded structure tables.  The upload is a blocking hipMemcpy on
-// first use of a structure; afterwards a solve issues no host→device traffic besides the
-// launch.  (A per-call stream-ordered alloc + pageable async copy was observed to leave
-// the device table stale on repeated calls with alternating structures.)
-int device_meta(const std::vector<int32_t> &meta, const int32_t **out)
+// Per-device cache of uploaded structure tables (process-wide, mutex-guarded), keyed on the
+// stream's device.  A structure's table is uploaded by a blocking copy on its first use;
+// afterwards a solve issues no host→device traffic besides the launch.  (A per-call
+// stream-ordered alloc + pageable async copy was observed to leave the device table stale on
+// repeated calls with alternating structures.)  The cache holds at most meta_cache_cap() tables
+// and never evicts (nothing is freed under work in flight on another stream); structures
+// beyond that get a per-call table from the stream-ordered pool, copied and waited for on
+// the CALL's stream only (*tmp set: the caller frees it, stream-ordered, after the launch).
+size_t meta_cache_cap()   // LQRX_META_CACHE overrides 4096 (tests exercise the overflow path)
+{
+    static const size_t v = [] { const char *e = std::getenv("LQRX_META_CACHE"); return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)4096; }();
+    return v;
+}
+int device_meta(const std::vector<int32_t> &meta, hipStream_t s, const int32_t **out, void **tmp)
 {
     static std::mutex mu;
     static std::map<std::pair<int, std::vector<int32_t>>, int32_t *> cache;
+    *tmp = nullptr;
     int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return hip_err(e, "hipGetDevice");
+    hipError_t e = lqrx::stream_device(s, &dev);
+    if (e != hipSuccess) return hip_err(e, "stream device");
+    const size_t bytes = meta.size() * sizeof(int32_t);
     std::lock_guard<std::mutex> lock(mu);
     auto key = std::make_pair(dev, meta);
     auto it = cache.find(key);
@@ -282,18 +308,28 @@ int device_meta(const std::vector<int32_t> &meta, const int32_t **out)
         *out = it->second;
         return 0;
     }
-    if (cache.size() >= 4096) { // bound the cache: drop every table (all work must be done)
-        if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_err(e, "hipDeviceSynchronize");
-        for (auto &kv : cache) (void)hipFree(kv.second);
-        cache.clear();
+    if (cache.size() >= meta_cache_cap()) {
+        if ((e = lqrx::scratch_alloc(tmp, bytes, s)) != hipSuccess) return hip_err(e, "meta scratch");
+        if ((e = hipMemcpyAsync(*tmp, meta.data(), bytes, hipMemcpyHostToDevice, s)) != hipSuccess ||
+            (e = hipStreamSynchronize(s)) != hipSuccess) {
+            (void)lqrx::scratch_free(*tmp, s);
+            *tmp = nullptr;
+            return hip_err(e, "meta H2D");
+        }
+        *out = (const int32_t *)*tmp;
+        return 0;
     }
+    int prev = -1;
+    if ((e = hipGetDevice(&prev)) != hipSuccess) return hip_err(e, "hipGetDevice");
+    if (prev != dev && (e = hipSetDevice(dev)) != hipSuccess) return hip_err(e, "hipSetDevice");
     int32_t *d = nullptr;
-    const size_t bytes = meta.size() * sizeof(int32_t);
-    if ((e = hipMalloc((void **)&d, bytes)) != hipSuccess) return hip_err(e, "hipMalloc meta");
-    if ((e = hipMemcpy(d, meta.data(), bytes, hipMemcpyHostToDevice)) != hipSuccess) {
+    e = hipMalloc((void **)&d, bytes);
+    if (e == hipSuccess && (e = hipMemcpy(d, meta.data(), bytes, hipMemcpyHostToDevice)) != hipSuccess) {
         (void)hipFree(d);
-        return hip_err(e, "meta H2D");
+        d = nullptr;
     }
+    if (prev != dev) (void)hipSetDevice(prev);
+    if (e != hipSuccess) return hip_err(e, "meta upload");
     cache.emplace(std::move(key), d);
     *out = d;
     return 0;
@@ -385,7 +421,8 @@ int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const v
     hipStream_t s = (hipStream_t)stream;
     // device copy of the block-structure table, uploaded once per distinct structure
     const int32_t *dmeta = nullptr;
-    if ((st = device_meta(L.meta, &dmeta))) return st;
+    void *meta_tmp = nullptr;
+    if ((st = device_meta(L.meta, s, &dmeta, &meta_tmp))) return st;
     hipError_t e;
     lqrx::KktArgs a = kkt_args(d, L);
     a.Y = (const double *)Y; a.y = (const double *)y; a.H = (const double *)H; a.g = (const double *)g;
@@ -400,6 +437,7 @@ int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const v
     static const int debug_meta = [] { const char *v = std::getenv("LQRX_DEBUG_META"); return v && *v == '1'; }();
     if (a.force_lane || kkt_force_generic() || !lqrx::kkt_fil_launch(a, d->n1, d->p, d->n2, d->w, s, &e))
         e = lqrx::kkt_launch(a, s);
+    if (meta_tmp) (void)lqrx::scratch_free(meta_tmp, s);   // stream-ordered after the launch
     if (debug_meta) {
         std::vector<int32_t> back(L.meta.size());
         (void)hipStreamSynchronize(s);

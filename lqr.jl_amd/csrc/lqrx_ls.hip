@@ -29,7 +29,8 @@ namespace {
 
 constexpr int LS_THREADS = 256;
 constexpr int LS_REG = 16;     // register fast paths (buildAb!, rollout!) for n, m ≤ 16, nm + n ≤ 64
-constexpr int LS_MAX_NM = 192; // (N−1)·m; LDS binds first (H is Nm² doubles: Nm ≤ 143)
+constexpr int LS_MAX_NM = 192; // (N−1)·m; H is a packed triangle (Nm(Nm+1)/2 doubles), the LDS
+                               // budget (≤ 163840 B, validate_ls) binds at Nm = 192
 
 // order one wave's LDS accesses across lanes (a wave executes LDS ops in order; this stops
 // the compiler from moving them across and waits for the writes)
@@ -120,6 +121,18 @@ __device__ bool small_chol_u(const double *M, double *U, int s)
     return true;
 }
 
+// A failed trajectory (Q/Qf/R not SPD, or a non-positive pivot of H) gets NaN in U and X
+// — never uninitialised memory — and its info code; the reference throws there
+// (cholesky / potrf!).  Called by every thread of the workgroup (uniform early return).
+__device__ void ls_fail(double *gU, double *gX, int32_t *ginfo, int64_t b, int n, int m, int N, int code)
+{
+    const double qnan = __builtin_nan("");
+    const int nu = (N - 1) * m, nx = N * n;
+    for (int i = threadIdx.x; i < nu; i += LS_THREADS) gU[b * nu + i] = qnan;
+    for (int i = threadIdx.x; i < nx; i += LS_THREADS) gX[b * nx + i] = qnan;
+    if (threadIdx.x == 0 && ginfo) ginfo[b] = code;
+}
+
 __global__ void __launch_bounds__(LS_THREADS)
 ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB, const double *__restrict__ gQ,
                     const double *__restrict__ gR, const double *__restrict__ gQf, const double *__restrict__ gx0,
@@ -157,7 +170,7 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
     }
     __syncthreads();
     if (*flag) {
-        if (tid == 0 && ginfo) ginfo[b] = -1;
+        ls_fail(gU, gX, ginfo, b, n, m, N, -1);
         return;
     }
 
@@ -299,7 +312,7 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
     for (int j = 0; j < Nm; ++j) {
         const double d = H[up(j, j, Nm)];
         if (!(d > 0.0)) {   // uniform: every thread reads the same LDS word
-            if (tid == 0 && ginfo) ginfo[b] = j + 1;
+            ls_fail(gU, gX, ginfo, b, n, m, N, j + 1);
             return;
         }
         const double rinv = rcp_nr2(d);

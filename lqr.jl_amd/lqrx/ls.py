@@ -73,10 +73,16 @@ class LeastSquaresSolver:
     @classmethod
     def of(cls, prob: LQRProblem):
         n, m, N = prob.size()
+        if (N - 1) * m > MAX_NM:
+            raise _lib.LqrxError(_lib.ERR_UNSUPPORTED,
+                                 f"n={n} m={m} N={N}: (N-1)m = {(N - 1) * m} > {MAX_NM} (LS kernel cap)")
         if lds_bytes(n, m, N) > 163840:
             raise _lib.LqrxError(_lib.ERR_UNSUPPORTED,
                                  f"n={n} m={m} N={N}: the condensed problem exceeds one CU's LDS")
         return cls(n, m, N)
+
+
+MAX_NM = 192      # (N−1)·m cap of ls_condensed_kernel (LS_MAX_NM, lqrx_ls.hip)
 
 
 def lds_bytes(n: int, m: int, N: int) -> int:
@@ -87,6 +93,18 @@ def _ptr(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p)
 
 
+def _check_symmetric(b: LQRBatch):
+    """LeastSquaresSolver(prob) factors Q, Qf (and R) with cholesky() (least_squares.jl:50-52),
+    which throws for a non-Hermitian matrix; the kernel reads only the upper triangles, so the
+    check is made here, exactly as ishermitian() does (no tolerance)."""
+    for name in ("Q", "Qf", "R"):
+        a = np.asarray(getattr(b, name), dtype=np.float64)
+        if not np.array_equal(a, np.swapaxes(a, -1, -2)):
+            bad = int(np.flatnonzero([not np.array_equal(x, x.T) for x in a])[0])
+            raise ValueError(f"{name} of trajectory {bad} is not symmetric "
+                             "(cholesky() throws PosDefException there)")
+
+
 def ls_solve_batch(b: LQRBatch, hu_mode: int = HU_ZERO) -> dict:
     """Batched solve! through lqrx_ls_solve_host.  Returns U (batch, N−1, m),
     X (batch, N, n), info (batch,), rc."""
@@ -95,6 +113,7 @@ def ls_solve_batch(b: LQRBatch, hu_mode: int = HU_ZERO) -> dict:
     if b.time_varying() != (0, 0):
         raise ValueError("LeastSquaresSolver is time-invariant (least_squares.jl:58-103)")
     bt = b.batch
+    _check_symmetric(b)
     ins = [to_abi(np.asarray(x, dtype=np.float64)) for x in (b.A, b.B, b.Q, b.R, b.Qf)]
     x0 = np.ascontiguousarray(np.asarray(b.x0, dtype=np.float64))
     U = np.zeros(bt * (N - 1) * m)

@@ -131,3 +131,18 @@ def test_kkt_workspace_entry(lqrx, gpu_ok):
         with pytest.raises(lqrx.LqrxError) as e:
             K.kkt_solve_device(st, t, K.H_DIAG, 1, workspace=ws[: nb - 8])
         assert e.value.code == -10
+
+
+def test_kkt_meta_cache_overflow(lqrx, gpu_ok):
+    """Beyond the structure-table cache (LQRX_META_CACHE, default 4096) a call uploads a
+    per-call table on its own stream and frees it stream-ordered — no device-wide sync.
+    Exercised with the cache capped at 1, alternating structures and streams."""
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, LQRX_META_CACHE="1")
+    r = subprocess.run([sys.executable, os.path.join(here, "_kkt_meta_overflow.py")], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr

@@ -124,9 +124,28 @@ def test_ls_lds_limits(lqrx):
 
     assert ls.lds_bytes(4, 1, 101) <= 163840      # cartpole N=101 fits one CU
     assert ls.lds_bytes(6, 3, 101) > 163840       # DoubleIntegrator(3,101): Nm = 300
+    assert ls.lds_bytes(2, 2, 97) <= 163840       # Nm = 192: the largest accepted
     with pytest.raises(lqrx.LqrxError):
         ls.LeastSquaresSolver.of(lqrx.LQRProblem(*[np.eye(6)] * 3 + [np.eye(6), np.ones((6, 3)),
                                                                       np.zeros(6)], N=101))
+    for n, m, N in ((2, 2, 98), (4, 1, 193)):     # Nm = 194 > 192; Nm = 192 but LDS > 160 KiB
+        with pytest.raises(lqrx.LqrxError) as e:
+            ls.LeastSquaresSolver.of(lqrx.LQRProblem(np.eye(n), np.eye(n), np.eye(m), np.eye(n),
+                                                     np.ones((n, m)), np.zeros(n), N=N))
+        assert e.value.code == lqrx._lib.ERR_UNSUPPORTED
+
+
+def test_ls_rejects_non_symmetric(lqrx):
+    """cholesky() throws for a non-Hermitian Q/Qf/R (least_squares.jl:50-52); the kernel
+    reads only upper triangles, so the host mirror checks (exactly, like ishermitian)."""
+    from lqrx import ls
+    from lqrx.dp import LQRBatch
+
+    rng = np.random.default_rng(5)
+    A, B, Q, R, Qf, x0 = _batch(rng, 4, 1, 3)
+    Q[2, 0, 1] += 1e-3
+    with pytest.raises(ValueError, match="Q of trajectory 2"):
+        ls.ls_solve_batch(LQRBatch(A, B, Q, R, Qf, x0, 20))
 
 
 # ------------------------------------------------------------------ GPU parity
@@ -138,7 +157,8 @@ def _batch(rng, n, m, bt):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,m,N,bt", [(4, 1, 101, 37), (3, 2, 40, 64), (6, 3, 12, 5), (2, 1, 2, 3),
-                                      (8, 4, 16, 9), (16, 4, 8, 5)])   # last: n·m + n > 64, LDS path
+                                      (8, 4, 16, 9), (16, 4, 8, 5),    # n·m + n > 64, LDS path
+                                      (2, 2, 97, 4)])                  # Nm = 192: the LS cap
 @pytest.mark.parametrize("hu", [0, 1, 2])
 def test_ls_gpu_parity(lqrx, gpu_ok, n, m, N, bt, hu):
     from lqrx import ls
@@ -201,6 +221,8 @@ def test_ls_gpu_info(lqrx, gpu_ok):
     assert out["info"][1] == -1 and out["info"][3] == 1
     ok = [0, 2, 4, 5]
     assert (out["info"][ok] == 0).all()
+    for b in (1, 3):                        # failed trajectories: NaN, never stale memory
+        assert np.isnan(out["U"][b]).all() and np.isnan(out["X"][b]).all()
     for b in ok:
         o = LO.ls_solve(A[b], B[b], Q[b], R[b], Qf[b], x0[b], N)
         assert np.abs(out["U"][b] - o["U"]).max() <= 1e-8 * np.abs(o["U"]).max()

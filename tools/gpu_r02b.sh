@@ -1,3 +1,5 @@
+#!/bin/bash
+# Round-2 check: full-size cfg4/cfg5 parity tests, then bench lines (cfg4, cfg5, kkt, cartpole) with the output checks.
 set -o pipefail
 mkdir -p gpurun_out/r02b
 timeout -k 10 400 python -u -m pytest tests/test_full_size_gpu.py -x -v -s --timeout 300 --timeout-method thread > gpurun_out/r02b/full.log 2>&1 && \
