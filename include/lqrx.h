@@ -74,7 +74,13 @@ typedef struct lqrx_dp_desc {
     int32_t n, m, N;        /* state dim, control dim, knots (N >= 2)                 */
     int32_t dtype;          /* LQRX_F64 (reference precision) or LQRX_F32            */
     int64_t batch;          /* number of independent problems                          */
-    int32_t layout;         /* 0 = column-major, batch slowest (only value supported)  */
+    int32_t layout;         /* 0 = column-major blocks, batch slowest (Julia Array{T,3});
+                               1 = batch fastest (SoA): element e of trajectory b at
+                               [e·batch + b], e = its layout-0 offset within the
+                               trajectory (Julia permutedims(X, (3,1,2)), Python [S][batch]);
+                               every array of the call (inputs and outputs) uses it.  Native
+                               in the n ≤ 4 kernels (coalesced per element); n ≥ 5 converts
+                               to layout 0 in stream-ordered scratch and back (2× traffic) */
     int32_t p_mode;         /* 0 = P_1 only (reference-observable), 1 = all P_k        */
     int64_t knot_stride_AB; /* 0 = time-invariant A, B (reference LQRProblem);
                                1 = per knot: A n·n·(N-1)·batch, B n·m·(N-1)·batch, knot k

@@ -66,7 +66,8 @@ int validate_dp(const lqrx_dp_desc *d)
     if (d->dtype != LQRX_F64 && d->dtype != LQRX_F32)
         return set_err(-1, "desc.dtype must be LQRX_F64 or LQRX_F32 (got %d)", d->dtype);
     if (d->batch < 0) return set_err(-1, "desc.batch must be >= 0");
-    if (d->layout != 0) return set_err(LQRX_ERR_UNSUPPORTED, "desc.layout %d not supported", d->layout);
+    if (d->layout != 0 && d->layout != 1)
+        return set_err(-1, "desc.layout must be 0 (batch slowest) or 1 (batch fastest, SoA) (got %d)", d->layout);
     if (d->p_mode != 0 && d->p_mode != 1) return set_err(-1, "desc.p_mode must be 0 or 1");
     if (d->knot_stride_AB != 0 && d->knot_stride_AB != 1)
         return set_err(-1, "desc.knot_stride_AB must be 0 (time-invariant) or 1 (per knot)");
@@ -126,6 +127,46 @@ hipError_t scratch_alloc(void **p, size_t bytes, hipStream_t s)
 hipError_t scratch_free(void *p, hipStream_t s) { return hipFreeAsync(p, s); }
 } // namespace lqrx
 
+namespace {
+// Layout 1 on the MFMA kernel (one trajectory per wave, contiguous blocks wanted): the SoA
+// inputs are transposed to layout 0 in one stream-ordered scratch block, solved, and the
+// outputs transposed back into the caller's SoA buffers.  Extra HBM traffic: one read + one
+// write of every input and output (2× the algorithmic bytes); the n ≤ 4 kernels read SoA
+// natively instead.
+hipError_t dp_launch_soa_staged(const lqrx::DpArgs &a, hipStream_t s)
+{
+    const int64_t B = a.batch, n = a.n, m = a.m, N = a.N, es = dsize(a.dtype);
+    const int64_t kAB = a.tv_AB ? N - 1 : 1, kQR = a.tv_QR ? N - 1 : 1;
+    const int64_t S_in[6] = {n * n * kAB, n * m * kAB, n * n * kQR, m * m * kQR, n * n, n};
+    const int64_t S_out[4] = {m * n * (N - 1), a.p_all ? n * n * N : n * n, n * N, m * (N - 1)};
+    const void *in[6] = {a.A, a.B, a.Q, a.R, a.Qf, a.x0};
+    void *out[4] = {a.K, a.P, a.X, a.U};
+    size_t off[10], total = 0;
+    for (int i = 0; i < 10; ++i) {
+        off[i] = total;
+        total += ((size_t)(i < 6 ? S_in[i] : S_out[i - 6]) * B * es + 255) & ~(size_t)255;
+    }
+    void *blk = nullptr;
+    hipError_t e = lqrx::scratch_alloc(&blk, total, s);
+    if (e != hipSuccess) return e;
+    char *base = (char *)blk;
+    lqrx::DpArgs a0 = a;
+    a0.layout = 0;
+    const void **pin[6] = {&a0.A, &a0.B, &a0.Q, &a0.R, &a0.Qf, &a0.x0};
+    void **pout[4] = {&a0.K, &a0.P, &a0.X, &a0.U};
+    for (int i = 0; i < 6 && e == hipSuccess; ++i) {          // [S][B] → [B][S]
+        *pin[i] = base + off[i];
+        e = lqrx::batch_transpose(in[i], base + off[i], S_in[i], B, (int)es, s);
+    }
+    for (int i = 0; i < 4; ++i) *pout[i] = base + off[6 + i];
+    if (e == hipSuccess) e = lqrx::dp_launch(a0, s);
+    for (int i = 0; i < 4 && e == hipSuccess; ++i)            // [B][S] → [S][B]
+        e = lqrx::batch_transpose(base + off[6 + i], out[i], B, S_out[i], (int)es, s);
+    hipError_t ef = lqrx::scratch_free(blk, s);
+    return e != hipSuccess ? e : ef;
+}
+} // namespace
+
 extern "C" {
 
 int lqrx_abi_version(void) { return LQRX_ABI_VERSION; }
@@ -173,8 +214,13 @@ int lqrx_dp_solve(const lqrx_dp_desc *d, const void *A, const void *B, const voi
     a.n = d->n; a.m = d->m; a.N = d->N; a.dtype = d->dtype; a.p_all = d->p_mode;
     a.batch = d->batch;
     a.tv_AB = (int)d->knot_stride_AB; a.tv_QR = (int)d->knot_stride_QR;
+    a.layout = d->layout;
     hipStream_t s = (hipStream_t)stream;
-    hipError_t e = lqrx::dp_launch(a, s);
+    hipError_t e;
+    if (d->layout == 1 && !lqrx::dp_lane_supported(d->n, d->m))
+        e = dp_launch_soa_staged(a, s);           // MFMA kernel: convert, solve, convert back
+    else
+        e = lqrx::dp_launch(a, s);
     if (e == hipErrorNotSupported)
         return set_err(LQRX_ERR_UNSUPPORTED, "no kernel for n=%d m=%d", d->n, d->m);
     if (e != hipSuccess) return hip_err(e, "dp kernel launch");

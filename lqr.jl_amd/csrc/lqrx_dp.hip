@@ -294,18 +294,19 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
 }
 
 // Kernel variants (compile-time VAR bits):
-//   VAR_EXACT  : reference op order (explicit APB = A'PB, all n×n tiles of P_ computed,
-//                Q register-resident).  Default (0) is the fast form: APBᵀ = PBᵀA equals
-//                G = BᵀPA for symmetric P, so P_ = Q + AᵀPA − GᵀK; P_ is symmetric, so
-//                only its lower tiles are computed and the upper ones mirrored (LDS
-//                transpose); Q is re-read (L2/MALL-resident, 8 KB/traj) into the P_
-//                accumulators each knot so it holds no registers.
+//   (0)        : the symmetric fast form: APBᵀ = PBᵀA equals G = BᵀPA for symmetric P,
+//                so P_ = Q + AᵀPA − GᵀK; P_ is symmetric, so only its lower tiles are
+//                computed and the upper ones mirrored (LDS transpose); Q lives in an LDS
+//                image and is read into the P_ accumulators each knot.  (The reference op
+//                order — explicit APB, all n×n tiles — was a round-1 A/B variant; it was
+//                never selectable through the ABI and is gone: parity is checked against
+//                the oracle, which keeps the reference order.)
 //   VAR_NOSOLVE / VAR_NOROLL / VAR_NOKSTORE : diagnostic ablations (tools/dp_ablate).
 //   VAR_TV     : time-varying A_k, B_k, Q_k, R_k (ABI knot strides 1):
 //                knot k-1's A, B, R are loaded into the same registers right after knot k's
 //                last product that reads them (the load hides behind the rest of the knot);
 //                Q_k is loaded from global straight into the P_ accumulators.
-enum : int { VAR_EXACT = 1, VAR_NOSOLVE = 2, VAR_NOROLL = 4, VAR_NOKSTORE = 8, VAR_SWEEPONLY = 16, VAR_TV = 32 };
+enum : int { VAR_NOSOLVE = 2, VAR_NOROLL = 4, VAR_NOKSTORE = 8, VAR_SWEEPONLY = 16, VAR_TV = 32 };
 
 template <typename T, int NT, int MT, int WAVES, int VAR, bool FULL>
 __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
@@ -313,12 +314,11 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
     using C = DpCfg<T, NT, MT>;
     using acc = typename Tile<T>::acc;
     constexpr int MP = C::MP, CS = C::CS;
-    constexpr bool EXACT = (VAR & VAR_EXACT) != 0;
     constexpr bool TV = (VAR & VAR_TV) != 0;
     __shared__ T lds[C::LDS_ELEMS];
     // Q (time-invariant, read every knot as the P_ accumulator start) lives in LDS for the
     // horizon: an LDS read per element instead of an L2 round trip per knot
-    __shared__ T qimg[(EXACT || TV) ? 1 : C::QIMG];
+    __shared__ T qimg[TV ? 1 : C::QIMG];
 
     const int lane = threadIdx.x;
     const int64_t b = blockIdx.x;
@@ -338,9 +338,7 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
     tiles_load<T, NT, MT, FULL>(Bt, Bb + k0 * sB, n, m, n, lane, false);
     tiles_load<T, MT, MT, FULL>(Rt, Rb + k0 * sR, m, m, m, lane, true);
     tiles_load<T, NT, NT, FULL>(P, (const T *)a.Qf + b * nn, n, n, n, lane, false); // :58 P = Qf
-    acc Qt[EXACT ? NT : 1][EXACT ? NT : 1];
-    if constexpr (EXACT) tiles_load<T, NT, NT, FULL>(Qt, Qg, n, n, n, lane, false);
-    else if constexpr (!TV) {
+    if constexpr (!TV) {
         // zero-padded NP×NP image of Q (padding rows/cols 0, as tiles_load_lower)
         for (int e = lane; e < C::NP * C::NP; e += 64) {
             const int i = e % C::NP, j = e / C::NP;
@@ -371,20 +369,13 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
         mma_tn<T, NT, NT, MT>(PB, P, Bt);                          // :38 PB = P B
         tiles_zero<T, NT, NT>(PA);
         mma_tn<T, NT, NT, NT>(PA, P, At);                          // :40 PA = P A
-        if constexpr (EXACT) {
-#pragma unroll
-            for (int i = 0; i < NT; ++i)
-#pragma unroll
-                for (int j = 0; j < NT; ++j) Pn[i][j] = Qt[i][j];
-        } else {
-            if constexpr (TV) {
-                tiles_load_lower<T, NT, FULL>(Pn, Qb + (size_t)(k - 1) * sQ, n, n, lane);
+        if constexpr (TV) {
+            tiles_load_lower<T, NT, FULL>(Pn, Qb + (size_t)(k - 1) * sQ, n, n, lane);
 #if LQRX_DP_TVWAIT
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
-            }
-            else tiles_lower_from_lds<T, NT>(Pn, qimg, C::QCS, lane);   // P_ ← Q (lower tiles)
         }
+        else tiles_lower_from_lds<T, NT>(Pn, qimg, C::QCS, lane);       // P_ ← Q (lower tiles)
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -392,8 +383,7 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
         mma_tn<T, NT, MT, MT>(E, Bt, PB);                          // :39 E = R + B'PB
         tiles_zero<T, MT, NT>(G);
         mma_tn<T, NT, MT, NT>(G, Bt, PA);                          // :41 K = B'PA
-        if constexpr (EXACT) mma_tn<T, NT, NT, NT>(Pn, At, PA);    // :51 Q + A'PA
-        else mma_tn_lower<T, NT, NT>(Pn, At, PA);
+        mma_tn_lower<T, NT, NT>(Pn, At, PA);                       // :51 Q + A'PA (lower)
         if constexpr (TV) {
             // knot k's A, B, R are consumed: bring in knot k-1's (lands during the solve)
             if (k > 1) {
@@ -461,15 +451,8 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
             if constexpr ((VAR & VAR_NOKSTORE) == 0)
                 tiles_store<T, MT, NT, FULL>(Kt, Kb + (size_t)(k - 1) * nm, m, n, m, lane);
         }
-        if constexpr (EXACT) {
-            acc APBt[MT][NT];
-            tiles_zero<T, MT, NT>(APBt);
-            mma_tn<T, NT, MT, NT>(APBt, PB, At);                   // :50 APBᵀ = PBᵀ A
-            mma_tn<T, MT, NT, NT, true>(Pn, APBt, Kt);             // :51 − APB K
-        } else {
-            mma_tn_lower<T, MT, NT, true>(Pn, G, Kt);              //     − GᵀK  (= APB K)
-            tiles_symmetrize_lower<T, NT>(Pn, lds, lane);          // P_ exactly symmetric
-        }
+        mma_tn_lower<T, MT, NT, true>(Pn, G, Kt);                  // :50-51 − GᵀK (= APB K)
+        tiles_symmetrize_lower<T, NT>(Pn, lds, lane);              // P_ exactly symmetric
 #pragma unroll
         for (int i = 0; i < NT; ++i)
 #pragma unroll

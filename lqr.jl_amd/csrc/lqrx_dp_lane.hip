@@ -29,59 +29,66 @@ template <> __device__ __forceinline__ double lane_rsqrt<double>(double a) { ret
 template <> __device__ __forceinline__ float lane_rsqrt<float>(float a) { return rsqrt_nr(a); }
 
 // load an r×c column-major block (ld = r) into a padded RP×CP register array; pad value
-// `dpad` on the padded diagonal (1 for R so the padded E stays SPD), 0 elsewhere
+// `dpad` on the padded diagonal (1 for R so the padded E stays SPD), 0 elsewhere.  `es` is
+// the element stride: 1 in layout 0, the batch in layout 1 (SoA: consecutive lanes read
+// consecutive words — one coalesced load per element across the wave)
 template <typename T, int RP, int CP>
-__device__ __forceinline__ void lane_load(T (&D)[RP][CP], const T *__restrict__ src, int r, int c, T dpad)
+__device__ __forceinline__ void lane_load(T (&D)[RP][CP], const T *__restrict__ src, int r, int c, T dpad,
+                                          int64_t es)
 {
 #pragma unroll
     for (int j = 0; j < CP; ++j)
 #pragma unroll
         for (int i = 0; i < RP; ++i) {
             const bool ok = i < r && j < c;
-            D[i][j] = ok ? src[i + j * r] : (i == j ? dpad : (T)0);
+            D[i][j] = ok ? src[(i + j * r) * es] : (i == j ? dpad : (T)0);
         }
 }
 
 } // namespace
 
-template <typename T, int NP, int MP, bool TV>
+template <typename T, int NP, int MP, bool TV, bool SOA>
 __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
 {
     const int64_t b = (int64_t)blockIdx.x * 64 + threadIdx.x;
     if (b >= a.batch) return;   // no barriers / cross-lane ops below
     const int n = a.n, m = a.m, N = a.N;
     const int64_t nn = (int64_t)n * n, nm = (int64_t)n * m, mm = (int64_t)m * m;
+    // layout: trajectory base offset of an array with S elements per trajectory, and the
+    // element stride (layout 0: b·S, 1; layout 1 / SoA: b, batch)
+    const int64_t es = SOA ? a.batch : 1;
+    auto tb = [&](int64_t S) { return SOA ? b : b * S; };
     // TV (template): matrices are re-read every knot; a time-invariant field of a
     // time-varying problem simply has knot stride 0 (it stays cache-resident)
     constexpr bool tvAB = TV, tvQR = TV;
     const int64_t kAB = a.tv_AB ? N - 1 : 1, kQR = a.tv_QR ? N - 1 : 1;    // knots stored
     const int64_t sA = a.tv_AB ? nn : 0, sB = a.tv_AB ? nm : 0;            // knot strides
     const int64_t sQ = a.tv_QR ? nn : 0, sR = a.tv_QR ? mm : 0;
-    const T *Ab = (const T *)a.A + b * nn * kAB;
-    const T *Bb = (const T *)a.B + b * nm * kAB;
-    const T *Qb = (const T *)a.Q + b * nn * kQR;
-    const T *Rb = (const T *)a.R + b * mm * kQR;
+    const T *Ab = (const T *)a.A + tb(nn * kAB);
+    const T *Bb = (const T *)a.B + tb(nm * kAB);
+    const T *Qb = (const T *)a.Q + tb(nn * kQR);
+    const T *Rb = (const T *)a.R + tb(mm * kQR);
 
     T A[NP][NP], B[NP][MP], Q[NP][NP], R[MP][MP], P[NP][NP];
-    lane_load<T, NP, NP>(P, (const T *)a.Qf + b * nn, n, n, (T)0);   // :58 P = Qf
+    lane_load<T, NP, NP>(P, (const T *)a.Qf + tb(nn), n, n, (T)0, es);   // :58 P = Qf
     if constexpr (!tvAB) {
-        lane_load<T, NP, NP>(A, Ab, n, n, (T)0);
-        lane_load<T, NP, MP>(B, Bb, n, m, (T)0);
+        lane_load<T, NP, NP>(A, Ab, n, n, (T)0, es);
+        lane_load<T, NP, MP>(B, Bb, n, m, (T)0, es);
     }
     if constexpr (!tvQR) {
-        lane_load<T, NP, NP>(Q, Qb, n, n, (T)0);
-        lane_load<T, MP, MP>(R, Rb, m, m, (T)1);
+        lane_load<T, NP, NP>(Q, Qb, n, n, (T)0, es);
+        lane_load<T, MP, MP>(R, Rb, m, m, (T)1, es);
     }
-    T *Kb = (T *)a.K + b * (int64_t)(N - 1) * nm;
-    T *Pall = a.p_all ? (T *)a.P + b * nn * N : nullptr;
+    T *Kb = (T *)a.K + tb((int64_t)(N - 1) * nm);
+    T *Pall = a.p_all ? (T *)a.P + tb(nn * N) : nullptr;
     auto store_P = [&](T *dst) {
 #pragma unroll
         for (int j = 0; j < NP; ++j)
 #pragma unroll
             for (int i = 0; i < NP; ++i)
-                if (i < n && j < n) dst[i + j * n] = (i >= j) ? P[i][j] : P[j][i];
+                if (i < n && j < n) dst[(i + j * n) * es] = (i >= j) ? P[i][j] : P[j][i];
     };
-    if (Pall) store_P(Pall + (int64_t)(N - 1) * nn);
+    if (Pall) store_P(Pall + (int64_t)(N - 1) * nn * es);
     int info = 0;
     // time-varying: knot k's matrices are prefetched during knot k+1
     constexpr int TN = TV ? NP : 1, TM = TV ? MP : 1;
@@ -89,12 +96,12 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
     auto fetch_tv = [&](int k) {
         if (k < 1) return;
         if constexpr (tvAB) {
-            lane_load<T, NP, NP>(An, Ab + (int64_t)(k - 1) * sA, n, n, (T)0);
-            lane_load<T, NP, MP>(Bn, Bb + (int64_t)(k - 1) * sB, n, m, (T)0);
+            lane_load<T, NP, NP>(An, Ab + (int64_t)(k - 1) * sA * es, n, n, (T)0, es);
+            lane_load<T, NP, MP>(Bn, Bb + (int64_t)(k - 1) * sB * es, n, m, (T)0, es);
         }
         if constexpr (tvQR) {
-            lane_load<T, NP, NP>(Qn, Qb + (int64_t)(k - 1) * sQ, n, n, (T)0);
-            lane_load<T, MP, MP>(Rn, Rb + (int64_t)(k - 1) * sR, m, m, (T)1);
+            lane_load<T, NP, NP>(Qn, Qb + (int64_t)(k - 1) * sQ * es, n, n, (T)0, es);
+            lane_load<T, MP, MP>(Rn, Rb + (int64_t)(k - 1) * sR * es, m, m, (T)1, es);
         }
     };
     if constexpr (TV) fetch_tv(N - 1);
@@ -198,12 +205,12 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
                 K[i][j] = s * Linv[i];
             }
         }
-        T *Kk = Kb + (int64_t)(k - 1) * nm;                      // sol.K[k], m×n col-major
+        T *Kk = Kb + (int64_t)(k - 1) * nm * es;                 // sol.K[k], m×n col-major
 #pragma unroll
         for (int j = 0; j < NP; ++j)
 #pragma unroll
             for (int i = 0; i < MP; ++i)
-                if (i < m && j < n) Kk[i + j * m] = K[i][j];
+                if (i < m && j < n) Kk[(i + j * m) * es] = K[i][j];
         // :51 P_ = Q + AᵀPA − GᵀK   (lower triangle)
 #pragma unroll
         for (int i = 0; i < NP; ++i)
@@ -216,20 +223,20 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
                 for (int c = 0; c < MP; ++c) s = fma(-G[c][i], K[c][j], s);
                 P[i][j] = s;
             }
-        if (Pall) store_P(Pall + (int64_t)(k - 1) * nn);
+        if (Pall) store_P(Pall + (int64_t)(k - 1) * nn * es);
     }
-    if (!a.p_all) store_P((T *)a.P + b * nn);
+    if (!a.p_all) store_P((T *)a.P + tb(nn));
     if (a.info) a.info[b] = info;
 
     // forward rollout  :66-70  u_k = −K_k x_k ; x_{k+1} = A_k x_k + B_k u_k
-    T *Xb = (T *)a.X + b * (int64_t)N * n, *Ub = (T *)a.U + b * (int64_t)(N - 1) * m;
-    const T *x0 = (const T *)a.x0 + b * n;
+    T *Xb = (T *)a.X + tb((int64_t)N * n), *Ub = (T *)a.U + tb((int64_t)(N - 1) * m);
+    const T *x0 = (const T *)a.x0 + tb(n);
     T x[NP];
 #pragma unroll
-    for (int i = 0; i < NP; ++i) x[i] = i < n ? x0[i] : (T)0;
+    for (int i = 0; i < NP; ++i) x[i] = i < n ? x0[i * es] : (T)0;
 #pragma unroll
     for (int i = 0; i < NP; ++i)
-        if (i < n) Xb[i] = x[i];
+        if (i < n) Xb[i * es] = x[i];
     // K_k (and A_k, B_k when time-varying) were written / live in HBM; the x-recurrence is a
     // short dependent chain per knot, so the loads are issued RD knots ahead from a
     // register ring (unrolled by RD so every ring index is static).
@@ -240,14 +247,14 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
     Knot ring[RD];
     auto fetch = [&](int k, Knot &d) {
         if (k > N - 1) return;
-        const T *Kk = Kb + (int64_t)(k - 1) * nm;
+        const T *Kk = Kb + (int64_t)(k - 1) * nm * es;
 #pragma unroll
         for (int j = 0; j < NP; ++j)
 #pragma unroll
-            for (int i = 0; i < MP; ++i) d.K[i][j] = (i < m && j < n) ? Kk[i + j * m] : (T)0;
+            for (int i = 0; i < MP; ++i) d.K[i][j] = (i < m && j < n) ? Kk[(i + j * m) * es] : (T)0;
         if constexpr (tvAB) {
-            lane_load<T, NP, NP>(d.A, Ab + (int64_t)(k - 1) * sA, n, n, (T)0);
-            lane_load<T, NP, MP>(d.B, Bb + (int64_t)(k - 1) * sB, n, m, (T)0);
+            lane_load<T, NP, NP>(d.A, Ab + (int64_t)(k - 1) * sA * es, n, n, (T)0, es);
+            lane_load<T, NP, MP>(d.B, Bb + (int64_t)(k - 1) * sB * es, n, m, (T)0, es);
         }
     };
 #pragma unroll
@@ -279,7 +286,7 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
 #pragma unroll
                 for (int j = 0; j < NP; ++j) s = fma(Kc[i][j], x[j], s);
                 u[i] = -s;
-                if (i < m) Ub[(int64_t)(k - 1) * m + i] = u[i];
+                if (i < m) Ub[((int64_t)(k - 1) * m + i) * es] = u[i];
             }
             T xn[NP];
 #pragma unroll
@@ -294,7 +301,7 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
 #pragma unroll
             for (int i = 0; i < NP; ++i) {
                 x[i] = xn[i];
-                if (i < n) Xb[(int64_t)k * n + i] = x[i];
+                if (i < n) Xb[((int64_t)k * n + i) * es] = x[i];
             }
         }
     }
@@ -328,7 +335,7 @@ __device__ __forceinline__ float qbcast(float v)
 template <int R, typename T>
 __device__ __forceinline__ T qfrom(T v) { return qbcast<R | (R << 2) | (R << 4) | (R << 6)>(v); }
 
-template <typename T, int MP>
+template <typename T, int MP, bool SOA>
 __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
 {
     constexpr int NP = 4;
@@ -337,28 +344,30 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
     if (b >= a.batch) return;   // whole quads retire together; DPP stays inside the quad
     const int n = a.n, m = a.m, N = a.N;
     const int64_t nn = (int64_t)n * n, nm = (int64_t)n * m, mm = (int64_t)m * m;
-    const T *Ag = (const T *)a.A + b * nn, *Bg = (const T *)a.B + b * nm;
-    const T *Qg = (const T *)a.Q + b * nn, *Rg = (const T *)a.R + b * mm;
+    const int64_t es = SOA ? a.batch : 1;                      // as dp_lane_kernel
+    auto tb = [&](int64_t S) { return SOA ? b : b * S; };
+    const T *Ag = (const T *)a.A + tb(nn), *Bg = (const T *)a.B + tb(nm);
+    const T *Qg = (const T *)a.Q + tb(nn), *Rg = (const T *)a.R + tb(mm);
 
     T A[NP][NP], B[NP][MP], R[MP][MP], P[NP][NP];
-    lane_load<T, NP, NP>(P, (const T *)a.Qf + b * nn, n, n, (T)0);   // :58 P = Qf
-    lane_load<T, NP, NP>(A, Ag, n, n, (T)0);
-    lane_load<T, NP, MP>(B, Bg, n, m, (T)0);
-    lane_load<T, MP, MP>(R, Rg, m, m, (T)1);
+    lane_load<T, NP, NP>(P, (const T *)a.Qf + tb(nn), n, n, (T)0, es);   // :58 P = Qf
+    lane_load<T, NP, NP>(A, Ag, n, n, (T)0, es);
+    lane_load<T, NP, MP>(B, Bg, n, m, (T)0, es);
+    lane_load<T, MP, MP>(R, Rg, m, m, (T)1, es);
     // this lane's column of A and Q, row of A and B (dynamic q → loaded, not indexed)
     T Acol[NP], Qcol[NP], Arow[NP], Brow[MP];
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
         const bool ok = i < n && q < n;
-        Acol[i] = ok ? Ag[i + q * n] : (T)0;
-        Qcol[i] = ok ? Qg[i + q * n] : (T)0;
-        Arow[i] = ok ? Ag[q + i * n] : (T)0;
+        Acol[i] = ok ? Ag[(i + q * n) * es] : (T)0;
+        Qcol[i] = ok ? Qg[(i + q * n) * es] : (T)0;
+        Arow[i] = ok ? Ag[(q + i * n) * es] : (T)0;
     }
 #pragma unroll
-    for (int c = 0; c < MP; ++c) Brow[c] = (q < n && c < m) ? Bg[q + c * n] : (T)0;
+    for (int c = 0; c < MP; ++c) Brow[c] = (q < n && c < m) ? Bg[(q + c * n) * es] : (T)0;
 
-    T *Kb = (T *)a.K + b * (int64_t)(N - 1) * nm;
-    T *Pall = a.p_all ? (T *)a.P + b * nn * N : nullptr;
+    T *Kb = (T *)a.K + tb((int64_t)(N - 1) * nm);
+    T *Pall = a.p_all ? (T *)a.P + tb(nn * N) : nullptr;
 #define PS(i, j) ((i) >= (j) ? P[i][j] : P[j][i])
     auto store_Pcol = [&](T *dst) {   // lane q writes column q
         if (q >= n) return;
@@ -368,10 +377,10 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
 #pragma unroll
             for (int r = 1; r < NP; ++r) v = q == r ? PS(i, r) : v;
             if (q == 0) v = PS(i, 0);
-            if (i < n) dst[i + q * n] = v;
+            if (i < n) dst[(i + q * n) * es] = v;
         }
     };
-    if (Pall) store_Pcol(Pall + (int64_t)(N - 1) * nn);
+    if (Pall) store_Pcol(Pall + (int64_t)(N - 1) * nn * es);
     int info = 0;
     for (int k = N - 1; k >= 1; --k) {   // :61
         T PB[NP][MP];
@@ -442,10 +451,10 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
             Kq[i] = s * Linv[i];
         }
         if (q < n) {
-            T *Kk = Kb + (int64_t)(k - 1) * nm + q * m;           // sol.K[k] column q
+            T *Kk = Kb + ((int64_t)(k - 1) * nm + q * m) * es;    // sol.K[k] column q
 #pragma unroll
             for (int c = 0; c < MP; ++c)
-                if (c < m) Kk[c] = Kq[c];
+                if (c < m) Kk[c * es] = Kq[c];
         }
         // :51 P_[:,q] = Q[:,q] + AᵀPA[:,q] − Gᵀ Kq = Q[:,q] + Aᵀ(PA[:,q] − PB·Kq)
         // (G = PBᵀA, so GᵀKq = Aᵀ(PB Kq): no full G)
@@ -472,27 +481,27 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
 #pragma unroll
         for (int i = 2; i < NP; ++i) P[i][2] = qfrom<2>(Pn[i]);
         P[3][3] = qfrom<3>(Pn[3]);
-        if (Pall) store_Pcol(Pall + (int64_t)(k - 1) * nn);
+        if (Pall) store_Pcol(Pall + (int64_t)(k - 1) * nn * es);
     }
-    if (!a.p_all) store_Pcol((T *)a.P + b * nn);
+    if (!a.p_all) store_Pcol((T *)a.P + tb(nn));
     if (a.info && q == 0) a.info[b] = info;
 
     // forward rollout :66-70 — x replicated; lane q forms x_{k+1}[q]
-    T *Xb = (T *)a.X + b * (int64_t)N * n, *Ub = (T *)a.U + b * (int64_t)(N - 1) * m;
-    const T *x0 = (const T *)a.x0 + b * n;
+    T *Xb = (T *)a.X + tb((int64_t)N * n), *Ub = (T *)a.U + tb((int64_t)(N - 1) * m);
+    const T *x0 = (const T *)a.x0 + tb(n);
     T x[NP];
 #pragma unroll
-    for (int i = 0; i < NP; ++i) x[i] = i < n ? x0[i] : (T)0;
-    if (q < n) Xb[q] = q == 0 ? x[0] : (q == 1 ? x[1] : (q == 2 ? x[2] : x[3]));
+    for (int i = 0; i < NP; ++i) x[i] = i < n ? x0[i * es] : (T)0;
+    if (q < n) Xb[q * es] = q == 0 ? x[0] : (q == 1 ? x[1] : (q == 2 ? x[2] : x[3]));
     constexpr int RD = 8;
     T ring[RD][MP][NP];
     auto fetch = [&](int k, T (&d)[MP][NP]) {
         if (k > N - 1) return;
-        const T *Kk = Kb + (int64_t)(k - 1) * nm;
+        const T *Kk = Kb + (int64_t)(k - 1) * nm * es;
 #pragma unroll
         for (int j = 0; j < NP; ++j)
 #pragma unroll
-            for (int i = 0; i < MP; ++i) d[i][j] = (i < m && j < n) ? Kk[i + j * m] : (T)0;
+            for (int i = 0; i < MP; ++i) d[i][j] = (i < m && j < n) ? Kk[(i + j * m) * es] : (T)0;
     };
     // K_k was written by this quad's own lanes above; make those stores visible to the
     // quad's loads (other lanes' stores: complete them and drop any stale L1 line, once)
@@ -519,14 +528,14 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
 #pragma unroll
                 for (int j = 0; j < NP; ++j) s = fma(Kc[i][j], x[j], s);
                 u[i] = -s;
-                if (q == 0 && i < m) Ub[(int64_t)(k - 1) * m + i] = u[i];
+                if (q == 0 && i < m) Ub[((int64_t)(k - 1) * m + i) * es] = u[i];
             }
             T s = (T)0;
 #pragma unroll
             for (int j = 0; j < NP; ++j) s = fma(Arow[j], x[j], s);
 #pragma unroll
             for (int c = 0; c < MP; ++c) s = fma(Brow[c], u[c], s);
-            if (q < n) Xb[(int64_t)k * n + q] = s;
+            if (q < n) Xb[((int64_t)k * n + q) * es] = s;
             x[0] = qfrom<0>(s);
             x[1] = qfrom<1>(s);
             x[2] = qfrom<2>(s);
@@ -540,10 +549,11 @@ template <typename T, int NP, int MP>
 static hipError_t launch_lane(const DpArgs &a, hipStream_t s)
 {
     dim3 grid((unsigned)((a.batch + 63) / 64)), block(64);
-    if (a.tv_AB || a.tv_QR)
-        hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, true>), grid, block, 0, s, a);
-    else
-        hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, false>), grid, block, 0, s, a);
+    const bool tv = a.tv_AB || a.tv_QR, soa = a.layout == 1;
+    if (tv && soa) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, true, true>), grid, block, 0, s, a);
+    else if (tv) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, true, false>), grid, block, 0, s, a);
+    else if (soa) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, false, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, false, false>), grid, block, 0, s, a);
     return hipGetLastError();
 }
 
@@ -564,7 +574,8 @@ template <typename T, int MP>
 static hipError_t launch_quad(const DpArgs &a, hipStream_t s)
 {
     dim3 grid((unsigned)((a.batch * 4 + 63) / 64)), block(64);
-    hipLaunchKernelGGL((dp_quad_kernel<T, MP>), grid, block, 0, s, a);
+    if (a.layout == 1) hipLaunchKernelGGL((dp_quad_kernel<T, MP, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((dp_quad_kernel<T, MP, false>), grid, block, 0, s, a);
     return hipGetLastError();
 }
 

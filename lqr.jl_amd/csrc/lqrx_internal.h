@@ -15,9 +15,15 @@ struct DpArgs {
     int p_all;
     int64_t batch;
     int tv_AB, tv_QR; // 1 = per-knot A_k,B_k / Q_k,R_k (N−1 knots per trajectory), 0 = time-invariant
+    int layout;       // 0 = per-trajectory blocks, batch slowest; 1 = batch fastest (SoA):
+                      // element e of trajectory b at [e·batch + b] (e = the layout-0 offset
+                      // within the trajectory) — native in the n ≤ 4 kernels
 };
 
 hipError_t dp_launch(const DpArgs &a, hipStream_t s);
+// out = inᵀ for a rows × cols row-major matrix of 4- or 8-byte elements (lqrx_layout.hip):
+// layout 1 (SoA, [S][batch]) ↔ layout 0 ([batch][S]) for the kernels that need layout 0
+hipError_t batch_transpose(const void *in, void *out, int64_t rows, int64_t cols, int elem_bytes, hipStream_t s);
 bool dp_supported(int dtype, int n, int m, bool tv);
 // lane-per-trajectory kernel for n ≤ 4, m ≤ 4 (lqrx_dp_lane.hip)
 hipError_t dp_lane_launch(const DpArgs &a, hipStream_t s);

@@ -33,6 +33,16 @@ def to_abi(a: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(np.swapaxes(a, -1, -2))
 
 
+def to_soa(flat: np.ndarray, batch: int) -> np.ndarray:
+    """Layout-0 flat buffer (batch slowest) → ABI layout 1 (batch fastest): [S][batch]."""
+    return np.ascontiguousarray(np.asarray(flat).reshape(batch, -1).T)
+
+
+def from_soa(soa: np.ndarray, batch: int) -> np.ndarray:
+    """ABI layout 1 ([S][batch]) → the layout-0 flat buffer."""
+    return np.ascontiguousarray(np.asarray(soa).reshape(-1, batch).T).ravel()
+
+
 def from_abi(a: np.ndarray, shape: tuple) -> np.ndarray:
     """Inverse of to_abi: flat ABI buffer → (…, r, c) logical matrices."""
     *lead, r, c = shape
@@ -137,10 +147,12 @@ def _ptr(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p)
 
 
-def solve_batch(b: LQRBatch, dtype: int = _lib.F64, all_P: bool = False):
+def solve_batch(b: LQRBatch, dtype: int = _lib.F64, all_P: bool = False, layout: int = 0):
     """Batched solve! through lqrx_dp_solve_host.  Returns dict of logical arrays
     K (batch, N-1, m, n), P (batch, n, n) or (batch, N, n, n), X (batch, N, n),
-    U (batch, N-1, m), info (batch,), and the ABI return code."""
+    U (batch, N-1, m), info (batch,), and the ABI return code.  layout = 1 hands the
+    library batch-fastest (SoA) buffers (the conversion here is host-side bookkeeping; the
+    result is the same logical arrays)."""
     lib = _lib.load()
     n, m, N = b.size()
     bt = b.batch
@@ -148,14 +160,19 @@ def solve_batch(b: LQRBatch, dtype: int = _lib.F64, all_P: bool = False):
     npdt = np.float64 if dtype == _lib.F64 else np.float32
     ins = [to_abi(np.asarray(x, dtype=npdt)) for x in (b.A, b.B, b.Q, b.R, b.Qf)]
     x0 = np.ascontiguousarray(np.asarray(b.x0, dtype=npdt))
+    if layout == 1:
+        ins = [to_soa(a, bt) for a in ins]
+        x0 = to_soa(x0, bt)
     K = np.zeros(bt * (N - 1) * m * n, npdt)
     P = np.zeros(bt * n * n * (N if all_P else 1), npdt)
     X = np.zeros(bt * N * n, npdt)
     U = np.zeros(bt * (N - 1) * m, npdt)
     info = np.zeros(bt, np.int32)
-    d = _lib.DpDesc(n, m, N, dtype, bt, 0, 1 if all_P else 0, tvAB, tvQR)
+    d = _lib.DpDesc(n, m, N, dtype, bt, layout, 1 if all_P else 0, tvAB, tvQR)
     rc = _lib.check(lib.lqrx_dp_solve_host(C.byref(d), *[_ptr(a) for a in ins], _ptr(x0),
                                            _ptr(K), _ptr(P), _ptr(X), _ptr(U), _ptr(info)))
+    if layout == 1:
+        K, P, X, U = (from_soa(a, bt) for a in (K, P, X, U))
     return dict(K=from_abi(K, (bt, N - 1, m, n)),
                 P=from_abi(P, (bt, N, n, n) if all_P else (bt, n, n)),
                 X=X.reshape(bt, N, n), U=U.reshape(bt, N - 1, m), info=info, rc=rc)
@@ -195,8 +212,9 @@ def abi_to_batch(d: dict) -> LQRBatch:
 
 
 def dp_solve_device(t: dict, N: int, p_mode: int = 0, stream: int | None = None,
-                    out: dict | None = None) -> dict:
-    """Device-pointer entry point on torch tensors already in ABI layout (flat).
+                    out: dict | None = None, layout: int = 0) -> dict:
+    """Device-pointer entry point on torch tensors already in ABI layout (flat; layout 1 =
+    batch fastest, every input and output).
 
     t: dict with torch tensors A, B, Q, R, Qf, x0 on the GPU and ints n, m, batch.
     Returns dict of output tensors (K, P, X, U, info).  `stream` is a raw hipStream_t
@@ -215,7 +233,7 @@ def dp_solve_device(t: dict, N: int, p_mode: int = 0, stream: int | None = None,
                    X=torch.empty(bt * N * n, dtype=tdt, device=dev),
                    U=torch.empty(bt * (N - 1) * m, dtype=tdt, device=dev),
                    info=torch.empty(bt, dtype=torch.int32, device=dev))
-    d = _lib.DpDesc(n, m, N, dtype, bt, 0, p_mode, int(t.get("tv_AB", 0)), int(t.get("tv_QR", 0)))
+    d = _lib.DpDesc(n, m, N, dtype, bt, layout, p_mode, int(t.get("tv_AB", 0)), int(t.get("tv_QR", 0)))
     p = lambda x: C.c_void_p(x.data_ptr())
     rc = lib.lqrx_dp_solve(C.byref(d), p(t["A"]), p(t["B"]), p(t["Q"]), p(t["R"]), p(t["Qf"]),
                            p(t["x0"]), p(out["K"]), p(out["P"]), p(out["X"]), p(out["U"]),

@@ -81,6 +81,44 @@ def dp_solve_abi(d: dict, N: int, all_P: bool = False, nthreads: int = 1) -> dic
     return dict(K=K, P=P, X=X, U=U, info=info)
 
 
+def dp_extended(A, B, Q, R, Qf, N):
+    """The backward pass of dynamic_programming.jl:54-64 (compute_gain! :37-43 with
+    chol_solve! :28-31, compute_ctg! :48-52, same op order) in x87 80-bit extended precision
+    (np.longdouble, unit roundoff 5.4e-20 vs 1.1e-16), batched over trajectories.  Inputs are
+    logical (batch, r, c) float64 arrays; returns K (batch, N−1, m, n) and P (batch, N, n, n)
+    as longdouble — the near-exact answer that the fp64 oracle and the GPU are both measured
+    against when a recursion is ill-conditioned (tests/test_dp_lane_gpu.py)."""
+    ld = np.longdouble
+    assert np.finfo(ld).eps < 1e-18, "needs x87 extended precision"
+    A, B, Q, R, Qf = (np.asarray(x, dtype=ld) for x in (A, B, Q, R, Qf))
+    bt, n, m = B.shape
+    T = lambda M: np.swapaxes(M, 1, 2)
+    P = Qf.copy()
+    Ks = np.zeros((bt, N - 1, m, n), dtype=ld)
+    Ps = np.zeros((bt, N, n, n), dtype=ld)
+    Ps[:, N - 1] = P
+    for k in range(N - 1, 0, -1):
+        PB = P @ B                                   # :38
+        E = R + T(B) @ PB                            # :39
+        PA = P @ A                                   # :40
+        K = T(B) @ PA                                # :41
+        U = np.zeros_like(E)                         # :29 potrf 'U'
+        for j in range(m):
+            d = E[:, j, j] - (U[:, :j, j] ** 2).sum(axis=1)
+            U[:, j, j] = np.sqrt(d)
+            for c in range(j + 1, m):
+                U[:, j, c] = (E[:, j, c] - (U[:, :j, j] * U[:, :j, c]).sum(axis=1)) / U[:, j, j]
+        for i in range(m):                           # :30 potrs: Uᵀ Y = K, then U X = Y
+            K[:, i] = (K[:, i] - (U[:, :i, i, None] * K[:, :i]).sum(axis=1)) / U[:, i, i, None]
+        for i in range(m - 1, -1, -1):
+            K[:, i] = (K[:, i] - (U[:, i, i + 1:, None] * K[:, i + 1:]).sum(axis=1)) / U[:, i, i, None]
+        APB = T(A) @ PB                              # :50
+        P = Q + T(A) @ PA - APB @ K                  # :51
+        Ks[:, k - 1] = K
+        Ps[:, k - 1] = P
+    return Ks, Ps
+
+
 def dp_dense_kkt(A, B, Q, R, Qf, x0, N):
     """Dense equality-constrained QP optimum of one LQR problem (logical row-major
     matrices).  Returns (X (N,n), U (N-1,m))."""

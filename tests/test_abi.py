@@ -23,7 +23,8 @@ def test_abi_version(lqrx):
 
 @pytest.mark.parametrize("field,val,code", [("n", 0, -1), ("m", 0, -1), ("N", 1, -1),
                                             ("dtype", 7, -1), ("p_mode", 3, -1),
-                                            ("layout", 1, -101), ("knot_stride_AB", 5, -1),
+                                            ("layout", 2, -1), ("knot_stride_AB", 5, -1),
+                                            ("layout", 1, -2),     # SoA is valid: first NULL is A
                                             ("knot_stride_QR", 2, -1),
                                             ("knot_stride_QR", 1, -2)])   # valid: first NULL is A
 def test_dp_validation(lqrx, field, val, code):

@@ -24,36 +24,22 @@ def per_traj_relerr(a, b):
     return (np.abs(a - b).max(axis=2) / den).max(axis=1)
 
 
-def intrinsic_spread(d, N, Kref, Pref):
-    """Per-trajectory conditioning of the reference recursion itself: the relative
-    difference between the oracle and an independent fp64 restatement in the reference op
-    order (numpy, LU-based solve instead of potrf/potrs).  On the random generator at small
-    n (A = I + 0.1/√n·G) a few trajectories per thousand have ρ(A) ≈ 1.1 and weak
-    actuation; their Riccati recursion amplifies rounding so that two faithful fp64
-    implementations already disagree above 1e-10."""
+def assert_parity(got, ref, d, N, tol=TOL64, eps_ratio=1.0, rare=0.01, c=4.0):
+    """K, P, X, U within `tol` per knot (vs the fp64 oracle) for every trajectory — except
+    trajectories whose Riccati recursion is itself ill-conditioned.  The §8(d) generator
+    A = I + 0.1/√n·G gives, at n ≤ 4, a few trajectories per thousand with ρ(A) ≈ 1.1 and
+    weak actuation; on them the fp64 oracle (reference op order) is itself off the exact
+    answer by up to ~3e-9 (measured against the same recursion in 80-bit extended precision,
+    oracle.dp_extended).  Such a trajectory passes iff the kernel is no less accurate than
+    the reference algorithm in fp64: its K/P error against the extended-precision solution
+    is ≤ c × the oracle's own error (× eps(dtype)/eps(fp64) for fp32 runs), its X/U within
+    c × that error of the oracle; and such trajectories are fewer than `rare`.  Measured on
+    MI355X (round 2): 17 of 4101 cartpole-shaped random trajectories fall back to this rule,
+    the kernel's error is ≤ 1.41× the oracle's own (fp64) and ≤ 2.0× its eps-scaled error
+    (fp32) — c = 4 leaves headroom."""
     from lqrx.dp import abi_to_batch
+    from oracle import oracle as orc
 
-    b = abi_to_batch(d)
-    A, B, Q, R = b.A, b.B, b.Q, b.R
-    P = b.Qf.copy()
-    K = np.zeros_like(Kref)
-    Ps = np.zeros_like(Pref)
-    Ps[:, N - 1] = P
-    T = lambda M: np.swapaxes(M, 1, 2)
-    for k in range(N - 1, 0, -1):
-        PB, PA = P @ B, P @ A
-        Kk = np.linalg.solve(R + T(B) @ PB, T(B) @ PA)
-        P = Q + T(A) @ PA - (T(A) @ PB) @ Kk
-        K[:, k - 1] = Kk
-        Ps[:, k - 1] = P
-    return np.maximum(per_traj_relerr(K, Kref), per_traj_relerr(Ps, Pref))
-
-
-def assert_parity(got, ref, d, N, tol=TOL64, eps_ratio=1.0, rare=0.01):
-    """K, P, X, U within `tol` per knot for every trajectory, except that a trajectory
-    whose intrinsic spread (above, measured in fp64 and scaled by eps_ratio = eps(dtype) /
-    eps(fp64) for fp32 runs) exceeds tol/10 is held to 10× that spread; such trajectories
-    must stay rare (fraction < `rare`)."""
     got = {k: np.asarray(got[k], dtype=np.float64) for k in ("K", "P", "X", "U")}
     bt = got["K"].shape[0]
     xs = lambda a: a.reshape(bt, 1, -1)                 # X, U: one block per trajectory
@@ -63,10 +49,22 @@ def assert_parity(got, ref, d, N, tol=TOL64, eps_ratio=1.0, rare=0.01):
                              per_traj_relerr(xs(got["U"]), xs(ref["U"]))])
     if (err <= tol).all():
         return
-    spread = intrinsic_spread(d, N, ref["K"], ref["P"])
-    lim = np.maximum(tol, 10.0 * spread * eps_ratio)
-    assert (err <= lim).all(), (err.max(), spread[err.argmax()])
-    assert (err > tol).mean() < rare
+    b = abi_to_batch(d)
+    Kx, Px = orc.dp_extended(b.A, b.B, b.Q, b.R, b.Qf, N)
+    Px = Px if ref["P"].ndim == 4 else Px[:, 0]
+    ld = lambda a: np.asarray(a, dtype=np.longdouble)
+    pt = lambda a, x: per_traj_relerr(ld(a), x).astype(np.float64)
+    P2 = (lambda a: a) if ref["P"].ndim == 4 else (lambda a: a[:, None])
+    e_orc = np.maximum(pt(ref["K"], Kx), pt(P2(ref["P"]), P2(Px)))
+    e_gpu = np.maximum(pt(got["K"], Kx), pt(P2(got["P"]), P2(Px)))
+    bad = err > tol
+    lim = np.maximum(tol, c * np.maximum(e_orc, 1e-16) * eps_ratio)
+    ratio = e_gpu[bad] / np.maximum(e_orc[bad], 1e-300)
+    print(f"\n{bad.sum()} of {bt} trajectories beyond {tol:g} vs the oracle; oracle's own error vs "
+          f"80-bit up to {e_orc[bad].max():.2e}; kernel/oracle error ratio max {ratio.max():.2f}")
+    assert (e_gpu[bad] <= lim[bad]).all(), (e_gpu[bad].max(), e_orc[bad].max())
+    assert (err[bad] <= lim[bad]).all(), (err[bad].max(), e_orc[bad].max())
+    assert bad.mean() < rare
 
 
 @pytest.mark.parametrize("n,m,N,batch", [
@@ -95,7 +93,7 @@ def test_lane_parity_f32(lqrx, oracle, gpu_ok, n, m):
     got, ref = run_pair(lqrx, oracle, n, m, 60, 100, seed=78, dtype=1)
     assert_parity(got, ref, lqrx.random_batch(n, m, 60, 100, 78), 60, tol=TOL32,
                   eps_ratio=float(np.finfo(np.float32).eps / np.finfo(np.float64).eps),
-                  rare=1.0)   # fp32 on weakly actuated random problems: the bound is the spread
+                  rare=1.0)   # fp32 on weakly actuated random problems: the bound is conditioning
 
 
 def test_lane_cartpole_problem(lqrx, oracle, gpu_ok):
@@ -183,3 +181,34 @@ def test_small_kernel_auto_large_batch(lqrx, oracle, gpu_ok):
     got, ref = run_pair(lqrx, oracle, 4, 1, 12, 16384 + 70, seed=77)
     assert got["rc"] == 0
     assert_parity(got, ref, lqrx.random_batch(4, 1, 12, 16384 + 70, 77), 12)
+
+
+@pytest.mark.parametrize("n,m,N,k0", [(4, 2, 30, 17), (6, 3, 30, 17), (32, 16, 24, 9), (20, 5, 20, 11)])
+def test_time_varying_info_middle_knot(lqrx, oracle, gpu_ok, n, m, N, k0):
+    """An indefinite E = R_k + BᵀPB at a MIDDLE knot k0 of a time-varying problem (R_k0 =
+    −100·I, B_k0 ≈ 0) is reported per trajectory as info = k0, as potrf's info at that knot
+    (dynamic_programming.jl:29; the oracle reports the same).  On the MFMA kernel (n ≥ 5)
+    knots after the first take the Newton–Schulz inverse; its residual test must reject the
+    step and hand the knot to the pivoted LDLᵀ sweep that detects the definiteness flip.
+    Knots solved before the break (k > k0, the backward sweep runs k = N−1 … 1) still match
+    the oracle."""
+    from lqrx.dp import to_abi, from_abi
+
+    bt = 5
+    b = _tv_batch(lqrx, n, m, N, bt, seed=55 + n, tv_ab=True, tv_qr=True)
+    b.R = np.array(b.R)
+    b.B = np.array(b.B)
+    b.R[1, k0 - 1] = -100.0 * np.eye(m)             # knot k0 (index k0 − 1)
+    b.B[1, k0 - 1] *= 1e-3
+    got = lqrx.solve_batch(b, all_P=True)
+    d = {k: to_abi(getattr(b, k)).ravel() for k in ("A", "B", "Q", "R", "Qf")}
+    d.update(x0=b.x0.ravel(), n=n, m=m, batch=bt, tv_AB=1, tv_QR=1)
+    ref = oracle.dp_solve_abi(d, N, all_P=True)
+    assert ref["info"][1] == k0 and (np.delete(ref["info"], 1) == 0).all()
+    assert got["rc"] == 1
+    assert got["info"][1] == k0
+    assert (np.delete(got["info"], 1) == 0).all()
+    refK = from_abi(ref["K"], (bt, N - 1, m, n))
+    ok = [0, 2, 3, 4]
+    assert relerr_per_knot(got["K"][ok], refK[ok]) <= TOL64
+    assert relerr_per_knot(got["K"][1:2, k0:], refK[1:2, k0:]) <= TOL64   # knots k0+1 … N−1

@@ -32,14 +32,14 @@ int main(int argc, char **argv) {
     a.K = p[6]; a.P = p[7]; a.X = p[8]; a.U = p[9]; a.info = info;
     a.n = (int)n; a.m = (int)m; a.N = (int)N; a.dtype = 0; a.p_all = 0; a.batch = B;
     hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
-    const char *names[] = {"W2 fast", "W3 fast", "W2 exact", "W3 exact", "W3 nosolve", "W3 noroll",
+    const char *names[] = {"W2 fast", "W3 fast", "W2 fast (rep)", "W3 fast (rep)", "W3 nosolve", "W3 noroll",
                            "W3 nosolve+noroll", "W3 noKstore", "W2 noroll", "W2 sweeponly"};
     std::vector<std::vector<float>> t(10);
     for (int rep = 0; rep < 4; ++rep) {
         t[0].push_back(run<2, 0>(a, e0, e1));
         t[1].push_back(run<3, 0>(a, e0, e1));
-        t[2].push_back(run<2, VAR_EXACT>(a, e0, e1));
-        t[3].push_back(run<3, VAR_EXACT>(a, e0, e1));
+        t[2].push_back(run<2, 0>(a, e0, e1));
+        t[3].push_back(run<3, 0>(a, e0, e1));
         t[4].push_back(run<3, VAR_NOSOLVE>(a, e0, e1));
         t[5].push_back(run<3, VAR_NOROLL>(a, e0, e1));
         t[6].push_back(run<3, VAR_NOSOLVE | VAR_NOROLL>(a, e0, e1));
