@@ -31,6 +31,9 @@
 namespace lqrx {
 namespace fil {
 
+#ifndef LQRX_FIL_ABL
+#define LQRX_FIL_ABL 0   // ablation builds for tools/ only (1: forward sweep alone)
+#endif
 #ifndef LQRX_FIL_N12
 #define LQRX_FIL_N12 1   // 12-byte LDS-DMA pieces for the short chunks (0: dwords only)
 #endif
@@ -79,10 +82,13 @@ template <int NX_, int M_, int P0_, int PK_, int PN_, bool HDIAG_, bool GINV_> s
     static constexpr int OFF_g = OFF_H + 64 * mx3<sb(LH<F>()), sb(LH<I>()), sb(LH<L>())>();
     static constexpr int BUF_BYTES = OFF_g + 64 * mx3<sb(Lg<F>()), sb(Lg<I>()), sb(Lg<L>())>();
     static constexpr int BUF = (BUF_BYTES + 15) / 16 * 2;       // doubles per staging buffer
-    // slab slot: B̃ (tri) | C̃ (tri) | D̃ | Ẽ | F̃ | μ | λ  (max over the classes)
+    // slab slot: B̃ (tri) | C̃ (tri) | D̃ | Ẽ | μ | λ  (max over the classes).  F̃ (p1×p2, non-
+    // empty only for interior knots) is NOT stored: the backward sweep recomputes
+    // F̃_{k+1} = C̃_k⁻ᵀ·D2_{k+1}H⁻¹D1_{k+1}ᵀ from knot k+1's Y/H, which it re-stages for the
+    // primal recovery anyway — 9 fewer doubles written and read back per interior knot
     template <class C> static constexpr int slab()
     {
-        return tri(C::PS) + tri(C::P2) + C::P1 * C::PS + C::PS * C::P2 + C::P1 * C::P2 + C::PS + C::P2;
+        return tri(C::PS) + tri(C::P2) + C::P1 * C::PS + C::PS * C::P2 + C::PS + C::P2;
     }
     static constexpr int SLOT = mx3<slab<F>(), slab<I>(), slab<L>()>();
 };
@@ -122,7 +128,7 @@ __device__ __forceinline__ u4_t make_rsrc4(const void *base)
 // knot staged two steps earlier) — which defeats the ring's prefetch entirely.  Issued here the
 // DMA is invisible to that pass: completion is tracked by hand (vm_wait<N>, which counts these
 // like any vector-memory op), the "memory" clobber keeps LDS accesses from moving across it,
-// and M0 is restored for the compiler.
+// and M0 is restored for the compiler (M0 is reserved: a clobber of it is not honoured).
 template <int BYTES>
 __device__ __forceinline__ void dma_lds(u4_t r, uint32_t vo, uint32_t so, uint32_t lds)
 {
@@ -219,6 +225,7 @@ template <int L> struct PatS {
 };
 // reader of a split image: element j of this lane's chunk
 typedef const __attribute__((address_space(3))) uint32_t lds_u32;
+typedef const __attribute__((address_space(3))) u4_t lds_u4;
 template <int L> struct SImg {
     using SP = Split<L>;
     uint32_t base;                                                  // LDS byte address
@@ -236,7 +243,44 @@ template <int L> struct SImg {
         const uint64_t lo = dw(8 * j), hi = dw(8 * j + 4);
         return __builtin_bit_cast(double, lo | (hi << 32));
     }
+    // the whole chunk into registers: one 16-byte LDS read per 12-byte piece (the image's
+    // 16-B slots of 16 consecutive lanes are distinct mod 16 — bank-conflict free, where
+    // dword reads at the 48/32-B lane stride conflicted 4–8 ways) plus the dword tail
+    __device__ __forceinline__ void load(double (&out)[L]) const
+    {
+        uint32_t w[2 * L];
+#pragma unroll
+        for (int s = 0; s < SP::n12; ++s) {
+            const u4_t q = *(lds_u4 *)(size_t)(base + (lane * SP::n12 + s) * 16);
+            w[3 * s] = q.x;
+            w[3 * s + 1] = q.y;
+            w[3 * s + 2] = q.z;
+        }
+#pragma unroll
+        for (int t = 0; t < SP::n4; ++t) w[3 * SP::n12 + t] = *(lds_u32 *)(size_t)(base + SP::bytesA + lane * (4 * SP::n4) + 4 * t);
+#pragma unroll
+        for (int j = 0; j < L; ++j) out[j] = __builtin_bit_cast(double, (uint64_t)w[2 * j] | ((uint64_t)w[2 * j + 1] << 32));
+    }
 };
+// a lane's Y chunk (L doubles at lane·L in the dense image) into registers: 16-byte reads
+// when L is even (chunks 16-B aligned), doubles otherwise
+typedef double d2_t __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(3))) d2_t lds_d2;
+typedef const __attribute__((address_space(3))) double lds_d;
+template <int L, bool WIDE> __device__ __forceinline__ void load_Y(uint32_t lds_base, int lane, double (&v)[L])
+{
+    if constexpr (WIDE && L % 2 == 0) {
+#pragma unroll
+        for (int p = 0; p < L / 2; ++p) {
+            const d2_t q = *(lds_d2 *)(size_t)(lds_base + (lane * L + 2 * p) * 8);
+            v[2 * p] = q.x;
+            v[2 * p + 1] = q.y;
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < L; ++e) v[e] = *(lds_d *)(size_t)(lds_base + (lane * L + e) * 8);
+    }
+}
 
 // staging buffer views (lane-linear [t][L] images)
 template <class S> struct Buf {
@@ -246,6 +290,12 @@ template <class S> struct Buf {
     template <int L> __device__ SImg<L> y(int lane) const { return SImg<L>{lds() + S::OFF_y, lane}; }
     template <int L> __device__ SImg<L> H(int lane) const { return SImg<L>{lds() + S::OFF_H, lane}; }
     template <int L> __device__ SImg<L> g(int lane) const { return SImg<L>{lds() + S::OFF_g, lane}; }
+    template <class C> __device__ void ld_Y(int lane, double (&v)[S::template LY<C>()]) const
+    {
+        load_Y<S::template LY<C>(), S::WIDE_Y>(lds(), lane, v);
+    }
+    template <class C> __device__ void ld_H(int lane, double (&v)[S::template LH<C>()]) const { H<S::template LH<C>()>(lane).load(v); }
+    template <class C> __device__ void ld_g(int lane, double (&v)[S::template Lg<C>()]) const { g<S::template Lg<C>()>(lane).load(v); }
 };
 
 // per-wave context: buffer resources, lane facts, the DMA patterns of interior knots
@@ -393,8 +443,8 @@ template <class C> struct Shur {
 };
 
 template <class S, class C>
-__device__ __forceinline__ bool compute_shur(Shur<C> &s, const double *Y, const SImg<S::template LH<C>()> &H,
-                                             const SImg<S::template Lg<C>()> &g)
+__device__ __forceinline__ bool compute_shur(Shur<C> &s, const double (&Y)[S::template LY<C>()],
+                                             const double (&H)[S::template LH<C>()], const double (&g)[S::template Lg<C>()])
 {
     constexpr int R = C::R, W = C::W;
 #pragma unroll
@@ -575,7 +625,7 @@ __device__ __forceinline__ void factor_knot(int k, const Shur<C> &sc, const doub
         la[i] = v;
     }
     if constexpr (p2 > 0) trsv_t<p2>(Cm, la);
-    // slab (batch-fastest, coalesced): B̃ | C̃ | D̃ | Ẽ | F̃ | μ | λ
+    // slab (batch-fastest, coalesced): B̃ | C̃ | D̃ | Ẽ | μ | λ  (F̃: recomputed, see Shape)
     int f = 0;
 #pragma unroll
     for (int i = 0; i < ps; ++i)
@@ -593,10 +643,6 @@ __device__ __forceinline__ void factor_knot(int k, const Shur<C> &sc, const doub
     for (int i = 0; i < ps; ++i)
 #pragma unroll
         for (int j = 0; j < p2; ++j) bstore(E[i][j], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
-#pragma unroll
-    for (int i = 0; i < p1; ++i)
-#pragma unroll
-        for (int j = 0; j < p2; ++j) bstore(F[i][j], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
 #pragma unroll
     for (int i = 0; i < ps; ++i) bstore(mu[i], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
 #pragma unroll
@@ -620,9 +666,11 @@ __device__ __forceinline__ void fwd_step(const KktArgs &a, const Ctx<S> &c, int 
 {
     if constexpr (!Cn::none) {
         Buf<S> b{stg + ((k + 1) % 3) * S::BUF};
-        const bool ok = compute_shur<S, Cn>(sn, b.Y(c.lane, S::template LY<Cn>()),
-                                           b.template H<S::template LH<Cn>()>(c.lane),
-                                           b.template g<S::template Lg<Cn>()>(c.lane));
+        double Yv[S::template LY<Cn>()], Hv[S::template LH<Cn>()], gv[S::template Lg<Cn>()];
+        b.template ld_Y<Cn>(c.lane, Yv);
+        b.template ld_H<Cn>(c.lane, Hv);
+        b.template ld_g<Cn>(c.lane, gv);
+        const bool ok = compute_shur<S, Cn>(sn, Yv, Hv, gv);
         if (!ok && info == 0) info = -(k + 2);
         const auto yk = b.template y<S::template Ly<Cn>()>(c.lane);
 #pragma unroll
@@ -660,10 +708,6 @@ __device__ __forceinline__ void slab_load(SlabV<C> &v, const Ctx<S> &c, int k)
 #pragma unroll
         for (int j = 0; j < p2; ++j) v.E[i][j] = at(f++);
 #pragma unroll
-    for (int i = 0; i < p1; ++i)
-#pragma unroll
-        for (int j = 0; j < p2; ++j) v.F[i][j] = at(f++);
-#pragma unroll
     for (int i = 0; i < ps; ++i) v.mu[i] = at(f++);
 #pragma unroll
     for (int i = 0; i < p2; ++i) v.la[i] = at(f++);
@@ -681,14 +725,77 @@ template <class S> constexpr int slab_ring_fields()
 }
 template <class S> constexpr int slab_dma_instrs() { return (slab_ring_fields<S>() + 1) / 2; }
 template <class S> constexpr int SLB = slab_dma_instrs<S>() * 128;     // doubles per ring slot
+// DMA instructions that stage one knot's slab chunk of class C (two fields per instruction)
+template <class S, class C> constexpr int slab_dma_of() { return (S::template slab<C>() + 1) / 2; }
 
-template <class S>
+template <class S, class C>
 __device__ __forceinline__ void stage_slab(const Ctx<S> &c, int k, double *ring)
 {
     const u4_t r = make_rsrc4(c.bS);
     const uint32_t so = slab_so<S>(k, 0), l0 = lds_addr(ring + (k % 3) * SLB<S>);
 #pragma unroll
-    for (int i = 0; i < slab_dma_instrs<S>(); ++i) dma_lds<16>(r, 2u * c.vS, so + 1024u * i, l0 + 1024u * i);
+    for (int i = 0; i < slab_dma_of<S, C>(); ++i) dma_lds<16>(r, 2u * c.vS, so + 1024u * i, l0 + 1024u * i);
+}
+
+// F̃ of knot k+1 (class Cn, p1 × p2) for the backward sweep, recomputed with the forward's
+// exact operation order (compute_shur's F block of the Schur pieces, then factor_knot's
+// trsm by the previous knot's C̃ factor Ua = C̃_k, inverse diagonal) — bit-identical to the
+// value the forward used.
+template <class S, class Cn>
+__device__ __forceinline__ void recompute_Ft(double (&Fo)[Z(Cn::P1)][Z(Cn::P2)], const double (&Ua)[Z(Cn::P1)][Z(Cn::P1)],
+                                             const double (&Y)[S::template LY<Cn>()],
+                                             const double (&H)[S::template LH<Cn>()])
+{
+    constexpr int R = Cn::R, W = Cn::W, p1 = Cn::P1, p2 = Cn::P2, O1 = Cn::O1, O2 = Cn::O2;
+    if constexpr (p1 > 0 && p2 > 0) {
+#pragma unroll
+        for (int i = 0; i < p1; ++i)
+#pragma unroll
+            for (int i2 = 0; i2 < p2; ++i2) Fo[i][i2] = 0.0;
+        if constexpr (!S::GINV || S::HDIAG) {
+#pragma unroll
+            for (int j = 0; j < W; ++j) {
+                double vh[p1];
+                if constexpr (S::GINV) {
+                    const double h = rcp_nr2(H[j]);
+#pragma unroll
+                    for (int i = 0; i < p1; ++i) vh[i] = Y[(O1 + i) + j * R] * h;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < p1; ++i) vh[i] = Y[(O1 + i) + j * R];
+                }
+#pragma unroll
+                for (int i = 0; i < p1; ++i)
+#pragma unroll
+                    for (int i2 = 0; i2 < p2; ++i2) Fo[i][i2] = fma(vh[i], Y[(O2 + i2) + j * R], Fo[i][i2]);
+            }
+        } else {
+            double U[W][W];
+#pragma unroll
+            for (int j = 0; j < W; ++j)
+#pragma unroll
+                for (int i = 0; i <= j; ++i) U[i][j] = H[i + j * W];
+            (void)potrf_inv<W>(U);
+            double Wt[p2][W];
+#pragma unroll
+            for (int i2 = 0; i2 < p2; ++i2) {
+                double x[W];
+#pragma unroll
+                for (int j = 0; j < W; ++j) x[j] = Y[(O2 + i2) + j * R];
+                trsv_t<W>(U, x);
+                trsv_n<W>(U, x);
+#pragma unroll
+                for (int j = 0; j < W; ++j) Wt[i2][j] = x[j];
+            }
+#pragma unroll
+            for (int j = 0; j < W; ++j)
+#pragma unroll
+                for (int i = 0; i < p1; ++i)
+#pragma unroll
+                    for (int i2 = 0; i2 < p2; ++i2) Fo[i][i2] = fma(Y[(O1 + i) + j * R], Wt[i2][j], Fo[i][i2]);
+        }
+        trsm_t<p1, p2>(Ua, Fo);                                   // cholesky_solve.jl:57
+    }
 }
 
 template <class S, class C>
@@ -714,10 +821,6 @@ __device__ __forceinline__ void slab_read(SlabV<C> &v, const Ctx<S> &c, int k, c
     for (int i = 0; i < ps; ++i)
 #pragma unroll
         for (int j = 0; j < p2; ++j) v.E[i][j] = b[64 * f++];
-#pragma unroll
-    for (int i = 0; i < p1; ++i)
-#pragma unroll
-        for (int j = 0; j < p2; ++j) v.F[i][j] = b[64 * f++];
 #pragma unroll
     for (int i = 0; i < ps; ++i) v.mu[i] = b[64 * f++];
 #pragma unroll
@@ -762,13 +865,25 @@ __device__ __forceinline__ void bwd_knot(SlabV<C> &v, const SlabV<Cn> &vn)
 
 // calc_residual! + calc_primals! of knot k (class C): needs λ_{k-1} (lp, class Cp's λ),
 // μ_k, λ_k (v).  cholesky_solver.jl:195-236 (SOC: :263-266).
+template <class S, class C> struct KnotIn {      // a staged knot's Y, H, g in registers
+    double Y[S::template LY<C>()], H[S::template LH<C>()], g[S::template Lg<C>()];
+    __device__ __forceinline__ void load(const Buf<S> &b, int lane)
+    {
+        b.template ld_Y<C>(lane, Y);
+        if constexpr (S::GINV) {
+            b.template ld_H<C>(lane, H);
+            b.template ld_g<C>(lane, g);
+        }
+    }
+};
+
 template <class S, class C, int NLP>
 __device__ __forceinline__ void primal_knot(const Ctx<S> &c, int k, const SlabV<C> &v, const double (&lp)[Z(NLP)],
-                                            const Buf<S> &b)
+                                            const KnotIn<S, C> &in)
 {
     constexpr int R = C::R, W = C::W;
     static_assert(NLP == C::P1, "λ_{k-1} has n1[k] entries");
-    const double *Y = b.Y(c.lane, S::template LY<C>());
+    const auto &Y = in.Y;
     double z[W];
 #pragma unroll
     for (int j = 0; j < W; ++j) {
@@ -782,8 +897,8 @@ __device__ __forceinline__ void primal_knot(const Ctx<S> &c, int k, const SlabV<
         z[j] = s;
     }
     if constexpr (S::GINV) {
-        const auto g = b.template g<S::template Lg<C>()>(c.lane);
-        const auto H = b.template H<S::template LH<C>()>(c.lane);
+        const auto &g = in.g;
+        const auto &H = in.H;
 #pragma unroll
         for (int j = 0; j < W; ++j) z[j] += g[j];                                     // add_gradient!
         if constexpr (S::HDIAG) {
@@ -838,8 +953,8 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     using F = typename S::F;
     using I = typename S::I;
     using L = typename S::L;
-    __shared__ double stg[3 * S::BUF];
-    __shared__ double sl[3 * SLB<S>];
+    __shared__ __attribute__((aligned(16))) double stg[3 * S::BUF];
+    __shared__ __attribute__((aligned(16))) double sl[3 * SLB<S>];
     const int N = a.N;                                          // ≥ 4 (host-checked)
     const int64_t t0 = (int64_t)blockIdx.x * 64;
     Ctx<S> c;
@@ -871,8 +986,11 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     double y0[Z(F::PS + F::P2)];
     {
         Buf<S> b{stg};
-        if (!compute_shur<S, F>(s0, b.Y(c.lane, S::template LY<F>()), b.template H<S::template LH<F>()>(c.lane),
-                                b.template g<S::template Lg<F>()>(c.lane)) && info == 0)
+        double Yv[S::template LY<F>()], Hv[S::template LH<F>()], gv[S::template Lg<F>()];
+        b.template ld_Y<F>(c.lane, Yv);
+        b.template ld_H<F>(c.lane, Hv);
+        b.template ld_g<F>(c.lane, gv);
+        if (!compute_shur<S, F>(s0, Yv, Hv, gv) && info == 0)
             info = -1;
         const auto yk = b.template y<S::template Ly<F>()>(c.lane);
 #pragma unroll
@@ -914,20 +1032,27 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
         factor_knot<S, L, NoCls>(N - 1, sL, yL, none, cy, c, info);
     }
 
+#if LQRX_FIL_ABL == 1
+    // ablation (tools only): forward sweep alone
+    if (a.info && c.live) a.info[t0 + c.lane] = info;
+    return;
+#endif
     // ---------------- backward + primal recovery ----------------
     // Step j finalises μ_j, λ_j (slab j) and recovers δz_{j+1} (staged knot j+1); it issues
     // the slab of j-2 and knot j-1, both consumed two steps later.  Stores per step: λ/μ of
     // knot j and δz of knot j+1; all of them count in vmcnt like the DMA (lower bounds below).
-    constexpr int nS = slab_dma_instrs<S>(), nK = S::template Dbwd<I>();
+    // nS: slab DMAs of an interior knot (the L-class chunk of knot N-1 is larger: lower bounds
+    // stay valid since it is staged first)
+    constexpr int nS = slab_dma_of<S, I>(), nK = S::template Dbwd<I>();
     constexpr int stL = L::PS + L::P2, stI = I::PS + I::P2;             // store_lam
     vm_wait<0>();                                               // forward slab stores landed
-    stage_slab<S>(c, N - 1, sl);
-    stage_slab<S>(c, N - 2, sl);
+    stage_slab<S, L>(c, N - 1, sl);
+    stage_slab<S, I>(c, N - 2, sl);
     c.stage_any(a, N - 1, stg, false);
     vm_wait<nS + S::template Dbwd<L>()>();                      // slab N-1
     SlabV<L> vL;
     slab_read<S, L>(vL, c, N - 1, sl);
-    stage_slab<S>(c, N - 3, sl);                                // N-3 ≥ 1: interior
+    stage_slab<S, I>(c, N - 3, sl);                             // N-3 ≥ 1: interior
     c.stage_I(N - 2, stg + ((N - 2) % 3) * S::BUF, false);
     SlabV<NoCls> vnone;
     bwd_knot<L, NoCls>(vL, vnone);                              // step N-1 (no primal)
@@ -936,12 +1061,13 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     vm_wait<nS + nK + stL>();
     SlabV<I> vI;
     slab_read<S, I>(vI, c, N - 2, sl);
-    if (N - 4 >= 1) stage_slab<S>(c, N - 4, sl);
+    if (N - 4 >= 1) stage_slab<S, I>(c, N - 4, sl);
     c.stage_I(N - 3, stg + ((N - 3) % 3) * S::BUF, false);
-    bwd_knot<I, L>(vI, vL);
+    bwd_knot<I, L>(vI, vL);                                     // class L: no F̃ (p2 = 0)
     {
-        Buf<S> b{stg + ((N - 1) % 3) * S::BUF};
-        primal_knot<S, L, L::P1>(c, N - 1, vL, vI.la, b);
+        KnotIn<S, L> in;
+        in.load(Buf<S>{stg + ((N - 1) % 3) * S::BUF}, c.lane);
+        primal_knot<S, L, L::P1>(c, N - 1, vL, vI.la, in);
     }
     store_lam<S, I>(c, N - 2, vI);
     for (int j = N - 3; j >= 1; --j) {
@@ -959,12 +1085,14 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
         }
         SlabV<I> v;
         slab_read<S, I>(v, c, j, sl);
-        if (j - 2 >= 1) stage_slab<S>(c, j - 2, sl);
+        KnotIn<S, I> in;                                        // knot j+1: F̃_{j+1} and δz_{j+1}
+        in.load(Buf<S>{stg + ((j + 1) % 3) * S::BUF}, c.lane);
+        if (j - 2 >= 1) stage_slab<S, I>(c, j - 2, sl);
         if (j - 1 >= 1) c.stage_I(j - 1, stg + ((j - 1) % 3) * S::BUF, false);
         else c.stage_any(a, 0, stg, false);
+        recompute_Ft<S, I>(vI.F, v.Cm, in.Y, in.H);
         bwd_knot<I, I>(v, vI);
-        Buf<S> b{stg + ((j + 1) % 3) * S::BUF};
-        primal_knot<S, I, I::P1>(c, j + 1, vI, v.la, b);
+        primal_knot<S, I, I::P1>(c, j + 1, vI, v.la, in);
         store_lam<S, I>(c, j, v);
         vI = v;
     }
@@ -974,13 +1102,16 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
         SlabV<F> v0;
         slab_load<S, F>(v0, c, 0);
         vm_wait<0>();
+        KnotIn<S, I> in1;
+        in1.load(Buf<S>{stg + (1 % 3) * S::BUF}, c.lane);
+        recompute_Ft<S, I>(vI.F, v0.Cm, in1.Y, in1.H);
         bwd_knot<F, I>(v0, vI);
-        Buf<S> b1{stg + (1 % 3) * S::BUF};
-        primal_knot<S, I, I::P1>(c, 1, vI, v0.la, b1);
+        primal_knot<S, I, I::P1>(c, 1, vI, v0.la, in1);
         store_lam<S, F>(c, 0, v0);
-        Buf<S> b0{stg};
+        KnotIn<S, F> in0;
+        in0.load(Buf<S>{stg}, c.lane);
         double none[1] = {0.0};
-        primal_knot<S, F, 0>(c, 0, v0, none, b0);
+        primal_knot<S, F, 0>(c, 0, v0, none, in0);
     }
     if (a.info && c.live) a.info[t0 + c.lane] = info;
 }
