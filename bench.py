@@ -434,6 +434,21 @@ def main():
                     "kernel_ms": kern_ms,
                     "flops_per_traj": dp_flops_per_traj(n, m, N),
                     "alg_bytes_per_launch": dp_bytes_per_traj(n, m, N, 8 if f64 else 4, args.tv) * bt}
+            if args.tv:
+                # time-varying: per-knot A_k, B_k, Q_k, R_k make the launch HBM-bound (SURVEY
+                # §8(d) 4-TV row: t_HBM vs t_FLOP near the ridge) — report the HBM roofline on
+                # the §8(d) algorithmic bytes, the fp64 fraction beside it, and the bytes the
+                # path must move at least (the rollout re-reads A_k, B_k and K_k: DESIGN §3.1)
+                ab = dp_bytes_per_traj(n, m, N, 8 if f64 else 4, True) * bt
+                s_ = 8 if f64 else 4
+                min_traffic = ab + bt * (N - 1) * (n * n + n * m + m * n) * s_
+                hbm = ab / (kern_ms * 1e-3) / 1e9
+                roof = {"bound": "hbm", "achieved": hbm, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": hbm / PEAK_HBM_GBS, "traffic": traffic,
+                        "kernel": _dp_kernel_name(n, m, bt, True), "kernel_ms": kern_ms,
+                        "alg_bytes_per_launch": ab, "min_traffic_bytes_per_launch": min_traffic,
+                        "min_traffic_frac": min_traffic / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                        "fp64_tflops": achieved, "fp64_frac": achieved / peak}
             headline = (n, m, N, bt, args.dtype) == (32, 16, 256, 65536, "f64") and not args.tv
             if args.workload == "cartpole":
                 metric = f"LQR trajectories/sec (Riccati bwd+fwd), cartpole n=4 m=1 N={N} B={bt}"

@@ -34,6 +34,15 @@
 #ifndef LQRX_DP_VAR
 #define LQRX_DP_VAR 0
 #endif
+#ifndef LQRX_DP_TVWAVES
+#define LQRX_DP_TVWAVES 0   // 0: per tile grid (launch_dp_tv); 1 or 2 forces waves/SIMD (A/B builds)
+#endif
+#ifndef LQRX_DP_TVEXTRA
+#define LQRX_DP_TVEXTRA 0   // extra VAR bits for the time-varying launch (ablations, tools only)
+#endif
+#ifndef LQRX_DP_TVABL
+#define LQRX_DP_TVABL 0     // ablation (tools only): re-read knot-1 inputs, see the kernel
+#endif
 #ifndef LQRX_DP_TVWAIT
 #define LQRX_DP_TVWAIT 0
 #endif
@@ -204,15 +213,20 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
     T arow[JX], brow[PX], arow_n[TV ? JX : 1], brow_n[TV ? PX : 1];
     auto load_rows = [&](int kk, T *ar, T *br) {   // row ix of A_kk, B_kk (this lane's part)
         const T *Ak = Ag + (int64_t)(kk - 1) * sA, *Bk = Bg + (int64_t)(kk - 1) * sB;
+        // per-knot (TV) loads: lane-derived offsets are laundered and kept 32-bit, so they
+        // are recomputed per call instead of hoisted out of the knot loop as 24 live
+        // 64-bit addresses (which spilled the whole time-varying kernel at 2 waves/SIMD)
+        int lx = ix, lh = hx;
+        if constexpr (TV) asm volatile("" : "+v"(lx), "+v"(lh));
 #pragma unroll
         for (int t = 0; t < JX; ++t) {
-            int j = hx * JX + t;
-            ar[t] = (ix < n && j < n) ? Ak[ix + (size_t)j * n] : (T)0;
+            int j = lh * JX + t;
+            ar[t] = (lx < n && j < n) ? Ak[lx + j * n] : (T)0;
         }
 #pragma unroll
         for (int t = 0; t < PX; ++t) {
-            int p = hx * PX + t;
-            br[t] = (ix < n && p < m) ? Bk[ix + (size_t)p * n] : (T)0;
+            int p = lh * PX + t;
+            br[t] = (lx < n && p < m) ? Bk[lx + p * n] : (T)0;
         }
     };
     load_rows(1, arow, brow);
@@ -327,7 +341,12 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
     const size_t nn = (size_t)n * n, nm = (size_t)n * m, mm = (size_t)m * m;
     // per-trajectory bases; time-varying fields hold N-1 knots (knot k at index k-1)
     const size_t kAB = (TV && a.tv_AB) ? (size_t)(N - 1) : 1, kQR = (TV && a.tv_QR) ? (size_t)(N - 1) : 1;
-    const size_t sA = kAB > 1 ? nn : 0, sB = kAB > 1 ? nm : 0, sQ = kQR > 1 ? nn : 0, sR = kQR > 1 ? mm : 0;
+    size_t sA = kAB > 1 ? nn : 0, sB = kAB > 1 ? nm : 0, sQ = kQR > 1 ? nn : 0, sR = kQR > 1 ? mm : 0;
+#if LQRX_DP_TVABL
+    // ablation (tools only): bit 1 = Q_k, bit 2 = A_k/B_k/R_k re-read from knot 1 (cache-resident)
+    if (LQRX_DP_TVABL & 1) sQ = 0;
+    if (LQRX_DP_TVABL & 2) sA = sB = sR = 0;
+#endif
     const T *Ab = (const T *)a.A + b * nn * kAB, *Bb = (const T *)a.B + b * nm * kAB;
     const T *Qb = (const T *)a.Q + b * nn * kQR, *Rb = (const T *)a.R + b * mm * kQR;
     const T *Qg = Qb;
@@ -479,7 +498,10 @@ static hipError_t launch_dp(const DpArgs &a, hipStream_t s);
 template <typename T, int NT, int MT, int WAVES = 2, int VAR = 0>
 static hipError_t launch_dp_tv(const DpArgs &a, hipStream_t s)
 {
-    if (a.tv_AB || a.tv_QR) return launch_dp<T, NT, MT, 1, VAR_TV>(a, s);   // 1 wave/SIMD: no spills
+    // 2 waves/SIMD where the time-varying kernel fits 256 registers without spills (tile
+    // grids up to 2×1, i.e. n ≤ 32, m ≤ 16 — cfg4's shape), else 1
+    constexpr int TVW = LQRX_DP_TVWAVES ? LQRX_DP_TVWAVES : ((NT <= 2 && MT <= 1) ? 2 : 1);
+    if (a.tv_AB || a.tv_QR) return launch_dp<T, NT, MT, TVW, VAR_TV | LQRX_DP_TVEXTRA>(a, s);
     return launch_dp<T, NT, MT, WAVES, VAR>(a, s);
 }
 

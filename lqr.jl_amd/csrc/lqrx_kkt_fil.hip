@@ -108,47 +108,7 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void *base)
     // raw buffer (stride 0), full 31-bit range; gfx9 dword-3 format bits
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7fffffff, 0x00020000);
 }
-// the same descriptor as four SGPRs, for the inline-asm DMA below
-typedef uint32_t u4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u4_t make_rsrc4(const void *base)
-{
-    const uint64_t a = (uint64_t)base;
-    u4_t r;
-    r.x = (uint32_t)a;
-    r.y = (uint32_t)(a >> 32) & 0xffffu;
-    r.z = 0x7fffffffu;
-    r.w = 0x00020000u;
-    return r;
-}
-
-// One LDS-DMA instruction (buffer_load_dword{,x3,x4} … lds; M0 = the wave's LDS destination,
-// each lane's piece lands at M0 + lane·slot).  Issued as inline asm ON PURPOSE: the compiler's
-// wait-count pass cannot tell which LDS bytes a DMA writes, so after a DMA issued through the
-// builtin it makes EVERY later LDS read wait for it (vmcnt(0) before the first read of the
-// knot staged two steps earlier) — which defeats the ring's prefetch entirely.  Issued here the
-// DMA is invisible to that pass: completion is tracked by hand (vm_wait<N>, which counts these
-// like any vector-memory op), the "memory" clobber keeps LDS accesses from moving across it,
-// and M0 is restored for the compiler (M0 is reserved: a clobber of it is not honoured).
-template <int BYTES>
-__device__ __forceinline__ void dma_lds(u4_t r, uint32_t vo, uint32_t so, uint32_t lds)
-{
-    uint32_t keep;
-    if constexpr (BYTES == 16)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, %4 offen lds\n\t"
-                     "s_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(vo), "s"(lds), "s"(r), "s"(so) : "memory");
-    else if constexpr (BYTES == 12)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx3 %1, %3, %4 offen lds\n\t"
-                     "s_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(vo), "s"(lds), "s"(r), "s"(so) : "memory");
-    else {
-        static_assert(BYTES == 4, "LDS-DMA piece of 4, 12 or 16 bytes");
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %1, %3, %4 offen lds\n\t"
-                     "s_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(vo), "s"(lds), "s"(r), "s"(so) : "memory");
-    }
-}
-__device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(size_t)(lptr_t)p; }
+// (u4_t, make_rsrc4, dma_lds, lds_addr: the inline-asm LDS-DMA issue, lqrx_stage.h)
 
 // DMA pattern of one packed array for a chunk of L doubles per trajectory: the wave's 64
 // chunks form a dense [t][L] image of `per` pieces per trajectory (16 B pieces when WIDE,

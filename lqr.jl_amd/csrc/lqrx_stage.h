@@ -49,6 +49,49 @@ __device__ __forceinline__ void stage_chunk(const double *X, int64_t s, int64_t 
 }
 
 
+// a raw buffer descriptor (stride 0, full 31-bit range, gfx9 dword-3 format bits) as four
+// SGPRs, for the inline-asm LDS-DMA below
+typedef uint32_t u4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u4_t make_rsrc4(const void *base)
+{
+    const uint64_t a = (uint64_t)base;
+    u4_t r;
+    r.x = (uint32_t)a;
+    r.y = (uint32_t)(a >> 32) & 0xffffu;
+    r.z = 0x7fffffffu;
+    r.w = 0x00020000u;
+    return r;
+}
+
+// One LDS-DMA instruction (buffer_load_dword{,x3,x4} … lds; M0 = the wave's LDS destination,
+// each lane's piece lands at M0 + lane·slot).  Issued as inline asm ON PURPOSE: the compiler's
+// wait-count pass cannot tell which LDS bytes a DMA writes, so after a DMA issued through the
+// builtin it makes EVERY later LDS read wait for it (vmcnt(0) before the first read of the
+// knot staged two steps earlier) — which defeats the ring's prefetch entirely.  Issued here the
+// DMA is invisible to that pass: completion is tracked by hand (vm_wait<N>, which counts these
+// like any vector-memory op), the "memory" clobber keeps LDS accesses from moving across it,
+// and M0 is restored for the compiler (M0 is reserved: a clobber of it is not honoured).
+template <int BYTES>
+__device__ __forceinline__ void dma_lds(u4_t r, uint32_t vo, uint32_t so, uint32_t lds)
+{
+    uint32_t keep;
+    if constexpr (BYTES == 16)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, %4 offen lds\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(vo), "s"(lds), "s"(r), "s"(so) : "memory");
+    else if constexpr (BYTES == 12)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx3 %1, %3, %4 offen lds\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(vo), "s"(lds), "s"(r), "s"(so) : "memory");
+    else {
+        static_assert(BYTES == 4, "LDS-DMA piece of 4, 12 or 16 bytes");
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %1, %3, %4 offen lds\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(vo), "s"(lds), "s"(r), "s"(so) : "memory");
+    }
+}
+__device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(size_t)(lptr_t)p; }
+
 // number of DMA instructions stage_chunk issues for a chunk of L doubles (same rule)
 __host__ __device__ constexpr int stage_instrs(int L, bool wide) { return L <= 0 ? 0 : (wide ? L / 2 : 2 * L); }
 
