@@ -193,9 +193,11 @@ int lqrx_dubins_sqp_solve_host(const lqrx_dubins_sqp_desc *desc, double *Z, cons
  * solve!(sol, ::LeastSquaresSolver, prob) (/root/reference/src/least_squares.jl:158-192)
  * with opts :solve_type => :cholesky — Ā/b̄ as buildAb! builds them (:58-103),
  * H = ĀᵀĀ + Hu, y = −Āᵀb̄ (:171-173), potrf/potrs 'U' (:181-182), rollout! (:197-202).
- * One workgroup per trajectory with the whole problem in LDS: requires
- * lqrx_ls_lds_bytes(n, m, N) <= 163840 and (N−1)·m <= 192 (e.g. n=4, m=1: N ≤ 189;
- * n=3, m=2: N ≤ 97; n=6, m=3: N ≤ 62).
+ * One workgroup per trajectory.  (N−1)·m ≤ 192 and lqrx_ls_lds_bytes(n, m, N) <= 163840
+ * (e.g. n=4, m=1: N ≤ 189; n=3, m=2: N ≤ 97): the whole problem in LDS.  Larger problems up to
+ * (N−1)·m ≤ 1024 keep H in stream-ordered global scratch (Nm(Nm+1)/2 doubles per trajectory)
+ * with a blocked factor — e.g. the reference's own LS test problem, DoubleIntegrator()
+ * n=6, m=3, N=101 (Nm = 300); lqrx_ls_lds_bytes reports the LDS of the path taken.
  *   hu_mode 0: Hu = 0 — a fresh LeastSquaresSolver (:44), the reference default; the
  *              solve then carries no control cost
  *           1: Hu = blkdiag(chol(R).U) — what build_least_squares! leaves (:121)

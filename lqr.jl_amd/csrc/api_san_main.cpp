@@ -135,10 +135,10 @@ int main()
 
     // ---- LS / SQP validation ----
     CHECK(lqrx_ls_lds_bytes(4, 1, 101) > 0 && lqrx_ls_lds_bytes(4, 1, 101) <= 163840);
-    CHECK(lqrx_ls_lds_bytes(6, 3, 101) > 163840);
+    CHECK(lqrx_ls_lds_bytes(6, 3, 101) <= 163840);   // Nm = 300: the global-H path
     lqrx_ls_desc ls{4, 1, 101, 5, 8};
     CHECK(lqrx_ls_solve(&ls, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, info, nullptr, nullptr, nullptr) < 0);
-    ls.hu_mode = 0; ls.N = 194; ls.m = 1;                       // (N-1)m = 193 > 192
+    ls.hu_mode = 0; ls.N = 1026; ls.m = 1;                      // (N-1)m = 1025 > 1024
     CHECK(lqrx_ls_solve_host(&ls, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, info) == LQRX_ERR_UNSUPPORTED);
     lqrx_dubins_sqp_desc q{};
     q.N = 1; q.max_iters = 10; q.batch = 1; q.dt = 0.1;

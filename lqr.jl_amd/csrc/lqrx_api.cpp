@@ -761,8 +761,8 @@ int validate_ls(const lqrx_ls_desc *d)
     if (d->N < 2) return set_err(-1, "desc.N must be >= 2 (got %d)", d->N);
     if (d->hu_mode < 0 || d->hu_mode > 2) return set_err(-1, "desc.hu_mode must be 0, 1 or 2");
     if (d->batch < 0 || d->batch > 0x7fffffff) return set_err(-1, "desc.batch must be in [0, 2^31)");
-    if ((int64_t)(d->N - 1) * d->m > 192)
-        return set_err(LQRX_ERR_UNSUPPORTED, "(N-1)*m = %lld > 192", (long long)(d->N - 1) * d->m);
+    if ((int64_t)(d->N - 1) * d->m > lqrx::ls_max_nm())
+        return set_err(LQRX_ERR_UNSUPPORTED, "(N-1)*m = %lld > %d", (long long)(d->N - 1) * d->m, lqrx::ls_max_nm());
     const size_t lds = lqrx::ls_lds_bytes(d->n, d->m, d->N);
     if (lds > LS_LDS_MAX)
         return set_err(LQRX_ERR_UNSUPPORTED, "n=%d m=%d N=%d needs %zu B of LDS (> %zu)", d->n, d->m, d->N, lds,

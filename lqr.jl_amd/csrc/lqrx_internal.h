@@ -109,6 +109,7 @@ struct LsArgs {
     int64_t batch;
 };
 size_t ls_lds_bytes(int n, int m, int N);
+int ls_max_nm();          // (N−1)·m cap (the big, global-H path)
 hipError_t ls_launch(const LsArgs &a, hipStream_t s);
 
 } // namespace lqrx

@@ -26,13 +26,11 @@ __global__ __launch_bounds__(256) void transpose_kernel(const T *__restrict__ in
     const int64_t t = blockIdx.x;
     const int64_t r0 = (t / tiles_c) * TT, c0 = (t % tiles_c) * TT;
     const int tx = threadIdx.x & (TT - 1), ty = threadIdx.x >> 6;
-#pragma unroll
     for (int i = ty; i < TT; i += TROWS) {
         const int64_t r = r0 + i, c = c0 + tx;
         if (r < rows && c < cols) tile[i][tx] = in[r * cols + c];
     }
     __syncthreads();
-#pragma unroll
     for (int i = ty; i < TT; i += TROWS) {
         const int64_t c = c0 + i, r = r0 + tx;     // out row c, column r
         if (r < rows && c < cols) out[c * rows + r] = tile[tx][i];

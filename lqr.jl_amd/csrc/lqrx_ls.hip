@@ -29,8 +29,12 @@ namespace {
 
 constexpr int LS_THREADS = 256;
 constexpr int LS_REG = 16;     // register fast paths (buildAb!, rollout!) for n, m ≤ 16, nm + n ≤ 64
-constexpr int LS_MAX_NM = 192; // (N−1)·m; H is a packed triangle (Nm(Nm+1)/2 doubles), the LDS
-                               // budget (≤ 163840 B, validate_ls) binds at Nm = 192
+constexpr int LS_MAX_NM = 192; // (N−1)·m with H in LDS: a packed triangle (Nm(Nm+1)/2 doubles);
+                               // the LDS budget (≤ 163840 B, validate_ls) binds at Nm = 192
+constexpr int LS_BIG_MAX_NM = 1024; // H in global scratch (the "big" path): blocked factor
+constexpr int LS_PB = 16;           // big path: max panel rows factored in LDS per pass (the host
+                                    // halves it until the panel fits the LDS budget)
+constexpr size_t LS_LDS_CAP = 163840;
 
 // order one wave's LDS accesses across lanes (a wave executes LDS ops in order; this stops
 // the compiler from moving them across and waits for the writes)
@@ -66,10 +70,12 @@ __device__ inline double bcast_slot(const double (&v)[S], int j)
 struct LsLayout {
     int n, m, N, K, Nm, Nn;
     // LDS offsets in doubles
-    int oSq, oSf, oHu, oA, oB, oPl, oW, oVq, oVf, obb, oH, oy, odi, oX, oFlag, total;
+    int oSq, oSf, oHu, oA, oB, oPl, oW, oVq, oVf, obb, oH, oy, odi, oX, oFlag, oPan, total;
 };
 
-__host__ __device__ inline LsLayout ls_layout(int n, int m, int N)
+// big = H in global scratch: the LDS keeps only the staging space for Q, Qf, R in place of
+// H, plus a panel of LS_PB rows for the blocked factor
+__host__ __device__ inline LsLayout ls_layout(int n, int m, int N, bool big = false, int pb = LS_PB)
 {
     LsLayout L;
     L.n = n; L.m = m; L.N = N; L.K = N - 1; L.Nm = L.K * m; L.Nn = N * n;
@@ -86,11 +92,12 @@ __host__ __device__ inline LsLayout ls_layout(int n, int m, int N)
     L.obb = o; o += N * n;
     L.oX = L.obb;   // X (rollout) reuses b̄'s space: b̄ is dead once y = −Āᵀb̄ is formed
     L.oH = o;  // also stages Q, Qf, R for the small factorisations
-    const int hp = L.Nm * (L.Nm + 1) / 2;   // packed upper triangle, column-major
+    const int hp = big ? 0 : L.Nm * (L.Nm + 1) / 2;   // packed upper triangle, rows contiguous
     o += hp > 2 * n * n + m * m ? hp : 2 * n * n + m * m;
     L.oy = o; o += L.Nm;
     L.odi = o; o += L.Nm;   // 1/U_jj of the factor (potrs multiplies instead of dividing)
     L.oFlag = o; o += 1;
+    L.oPan = o; o += big ? pb * L.Nm : 0;
     L.total = o;
     return L;
 }
@@ -133,24 +140,33 @@ __device__ void ls_fail(double *gU, double *gX, int32_t *ginfo, int64_t b, int n
     if (threadIdx.x == 0 && ginfo) ginfo[b] = code;
 }
 
+// BIG = false: the whole problem in LDS (Nm ≤ 192).  BIG = true: H = ĀᵀĀ + Hu lives in a
+// per-trajectory global scratch block (packed, rows contiguous: gH + b·Nm(Nm+1)/2), built by
+// the same code, factored by a blocked right-looking Cholesky (LS_PB-row panels factored in
+// LDS, one trailing update of the remaining rows per panel), solved by the same potrs —
+// the reference's own LS test problem (test/least_squares.jl: DoubleIntegrator(), Nm = 300)
+// takes this path.
+template <bool BIG>
 __global__ void __launch_bounds__(LS_THREADS)
 ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB, const double *__restrict__ gQ,
                     const double *__restrict__ gR, const double *__restrict__ gQf, const double *__restrict__ gx0,
                     double *__restrict__ gU, double *__restrict__ gX, int32_t *__restrict__ ginfo,
-                    double *__restrict__ gAb, double *__restrict__ gbb, int n, int m, int N, int hu_mode)
+                    double *__restrict__ gAb, double *__restrict__ gbb, int n, int m, int N, int hu_mode,
+                    double *__restrict__ gH, int pb)
 {
     extern __shared__ double lds[];
-    const LsLayout L = ls_layout(n, m, N);
+    const LsLayout L = ls_layout(n, m, N, BIG, pb);
     const int K = L.K, Nm = L.Nm, tid = threadIdx.x;
     const int64_t b = blockIdx.x;
     double *Sq = lds + L.oSq, *Sf = lds + L.oSf, *Hu = lds + L.oHu, *A = lds + L.oA, *B = lds + L.oB;
     double *Pl = lds + L.oPl, *W = lds + L.oW, *Vq = lds + L.oVq, *Vf = lds + L.oVf, *bb = lds + L.obb;
-    double *H = lds + L.oH, *y = lds + L.oy, *X = lds + L.oX, *dinv = lds + L.odi;
+    double *y = lds + L.oy, *X = lds + L.oX, *dinv = lds + L.odi;
+    double *H = BIG ? gH + b * ((int64_t)Nm * (Nm + 1) / 2) : lds + L.oH;
     int *flag = (int *)(lds + L.oFlag);
     const int nn = n * n, nm = n * m, mm = m * m;
 
-    // ---- inputs: A, B, x0 into LDS; Q, Qf, R staged in H's space for the factorisations
-    double *tQ = H, *tQf = H + nn, *tR = H + 2 * nn;
+    // ---- inputs: A, B, x0 into LDS; Q, Qf, R staged in H's LDS space for the factorisations
+    double *tQ = lds + L.oH, *tQf = tQ + nn, *tR = tQ + 2 * nn;
     for (int i = tid; i < nn; i += LS_THREADS) {
         A[i] = gA[b * nn + i];
         tQ[i] = gQ[b * nn + i];
@@ -303,11 +319,61 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
     if (tid == 0) *flag = 0;
     __syncthreads();
 
+    const int wave = tid >> 6, lane = tid & 63;
+    if constexpr (BIG) {
+    // ---- potrf 'U' (:181), big path: blocked right-looking over LS_PB-row panels.  A panel
+    // (rows r0..r0+pr−1, columns r0..Nm−1 of the upper triangle) is brought to LDS, factored
+    // there (one barrier per pivot, rows scaled to U as each pivot completes), written back,
+    // and the trailing rows get one update H[i,k] −= Σ_u U[u,i]·U[u,k] per panel — global
+    // read-modify-writes once per panel instead of once per pivot.
+    double *Pn = lds + L.oPan;
+    for (int r0 = 0; r0 < Nm; r0 += pb) {
+        const int pr = Nm - r0 < pb ? Nm - r0 : pb, w = Nm - r0;
+        for (int e = tid; e < pr * w; e += LS_THREADS) {
+            const int u = e / w, c = e - u * w;
+            Pn[e] = c >= u ? H[rbase(r0 + u, Nm) + r0 + c] : 0.0;
+        }
+        __syncthreads();
+        for (int u = 0; u < pr; ++u) {
+            const double d = Pn[u * w + u];
+            if (!(d > 0.0)) {   // uniform: every thread reads the same LDS word
+                ls_fail(gU, gX, ginfo, b, n, m, N, r0 + u + 1);
+                return;
+            }
+            const double ri = rsqrt_nr(d);
+            for (int c = u + tid; c < w; c += LS_THREADS) Pn[u * w + c] = c == u ? d * ri : Pn[u * w + c] * ri;
+            if (tid == 0) dinv[r0 + u] = ri;
+            __syncthreads();
+            for (int v = u + 1 + wave; v < pr; v += LS_THREADS / 64) {
+                const double uv = Pn[u * w + v];
+                for (int c = v + lane; c < w; c += 64) Pn[v * w + c] = fma(-uv, Pn[u * w + c], Pn[v * w + c]);
+            }
+            __syncthreads();
+        }
+        for (int e = tid; e < pr * w; e += LS_THREADS) {
+            const int u = e / w, c = e - u * w;
+            if (c >= u) H[rbase(r0 + u, Nm) + r0 + c] = Pn[e];
+        }
+        for (int i = r0 + pr + wave; i < Nm; i += LS_THREADS / 64) {
+            double ui[LS_PB];
+#pragma unroll
+            for (int u = 0; u < LS_PB; ++u) ui[u] = u < pr ? Pn[u * w + (i - r0)] : 0.0;
+            const int ri0 = rbase(i, Nm);
+            for (int k = i + lane; k < Nm; k += 64) {
+                double v = H[ri0 + k];
+#pragma unroll
+                for (int u = 0; u < LS_PB; ++u)
+                    if (u < pr) v = fma(-ui[u], Pn[u * w + (k - r0)], v);
+                H[ri0 + k] = v;
+            }
+        }
+        __syncthreads();
+    }
+    } else {
     // ---- potrf 'U' (:181): right-looking, one barrier per pivot.  Step j updates the trailing
     // upper triangle with the unscaled row j (H[i,k] −= H[j,i]·H[j,k]/d_j) and scales row j−1
     // (read by nobody in step j); info = first non-positive pivot.  Waves own rows (4 per
     // pass, sharing each loaded H[j,k]), lanes columns: every LDS access is row-contiguous.
-    const int wave = tid >> 6, lane = tid & 63;
     double dprev = 1.0;
     for (int j = 0; j < Nm; ++j) {
         const double d = H[up(j, j, Nm)];
@@ -355,10 +421,11 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
         dinv[Nm - 1] = rdp;
     }
     __syncthreads();
+    }
     // ---- potrs 'U' (:182): Uᵀz = y, then U x = z — wave 0, y held in registers (lane l owns
     // y[l + 64 s]), the pivot broadcast by readlane: no barriers in the 2·Nm-step chain
     if (tid < 64) {
-        constexpr int S = LS_MAX_NM / 64;
+        constexpr int S = (BIG ? LS_BIG_MAX_NM : LS_MAX_NM) / 64;
         double yr[S];
 #pragma unroll
         for (int s2 = 0; s2 < S; ++s2) {
@@ -436,21 +503,53 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
 
 } // namespace
 
+// the big path (H in global scratch) serves what the LDS-resident kernel cannot hold
+bool ls_big(int n, int m, int N)
+{
+    const LsLayout L = ls_layout(n, m, N);
+    return L.Nm > LS_MAX_NM || (size_t)L.total * sizeof(double) > LS_LDS_CAP;
+}
+// big path panel rows: the widest of 16, 8, 4, 2 whose panel fits the LDS budget
+int ls_panel(int n, int m, int N)
+{
+    int pb = LS_PB;
+    while (pb > 2 && (size_t)ls_layout(n, m, N, true, pb).total * sizeof(double) > LS_LDS_CAP) pb /= 2;
+    return pb;
+}
+
 size_t ls_lds_bytes(int n, int m, int N)
 {
-    return (size_t)ls_layout(n, m, N).total * sizeof(double);
+    const bool big = ls_big(n, m, N);
+    return (size_t)ls_layout(n, m, N, big, big ? ls_panel(n, m, N) : LS_PB).total * sizeof(double);
 }
+
+int ls_max_nm() { return LS_BIG_MAX_NM; }
 
 hipError_t ls_launch(const LsArgs &a, hipStream_t s)
 {
+    const bool big = ls_big(a.n, a.m, a.N);
     const size_t lds = ls_lds_bytes(a.n, a.m, a.N);
-    hipError_t e = hipFuncSetAttribute((const void *)ls_condensed_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const void *fn = big ? (const void *)ls_condensed_kernel<true> : (const void *)ls_condensed_kernel<false>;
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
+    Scratch sc;                          // big path: packed H per trajectory, stream-ordered
+    const int Nm = (a.N - 1) * a.m;
+    if (big) {
+        e = scratch_alloc(&sc.p, (size_t)a.batch * ((size_t)Nm * (Nm + 1) / 2) * sizeof(double), s);
+        if (e != hipSuccess) return e;
+        sc.owned = true;
+    }
     // one workgroup per trajectory; the grid dimension is capped at 2^31−1 by the ABI check
-    hipLaunchKernelGGL(ls_condensed_kernel, dim3((unsigned)a.batch), dim3(LS_THREADS), lds, s, a.A, a.B, a.Q,
-                       a.R, a.Qf, a.x0, a.U, a.X, a.info, a.Ab, a.bb, a.n, a.m, a.N, a.hu_mode);
-    return hipGetLastError();
+    if (big)
+        hipLaunchKernelGGL(ls_condensed_kernel<true>, dim3((unsigned)a.batch), dim3(LS_THREADS), lds, s, a.A, a.B,
+                           a.Q, a.R, a.Qf, a.x0, a.U, a.X, a.info, a.Ab, a.bb, a.n, a.m, a.N, a.hu_mode, (double *)sc.p,
+                           ls_panel(a.n, a.m, a.N));
+    else
+        hipLaunchKernelGGL(ls_condensed_kernel<false>, dim3((unsigned)a.batch), dim3(LS_THREADS), lds, s, a.A, a.B,
+                           a.Q, a.R, a.Qf, a.x0, a.U, a.X, a.info, a.Ab, a.bb, a.n, a.m, a.N, a.hu_mode, nullptr, LS_PB);
+    e = hipGetLastError();
+    hipError_t ef = sc.release(s);
+    return e != hipSuccess ? e : ef;
 }
 
 } // namespace lqrx

@@ -82,7 +82,8 @@ class LeastSquaresSolver:
         return cls(n, m, N)
 
 
-MAX_NM = 192      # (N−1)·m cap of ls_condensed_kernel (LS_MAX_NM, lqrx_ls.hip)
+MAX_NM = 1024     # (N−1)·m cap of ls_condensed_kernel (LS_BIG_MAX_NM, lqrx_ls.hip; above 192 H lives in
+                  # global scratch with a blocked factor)
 
 
 def lds_bytes(n: int, m: int, N: int) -> int:

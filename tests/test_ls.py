@@ -120,19 +120,36 @@ def test_sparse_gather_roundtrip(lqrx):
 
 
 def test_ls_lds_limits(lqrx):
+    """Nm = (N−1)m ≤ 192 with the problem in LDS; larger problems (up to Nm = 1024) keep H in
+    global scratch (blocked factor) and need far less LDS — including the reference's own LS
+    test problem, DoubleIntegrator() n=6 m=3 N=101 (test/least_squares.jl:2), Nm = 300."""
     from lqrx import ls
 
     assert ls.lds_bytes(4, 1, 101) <= 163840      # cartpole N=101 fits one CU
-    assert ls.lds_bytes(6, 3, 101) > 163840       # DoubleIntegrator(3,101): Nm = 300
-    assert ls.lds_bytes(2, 2, 97) <= 163840       # Nm = 192: the largest accepted
-    with pytest.raises(lqrx.LqrxError):
-        ls.LeastSquaresSolver.of(lqrx.LQRProblem(*[np.eye(6)] * 3 + [np.eye(6), np.ones((6, 3)),
-                                                                      np.zeros(6)], N=101))
-    for n, m, N in ((2, 2, 98), (4, 1, 193)):     # Nm = 194 > 192; Nm = 192 but LDS > 160 KiB
-        with pytest.raises(lqrx.LqrxError) as e:
-            ls.LeastSquaresSolver.of(lqrx.LQRProblem(np.eye(n), np.eye(n), np.eye(m), np.eye(n),
-                                                     np.ones((n, m)), np.zeros(n), N=N))
-        assert e.value.code == lqrx._lib.ERR_UNSUPPORTED
+    assert ls.lds_bytes(2, 2, 97) <= 163840       # Nm = 192: the largest LDS-resident H
+    assert ls.lds_bytes(6, 3, 101) <= 163840      # DoubleIntegrator(3,101): Nm = 300, global H
+    assert ls.lds_bytes(4, 1, 193) <= 163840      # Nm = 192 but H would overflow LDS: global H
+    ls.LeastSquaresSolver.of(lqrx.LQRProblem(*[np.eye(6)] * 3 + [np.eye(6), np.ones((6, 3)),
+                                                                  np.zeros(6)], N=101))
+    for n, m, N in ((2, 2, 98), (4, 1, 193), (1, 1, 1025)):
+        ls.LeastSquaresSolver.of(lqrx.LQRProblem(np.eye(n), np.eye(n), np.eye(m), np.eye(n),
+                                                 np.ones((n, m)), np.zeros(n), N=N))
+    with pytest.raises(lqrx.LqrxError) as e:                # Nm = 1025 > 1024
+        ls.LeastSquaresSolver.of(lqrx.LQRProblem(np.eye(1), np.eye(1), np.eye(1), np.eye(1),
+                                                 np.ones((1, 1)), np.zeros(1), N=1026))
+    assert e.value.code == lqrx._lib.ERR_UNSUPPORTED
+
+
+def double_integrator_ls(N=101, D=3):
+    """RobotZoo.DoubleIntegrator(D) (test/problems.jl:14-56) as the LS path sees it: exact
+    discretisation of ẍ = u at dt = tf/(N−1), tf = 2; Q = diag(10·1_D, 1_D), R = 0.1·I,
+    Qf = 10Q, x0 = [1_D; 0_D] (problems.jl:20-27)."""
+    dt = 2.0 / (N - 1)
+    I = np.eye(D)
+    A = np.block([[I, dt * I], [0 * I, I]])
+    B = np.vstack([0.5 * dt * dt * I, dt * I])
+    Q = np.diag([10.0] * D + [1.0] * D)
+    return A, B, Q, 0.1 * np.eye(D), 10 * Q, np.concatenate([np.ones(D), np.zeros(D)])
 
 
 def test_ls_rejects_non_symmetric(lqrx):
@@ -278,3 +295,77 @@ def test_sparse_solver_gpu(lqrx, gpu_ok, name, h_mode):
         assert np.abs(out["lam"][b] - ref["lam"]).max() <= 1e-10 * np.abs(ref["lam"]).max()
         rs = LO.sparse_soc(D[b], d[b])
         assert np.abs(soc["dz"][b] - rs).max() <= 1e-10 * np.abs(rs).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hu", [0, 1, 2])
+def test_ls_gpu_reference_double_integrator(lqrx, gpu_ok, hu):
+    """The reference's own LS test problem (test/least_squares.jl:29-38: DoubleIntegrator(),
+    n=6 m=3 N=101, Nm = 300 — the global-H blocked path): U, X against the numpy oracle, and
+    the optimality condition that test asserts, ‖Āᵀ(ĀU + b̄) + Hu·U‖∞ < 1e-12 (scaled)."""
+    import torch
+    from lqrx import ls
+    from lqrx.dp import to_abi
+
+    A, B, Q, R, Qf, x0 = double_integrator_ls()
+    n, m, N, bt = 6, 3, 101, 6
+    rng = np.random.default_rng(4)
+    X0 = x0[None] + 0.1 * rng.standard_normal((bt, n))
+    st = lambda M: np.repeat(M[None], bt, axis=0)
+    dev = torch.device("cuda:0")
+    t = {k: torch.from_numpy(to_abi(st(v)).reshape(-1)).to(dev) for k, v in dict(A=A, B=B, Q=Q, R=R, Qf=Qf).items()}
+    t["x0"] = torch.from_numpy(np.ascontiguousarray(X0).reshape(-1)).to(dev)
+    t.update(n=n, m=m, batch=bt)
+    out = ls.ls_solve_device(t, N, hu_mode=hu, with_Ab=True)
+    torch.cuda.synchronize()
+    assert int((out["info"] != 0).sum()) == 0
+    U = out["U"].cpu().numpy().reshape(bt, (N - 1) * m)
+    X = out["X"].cpu().numpy().reshape(bt, N, n)
+    Ab = out["Ab"].cpu().numpy().reshape(bt, (N - 1) * m, N * n)
+    bb = out["bb"].cpu().numpy().reshape(bt, N * n)
+    for b in range(bt):
+        o = LO.ls_solve(A, B, Q, R, Qf, X0[b], N, hu=hu)
+        assert np.linalg.cond(o["H"]) <= 1e6
+        assert np.abs(U[b] - o["U"].ravel()).max() <= 1e-9 * np.abs(o["U"]).max()
+        assert np.abs(X[b] - o["X"]).max() <= 1e-9 * np.abs(o["X"]).max()
+        Abar = Ab[b].T
+        Hu = np.kron(np.eye(N - 1), {0: np.zeros((m, m)), 1: np.linalg.cholesky(R).T, 2: R}[hu])
+        res = Abar.T @ (Abar @ U[b] + bb[b]) + Hu @ U[b]
+        scale = np.abs(Abar.T @ Abar).max() * np.abs(U[b]).max()
+        assert np.abs(res).max() <= 1e-12 * max(1.0, scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,m,N,bt", [(4, 1, 193, 3), (2, 2, 98, 5), (3, 2, 150, 2), (2, 1, 400, 2)])
+def test_ls_gpu_big_path_parity(lqrx, gpu_ok, n, m, N, bt):
+    """Problems past the LDS-resident kernel (Nm > 192 or H > LDS): global H, blocked factor."""
+    from lqrx import ls
+    from lqrx.dp import LQRBatch
+
+    rng = np.random.default_rng(3 * n + m + N)
+    A, B, Q, R, Qf, x0 = _batch(rng, n, m, bt)
+    out = ls.ls_solve_batch(LQRBatch(A, B, Q, R, Qf, x0, N), hu_mode=2)
+    assert out["rc"] == 0 and (out["info"] == 0).all()
+    for b in range(bt):
+        o = LO.ls_solve(A[b], B[b], Q[b], R[b], Qf[b], x0[b], N, hu=2)
+        cond = np.linalg.cond(o["H"])
+        tol = 1e-9 if cond <= 1e6 else 1e-15 * cond * 10
+        assert np.abs(out["U"][b] - o["U"]).max() <= tol * np.abs(o["U"]).max(), cond
+        assert np.abs(out["X"][b] - o["X"]).max() <= tol * np.abs(o["X"]).max(), cond
+
+
+@pytest.mark.gpu
+def test_ls_gpu_big_path_info(lqrx, gpu_ok):
+    from lqrx import ls
+    from lqrx.dp import LQRBatch
+
+    rng = np.random.default_rng(9)
+    n, m, N, bt = 3, 2, 120, 4
+    A, B, Q, R, Qf, x0 = _batch(rng, n, m, bt)
+    Q[1] = -np.eye(n)
+    B[2] = 0.0
+    out = ls.ls_solve_batch(LQRBatch(A, B, Q, R, Qf, x0, N), hu_mode=ls.HU_ZERO)
+    assert out["rc"] == 1 and out["info"][1] == -1 and out["info"][2] == 1
+    assert out["info"][0] == 0 and out["info"][3] == 0
+    for b in (1, 2):
+        assert np.isnan(out["U"][b]).all() and np.isnan(out["X"][b]).all()
