@@ -80,13 +80,20 @@ def cpu_baseline(n, m, N, target_s=12.0, threads=None):
                        f"{threads} threads, {dt:.1f} s")
 
 
-def cpu_baseline_kkt(N, target_s=12.0, threads=None):
-    """CPU oracle (C restatement of cholesky_solver.jl _solve!) on a bounded Dubins sample."""
+def kkt_structure(name, N):
+    """The KKT block structure of the kkt workload: the Dubins car of BASELINE configs[2], or
+    the reference's own known-answer structure DoubleIntegrator(3, N) (test/problems.jl:14-56)."""
+    import lqrx.kkt as K
+    return K.dubins_structure(N) if name == "dubins" else K.double_integrator_structure(3, N)
+
+
+def cpu_baseline_kkt(N, target_s=12.0, threads=None, structure="dubins"):
+    """CPU oracle (C restatement of cholesky_solver.jl _solve!) on a bounded sample."""
     import lqrx.kkt as K
     from oracle import oracle as orc
 
     threads = threads or max(1, min(16, os.cpu_count() or 1))
-    st = K.dubins_structure(N)
+    st = kkt_structure(structure, N)
     os_ = orc.KktStructure(st.n, st.m, st.N, st.p)
     probe = 256
     pb = K.random_kkt(st, probe, seed=1, h_mode=K.H_DIAG)
@@ -188,6 +195,11 @@ def main():
     ap.add_argument("--no-gather", action="store_true",
                     help="skip the final info + P_1 gather to rank 0 (N > 1)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--kkt-structure", choices=["dubins", "di"], default="dubins",
+                    help="kkt workload: Dubins (configs[2]) or DoubleIntegrator(3,N) (test/problems.jl)")
+    ap.add_argument("--sqp-model", choices=["dubins", "cartpole"], default="dubins",
+                    help="sqp workload: Dubins car (test/dubins_sqp.jl, mu 10, N 101) or the swing-up "
+                         "Cartpole() of test/problems.jl:58-88 (mu 1, N 101, tf 5)")
     ap.add_argument("--workload", choices=["dp", "cartpole", "kkt", "sqp", "ls"], default="dp",
                     help="dp = random dense LQR (BASELINE configs[3], the headline); "
                          "cartpole = configs[1] (n=4 m=1 N=101 B=4096); "
@@ -203,6 +215,10 @@ def main():
             args.batch = 4096
     if args.workload in ("kkt", "sqp"):
         args.n, args.m = 3, 2                       # Dubins car (test/dubins.jl)
+        if args.workload == "sqp" and args.sqp_model == "cartpole":
+            args.n, args.m = 4, 1
+        if args.workload == "kkt" and args.kkt_structure == "di":
+            args.n, args.m = 6, 3                   # DoubleIntegrator(3) (test/problems.jl)
         if args.batch == 65536:
             args.batch = 16384
         if args.N == 256:
@@ -273,22 +289,26 @@ def main():
             lqrx.dp_solve_device(t, N, p_mode=0, stream=sh, out=out)
     elif args.workload == "sqp":
         import lqrx.sqp as Q
-        dt_, x0_, xf_, Z0_ = Q.random_dubins_batch(N, bt, seed=args.seed + rank)
-        sqp_prob = Q.DubinsSQP(N, dt_, mu=10.0)
+        if args.sqp_model == "cartpole":
+            sqp_prob = Q.CartpoleSQP(N, mu=1.0)
+            x0_, xf_, Z0_ = Q.random_cartpole_batch(sqp_prob, bt, seed=args.seed + rank)
+        else:
+            dt_, x0_, xf_, Z0_ = Q.random_dubins_batch(N, bt, seed=args.seed + rank)
+            sqp_prob = Q.DubinsSQP(N, dt_, mu=10.0)
         z0 = torch.from_numpy(Z0_.ravel()).to(dev)
         t = dict(Z=z0.clone(), x0=torch.from_numpy(x0_.ravel()).to(dev),
                  xf=torch.from_numpy(xf_.ravel()).to(dev),
-                 lam=torch.empty(bt * Q.num_multipliers(N), dtype=torch.float64, device=dev),
+                 lam=torch.empty(bt * Q.num_multipliers(N, sqp_prob.model), dtype=torch.float64, device=dev),
                  iters=torch.empty(bt, dtype=torch.int32, device=dev),
                  status=torch.empty(bt, dtype=torch.int32, device=dev))
         out = {"info": t["status"]}
 
         def step():
             t["Z"].copy_(z0)                                  # same problem every step
-            Q.dubins_sqp_solve_device(sqp_prob, t, stream=sh)
+            Q.sqp_solve_device(sqp_prob, t, stream=sh)
     else:
         import lqrx.kkt as K
-        st = K.dubins_structure(N)
+        st = kkt_structure(args.kkt_structure, N)
         pb = K.random_kkt(st, bt, seed=args.seed + rank, h_mode=K.H_DIAG)
         t = {k: torch.from_numpy(getattr(pb, k).ravel()).to(dev) for k in ("Y", "y", "H", "g")}
         t["batch"] = bt
@@ -345,7 +365,7 @@ def main():
         if args.workload == "sqp":
             import lqrx.kkt as K
             import lqrx.sqp as Q
-            sY, sy, sH, sg = K.dubins_structure(N).sizes(K.H_DIAG)
+            sY, sy, sH, sg = K.trajectory_structure(n, m, N).sizes(K.H_DIAG)
             it_max = int(t["iters"].max().item()) + 1                # loop passes (last = check only)
             # algorithmic bytes per trajectory and loop pass: assembly (z, λ in; Y, y, H, g out),
             # Newton KKT (41 KB class), SOC KKT (Y, y in; δẑ, λ out), line search (z, δz, g, δẑ, λ)
@@ -358,20 +378,31 @@ def main():
                     "frac": achieved / PEAK_HBM_GBS, "traffic": None,
                     "kernel": "whole SQP step (assembly + 2 KKT + line search per pass)",
                     "kernel_ms": kern_ms, "alg_bytes_per_traj": alg_bytes / bt, "loop_passes": it_max}
-            metric = f"Dubins SQP solves/sec (n=3 m=2 N={N}, <=10 steps, L1-merit line search + SOC)"
-            workload = "Dubins SQP around the KKT solve (SURVEY.md 8(f) ranks 2-3)"
+            mname = "Cartpole swing-up" if args.sqp_model == "cartpole" else "Dubins"
+            metric = f"{mname} SQP solves/sec (n={n} m={m} N={N}, <=10 steps, L1-merit line search + SOC)"
+            workload = f"{mname} SQP around the KKT solve (SURVEY.md 8(f) ranks 2-3)"
             cpu = None
             if not args.no_cpu_baseline and world == 1:
                 sys.path.insert(0, ROOT)
+                import numpy as np
                 from oracle import sqp_oracle as S
+                model = S.CARTPOLE if args.sqp_model == "cartpole" else S.DUBINS
                 nb = 4
                 t0c = time.perf_counter()
-                for b in range(nb):
-                    S.solve(S.DubinsSQP(N, dt_, sqp_prob.Q, sqp_prob.R, sqp_prob.Qf, x0_[b], xf_[b], mu=10.0), Z0_[b])
+                refs = [S.solve(S.TrajSQP(N, sqp_prob.dt, sqp_prob.Q, sqp_prob.R, sqp_prob.Qf, x0_[b], xf_[b],
+                                          mu=sqp_prob.mu, model=model), Z0_[b]) for b in range(nb)]
                 el = time.perf_counter() - t0c
                 cpu = {"value": nb / el, "unit": "trajectories/s", "cores": 1, "kind": "port",
                        "sample": f"{nb} trajectories, oracle/sqp_oracle.py (numpy dense KKT restatement of "
                                  f"test/dubins_sqp.jl), {el:.1f} s"}
+                # the same trajectories of the last GPU step against the oracle (status, steps,
+                # iterate within 1e-8 relative)
+                zg = t["Z"].view(bt, -1)[:nb].cpu().numpy()
+                sg_, ig_ = t["status"][:nb].cpu().numpy(), t["iters"][:nb].cpu().numpy()
+                errs = [float(np.abs(zg[b] - r["z"]).max() / np.abs(r["z"]).max()) for b, r in enumerate(refs)]
+                ok = all(sg_[b] == r["status"] and ig_[b] == r["iters"] for b, r in enumerate(refs))
+                sampled = {"n": nb, "max_rel_err_z": max(errs), "tol": 1e-8,
+                           "status_iters_equal": bool(ok), "pass": bool(ok and max(errs) <= 1e-8)}
         elif args.workload == "ls":
             Nm, Nn = (N - 1) * m, N * n
             # reference op count (least_squares.jl:171-182): ĀᵀĀ as a dense gemm, Āᵀb̄, potrf, potrs
@@ -397,24 +428,29 @@ def main():
                                  f"least_squares.jl solve!, OpenBLAS), {el:.1f} s"}
         elif args.workload == "kkt":
             import lqrx.kkt as K
-            sY, sy, sH, sg = K.dubins_structure(N).sizes(K.H_DIAG)
+            sY, sy, sH, sg = st.sizes(K.H_DIAG)
             alg_bytes = (sY + sy + sH + sg + sg + sy) * 8 * bt     # inputs + dz + λ
             achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
             traffic = None
+            key = f"kkt_{args.kkt_structure}_N{N}_B{bt}_f64"
             if os.path.exists(args.traffic_json):
                 try:
-                    traffic = json.load(open(args.traffic_json)).get(
-                        f"kkt_dubins_N{N}_B{bt}_f64", {}).get("hbm_bytes_per_launch")
+                    traffic = json.load(open(args.traffic_json)).get(key, {}).get("hbm_bytes_per_launch")
                 except Exception:
                     traffic = None
+            fil = args.kkt_structure == "dubins" and N >= 4
             roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
-                    "kernel": "kkt_fil_kernel" if N >= 4 else "kkt_staged_kernel",
+                    "kernel": "kkt_fil_kernel" if fil else "kkt_staged_kernel",
                     "kernel_ms": kern_ms,
                     "alg_bytes_per_traj": alg_bytes / bt}
-            metric = "KKT solves/sec (Dubins n=3 m=2 N=101 block-tridiagonal _solve!)"
-            workload = "Dubins constrained KKT inner solve (BASELINE.json configs[2])"
-            cpu = cpu_baseline_kkt(N, target_s=args.cpu_seconds) \
+            if args.kkt_structure == "dubins":
+                metric = "KKT solves/sec (Dubins n=3 m=2 N=101 block-tridiagonal _solve!)"
+                workload = "Dubins constrained KKT inner solve (BASELINE.json configs[2])"
+            else:
+                metric = f"KKT solves/sec (DoubleIntegrator(3,{N}) n=6 m=3 block-tridiagonal _solve!)"
+                workload = "DoubleIntegrator KKT structure of test/cholesky_solve.jl (non-baseline)"
+            cpu = cpu_baseline_kkt(N, target_s=args.cpu_seconds, structure=args.kkt_structure) \
                 if not args.no_cpu_baseline and world == 1 else None
         else:
             flops = dp_flops_per_traj(n, m, N) * bt

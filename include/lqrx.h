@@ -154,32 +154,63 @@ int lqrx_kkt_sizes(const lqrx_kkt_desc *desc, int64_t *nY, int64_t *ny, int64_t 
                    int64_t *ng, int64_t *nlam);
 
 /* ------------------------------------------------------------------------------------
- * Batched Dubins-car SQP around the KKT path: per trajectory,
- * the outer loop of CholeskySolver.solve!/step! (/root/reference/src/cholesky_solver.jl:
- * 109-153) with the KKT inputs assembled on the device (update!, :155-164: RK3 Dubins
- * Jacobians, diagonal LQRObjective expansion), _solve! (:166-182), and the L1-merit
- * backtracking line search with second-order correction of test/dubins_sqp.jl:58-97
+ * Batched trajectory-optimisation SQP around the KKT path: per
+ * trajectory, the outer loop of CholeskySolver.solve!/step! (/root/reference/src/
+ * cholesky_solver.jl:109-153) with the KKT inputs assembled on the device (update!, :155-164:
+ * RK3 dynamics Jacobians, diagonal LQRObjective expansion), _solve! (:166-182), and the
+ * L1-merit backtracking line search with second-order correction of test/dubins_sqp.jl:58-97
  * (SOC = second_order_correction!, cholesky_solver.jl:254-273).
  *
- * Model: RobotZoo.DubinsCar ẋ = [v cosθ, v sinθ, ω], RK3 (RobotDynamics) with step dt.
+ * Models (continuous dynamics, integrated with RobotDynamics' RK3 at step dt; Jacobians by
+ * forward-mode dual numbers on the device, as ForwardDiff does in the reference):
+ *   LQRX_MODEL_DUBINS   nx 3, nu 2: RobotZoo.DubinsCar ẋ = [v cosθ, v sinθ, ω]
+ *                       (test/dubins_sqp.jl); params unused
+ *   LQRX_MODEL_CARTPOLE nx 4, nu 1: RobotZoo.Cartpole, x = [x, θ, ẋ, θ̇],
+ *                       params = {mc, mp, l, g} (RobotZoo defaults 1, 0.2, 0.5, 9.81;
+ *                       test/problems.jl:58-88 Cartpole())
  * Problem: min Σ_{k<N} ½(x_k−xf)ᵀQ(x_k−xf) + ½u_kᵀRu_k + ½(x_N−xf)ᵀQf(x_N−xf)
  *          s.t. x_1 = x0, x_{k+1} = rk3(x_k, u_k), x_N = xf      (Q, R, Qf diagonal)
- * Buffers (device; layout 0, batch slowest):
- *   Z      (5N−2)·batch in/out: z = [x_1; u_1; …; x_{N−1}; u_{N−1}; x_N] (the KKT δz order)
- *   x0, xf 3·batch
- *   lam    3(N+1)·batch out: multipliers of the last accepted Newton step (KKT λ order)
+ * Buffers (device; layout 0, batch slowest), nx / nu of the model:
+ *   Z      (N·nx + (N−1)·nu)·batch in/out: z = [x_1; u_1; …; x_{N−1}; u_{N−1}; x_N]
+ *          (the KKT δz order)
+ *   x0, xf nx·batch
+ *   lam    nx(N+1)·batch out: multipliers of the last accepted Newton step (KKT λ order)
  *   iters  int32·batch out: accepted steps
  *   status int32·batch out: 0 converged (‖c‖∞ < tol_p and ‖∇f+∇cᵀλ‖₂ < tol_d before a
  *          step), 1 max_iters reached, 2 line search failed (iterate left unchanged)
  * ------------------------------------------------------------------------------------ */
-typedef struct lqrx_dubins_sqp_desc {
+enum { LQRX_MODEL_DUBINS = 0, LQRX_MODEL_CARTPOLE = 1 };
+
+typedef struct lqrx_sqp_desc {
+    int32_t model;          /* LQRX_MODEL_*                                            */
     int32_t N;              /* knots (>= 2)                                            */
     int32_t max_iters;      /* CholeskySolver.solve!: 10                               */
+    int32_t reserved;       /* 0                                                       */
     int64_t batch;
     double dt;              /* tf / (N−1)                                              */
-    double Q[3], R[2], Qf[3]; /* diagonal cost weights (> 0), shared by the batch       */
+    double Q[8], R[8], Qf[8]; /* diagonal cost weights (> 0), first nx / nu used         */
+    double params[4];       /* model parameters (see above)                            */
     double mu;              /* L1 merit weight (dubins_sqp.jl:59 uses 1)               */
     double tol_p, tol_d;    /* 1e-5, 1e-5 (cholesky_solver.jl:131-132)                 */
+} lqrx_sqp_desc;
+
+/* state / control dimension of a model; -1 for an unknown model */
+int lqrx_sqp_model_dims(int32_t model, int32_t *nx, int32_t *nu);
+int lqrx_sqp_solve(const lqrx_sqp_desc *desc, double *Z, const double *x0, const double *xf,
+                   double *lam, int32_t *iters, int32_t *status, void *stream);
+int lqrx_sqp_solve_host(const lqrx_sqp_desc *desc, double *Z, const double *x0, const double *xf,
+                        double *lam, int32_t *iters, int32_t *status);
+
+/* The round-1 Dubins-only entry points (model fixed to LQRX_MODEL_DUBINS); they forward to
+ * lqrx_sqp_solve[_host]. */
+typedef struct lqrx_dubins_sqp_desc {
+    int32_t N;
+    int32_t max_iters;
+    int64_t batch;
+    double dt;
+    double Q[3], R[2], Qf[3];
+    double mu;
+    double tol_p, tol_d;
 } lqrx_dubins_sqp_desc;
 
 int lqrx_dubins_sqp_solve(const lqrx_dubins_sqp_desc *desc, double *Z, const double *x0,

@@ -143,6 +143,25 @@ int main()
     lqrx_dubins_sqp_desc q{};
     q.N = 1; q.max_iters = 10; q.batch = 1; q.dt = 0.1;
     CHECK(lqrx_dubins_sqp_solve(&q, dummy, dummy, dummy, dummy, info, info, nullptr) < 0);
+    lqrx_sqp_desc g{};
+    g.model = LQRX_MODEL_CARTPOLE; g.N = 21; g.max_iters = 10; g.batch = 2; g.dt = 0.25; g.mu = 1.0;
+    for (int i = 0; i < 4; ++i) g.Q[i] = 0.01, g.Qf[i] = 100.0;
+    g.R[0] = 0.1;
+    g.params[0] = 1.0; g.params[1] = 0.2; g.params[2] = 0.5; g.params[3] = 9.81;
+    lqrx_sqp_desc gb = g; gb.model = 5;
+    CHECK(lqrx_sqp_solve(&gb, dummy, dummy, dummy, dummy, info, info, nullptr) == -1);
+    gb = g; gb.params[2] = 0.0;
+    CHECK(lqrx_sqp_solve(&gb, dummy, dummy, dummy, dummy, info, info, nullptr) == -1);
+    gb = g; gb.R[0] = 0.0;
+    CHECK(lqrx_sqp_solve_host(&gb, dummy, dummy, dummy, dummy, info, info) == -1);
+    CHECK(lqrx_sqp_solve(&g, nullptr, dummy, dummy, dummy, info, info, nullptr) == -2);
+    int32_t nx = 0, nu = 0;
+    CHECK(lqrx_sqp_model_dims(LQRX_MODEL_CARTPOLE, &nx, &nu) == 0 && nx == 4 && nu == 1);
+    CHECK(lqrx_sqp_model_dims(-1, &nx, &nu) == -1);
+    if (!have_gpu) {
+        std::vector<double> Zh(2 * (21 * 4 + 20)), x0h(8), lamh(2 * 22 * 4);
+        CHECK(lqrx_sqp_solve_host(&g, Zh.data(), x0h.data(), x0h.data(), lamh.data(), info, info) <= LQRX_ERR_HIP + 0);
+    }
 
     std::printf("api sanitizer run: %s (%d failed checks, device %d)\n", fails ? "FAILED" : "ok", fails, have_gpu);
     return fails ? 1 : 0;

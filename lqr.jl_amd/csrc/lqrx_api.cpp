@@ -624,22 +624,39 @@ int lqrx_make_random_dp(int32_t n, int32_t m, int64_t batch, int64_t traj0, uint
 
 } // extern "C"
 
-// ------------------------------------------------------------------ batched Dubins SQP
+// ------------------------------------------------------------------ batched trajectory SQP
 namespace {
-int validate_sqp(const lqrx_dubins_sqp_desc *d)
+int validate_sqp(const lqrx_sqp_desc *d, int *nx, int *nu)
 {
     if (!d) return set_err(-1, "desc is NULL");
+    if (!lqrx::sqp_model_dims(d->model, nx, nu)) return set_err(-1, "desc.model %d is not a known model", d->model);
     if (d->N < 2) return set_err(-1, "desc.N must be >= 2 (got %d)", d->N);
     if (d->batch < 0) return set_err(-1, "desc.batch must be >= 0");
     if (d->max_iters < 0) return set_err(-1, "desc.max_iters must be >= 0");
+    if (d->reserved != 0) return set_err(-1, "desc.reserved must be 0");
     if (!(d->dt > 0)) return set_err(-1, "desc.dt must be > 0");
-    for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < *nx; ++i)
         if (!(d->Q[i] > 0) || !(d->Qf[i] > 0)) return set_err(-1, "desc.Q / desc.Qf must be positive");
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < *nu; ++i)
         if (!(d->R[i] > 0)) return set_err(-1, "desc.R must be positive");
+    if (d->model == LQRX_MODEL_CARTPOLE)
+        for (int i = 0; i < 4; ++i)
+            if (!(d->params[i] > 0) || !std::isfinite(d->params[i]))
+                return set_err(-1, "desc.params (mc, mp, l, g) must be positive and finite");
     if (!(d->mu >= 0) || !(d->tol_p >= 0) || !(d->tol_d >= 0))
         return set_err(-1, "desc.mu / tol_p / tol_d must be >= 0");
     return 0;
+}
+
+lqrx_sqp_desc from_dubins(const lqrx_dubins_sqp_desc *d)
+{
+    lqrx_sqp_desc q{};
+    q.model = LQRX_MODEL_DUBINS;
+    q.N = d->N; q.max_iters = d->max_iters; q.batch = d->batch; q.dt = d->dt;
+    for (int i = 0; i < 3; ++i) q.Q[i] = d->Q[i], q.Qf[i] = d->Qf[i];
+    for (int i = 0; i < 2; ++i) q.R[i] = d->R[i];
+    q.mu = d->mu; q.tol_p = d->tol_p; q.tol_d = d->tol_d;
+    return q;
 }
 
 struct SqpKkt {
@@ -662,10 +679,20 @@ int sqp_kkt(void *ctx, int ginv, double *dz)
 }
 } // namespace
 
-extern "C" int lqrx_dubins_sqp_solve(const lqrx_dubins_sqp_desc *d, double *Z, const double *x0, const double *xf,
-                                     double *lam, int32_t *iters, int32_t *status, void *stream)
+extern "C" int lqrx_sqp_model_dims(int32_t model, int32_t *nx, int32_t *nu)
 {
-    int st = validate_sqp(d);
+    int a = 0, b = 0;
+    if (!lqrx::sqp_model_dims(model, &a, &b)) return set_err(-1, "model %d is not a known model", model);
+    if (nx) *nx = a;
+    if (nu) *nu = b;
+    return 0;
+}
+
+extern "C" int lqrx_sqp_solve(const lqrx_sqp_desc *d, double *Z, const double *x0, const double *xf, double *lam,
+                              int32_t *iters, int32_t *status, void *stream)
+{
+    int nx = 0, nu = 0;
+    int st = validate_sqp(d, &nx, &nu);
     if (st) return st;
     if (d->batch == 0) return 0;
     if (!Z) return set_err(-2, "Z is NULL");
@@ -675,10 +702,10 @@ extern "C" int lqrx_dubins_sqp_solve(const lqrx_dubins_sqp_desc *d, double *Z, c
     if (!iters) return set_err(-6, "iters is NULL");
     if (!status) return set_err(-7, "status is NULL");
     const int N = d->N;
-    const int64_t B = d->batch, NN = (int64_t)N * 3 + (int64_t)(N - 1) * 2, P = (int64_t)(N + 1) * 3;
+    const int64_t B = d->batch, NN = (int64_t)N * nx + (int64_t)(N - 1) * nu, P = (int64_t)(N + 1) * nx;
     hipStream_t s = (hipStream_t)stream;
     SqpKkt c{};
-    lqrx::sqp_structure(N, c.n1, c.p, c.n2, c.w);
+    lqrx::sqp_structure(nx, nu, N, c.n1, c.p, c.n2, c.w);
     c.kd.N = N; c.kd.dtype = LQRX_F64; c.kd.batch = B;
     c.kd.n1 = c.n1.data(); c.kd.p = c.p.data(); c.kd.n2 = c.n2.data(); c.kd.w = c.w.data();
     c.kd.h_mode = 2; c.kd.ginv = 1; c.kd.layout = 0;
@@ -700,9 +727,9 @@ extern "C" int lqrx_dubins_sqp_solve(const lqrx_dubins_sqp_desc *d, double *Z, c
     if (e != hipSuccess) return hip_err(e, "sqp scratch");
     char *b = (char *)blk;
     lqrx::SqpArgs A{};
-    A.N = N; A.B = B; A.dt = d->dt; A.mu = d->mu; A.tol_p = d->tol_p; A.tol_d = d->tol_d;
-    for (int i = 0; i < 3; ++i) A.Q[i] = d->Q[i], A.Qf[i] = d->Qf[i];
-    for (int i = 0; i < 2; ++i) A.R[i] = d->R[i];
+    A.model = d->model; A.N = N; A.B = B; A.dt = d->dt; A.mu = d->mu; A.tol_p = d->tol_p; A.tol_d = d->tol_d;
+    for (int i = 0; i < 8; ++i) A.Q[i] = d->Q[i], A.Qf[i] = d->Qf[i], A.R[i] = d->R[i];
+    for (int i = 0; i < 4; ++i) A.par[i] = d->params[i];
     A.x0 = x0; A.xf = xf; A.Z = Z; A.lam = lam; A.iters = iters; A.status = status;
     A.Y = (double *)(b + oY); A.y = (double *)(b + oy); A.H = (double *)(b + oH); A.g = (double *)(b + og);
     A.dz = (double *)(b + odz); A.lamn = (double *)(b + olamn); A.dzs = (double *)(b + odzs);
@@ -720,26 +747,27 @@ extern "C" int lqrx_dubins_sqp_solve(const lqrx_dubins_sqp_desc *d, double *Z, c
     return 0;
 }
 
-extern "C" int lqrx_dubins_sqp_solve_host(const lqrx_dubins_sqp_desc *d, double *Z, const double *x0,
-                                          const double *xf, double *lam, int32_t *iters, int32_t *status)
+extern "C" int lqrx_sqp_solve_host(const lqrx_sqp_desc *d, double *Z, const double *x0, const double *xf,
+                                   double *lam, int32_t *iters, int32_t *status)
 {
-    int st = validate_sqp(d);
+    int nx = 0, nu = 0;
+    int st = validate_sqp(d, &nx, &nu);
     if (st) return st;
     if (d->batch == 0) return 0;
     if (!Z || !x0 || !xf || !lam || !iters || !status) return set_err(-2, "NULL host pointer");
-    const int64_t B = d->batch, NN = (int64_t)d->N * 3 + (int64_t)(d->N - 1) * 2, P = (int64_t)(d->N + 1) * 3;
+    const int64_t B = d->batch, NN = (int64_t)d->N * nx + (int64_t)(d->N - 1) * nu, P = (int64_t)(d->N + 1) * nx;
     DevBuf dZ, dx0, dxf, dlam, dit, dst;
-    if ((st = dev_alloc(dZ, B * NN * 8, "Z")) || (st = dev_alloc(dx0, B * 24, "x0")) ||
-        (st = dev_alloc(dxf, B * 24, "xf")) || (st = dev_alloc(dlam, B * P * 8, "lam")) ||
+    if ((st = dev_alloc(dZ, B * NN * 8, "Z")) || (st = dev_alloc(dx0, B * nx * 8, "x0")) ||
+        (st = dev_alloc(dxf, B * nx * 8, "xf")) || (st = dev_alloc(dlam, B * P * 8, "lam")) ||
         (st = dev_alloc(dit, B * 4, "iters")) || (st = dev_alloc(dst, B * 4, "status")))
         return st;
     hipError_t e;
     if ((e = hipMemcpy(dZ.p, Z, B * NN * 8, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(dx0.p, x0, B * 24, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(dxf.p, xf, B * 24, hipMemcpyHostToDevice)) != hipSuccess)
+        (e = hipMemcpy(dx0.p, x0, B * nx * 8, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(dxf.p, xf, B * nx * 8, hipMemcpyHostToDevice)) != hipSuccess)
         return hip_err(e, "sqp H2D");
-    if ((st = lqrx_dubins_sqp_solve(d, (double *)dZ.p, (const double *)dx0.p, (const double *)dxf.p,
-                                    (double *)dlam.p, (int32_t *)dit.p, (int32_t *)dst.p, nullptr)))
+    if ((st = lqrx_sqp_solve(d, (double *)dZ.p, (const double *)dx0.p, (const double *)dxf.p, (double *)dlam.p,
+                             (int32_t *)dit.p, (int32_t *)dst.p, nullptr)))
         return st;
     if ((e = hipMemcpy(Z, dZ.p, B * NN * 8, hipMemcpyDeviceToHost)) != hipSuccess ||
         (e = hipMemcpy(lam, dlam.p, B * P * 8, hipMemcpyDeviceToHost)) != hipSuccess ||
@@ -747,6 +775,22 @@ extern "C" int lqrx_dubins_sqp_solve_host(const lqrx_dubins_sqp_desc *d, double 
         (e = hipMemcpy(status, dst.p, B * 4, hipMemcpyDeviceToHost)) != hipSuccess)
         return hip_err(e, "sqp D2H");
     return 0;
+}
+
+extern "C" int lqrx_dubins_sqp_solve(const lqrx_dubins_sqp_desc *d, double *Z, const double *x0, const double *xf,
+                                     double *lam, int32_t *iters, int32_t *status, void *stream)
+{
+    if (!d) return set_err(-1, "desc is NULL");
+    const lqrx_sqp_desc q = from_dubins(d);
+    return lqrx_sqp_solve(&q, Z, x0, xf, lam, iters, status, stream);
+}
+
+extern "C" int lqrx_dubins_sqp_solve_host(const lqrx_dubins_sqp_desc *d, double *Z, const double *x0,
+                                          const double *xf, double *lam, int32_t *iters, int32_t *status)
+{
+    if (!d) return set_err(-1, "desc is NULL");
+    const lqrx_sqp_desc q = from_dubins(d);
+    return lqrx_sqp_solve_host(&q, Z, x0, xf, lam, iters, status);
 }
 
 

@@ -79,13 +79,15 @@ bool kkt_fil_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const
 bool kkt_fil_scratch_bytes(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
                            const int32_t *w, size_t *bytes);
 
-// ---- batched Dubins SQP (lqrx_sqp.hip) ----
+// ---- batched trajectory SQP (lqrx_sqp.hip) ----
+enum { SQP_DUBINS = 0, SQP_CARTPOLE = 1 };   // = LQRX_MODEL_*
 struct SqpArgs {
-    int N;
+    int model, N;
     int64_t B;
     double dt, mu, tol_p, tol_d;
-    double Q[3], R[2], Qf[3];
-    const double *x0, *xf;            // B×3
+    double Q[8], R[8], Qf[8];         // diagonal weights, first NX / NU used
+    double par[4];                    // model parameters (cartpole: mc, mp, l, g)
+    const double *x0, *xf;            // B×NX
     double *Z;                        // B×NN, in/out
     double *lam;                      // B×P: multipliers of the last accepted Newton step
     int32_t *iters, *status;          // B
@@ -97,8 +99,9 @@ struct SqpArgs {
 };
 hipError_t sqp_run(const SqpArgs &A, int max_iters, hipStream_t s, int (*kkt)(void *ctx, int ginv, double *dz),
                    void *ctx, int *kkt_rc);
-void sqp_structure(int N, std::vector<int32_t> &n1, std::vector<int32_t> &p, std::vector<int32_t> &n2,
-                   std::vector<int32_t> &w);
+void sqp_structure(int nx, int nu, int N, std::vector<int32_t> &n1, std::vector<int32_t> &p,
+                   std::vector<int32_t> &n2, std::vector<int32_t> &w);
+bool sqp_model_dims(int model, int *nx, int *nu);
 
 // ---- condensed least-squares LQR (lqrx_ls.hip) ----
 struct LsArgs {

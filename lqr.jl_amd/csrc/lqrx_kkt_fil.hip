@@ -1102,8 +1102,14 @@ hipError_t launch(const KktArgs &a, hipStream_t s)
     template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, true>>(const KktArgs, double *__restrict__);  \
     template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, false, true>>(const KktArgs, double *__restrict__); \
     template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, false>>(const KktArgs, double *__restrict__);
+// diagonal-H variants only (the dense-H staging ring of these shapes exceeds 160 KB of LDS)
+#define LQRX_FIL_INST_DIAG(NX, M, A0, AK, AN)                                                            \
+    template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, true>>(const KktArgs, double *__restrict__);  \
+    template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, false>>(const KktArgs, double *__restrict__);
 LQRX_FIL_INST(3, 2, 3, 0, 3)
+LQRX_FIL_INST_DIAG(4, 1, 4, 0, 4)
 #undef LQRX_FIL_INST
+#undef LQRX_FIL_INST_DIAG
 
 } // namespace fil
 
@@ -1128,8 +1134,16 @@ static bool fil_dispatch(const KktArgs &a, const int32_t *n1, const int32_t *p, 
         else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{});                                           \
         return true;                                                                                     \
     }
-    LQRX_FIL(3, 2, 3, 0, 3)   // Dubins car (BASELINE cfg3), test/dubins.jl
+#define LQRX_FIL_DIAG(NX, M, A0, AK, AN)                                                                 \
+    if (nx == NX && m == M && P0 == A0 && PK == AK && PN == AN && (diag || !ginv)) {                     \
+        if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true>{});                                       \
+        else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{});                                           \
+        return true;                                                                                     \
+    }
+    LQRX_FIL(3, 2, 3, 0, 3)        // Dubins car (BASELINE cfg3), test/dubins.jl
+    LQRX_FIL_DIAG(4, 1, 4, 0, 4)   // cartpole trajectory problem (test/problems.jl:58-88, device SQP)
 #undef LQRX_FIL
+#undef LQRX_FIL_DIAG
     return false;
 }
 

@@ -1,11 +1,15 @@
-// lqrx_sqp.hip — batched Dubins-car SQP on the device (SURVEY.md §8(f) ranks 2–3).
+// lqrx_sqp.hip — batched trajectory-optimisation SQP on the device (SURVEY.md §8(f) ranks 2–3)
+// for the reference's test models: the Dubins car (test/dubins_sqp.jl, BASELINE cfg3) and the
+// cartpole (test/cartpole.jl, test/problems.jl:58-88).
 //
 // Around the block-tridiagonal KKT kernel this adds the two steps the reference runs on
 // either side of _solve! (cholesky_solver.jl:166-182):
 //   before — KKT input assembly (CholeskySolver.update!, cholesky_solver.jl:155-164, which
 //            calls TrajOptCore): constraint Jacobian blocks Y_k = [D2; C; D1] from the RK3
-//            Dubins dynamics (analytic chain rule), constraint values y_k, the diagonal cost
-//            Hessian H_k and gradient g_k of the LQRObjective;
+//            model dynamics (forward-mode dual numbers through the three RK3 stages, as
+//            ForwardDiff differentiates RobotDynamics.discrete_dynamics in the reference),
+//            constraint values y_k, the diagonal cost Hessian H_k and gradient g_k of the
+//            LQRObjective;
 //   after  — the L1-merit backtracking line search with a second-order correction
 //            (test/dubins_sqp.jl:58-97; the SOC step −Dᵀ(DDᵀ)⁻¹c(z+dz) is the ginv = 0 KKT
 //            variant, second_order_correction!, cholesky_solver.jl:254-273), inside the outer
@@ -26,81 +30,157 @@
 namespace lqrx {
 namespace sqp {
 
-constexpr int NX = 3, NU = 2, W = NX + NU;
 constexpr double ETA = 1e-4, RHO = 0.5;   // dubins_sqp.jl:76-77
 constexpr int LS_TRIES = 10;              // :78
 enum : int32_t { ACTIVE = -1, CONVERGED = 0, LIMIT = 1, LS_FAILED = 2 };
 
 using Args = SqpArgs;
 
-__host__ __device__ constexpr int64_t nn(int N) { return (int64_t)N * NX + (int64_t)(N - 1) * NU; }
-__host__ __device__ constexpr int64_t np_(int N) { return (int64_t)(N + 1) * NX; }
-__host__ __device__ constexpr int64_t ny_(int N) { return 30 * (int64_t)(N - 1) + 18; }
-__device__ __forceinline__ int64_t oy(int k) { return k == 0 ? 0 : 3 * (int64_t)k + 3; }   // y / λ blocks
-__device__ __forceinline__ int64_t om(int k) { return k == 0 ? 0 : 3 * (int64_t)k; }       // [λ_{k-1}; μ_k; λ_k]
-
-// RobotZoo.DubinsCar: ẋ = [v cosθ, v sinθ, ω]
-__device__ __forceinline__ void dubins(const double x[NX], const double u[NU], double f[NX])
+// ---------------------------------------------------------------- forward-mode dual numbers
+// value + D directional derivatives (seeded with the unit vectors of [x u]): the dynamics are
+// written once, generic in the scalar, and their RK3 Jacobian falls out exactly (to rounding)
+template <int D> struct Dual {
+    double v, d[D];
+};
+template <int D> __device__ __forceinline__ Dual<D> operator+(const Dual<D> &a, const Dual<D> &b)
+{
+    Dual<D> r{a.v + b.v, {}};
+    for (int i = 0; i < D; ++i) r.d[i] = a.d[i] + b.d[i];
+    return r;
+}
+template <int D> __device__ __forceinline__ Dual<D> operator-(const Dual<D> &a, const Dual<D> &b)
+{
+    Dual<D> r{a.v - b.v, {}};
+    for (int i = 0; i < D; ++i) r.d[i] = a.d[i] - b.d[i];
+    return r;
+}
+template <int D> __device__ __forceinline__ Dual<D> operator-(const Dual<D> &a)
+{
+    Dual<D> r{-a.v, {}};
+    for (int i = 0; i < D; ++i) r.d[i] = -a.d[i];
+    return r;
+}
+template <int D> __device__ __forceinline__ Dual<D> operator*(const Dual<D> &a, const Dual<D> &b)
+{
+    Dual<D> r{a.v * b.v, {}};
+    for (int i = 0; i < D; ++i) r.d[i] = a.d[i] * b.v + a.v * b.d[i];
+    return r;
+}
+template <int D> __device__ __forceinline__ Dual<D> operator*(double a, const Dual<D> &b)
+{
+    Dual<D> r{a * b.v, {}};
+    for (int i = 0; i < D; ++i) r.d[i] = a * b.d[i];
+    return r;
+}
+template <int D> __device__ __forceinline__ Dual<D> operator/(const Dual<D> &a, const Dual<D> &b)
+{
+    const double q = a.v / b.v;
+    Dual<D> r{q, {}};
+    for (int i = 0; i < D; ++i) r.d[i] = (a.d[i] - q * b.d[i]) / b.v;
+    return r;
+}
+template <int D> __device__ __forceinline__ void dsincos(const Dual<D> &a, Dual<D> *sn, Dual<D> *cs)
 {
     double s, c;
-    sincos(x[2], &s, &c);
-    f[0] = u[0] * c;
-    f[1] = u[0] * s;
-    f[2] = u[1];
+    sincos(a.v, &s, &c);
+    sn->v = s;
+    cs->v = c;
+    for (int i = 0; i < D; ++i) sn->d[i] = c * a.d[i], cs->d[i] = -s * a.d[i];
 }
+__device__ __forceinline__ void dsincos(double a, double *sn, double *cs) { sincos(a, sn, cs); }
+// mixed Dual / double arithmetic the models use
+template <int D> __device__ __forceinline__ Dual<D> operator+(const Dual<D> &a, double b)
+{
+    Dual<D> r = a;
+    r.v += b;
+    return r;
+}
+template <int D> __device__ __forceinline__ Dual<D> operator-(double a, const Dual<D> &b) { return -(b + (-a)); }
+
+
+// ---------------------------------------------------------------- models (continuous dynamics)
+// RobotZoo.DubinsCar: ẋ = [v cosθ, v sinθ, ω]
+struct Dubins {
+    static constexpr int NX = 3, NU = 2;
+    template <class T> __device__ static void f(const T *x, const T *u, T *out, const double *)
+    {
+        T s, c;
+        dsincos(x[2], &s, &c);
+        out[0] = u[0] * c;
+        out[1] = u[0] * s;
+        out[2] = u[1];
+    }
+};
+// RobotZoo.Cartpole (test/problems.jl:58-88; SURVEY §8(c) constants mc, mp, l, g in par[0..3]):
+// q = [x, θ], q̈ = −H⁻¹(C q̇ + G − B u), H = [mc+mp, mp·l·cθ; mp·l·cθ, mp·l²],
+// C q̇ = [−mp·l·sθ·θ̇², 0], G = [0, mp·g·l·sθ], B = [1, 0]
+struct Cartpole {
+    static constexpr int NX = 4, NU = 1;
+    template <class T> __device__ static void f(const T *x, const T *u, T *out, const double *par)
+    {
+        const double mc = par[0], mp = par[1], l = par[2], g = par[3];
+        T s, c;
+        dsincos(x[1], &s, &c);
+        const T h01 = (mp * l) * c;
+        const T r0 = (mp * l) * (s * (x[3] * x[3])) + u[0];      // −(C q̇ + G − B u), row 0
+        const T r1 = -((mp * g * l) * s);                       //                    row 1
+        const T det = (mc + mp) * (mp * l * l) - h01 * h01;
+        out[0] = x[2];
+        out[1] = x[3];
+        out[2] = ((mp * l * l) * r0 - h01 * r1) / det;
+        out[3] = ((mc + mp) * r1 - h01 * r0) / det;
+    }
+};
 
 // RobotDynamics RK3: k1 = f(x)dt, k2 = f(x + k1/2)dt, k3 = f(x − k1 + 2k2)dt,
-// x⁺ = x + (k1 + 4k2 + k3)/6
-__device__ __forceinline__ void rk3(const double x[NX], const double u[NU], double dt, double xn[NX])
+// x⁺ = x + (k1 + 4k2 + k3)/6 — generic in the scalar type
+template <class M, class T>
+__device__ __forceinline__ void rk3_t(const T *x, const T *u, double dt, T *xn, const double *par)
 {
-    double k1[NX], k2[NX], k3[NX], t[NX];
-    dubins(x, u, k1);
-    for (int i = 0; i < NX; ++i) k1[i] *= dt, t[i] = x[i] + 0.5 * k1[i];
-    dubins(t, u, k2);
-    for (int i = 0; i < NX; ++i) k2[i] *= dt, t[i] = x[i] - k1[i] + 2.0 * k2[i];
-    dubins(t, u, k3);
-    for (int i = 0; i < NX; ++i) k3[i] *= dt, xn[i] = x[i] + (k1[i] + 4.0 * k2[i] + k3[i]) / 6.0;
+    constexpr int NX = M::NX;
+    T k1[NX], k2[NX], k3[NX], t[NX];
+    M::f(x, u, k1, par);
+    for (int i = 0; i < NX; ++i) k1[i] = dt * k1[i], t[i] = x[i] + 0.5 * k1[i];
+    M::f(t, u, k2, par);
+    for (int i = 0; i < NX; ++i) k2[i] = dt * k2[i], t[i] = (x[i] - k1[i]) + 2.0 * k2[i];
+    M::f(t, u, k3, par);
+    for (int i = 0; i < NX; ++i) k3[i] = dt * k3[i], xn[i] = x[i] + (1.0 / 6.0) * ((k1[i] + 4.0 * k2[i]) + k3[i]);
+}
+template <class M> __device__ __forceinline__ void rk3(const double *x, const double *u, double dt, double *xn, const double *par)
+{
+    rk3_t<M, double>(x, u, dt, xn, par);
+}
+// the same with J = ∂x⁺/∂[x u] (NX × (NX+NU)) by forward-mode duals
+template <class M>
+__device__ __forceinline__ void rk3_jac(const double *x, const double *u, double dt, double *xn, double (*J)[M::NX + M::NU],
+                                        const double *par)
+{
+    constexpr int NX = M::NX, NU = M::NU, W = NX + NU;
+    Dual<W> xd[NX], ud[NU], xo[NX];
+    for (int i = 0; i < NX; ++i) {
+        xd[i].v = x[i];
+        for (int j = 0; j < W; ++j) xd[i].d[j] = (i == j) ? 1.0 : 0.0;
+    }
+    for (int i = 0; i < NU; ++i) {
+        ud[i].v = u[i];
+        for (int j = 0; j < W; ++j) ud[i].d[j] = (NX + i == j) ? 1.0 : 0.0;
+    }
+    rk3_t<M, Dual<W>>(xd, ud, dt, xo, par);
+    for (int i = 0; i < NX; ++i) {
+        xn[i] = xo[i].v;
+        for (int j = 0; j < W; ++j) J[i][j] = xo[i].d[j];
+    }
 }
 
-// the same with J = ∂x⁺/∂[x u] (3×5) by the chain rule through the three stages.  The only
-// state dependence of f is through θ: ∂f/∂x = e_θᵀ ⊗ [−v sinθ, v cosθ, 0]ᵀ.
-__device__ __forceinline__ void rk3_jac(const double x[NX], const double u[NU], double dt, double xn[NX],
-                                        double J[NX][W])
-{
-    double k[3][NX], Jk[3][NX][W], t[NX], Jt[NX][W];
-    for (int st = 0; st < 3; ++st) {
-        // stage input t = x (+ combination of previous stages) and its Jacobian Jt
-        for (int i = 0; i < NX; ++i) {
-            double v = x[i];
-            if (st == 1) v += 0.5 * k[0][i];
-            if (st == 2) v += -k[0][i] + 2.0 * k[1][i];
-            t[i] = v;
-            for (int j = 0; j < W; ++j) {
-                double a = (i == j) ? 1.0 : 0.0;
-                if (st == 1) a += 0.5 * Jk[0][i][j];
-                if (st == 2) a += -Jk[0][i][j] + 2.0 * Jk[1][i][j];
-                Jt[i][j] = a;
-            }
-        }
-        double s, c;
-        sincos(t[2], &s, &c);
-        const double v = u[0];
-        k[st][0] = dt * v * c;
-        k[st][1] = dt * v * s;
-        k[st][2] = dt * u[1];
-        // Jk = dt·(fθ ⊗ row θ of Jt + [0 | fu])
-        const double fth[NX] = {-v * s, v * c, 0.0};
-        for (int i = 0; i < NX; ++i)
-            for (int j = 0; j < W; ++j) Jk[st][i][j] = dt * fth[i] * Jt[2][j];
-        Jk[st][0][NX] += dt * c;
-        Jk[st][1][NX] += dt * s;
-        Jk[st][2][NX + 1] += dt;
-    }
-    for (int i = 0; i < NX; ++i) {
-        xn[i] = x[i] + (k[0][i] + 4.0 * k[1][i] + k[2][i]) / 6.0;
-        for (int j = 0; j < W; ++j) J[i][j] = ((i == j) ? 1.0 : 0.0) + (Jk[0][i][j] + 4.0 * Jk[1][i][j] + Jk[2][i][j]) / 6.0;
-    }
-}
+template <class M> struct Dims {
+    static constexpr int NX = M::NX, NU = M::NU, W = NX + NU;
+    __host__ __device__ static constexpr int64_t nn(int N) { return (int64_t)N * NX + (int64_t)(N - 1) * NU; }
+    __host__ __device__ static constexpr int64_t np_(int N) { return (int64_t)(N + 1) * NX; }
+    // Y: knots 0..N-2 are 2NX × W, the last 2NX × NX
+    __host__ __device__ static constexpr int64_t ny_(int N) { return 2 * NX * W * (int64_t)(N - 1) + 2 * NX * NX; }
+    __device__ static int64_t oy(int k) { return k == 0 ? 0 : (int64_t)NX * k + NX; }   // y / λ blocks
+    __device__ static int64_t om(int k) { return k == 0 ? 0 : (int64_t)NX * k; }        // [λ_{k-1}; μ_k; λ_k]
+};
 
 // merit pieces of knot k at the point zk (+ a·dk + b·ek): cost and Σ|c| of the constraint
 // values the knot owns (knot 0: initial state + dynamics 0; knot k: dynamics k; last: goal)
@@ -116,11 +196,13 @@ struct KnotPt {
     }
 };
 
+template <class M>
 __device__ __forceinline__ void knot_merit(const Args &A, int t, int k, const KnotPt &p, double &cost, double &c1)
 {
+    constexpr int NX = M::NX, NU = M::NU, W = NX + NU;
     const int N = A.N;
     const int64_t o = (int64_t)W * k;
-    double x[NX], u[NU] = {0.0, 0.0};
+    double x[NX], u[NU];
     for (int i = 0; i < NX; ++i) x[i] = p.at(o + i);
     const double *xf = A.xf + (int64_t)t * NX;
     cost = 0.0;
@@ -130,7 +212,7 @@ __device__ __forceinline__ void knot_merit(const Args &A, int t, int k, const Kn
         for (int i = 0; i < NX; ++i) cost += 0.5 * (x[i] - xf[i]) * A.Q[i] * (x[i] - xf[i]);
         for (int i = 0; i < NU; ++i) cost += 0.5 * u[i] * A.R[i] * u[i];
         double xn[NX];
-        rk3(x, u, A.dt, xn);
+        rk3<M>(x, u, A.dt, xn, A.par);
         if (k == 0)
             for (int i = 0; i < NX; ++i) c1 += fabs(x[i] - A.x0[(int64_t)t * NX + i]);
         for (int i = 0; i < NX; ++i) c1 += fabs(xn[i] - p.at(o + W + i));
@@ -157,12 +239,12 @@ __device__ __forceinline__ double wave_max(double v)
 }
 
 // ϕ = f + μ‖c‖₁ at the point p (dubins_sqp.jl:60)
-__device__ double merit(const Args &A, int t, const KnotPt &p, int lane)
+template <class M> __device__ double merit(const Args &A, int t, const KnotPt &p, int lane)
 {
     double f = 0.0, c = 0.0;
     for (int k = lane; k < A.N; k += 64) {
         double ck, c1;
-        knot_merit(A, t, k, p, ck, c1);
+        knot_merit<M>(A, t, k, p, ck, c1);
         f += ck;
         c += c1;
     }
@@ -170,9 +252,9 @@ __device__ double merit(const Args &A, int t, const KnotPt &p, int lane)
 }
 
 // z ← p, λ ← λ of the Newton solve, one more accepted step (wave-cooperative, coalesced)
-__device__ void accept(const Args &A, int64_t t, const KnotPt &p, int lane)
+template <class M> __device__ void accept(const Args &A, int64_t t, const KnotPt &p, int lane)
 {
-    const int64_t NN = nn(A.N), P = np_(A.N);
+    const int64_t NN = Dims<M>::nn(A.N), P = Dims<M>::np_(A.N);
     double *z = A.Z + t * NN;
     for (int64_t i = lane; i < NN; i += 64) z[i] = p.at(i);
     for (int64_t i = lane; i < P; i += 64) A.lam[t * P + i] = A.lamn[t * P + i];
@@ -180,22 +262,25 @@ __device__ void accept(const Args &A, int64_t t, const KnotPt &p, int lane)
 }
 
 // ---------------------------------------------------------------- assembly (update!) + check
-// Knot k: Y_k, y_k, H_k, g_k of the Dubins structure (knot 0: (n1 0, p 3, n2 3, w 5),
-// interior (3, 0, 3, 5), last (3, 3, 0, 3)) and its share of the convergence check: cost,
+// Knot k: Y_k, y_k, H_k, g_k of the trajectory structure (knot 0: (n1 0, p NX, n2 NX, w W),
+// interior (NX, 0, NX, W), last (NX, NX, 0, NX)) and its share of the convergence check: cost,
 // Σ|c|, max|c|, ‖g_k + Y_kᵀ m_k‖² with m_k = [λ_{k-1}; μ_k; λ_k] the multipliers of the
 // last Newton step (calc_residual!, cholesky_solver.jl:201-236).  Then the wave's check:
 // ‖c‖∞ < tol_p and ‖∇f + ∇cᵀλ‖₂ < tol_d → converged (cholesky_solver.jl:129-137).
+template <class M>
 __device__ void expand_knot(const Args &A, int t, int k, double &cost, double &c1, double &cinf, double &r2)
 {
+    using D = Dims<M>;
+    constexpr int NX = M::NX, NU = M::NU, W = NX + NU, R2 = 2 * NX;
     const int N = A.N;
-    const int64_t NN = nn(N), P = np_(N);
+    const int64_t NN = D::nn(N), P = D::np_(N);
     const double *z = A.Z + t * NN + (int64_t)W * k;
     const double *xf = A.xf + (int64_t)t * NX;
-    double *Y = A.Y + t * ny_(N) + 30 * (int64_t)k;
-    double *y = A.y + t * P + oy(k);
+    double *Y = A.Y + t * D::ny_(N) + (int64_t)R2 * W * k;
+    double *y = A.y + t * P + D::oy(k);
     double *H = A.H + t * NN + (int64_t)W * k;
     double *g = A.g + t * NN + (int64_t)W * k;
-    const double *m = A.lam + t * P + om(k);
+    const double *m = A.lam + t * P + D::om(k);
     double x[NX];
     for (int i = 0; i < NX; ++i) x[i] = z[i];
     auto con = [&](double v, int i) {
@@ -204,18 +289,19 @@ __device__ void expand_knot(const Args &A, int t, int k, double &cost, double &c
         cinf = fmax(cinf, fabs(v));
     };
     if (k < N - 1) {
-        const double u[NU] = {z[NX], z[NX + 1]};
+        double u[NU];
+        for (int i = 0; i < NU; ++i) u[i] = z[NX + i];
         double xn[NX], J[NX][W];
-        rk3_jac(x, u, A.dt, xn, J);
+        rk3_jac<M>(x, u, A.dt, xn, J, A.par);
         // rows: k == 0: [C = [I 0] (initial state); D1 = J]; else [D2 = [−I 0]; D1 = J]
-        double Yk[6][W];
+        double Yk[R2][W];
         for (int i = 0; i < NX; ++i)
             for (int j = 0; j < W; ++j) {
                 Yk[i][j] = (i == j) ? (k == 0 ? 1.0 : -1.0) : 0.0;
                 Yk[NX + i][j] = J[i][j];
             }
         for (int j = 0; j < W; ++j)
-            for (int i = 0; i < 6; ++i) Y[i + 6 * j] = Yk[i][j];
+            for (int i = 0; i < R2; ++i) Y[i + R2 * j] = Yk[i][j];
         int r = 0;
         if (k == 0)
             for (int i = 0; i < NX; ++i) con(x[i] - A.x0[(int64_t)t * NX + i], r++);
@@ -235,15 +321,15 @@ __device__ void expand_knot(const Args &A, int t, int k, double &cost, double &c
         for (int j = 0; j < W; ++j) {
             g[j] = gk[j];
             double sres = gk[j];
-            for (int i = 0; i < 6; ++i) sres += Yk[i][j] * m[i];
+            for (int i = 0; i < R2; ++i) sres += Yk[i][j] * m[i];
             r2 += sres * sres;
         }
     } else {
-        // last knot: [D2 = −I; C = I (goal)], 6×3
+        // last knot: [D2 = −I; C = I (goal)], 2NX × NX
         for (int j = 0; j < NX; ++j)
             for (int i = 0; i < NX; ++i) {
-                Y[i + 6 * j] = (i == j) ? -1.0 : 0.0;
-                Y[NX + i + 6 * j] = (i == j) ? 1.0 : 0.0;
+                Y[i + R2 * j] = (i == j) ? -1.0 : 0.0;
+                Y[NX + i + R2 * j] = (i == j) ? 1.0 : 0.0;
             }
         for (int i = 0; i < NX; ++i) con(x[i] - xf[i], i);
         for (int i = 0; i < NX; ++i) {
@@ -257,13 +343,13 @@ __device__ void expand_knot(const Args &A, int t, int k, double &cost, double &c
     }
 }
 
-__global__ __launch_bounds__(64 * TPB) void sqp_expand_kernel(const Args A)
+template <class M> __global__ __launch_bounds__(64 * TPB) void sqp_expand_kernel(const Args A)
 {
     const int lane = threadIdx.x & 63;
     const int64_t t = (int64_t)blockIdx.x * TPB + (threadIdx.x >> 6);
     if (t >= A.B || A.status[t] != ACTIVE) return;                 // wave-uniform
     double cost = 0.0, c1 = 0.0, cinf = 0.0, r2 = 0.0;
-    for (int k = lane; k < A.N; k += 64) expand_knot(A, (int)t, k, cost, c1, cinf, r2);
+    for (int k = lane; k < A.N; k += 64) expand_knot<M>(A, (int)t, k, cost, c1, cinf, r2);
     const double f = wave_sum(cost), cs = wave_sum(c1), cm = wave_max(cinf), rs = wave_sum(r2);
     if (lane != 0) return;
     if (cm < A.tol_p && sqrt(rs) < A.tol_d) {
@@ -278,24 +364,26 @@ __global__ __launch_bounds__(64 * TPB) void sqp_expand_kernel(const Args A)
 // ---------------------------------------------------------------- line search, full step
 // ϕ′ = ∇fᵀdz − μ‖c‖₁ (dubins_sqp.jl:61); Armijo at α = 1 (:79); otherwise the constraint
 // values at z + dz go to y for the second-order-correction solve.
-__global__ __launch_bounds__(64 * TPB) void sqp_ls1_kernel(const Args A)
+template <class M> __global__ __launch_bounds__(64 * TPB) void sqp_ls1_kernel(const Args A)
 {
+    using D = Dims<M>;
+    constexpr int NX = M::NX, NU = M::NU, W = NX + NU;
     const int lane = threadIdx.x & 63;
     const int64_t t = (int64_t)blockIdx.x * TPB + (threadIdx.x >> 6);
     if (t >= A.B) return;
     if (lane == 0) A.need_soc[t] = 0;
     if (A.status[t] != ACTIVE) return;
     const int N = A.N;
-    const int64_t NN = nn(N), P = np_(N);
+    const int64_t NN = D::nn(N), P = D::np_(N);
     const double *z = A.Z + t * NN, *dz = A.dz + t * NN, *g = A.g + t * NN;
     double gd = 0.0;
     for (int64_t i = lane; i < NN; i += 64) gd += g[i] * dz[i];
     const double dphi = wave_sum(gd) + A.dphi[t];
     const KnotPt p1{z, dz, nullptr, 1.0, 0.0};
-    const double phi1 = merit(A, (int)t, p1, lane);
+    const double phi1 = merit<M>(A, (int)t, p1, lane);
     if (lane == 0) A.dphi[t] = dphi;
     if (phi1 <= A.phi0[t] + ETA * dphi) {
-        accept(A, t, p1, lane);
+        accept<M>(A, t, p1, lane);
         return;
     }
     if (lane == 0) A.need_soc[t] = 1;
@@ -304,11 +392,12 @@ __global__ __launch_bounds__(64 * TPB) void sqp_ls1_kernel(const Args A)
         const int64_t o = (int64_t)W * k;
         double x[NX];
         for (int i = 0; i < NX; ++i) x[i] = p1.at(o + i);
-        double *yk = y + oy(k);
+        double *yk = y + D::oy(k);
         if (k < N - 1) {
-            const double u[NU] = {p1.at(o + NX), p1.at(o + NX + 1)};
+            double u[NU];
+            for (int i = 0; i < NU; ++i) u[i] = p1.at(o + NX + i);
             double xn[NX];
-            rk3(x, u, A.dt, xn);
+            rk3<M>(x, u, A.dt, xn, A.par);
             int r = 0;
             if (k == 0)
                 for (int i = 0; i < NX; ++i) yk[r++] = x[i] - A.x0[t * NX + i];
@@ -321,34 +410,33 @@ __global__ __launch_bounds__(64 * TPB) void sqp_ls1_kernel(const Args A)
 
 // ---------------------------------------------------------------- line search, SOC + backtracking
 // dubins_sqp.jl:82-94: z + dz + dẑ accepted on strict decrease below ϕ + ηϕ′; else α = ρ, ρ², …
-__global__ __launch_bounds__(64 * TPB) void sqp_ls2_kernel(const Args A)
+template <class M> __global__ __launch_bounds__(64 * TPB) void sqp_ls2_kernel(const Args A)
 {
     const int lane = threadIdx.x & 63;
     const int64_t t = (int64_t)blockIdx.x * TPB + (threadIdx.x >> 6);
     if (t >= A.B || !A.need_soc[t]) return;
-    const int64_t NN = nn(A.N);
+    const int64_t NN = Dims<M>::nn(A.N);
     const double *z = A.Z + t * NN, *dz = A.dz + t * NN, *ds = A.dzs + t * NN;
     const double phi0 = A.phi0[t], dphi = A.dphi[t];
     const KnotPt ps{z, dz, ds, 1.0, 1.0};
-    if (merit(A, (int)t, ps, lane) < phi0 + ETA * dphi) {
-        accept(A, t, ps, lane);
+    if (merit<M>(A, (int)t, ps, lane) < phi0 + ETA * dphi) {
+        accept<M>(A, t, ps, lane);
         return;
     }
     double a = RHO;
     for (int i = 1; i < LS_TRIES; ++i, a *= RHO) {
         const KnotPt pa{z, dz, nullptr, a, 0.0};
-        if (merit(A, (int)t, pa, lane) <= phi0 + ETA * a * dphi) {
-            accept(A, t, pa, lane);
+        if (merit<M>(A, (int)t, pa, lane) <= phi0 + ETA * a * dphi) {
+            accept<M>(A, t, pa, lane);
             return;
         }
     }
     if (lane == 0) A.status[t] = LS_FAILED;
 }
 
-__global__ __launch_bounds__(256) void sqp_init_kernel(const Args A)
+__global__ __launch_bounds__(256) void sqp_init_kernel(const Args A, int64_t P)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t P = np_(A.N);
     if (i < A.B * P) A.lam[i] = 0.0;
     if (i < A.B) {
         A.status[i] = ACTIVE;
@@ -364,51 +452,69 @@ __global__ __launch_bounds__(256) void sqp_finish_kernel(const Args A)
 
 static dim3 grid_for(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 
-} // namespace sqp
-
-// the structure tables of the Dubins KKT (ConstraintBlocks, conblocks.jl:403-425)
-void sqp_structure(int N, std::vector<int32_t> &n1, std::vector<int32_t> &p, std::vector<int32_t> &n2,
-                   std::vector<int32_t> &w)
+template <class M>
+hipError_t run(const SqpArgs &A, int max_iters, hipStream_t s, int (*kkt)(void *ctx, int ginv, double *dz), void *ctx,
+               int *kkt_rc)
 {
-    using namespace sqp;
-    n1.assign(N, NX);
-    p.assign(N, 0);
-    n2.assign(N, NX);
-    w.assign(N, W);
-    n1[0] = 0;
-    p[0] = NX;
-    p[N - 1] = NX;
-    n2[N - 1] = 0;
-    w[N - 1] = NX;
-}
-
-// Device driver (lqrx_api.cpp validates and calls this).  kkt(ctx, ginv, dz) runs one KKT
-// solve of the Dubins structure on Y, y, H, g → dz, lamn; a negative return stops the loop.
-hipError_t sqp_run(const SqpArgs &A0, int max_iters, hipStream_t s, int (*kkt)(void *ctx, int ginv, double *dz),
-                   void *ctx, int *kkt_rc)
-{
-    using namespace sqp;
-    SqpArgs A = A0;
-    const int64_t BP = A.B * np_(A.N);
-    hipLaunchKernelGGL(sqp_init_kernel, grid_for(BP > A.B ? BP : A.B), dim3(256), 0, s, A);
+    const int64_t BP = A.B * Dims<M>::np_(A.N);
+    hipLaunchKernelGGL(sqp_init_kernel, grid_for(BP > A.B ? BP : A.B), dim3(256), 0, s, A, Dims<M>::np_(A.N));
     int32_t h_active = 0;
     for (int it = 0; it < max_iters; ++it) {
         hipError_t e = hipMemsetAsync(A.n_active, 0, sizeof(int32_t), s);
         if (e != hipSuccess) return e;
         const dim3 gw((unsigned)((A.B + TPB - 1) / TPB)), bw(64 * TPB);
-        hipLaunchKernelGGL(sqp_expand_kernel, gw, bw, 0, s, A);
+        hipLaunchKernelGGL(sqp_expand_kernel<M>, gw, bw, 0, s, A);
         if ((e = hipMemcpyAsync(&h_active, A.n_active, sizeof(int32_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
             (e = hipStreamSynchronize(s)) != hipSuccess)
             return e;
         if (h_active == 0) break;
         if ((*kkt_rc = kkt(ctx, 1, A.dz)) < 0) return hipSuccess;
-        hipLaunchKernelGGL(sqp_ls1_kernel, gw, bw, 0, s, A);
+        hipLaunchKernelGGL(sqp_ls1_kernel<M>, gw, bw, 0, s, A);
         if ((*kkt_rc = kkt(ctx, 0, A.dzs)) < 0) return hipSuccess;
-        hipLaunchKernelGGL(sqp_ls2_kernel, gw, bw, 0, s, A);
+        hipLaunchKernelGGL(sqp_ls2_kernel<M>, gw, bw, 0, s, A);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(sqp_finish_kernel, grid_for(A.B), dim3(256), 0, s, A);
     return hipGetLastError();
+}
+
+} // namespace sqp
+
+bool sqp_model_dims(int model, int *nx, int *nu)
+{
+    switch (model) {
+    case SQP_DUBINS: *nx = sqp::Dubins::NX, *nu = sqp::Dubins::NU; return true;
+    case SQP_CARTPOLE: *nx = sqp::Cartpole::NX, *nu = sqp::Cartpole::NU; return true;
+    default: return false;
+    }
+}
+
+// the structure tables of the trajectory KKT (ConstraintBlocks, conblocks.jl:403-425):
+// knot 0 (0, NX, NX, NX+NU), interior (NX, 0, NX, NX+NU), last (NX, NX, 0, NX)
+void sqp_structure(int nx, int nu, int N, std::vector<int32_t> &n1, std::vector<int32_t> &p,
+                   std::vector<int32_t> &n2, std::vector<int32_t> &w)
+{
+    n1.assign(N, nx);
+    p.assign(N, 0);
+    n2.assign(N, nx);
+    w.assign(N, nx + nu);
+    n1[0] = 0;
+    p[0] = nx;
+    p[N - 1] = nx;
+    n2[N - 1] = 0;
+    w[N - 1] = nx;
+}
+
+// Device driver (lqrx_api.cpp validates and calls this).  kkt(ctx, ginv, dz) runs one KKT
+// solve of the trajectory structure on Y, y, H, g → dz, lamn; a negative return stops the loop.
+hipError_t sqp_run(const SqpArgs &A, int max_iters, hipStream_t s, int (*kkt)(void *ctx, int ginv, double *dz),
+                   void *ctx, int *kkt_rc)
+{
+    switch (A.model) {
+    case SQP_DUBINS: return sqp::run<sqp::Dubins>(A, max_iters, s, kkt, ctx, kkt_rc);
+    case SQP_CARTPOLE: return sqp::run<sqp::Cartpole>(A, max_iters, s, kkt, ctx, kkt_rc);
+    default: return hipErrorInvalidValue;
+    }
 }
 
 } // namespace lqrx

@@ -49,6 +49,17 @@ class SqpDesc(C.Structure):
     ]
 
 
+class TrajSqpDesc(C.Structure):
+    """Mirror of ``lqrx_sqp_desc``."""
+
+    _fields_ = [
+        ("model", C.c_int32), ("N", C.c_int32), ("max_iters", C.c_int32), ("reserved", C.c_int32),
+        ("batch", C.c_int64), ("dt", C.c_double), ("Q", C.c_double * 8), ("R", C.c_double * 8),
+        ("Qf", C.c_double * 8), ("params", C.c_double * 4), ("mu", C.c_double),
+        ("tol_p", C.c_double), ("tol_d", C.c_double),
+    ]
+
+
 class LsDesc(C.Structure):
     """Mirror of ``lqrx_ls_desc``."""
 
@@ -71,6 +82,9 @@ _SIGS = {
     "lqrx_kkt_solve_ws": (C.c_int, [C.POINTER(KktDesc)] + [_VP] * 7 + [_VP, C.c_size_t, _VP]),
     "lqrx_dubins_sqp_solve": (C.c_int, [C.POINTER(SqpDesc)] + [_VP] * 6 + [_VP]),
     "lqrx_dubins_sqp_solve_host": (C.c_int, [C.POINTER(SqpDesc)] + [_VP] * 6),
+    "lqrx_sqp_model_dims": (C.c_int, [C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "lqrx_sqp_solve": (C.c_int, [C.POINTER(TrajSqpDesc)] + [_VP] * 6 + [_VP]),
+    "lqrx_sqp_solve_host": (C.c_int, [C.POINTER(TrajSqpDesc)] + [_VP] * 6),
     "lqrx_ls_lds_bytes": (C.c_size_t, [C.c_int32, C.c_int32, C.c_int32]),
     "lqrx_ls_solve": (C.c_int, [C.POINTER(LsDesc)] + [_VP] * 11 + [_VP]),
     "lqrx_ls_solve_host": (C.c_int, [C.POINTER(LsDesc)] + [_VP] * 9),

@@ -69,10 +69,16 @@ def ConstraintBlocks(n, m, N, stage_p):
     return KktStructure(n, m, N, n1, p, n2, w)
 
 
+def trajectory_structure(n, m, N):
+    """Initial-state constraint at knot 1, dynamics, goal at knot N (the SQP problems of
+    test/dubins_sqp.jl and test/problems.jl Cartpole()) — block 1 (0,n,n), blocks 2..N-1
+    (n,0,n), block N (n,n,0)."""
+    return ConstraintBlocks(n, m, N, [n] + [0] * (N - 2) + [n])
+
+
 def dubins_structure(N=101):
-    """Dubins car n=3, m=2 (BASELINE cfg3): initial-state constraint at knot 1, dynamics,
-    goal at knot N — block 1 (0,3,3), blocks 2..N-1 (3,0,3), block N (3,3,0)."""
-    return ConstraintBlocks(3, 2, N, [3] + [0] * (N - 2) + [3])
+    """Dubins car n=3, m=2 (BASELINE cfg3)."""
+    return trajectory_structure(3, 2, N)
 
 
 def double_integrator_structure(D=3, N=101):

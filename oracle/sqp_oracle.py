@@ -1,4 +1,4 @@
-"""Dubins SQP oracle — TEST INFRASTRUCTURE ONLY (CPU restatement, numpy).
+"""Trajectory SQP oracle (Dubins car, cartpole) — TEST INFRASTRUCTURE ONLY (CPU restatement, numpy).
 
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module;
 the product path (lqrx.sqp → liblqrx.so) never does.
@@ -20,19 +20,26 @@ before its step with the λ of its previous Newton solve (zero at the start).  A
 that finds no acceptable step leaves the iterate unchanged and ends that trajectory
 (status 2; the script only warns, :96).
 
+The same loop serves the cartpole of test/problems.jl:58-88 (Cartpole(): Q = 1e-2·I,
+R = 1e-1·I, Qf = 100·I, x0 = 0, xf = [0, π, 0, 0], tf = 5, U0 = 0.01 rolled out from x0;
+the SQP of test/cartpole.jl drives the same update! / _solve! / L1-merit pieces).
+
 Parity anchor: the reference's own functions above.  TrajOptCore / RobotZoo are absent, so the
-Dubins model (RobotZoo.DubinsCar: ẋ = [v cosθ, v sinθ, ω]) and RK3 (RobotDynamics:
+models — RobotZoo.DubinsCar: ẋ = [v cosθ, v sinθ, ω]; RobotZoo.Cartpole (mc 1, mp 0.2,
+l 0.5, g 9.81): q̈ = −H⁻¹(C q̇ + G − B u) with H = [mc+mp, mp l cθ; mp l cθ, mp l²],
+C q̇ = [−mp l sθ θ̇², 0], G = [0, mp g l sθ], B = [1, 0] — and RK3 (RobotDynamics:
 k1 = f(x)dt, k2 = f(x + k1/2)dt, k3 = f(x − k1 + 2k2)dt, x⁺ = x + (k1 + 4k2 + k3)/6) are
 restated from their published definitions; Jacobians here by complex-step differentiation
-(exact to rounding; the device path uses the analytic chain rule — an independent check).
+(exact to rounding; the device path uses forward-mode dual numbers — an independent check).
 The merit weight μ is fixed (the script's μ = 1; TO.update_penalty! is absent).
 """
 from __future__ import annotations
 
 import numpy as np
 
-NX, NU = 3, 2
+NX, NU = 3, 2          # the Dubins car (module-level names kept for the Dubins helpers)
 ETA, RHO, LS_TRIES = 1e-4, 0.5, 10
+CARTPOLE_PARAMS = (1.0, 0.2, 0.5, 9.81)   # RobotZoo.Cartpole() defaults: mc, mp, l, g
 
 
 def dubins(x, u):
@@ -40,38 +47,72 @@ def dubins(x, u):
     return np.array([u[0] * np.cos(x[2]), u[0] * np.sin(x[2]), u[1]], dtype=np.result_type(x, u))
 
 
-def rk3(x, u, dt):
-    k1 = dubins(x, u) * dt
-    k2 = dubins(x + k1 / 2, u) * dt
-    k3 = dubins(x - k1 + 2 * k2, u) * dt
+def cartpole(x, u, params=CARTPOLE_PARAMS):
+    """RobotZoo.Cartpole continuous dynamics, q = [x, θ]: q̈ = −H⁻¹(C q̇ + G − B u)."""
+    mc, mp, l, g = params
+    s, c = np.sin(x[1]), np.cos(x[1])
+    H = np.array([[mc + mp, mp * l * c], [mp * l * c, mp * l * l]], dtype=np.result_type(x, u))
+    rhs = np.array([mp * l * s * x[3] ** 2 + u[0], -mp * g * l * s], dtype=H.dtype)
+    qdd = np.linalg.solve(H, rhs)
+    return np.concatenate([x[2:4], qdd])
+
+
+class Model:
+    """A continuous model f(x, u) with its sizes (the device's LQRX_MODEL_* id in `model_id`)."""
+
+    def __init__(self, name, nx, nu, f, model_id, params=(0.0, 0.0, 0.0, 0.0)):
+        self.name, self.nx, self.nu, self.f, self.model_id, self.params = name, nx, nu, f, model_id, params
+
+
+DUBINS = Model("dubins", 3, 2, dubins, 0)
+CARTPOLE = Model("cartpole", 4, 1, cartpole, 1, CARTPOLE_PARAMS)
+
+
+def rk3(x, u, dt, model=DUBINS):
+    f = model.f
+    k1 = f(x, u) * dt
+    k2 = f(x + k1 / 2, u) * dt
+    k3 = f(x - k1 + 2 * k2, u) * dt
     return x + (k1 + 4 * k2 + k3) / 6
 
 
-def rk3_jac(x, u, dt, h=1e-30):
+def rk3_jac(x, u, dt, model=DUBINS, h=1e-30):
     """[A B] = ∂rk3/∂[x u] by complex step."""
-    J = np.zeros((NX, NX + NU))
-    for i in range(NX + NU):
+    nx, nu = model.nx, model.nu
+    J = np.zeros((nx, nx + nu))
+    for i in range(nx + nu):
         xc = x.astype(complex)
         uc = u.astype(complex)
-        if i < NX:
+        if i < nx:
             xc[i] += 1j * h
         else:
-            uc[i - NX] += 1j * h
-        J[:, i] = np.imag(rk3(xc, uc, dt)) / h
+            uc[i - nx] += 1j * h
+        J[:, i] = np.imag(rk3(xc, uc, dt, model)) / h
     return J
 
 
-class DubinsSQP:
+def rollout(model, x0, U, dt):
+    """rollout! (problems.jl:83): states from x0 under the controls U (N−1 × nu)."""
+    X = [np.asarray(x0, float)]
+    for u in U:
+        X.append(rk3(X[-1], np.asarray(u, float), dt, model))
+    return X
+
+
+class TrajSQP:
     """One trajectory's NLP, variables in the reference's order z = [x₁; u₁; …; x_{N-1}; u_{N-1}; x_N]."""
 
-    def __init__(self, N, dt, Q, R, Qf, x0, xf, mu=1.0):
+    def __init__(self, N, dt, Q, R, Qf, x0, xf, mu=1.0, model=DUBINS):
+        self.model = model
+        self.nx, self.nu = model.nx, model.nu
         self.N, self.dt, self.mu = N, dt, mu
         self.Q, self.R, self.Qf = (np.asarray(v, float) for v in (Q, R, Qf))
         self.x0, self.xf = np.asarray(x0, float), np.asarray(xf, float)
-        self.NN = N * NX + (N - 1) * NU
-        self.P = (N + 1) * NX
+        self.NN = N * self.nx + (N - 1) * self.nu
+        self.P = (N + 1) * self.nx
 
     def split(self, z):
+        NX, NU = self.nx, self.nu
         w = NX + NU
         X = [z[k * w:k * w + NX] for k in range(self.N - 1)] + [z[(self.N - 1) * w:]]
         U = [z[k * w + NX:(k + 1) * w] for k in range(self.N - 1)]
@@ -101,18 +142,19 @@ class DubinsSQP:
         X, U = self.split(z)
         v = [X[0] - self.x0]
         for k in range(self.N - 1):
-            v.append(rk3(X[k], U[k], self.dt) - X[k + 1])
+            v.append(rk3(X[k], U[k], self.dt, self.model) - X[k + 1])
         v.append(X[-1] - self.xf)
         return np.concatenate(v)
 
     def jac(self, z):
         X, U = self.split(z)
+        NX = self.nx
         A = np.zeros((self.P, self.NN))
-        w = NX + NU
+        w = NX + self.nu
         A[:NX, :NX] = np.eye(NX)
         for k in range(self.N - 1):
             r = NX * (k + 1)
-            A[r:r + NX, k * w:(k + 1) * w] = rk3_jac(X[k], U[k], self.dt)
+            A[r:r + NX, k * w:(k + 1) * w] = rk3_jac(X[k], U[k], self.dt, self.model)
             A[r:r + NX, (k + 1) * w:(k + 1) * w + NX] = -np.eye(NX)
         A[-NX:, (self.N - 1) * w:] = np.eye(NX)
         return A
@@ -156,7 +198,25 @@ class DubinsSQP:
         return np.abs(self.c(z)).max(), np.linalg.norm(self.grad(z) + self.jac(z).T @ lam)
 
 
-def solve(prob: DubinsSQP, z0, iters=10, tol_p=1e-5, tol_d=1e-5):
+class DubinsSQP(TrajSQP):
+    """The Dubins car NLP (test/dubins_sqp.jl)."""
+
+    def __init__(self, N, dt, Q, R, Qf, x0, xf, mu=1.0):
+        super().__init__(N, dt, Q, R, Qf, x0, xf, mu, DUBINS)
+
+
+def cartpole_problem(N, mu=1.0, x0=(0.0, 0.0, 0.0, 0.0), xf=(0.0, np.pi, 0.0, 0.0), tf=5.0):
+    """Cartpole() of test/problems.jl:58-88 (Q 1e-2·I, R 1e-1·I, Qf 100·I, tf 5) and its
+    initial guess: U0 = 0.01 rolled out from x0 (:80-84).  Returns (TrajSQP, z0)."""
+    dt = tf / (N - 1)
+    p = TrajSQP(N, dt, [1e-2] * 4, [1e-1], [100.0] * 4, x0, xf, mu, CARTPOLE)
+    U = np.full((N - 1, 1), 0.01)
+    X = rollout(CARTPOLE, p.x0, U, dt)
+    z = np.concatenate([np.concatenate([X[k], U[k]]) for k in range(N - 1)] + [X[-1]])
+    return p, z
+
+
+def solve(prob: TrajSQP, z0, iters=10, tol_p=1e-5, tol_d=1e-5):
     """CholeskySolver.solve! loop (cholesky_solver.jl:109-153).  Returns dict z, lam, iters
     (steps taken), status (0 converged, 1 iteration limit, 2 line search failed), hist
     (iterates), soc (per step: second-order correction used)."""
@@ -193,21 +253,21 @@ def initial_guess(N, dt, x0, xf):
     return z
 
 
-def assemble(prob: DubinsSQP, z):
+def assemble(prob: TrajSQP, z):
     """The Newton step's KKT inputs at z in the liblqrx ABI layout (h_mode 2): per knot
     Y_k = [D2; C; D1] (column-major), y_k = [c; d], H_k (diagonal), g_k — the blocks
     ConstraintBlocks / InvertedQuadratic hold (conblocks.jl:36-98, block_cholesky.jl:82-91,
     126-132), cut from the dense ∇c, c, ∇²f, ∇f above.  Knot k's rows are the constraints
-    [λ_{k-1}; μ_k; λ_k] = c[mk : mk+6], mk = 0 (k = 0) or 3k; its columns are z_k."""
+    [λ_{k-1}; μ_k; λ_k] = c[mk : mk+2n], mk = 0 (k = 0) or n·k; its columns are z_k."""
     A, c, g, h = prob.jac(z), prob.c(z), prob.grad(z), prob.hess_diag()
-    N = prob.N
+    N, NX, W = prob.N, prob.nx, prob.nx + prob.nu
     Y, y, H, G = [], [], [], []
     for k in range(N):
-        w = NX + NU if k < N - 1 else NX
-        mk = 0 if k == 0 else 3 * k
-        Y.append(A[mk:mk + 6, 5 * k:5 * k + w].T.ravel())     # column-major
-        oy = 0 if k == 0 else 3 * k + 3
-        y.append(c[oy:oy + (6 if k == 0 else 3)])
-        H.append(h[5 * k:5 * k + w])
-        G.append(g[5 * k:5 * k + w])
+        w = W if k < N - 1 else NX
+        mk = 0 if k == 0 else NX * k
+        Y.append(A[mk:mk + 2 * NX, W * k:W * k + w].T.ravel())     # column-major
+        oy = 0 if k == 0 else NX * k + NX
+        y.append(c[oy:oy + (2 * NX if k == 0 else NX)])
+        H.append(h[W * k:W * k + w])
+        G.append(g[W * k:W * k + w])
     return tuple(np.concatenate(v) for v in (Y, y, H, G))

@@ -139,7 +139,7 @@ def test_ls_validation(lqrx):
     ptrs = [C.cast(buf, C.c_void_p)] * 9
     ok = dict(n=4, m=1, N=101, hu_mode=0, batch=2)
     for field, val, code in [("n", 0, -1), ("N", 1, -1), ("hu_mode", 3, -1), ("batch", -1, -1),
-                             ("N", 400, _lib.ERR_UNSUPPORTED)]:
+                             ("N", 1100, _lib.ERR_UNSUPPORTED)]:
         d = _lib.LsDesc(**{**ok, field: val})
         assert lib.lqrx_ls_solve(C.byref(d), *ptrs, None, None, None) == code, (field, val)
     d = _lib.LsDesc(**ok)

@@ -94,15 +94,19 @@ def test_kkt_alternating_structures(lqrx, gpu_ok):
             assert rel(got["dz"], rd) <= TOL and rel(got["lam"], rl) <= TOL
 
 
-@pytest.mark.parametrize("N,batch", [(4, 130), (5, 64), (6, 1), (101, 16384 + 3)])
+@pytest.mark.parametrize("model,N,batch", [("dubins", 4, 130), ("dubins", 5, 64), ("dubins", 6, 1),
+                                           ("dubins", 101, 16384 + 3), ("cartpole", 5, 130), ("cartpole", 6, 1),
+                                           ("cartpole", 101, 4096 + 5)])
 @pytest.mark.parametrize("h_mode,ginv", [(2, 1), (0, 1), (2, 0)])
-def test_kkt_fil_shapes(lqrx, gpu_ok, N, batch, h_mode, ginv):
+def test_kkt_fil_shapes(lqrx, gpu_ok, model, N, batch, h_mode, ginv):
     """The compile-time-shaped first/interior/last kernel (lqrx_kkt_fil.hip) at its edge
     cases: the shortest horizon it serves (N = 4), one trajectory, ragged last waves, the
-    full cfg3 batch; Ginv = 0 is the second-order-correction variant."""
+    full cfg3 batch; Ginv = 0 is the second-order-correction variant.  The cartpole shape
+    (n 4, m 1; the device SQP's structure) is instantiated for diagonal H (dense H → the
+    generic kernel, also checked here); N ≥ 5 (N = 4 is over-constrained: 20 rows, 19 vars)."""
     import lqrx.kkt as K
 
-    st = K.dubins_structure(N)
+    st = K.dubins_structure(N) if model == "dubins" else K.trajectory_structure(4, 1, N)
     pb = K.random_kkt(st, batch, seed=7 * N + h_mode, h_mode=h_mode)
     got = K.kkt_solve(pb, ginv=ginv)
     ref = _ref(st, pb, ginv)
