@@ -106,7 +106,8 @@ def cpu_baseline_kkt(N, target_s=12.0, threads=None, structure="dubins"):
     orc.kkt_solve_batch(os_, sample, pb.Y, pb.y, pb.H, pb.g, h_mode=2, nthreads=threads)
     dt = time.perf_counter() - t0
     return dict(value=sample / dt, unit="trajectories/s", cores=threads, kind="port",
-                sample=f"{sample} Dubins KKT solves N={N}, oracle/lqr_oracle.c (C restatement "
+                sample=f"{sample} {'Dubins' if structure == 'dubins' else 'DoubleIntegrator(3)'} KKT solves "
+                       f"N={N}, oracle/lqr_oracle.c (C restatement "
                        f"of _solve!), OpenMP {threads} threads, {dt:.1f} s")
 
 
@@ -194,7 +195,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-gather", action="store_true",
                     help="skip the final info + P_1 gather to rank 0 (N > 1)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     ap.add_argument("--kkt-structure", choices=["dubins", "di"], default="dubins",
                     help="kkt workload: Dubins (configs[2]) or DoubleIntegrator(3,N) (test/problems.jl)")
     ap.add_argument("--sqp-model", choices=["dubins", "cartpole"], default="dubins",
@@ -408,8 +409,15 @@ def main():
             # reference op count (least_squares.jl:171-182): ĀᵀĀ as a dense gemm, Āᵀb̄, potrf, potrs
             fl = 2.0 * Nn * Nm * Nm + 2.0 * Nn * Nm + Nm ** 3 / 3.0 + 2.0 * Nm * Nm
             achieved = fl * bt / (kern_ms * 1e-3) / 1e12
+            traffic = None
+            if os.path.exists(args.traffic_json):
+                try:
+                    traffic = json.load(open(args.traffic_json)).get(f"ls_cartpole_N{N}_B{bt}_f64", {}) \
+                        .get("hbm_bytes_per_launch")
+                except Exception:
+                    traffic = None
             roof = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                    "frac": achieved / PEAK_FP64_TFLOPS, "traffic": None,
+                    "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic,
                     "kernel": "ls_condensed_kernel (fp64 VALU, LDS-resident H)", "kernel_ms": kern_ms,
                     "flops_per_traj": fl}
             metric = f"condensed least-squares LQR solves/sec (cartpole n=4 m=1 N={N} B={bt}, Hu=0 as a fresh solver)"
@@ -438,10 +446,11 @@ def main():
                     traffic = json.load(open(args.traffic_json)).get(key, {}).get("hbm_bytes_per_launch")
                 except Exception:
                     traffic = None
-            fil = args.kkt_structure == "dubins" and N >= 4
+            kname = ("kkt_fil_kernel" if args.kkt_structure == "dubins" else "kkt_fild_kernel") if N >= 4 \
+                else "kkt_staged_kernel"
             roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
-                    "kernel": "kkt_fil_kernel" if fil else "kkt_staged_kernel",
+                    "kernel": kname,
                     "kernel_ms": kern_ms,
                     "alg_bytes_per_traj": alg_bytes / bt}
             if args.kkt_structure == "dubins":
@@ -460,7 +469,7 @@ def main():
             if os.path.exists(args.traffic_json):
                 try:
                     tj = json.load(open(args.traffic_json))
-                    key = f"n{n}_m{m}_N{N}_B{bt}_{args.dtype}"
+                    key = f"n{n}_m{m}_N{N}_B{bt}_{args.dtype}" + ("_tv" if args.tv else "")
                     traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
                 except Exception:
                     traffic = None

@@ -168,30 +168,43 @@ int lqrx_kkt_sizes(const lqrx_kkt_desc *desc, int64_t *nY, int64_t *ny, int64_t 
  *   LQRX_MODEL_CARTPOLE nx 4, nu 1: RobotZoo.Cartpole, x = [x, θ, ẋ, θ̇],
  *                       params = {mc, mp, l, g} (RobotZoo defaults 1, 0.2, 0.5, 9.81;
  *                       test/problems.jl:58-88 Cartpole())
+ *   LQRX_MODEL_DOUBLE_INTEGRATOR{1,2,3}  nx 2D, nu D: RobotZoo.DoubleIntegrator(D),
+ *                       ẋ = [q̇; u] (test/problems.jl:14-56 DoubleIntegrator(D)); params unused
  * Problem: min Σ_{k<N} ½(x_k−xf)ᵀQ(x_k−xf) + ½u_kᵀRu_k + ½(x_N−xf)ᵀQf(x_N−xf)
  *          s.t. x_1 = x0, x_{k+1} = rk3(x_k, u_k), x_N = xf      (Q, R, Qf diagonal)
+ *          and, when stage_rows > 0, A_s x_k = b_s on the interior knots k = 2..N−1 (the
+ *          LinearConstraint DoubleIntegrator() adds on 2:N−1; A_s shared by the batch)
  * Buffers (device; layout 0, batch slowest), nx / nu of the model:
  *   Z      (N·nx + (N−1)·nu)·batch in/out: z = [x_1; u_1; …; x_{N−1}; u_{N−1}; x_N]
  *          (the KKT δz order)
  *   x0, xf nx·batch
- *   lam    nx(N+1)·batch out: multipliers of the last accepted Newton step (KKT λ order)
+ *   lam    (nx(N+1) + stage_rows(N−2))·batch out: multipliers of the last accepted Newton
+ *          step (KKT λ order)
  *   iters  int32·batch out: accepted steps
  *   status int32·batch out: 0 converged (‖c‖∞ < tol_p and ‖∇f+∇cᵀλ‖₂ < tol_d before a
  *          step), 1 max_iters reached, 2 line search failed (iterate left unchanged)
  * ------------------------------------------------------------------------------------ */
-enum { LQRX_MODEL_DUBINS = 0, LQRX_MODEL_CARTPOLE = 1 };
+enum {
+    LQRX_MODEL_DUBINS = 0,
+    LQRX_MODEL_CARTPOLE = 1,
+    LQRX_MODEL_DOUBLE_INTEGRATOR1 = 2,
+    LQRX_MODEL_DOUBLE_INTEGRATOR2 = 3,
+    LQRX_MODEL_DOUBLE_INTEGRATOR3 = 4
+};
 
 typedef struct lqrx_sqp_desc {
     int32_t model;          /* LQRX_MODEL_*                                            */
     int32_t N;              /* knots (>= 2)                                            */
     int32_t max_iters;      /* CholeskySolver.solve!: 10                               */
-    int32_t reserved;       /* 0                                                       */
+    int32_t stage_rows;     /* rows of the interior linear constraint, 0..2 (nx·rows ≤ 32) */
     int64_t batch;
     double dt;              /* tf / (N−1)                                              */
     double Q[8], R[8], Qf[8]; /* diagonal cost weights (> 0), first nx / nu used         */
     double params[4];       /* model parameters (see above)                            */
     double mu;              /* L1 merit weight (dubins_sqp.jl:59 uses 1)               */
     double tol_p, tol_d;    /* 1e-5, 1e-5 (cholesky_solver.jl:131-132)                 */
+    double stage_A[32];     /* A_s, stage_rows × nx column-major                        */
+    double stage_b[4];      /* b_s                                                      */
 } lqrx_sqp_desc;
 
 /* state / control dimension of a model; -1 for an unknown model */

@@ -157,7 +157,10 @@ int main()
     CHECK(lqrx_sqp_solve(&g, nullptr, dummy, dummy, dummy, info, info, nullptr) == -2);
     int32_t nx = 0, nu = 0;
     CHECK(lqrx_sqp_model_dims(LQRX_MODEL_CARTPOLE, &nx, &nu) == 0 && nx == 4 && nu == 1);
-    CHECK(lqrx_sqp_model_dims(-1, &nx, &nu) == -1);
+    CHECK(lqrx_sqp_model_dims(-1, &nx, &nu) == -1 && lqrx_sqp_model_dims(5, &nx, &nu) == -1);
+    CHECK(lqrx_sqp_model_dims(LQRX_MODEL_DOUBLE_INTEGRATOR3, &nx, &nu) == 0 && nx == 6 && nu == 3);
+    gb = g; gb.stage_rows = 3;
+    CHECK(lqrx_sqp_solve(&gb, dummy, dummy, dummy, dummy, info, info, nullptr) == -1);
     if (!have_gpu) {
         std::vector<double> Zh(2 * (21 * 4 + 20)), x0h(8), lamh(2 * 22 * 4);
         CHECK(lqrx_sqp_solve_host(&g, Zh.data(), x0h.data(), x0h.data(), lamh.data(), info, info) <= LQRX_ERR_HIP + 0);

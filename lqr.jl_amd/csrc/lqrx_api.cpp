@@ -633,7 +633,12 @@ int validate_sqp(const lqrx_sqp_desc *d, int *nx, int *nu)
     if (d->N < 2) return set_err(-1, "desc.N must be >= 2 (got %d)", d->N);
     if (d->batch < 0) return set_err(-1, "desc.batch must be >= 0");
     if (d->max_iters < 0) return set_err(-1, "desc.max_iters must be >= 0");
-    if (d->reserved != 0) return set_err(-1, "desc.reserved must be 0");
+    if (d->stage_rows < 0 || d->stage_rows > 2 || d->stage_rows * *nx > 32)
+        return set_err(-1, "desc.stage_rows must be 0..2 with stage_rows·nx <= 32 (got %d)", d->stage_rows);
+    for (int i = 0; i < d->stage_rows * *nx; ++i)
+        if (!std::isfinite(d->stage_A[i])) return set_err(-1, "desc.stage_A must be finite");
+    for (int i = 0; i < d->stage_rows; ++i)
+        if (!std::isfinite(d->stage_b[i])) return set_err(-1, "desc.stage_b must be finite");
     if (!(d->dt > 0)) return set_err(-1, "desc.dt must be > 0");
     for (int i = 0; i < *nx; ++i)
         if (!(d->Q[i] > 0) || !(d->Qf[i] > 0)) return set_err(-1, "desc.Q / desc.Qf must be positive");
@@ -702,10 +707,12 @@ extern "C" int lqrx_sqp_solve(const lqrx_sqp_desc *d, double *Z, const double *x
     if (!iters) return set_err(-6, "iters is NULL");
     if (!status) return set_err(-7, "status is NULL");
     const int N = d->N;
-    const int64_t B = d->batch, NN = (int64_t)N * nx + (int64_t)(N - 1) * nu, P = (int64_t)(N + 1) * nx;
+    const int pk = d->stage_rows;
+    const int64_t B = d->batch, NN = (int64_t)N * nx + (int64_t)(N - 1) * nu,
+                  P = (int64_t)(N + 1) * nx + (int64_t)(N - 2) * pk;
     hipStream_t s = (hipStream_t)stream;
     SqpKkt c{};
-    lqrx::sqp_structure(nx, nu, N, c.n1, c.p, c.n2, c.w);
+    lqrx::sqp_structure(nx, nu, pk, N, c.n1, c.p, c.n2, c.w);
     c.kd.N = N; c.kd.dtype = LQRX_F64; c.kd.batch = B;
     c.kd.n1 = c.n1.data(); c.kd.p = c.p.data(); c.kd.n2 = c.n2.data(); c.kd.w = c.w.data();
     c.kd.h_mode = 2; c.kd.ginv = 1; c.kd.layout = 0;
@@ -730,6 +737,9 @@ extern "C" int lqrx_sqp_solve(const lqrx_sqp_desc *d, double *Z, const double *x
     A.model = d->model; A.N = N; A.B = B; A.dt = d->dt; A.mu = d->mu; A.tol_p = d->tol_p; A.tol_d = d->tol_d;
     for (int i = 0; i < 8; ++i) A.Q[i] = d->Q[i], A.Qf[i] = d->Qf[i], A.R[i] = d->R[i];
     for (int i = 0; i < 4; ++i) A.par[i] = d->params[i];
+    A.stage_rows = pk;
+    for (int i = 0; i < 32; ++i) A.SA[i] = d->stage_A[i];
+    for (int i = 0; i < 4; ++i) A.Sb[i] = d->stage_b[i];
     A.x0 = x0; A.xf = xf; A.Z = Z; A.lam = lam; A.iters = iters; A.status = status;
     A.Y = (double *)(b + oY); A.y = (double *)(b + oy); A.H = (double *)(b + oH); A.g = (double *)(b + og);
     A.dz = (double *)(b + odz); A.lamn = (double *)(b + olamn); A.dzs = (double *)(b + odzs);
@@ -755,7 +765,8 @@ extern "C" int lqrx_sqp_solve_host(const lqrx_sqp_desc *d, double *Z, const doub
     if (st) return st;
     if (d->batch == 0) return 0;
     if (!Z || !x0 || !xf || !lam || !iters || !status) return set_err(-2, "NULL host pointer");
-    const int64_t B = d->batch, NN = (int64_t)d->N * nx + (int64_t)(d->N - 1) * nu, P = (int64_t)(d->N + 1) * nx;
+    const int64_t B = d->batch, NN = (int64_t)d->N * nx + (int64_t)(d->N - 1) * nu,
+                  P = (int64_t)(d->N + 1) * nx + (int64_t)(d->N - 2) * d->stage_rows;
     DevBuf dZ, dx0, dxf, dlam, dit, dst;
     if ((st = dev_alloc(dZ, B * NN * 8, "Z")) || (st = dev_alloc(dx0, B * nx * 8, "x0")) ||
         (st = dev_alloc(dxf, B * nx * 8, "xf")) || (st = dev_alloc(dlam, B * P * 8, "lam")) ||

@@ -80,9 +80,10 @@ bool kkt_fil_scratch_bytes(const KktArgs &a, const int32_t *n1, const int32_t *p
                            const int32_t *w, size_t *bytes);
 
 // ---- batched trajectory SQP (lqrx_sqp.hip) ----
-enum { SQP_DUBINS = 0, SQP_CARTPOLE = 1 };   // = LQRX_MODEL_*
+enum { SQP_DUBINS = 0, SQP_CARTPOLE = 1, SQP_DI1 = 2, SQP_DI2 = 3, SQP_DI3 = 4 };   // = LQRX_MODEL_*
 struct SqpArgs {
-    int model, N;
+    int model, N, stage_rows;         // stage_rows: PK of the interior-knot linear constraint
+    double SA[32], Sb[4];             // A_s (PK × NX, column-major), b_s
     int64_t B;
     double dt, mu, tol_p, tol_d;
     double Q[8], R[8], Qf[8];         // diagonal weights, first NX / NU used
@@ -99,7 +100,7 @@ struct SqpArgs {
 };
 hipError_t sqp_run(const SqpArgs &A, int max_iters, hipStream_t s, int (*kkt)(void *ctx, int ginv, double *dz),
                    void *ctx, int *kkt_rc);
-void sqp_structure(int nx, int nu, int N, std::vector<int32_t> &n1, std::vector<int32_t> &p,
+void sqp_structure(int nx, int nu, int pk, int N, std::vector<int32_t> &n1, std::vector<int32_t> &p,
                    std::vector<int32_t> &n2, std::vector<int32_t> &w);
 bool sqp_model_dims(int model, int *nx, int *nu);
 

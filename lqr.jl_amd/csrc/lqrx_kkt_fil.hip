@@ -1076,6 +1076,196 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     if (a.info && c.live) a.info[t0 + c.lane] = info;
 }
 
+// ------------------------------------------------------------------ the direct variant
+// Shapes whose knot images do not fit the three-deep LDS ring (e.g. DoubleIntegrator(3):
+// 13×9 Y blocks, 60 KB per staged knot image of 64 trajectories) run the same per-knot code
+// with each lane reading its own trajectory's Y/H/g/y straight from HBM (compile-time
+// offsets, no LDS): a lane streams a contiguous chunk per knot, its 64 neighbours the chunks
+// of the next trajectories; L2 absorbs the partial lines.  Same operation order as the staged
+// kernel, so the two agree bit for bit on a shape both serve.
+template <class S, class C> struct GIn {          // knot k's inputs (class C) of one trajectory
+    double Y[S::template LY<C>()], H[S::template LH<C>()], g[S::template Lg<C>()];
+    __device__ __forceinline__ void load(const KktArgs &a, int64_t t, int k)
+    {
+        using O = Off<S>;
+        const double *Yp = a.Y + t * a.sY + O::Y(k);
+#pragma unroll
+        for (int e = 0; e < S::template LY<C>(); ++e) Y[e] = Yp[e];
+        if constexpr (S::GINV) {
+            const double *Hp = a.H + t * a.sH + O::H(k), *gp = a.g + t * a.sg + O::g(k);
+#pragma unroll
+            for (int e = 0; e < S::template LH<C>(); ++e) H[e] = Hp[e];
+#pragma unroll
+            for (int e = 0; e < S::template Lg<C>(); ++e) g[e] = gp[e];
+        }
+    }
+    __device__ __forceinline__ const KnotIn<S, C> &as_in() const { return *reinterpret_cast<const KnotIn<S, C> *>(this); }
+};
+
+// Schur pieces of knot k (class C, diagonal H or the SOC variant) in two parts, each streamed
+// from HBM column by column, same per-entry operation order as compute_shur:
+//   HEAD: the D2×D2 block S[O1..][O1..] and r[O1..] — all that knot k−1's factor needs
+//         (added to its C̃ block, copy_shur! :166, :277), computed one knot ahead;
+//   REST: everything knot k's own factor reads (the D2×(C, D1) rows and the C, D1 rows).
+// Only one full Schur image is live at a time (plus the p1×p1 head of the next knot).
+template <class S, class C, bool HEAD>
+__device__ __forceinline__ void shur_part(Shur<C> &sc, const KktArgs &a, int64_t t, int k)
+{
+    static_assert(!S::GINV || S::HDIAG, "direct kernel: diagonal H or the SOC variant");
+    constexpr int R = C::R, W = C::W, p1 = C::P1;
+    constexpr int lo = 0, hi = HEAD ? p1 : R;                     // rows i in [lo, hi)
+    const double *Yp = a.Y + t * a.sY + Off<S>::Y(k);
+    const double *Hp = a.H + t * a.sH + Off<S>::H(k), *gp = a.g + t * a.sg + Off<S>::g(k);
+    auto want = [](int i, int i2) { return HEAD ? (i < p1 && i2 < p1) : !(i < p1 && i2 < p1); };
+#pragma unroll
+    for (int i = lo; i < hi; ++i) {
+        if (HEAD || i >= p1) sc.r[i] = 0.0;
+#pragma unroll
+        for (int i2 = i; i2 < R; ++i2)
+            if (want(i, i2)) sc.S[i][i2] = 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        double v[R], vh[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+            if (!HEAD || i < p1) v[i] = Yp[i + j * R];
+        if constexpr (S::GINV) {
+            const double h = rcp_nr2(Hp[j]);                      // block_cholesky.jl:86 inv
+            const double gh = gp[j];
+#pragma unroll
+            for (int i = lo; i < hi; ++i) {
+                vh[i] = v[i] * h;
+                if (HEAD || i >= p1) sc.r[i] = fma(vh[i], gh, sc.r[i]);
+            }
+        } else {
+#pragma unroll
+            for (int i = lo; i < hi; ++i) vh[i] = v[i];
+        }
+#pragma unroll
+        for (int i = lo; i < hi; ++i)
+#pragma unroll
+            for (int i2 = i; i2 < R; ++i2)
+                if (want(i, i2)) sc.S[i][i2] = fma(vh[i], v[i2], sc.S[i][i2]);
+    }
+}
+
+template <class S, class C>
+__device__ __forceinline__ void y_direct(double (&yc)[Z(C::PS + C::P2)], const KktArgs &a, int64_t t, int k)
+{
+    const double *yp = a.y + t * a.sy + Off<S>::y(k);
+#pragma unroll
+    for (int i = 0; i < C::PS + C::P2; ++i) yc[i] = yp[i];
+}
+
+template <class S>
+__global__ __launch_bounds__(64) void kkt_fild_kernel(const KktArgs a, double *__restrict__ scratch)
+{
+    using F = typename S::F;
+    using I = typename S::I;
+    using L = typename S::L;
+    const int N = a.N;                                          // ≥ 4 (host-checked)
+    const int64_t t0 = (int64_t)blockIdx.x * 64;
+    Ctx<S> c;
+    c.lane = threadIdx.x;
+    c.nlive = (int)(a.batch - t0 < 64 ? a.batch - t0 : 64);
+    c.live = c.lane < c.nlive;
+    const int64_t t = t0 + (c.live ? c.lane : c.nlive - 1);     // dead lanes re-read a live one
+    c.bdz = a.dz + t0 * a.sg;
+    c.blam = a.lam + t0 * a.sl;
+    c.bS = scratch + (int64_t)blockIdx.x * N * S::SLOT * 64;
+    c.vS = 8u * c.lane;
+    c.vdz = (uint32_t)(c.lane * a.sg * 8);
+    c.vlam = (uint32_t)(c.lane * a.sl * 8);
+    int info = 0;
+
+    // ---------------- forward ----------------
+    // (diagonal H has no factor to fail: compute_shur's ok is always true on this path)
+    Carry<S> cy;
+#pragma unroll
+    for (int i = 0; i < S::NX; ++i) {
+        cy.lprev[i] = 0.0;
+#pragma unroll
+        for (int j = 0; j < S::NX; ++j) cy.Ua[i][j] = 0.0;
+    }
+    {
+        Shur<F> s0;
+        double y0[Z(F::PS + F::P2)];
+        shur_part<S, F, false>(s0, a, t, 0);                    // F: p1 = 0, REST = all
+        y_direct<S, F>(y0, a, t, 0);
+        Shur<I> h1;
+        shur_part<S, I, true>(h1, a, t, 1);
+        factor_knot<S, F, I>(0, s0, y0, h1, cy, c, info);
+    }
+    for (int k = 1; k <= N - 3; ++k) {
+        Shur<I> sk;
+        double yk[Z(I::PS + I::P2)];
+        shur_part<S, I, false>(sk, a, t, k);
+        y_direct<S, I>(yk, a, t, k);
+        Shur<I> hn;
+        shur_part<S, I, true>(hn, a, t, k + 1);
+        factor_knot<S, I, I>(k, sk, yk, hn, cy, c, info);   // (knot k's own HEAD went to k−1)
+    }
+    Shur<L> sL;
+    double yL[Z(L::PS + L::P2)];
+    {
+        Shur<I> sk;
+        double yk[Z(I::PS + I::P2)];
+        shur_part<S, I, false>(sk, a, t, N - 2);
+        y_direct<S, I>(yk, a, t, N - 2);
+        shur_part<S, L, true>(sL, a, t, N - 1);
+        factor_knot<S, I, L>(N - 2, sk, yk, sL, cy, c, info);
+    }
+    shur_part<S, L, false>(sL, a, t, N - 1);
+    y_direct<S, L>(yL, a, t, N - 1);
+    {
+        Shur<NoCls> none;
+        factor_knot<S, L, NoCls>(N - 1, sL, yL, none, cy, c, info);
+    }
+
+    // ---------------- backward + primal recovery ----------------
+    SlabV<L> vL;
+    slab_load<S, L>(vL, c, N - 1);
+    SlabV<NoCls> vnone;
+    bwd_knot<L, NoCls>(vL, vnone);
+    store_lam<S, L>(c, N - 1, vL);
+    SlabV<I> vI;
+    slab_load<S, I>(vI, c, N - 2);
+    bwd_knot<I, L>(vI, vL);
+    {
+        GIn<S, L> in;
+        in.load(a, t, N - 1);
+        primal_knot<S, L, L::P1>(c, N - 1, vL, vI.la, in.as_in());
+    }
+    store_lam<S, I>(c, N - 2, vI);
+    for (int j = N - 3; j >= 1; --j) {
+        SlabV<I> v;
+        slab_load<S, I>(v, c, j);
+        GIn<S, I> in;                                            // knot j+1: F̃_{j+1} and δz_{j+1}
+        in.load(a, t, j + 1);
+        recompute_Ft<S, I>(vI.F, v.Cm, in.Y, in.H);
+        bwd_knot<I, I>(v, vI);
+        primal_knot<S, I, I::P1>(c, j + 1, vI, v.la, in.as_in());
+        store_lam<S, I>(c, j, v);
+        vI = v;
+    }
+    {
+        SlabV<F> v0;
+        slab_load<S, F>(v0, c, 0);
+        GIn<S, I> in1;
+        in1.load(a, t, 1);
+        recompute_Ft<S, I>(vI.F, v0.Cm, in1.Y, in1.H);
+        bwd_knot<F, I>(v0, vI);
+        primal_knot<S, I, I::P1>(c, 1, vI, v0.la, in1.as_in());
+        store_lam<S, F>(c, 0, v0);
+        GIn<S, F> in0;
+        in0.load(a, t, 0);
+        double none[1] = {0.0};
+        primal_knot<S, F, 0>(c, 0, v0, none, in0.as_in());
+    }
+    if (a.info && c.live) a.info[t0 + c.lane] = info;
+}
+
 template <class S> size_t slab_bytes(const KktArgs &a)
 {
     const size_t Bp = ((size_t)a.batch + 63) & ~(size_t)63;   // wave-major slab, 64 lanes/wave
@@ -1083,14 +1273,17 @@ template <class S> size_t slab_bytes(const KktArgs &a)
     return Bp * (size_t)a.N * S::SLOT * sizeof(double) + 1024;
 }
 
-template <class S>
+template <class S, bool DIRECT = false>
 hipError_t launch(const KktArgs &a, hipStream_t s)
 {
     Scratch sc;
     hipError_t e = sc.get(a, slab_bytes<S>(a), s);
     if (e != hipSuccess) return e;
     dim3 grid((unsigned)((a.batch + 63) / 64)), block(64);
-    hipLaunchKernelGGL((kkt_fil_kernel<S>), grid, block, 0, s, a, (double *)sc.p);
+    if constexpr (DIRECT)
+        hipLaunchKernelGGL((kkt_fild_kernel<S>), grid, block, 0, s, a, (double *)sc.p);
+    else
+        hipLaunchKernelGGL((kkt_fil_kernel<S>), grid, block, 0, s, a, (double *)sc.p);
     e = hipGetLastError();
     hipError_t ef = sc.release(s);
     return e != hipSuccess ? e : ef;
@@ -1106,10 +1299,16 @@ hipError_t launch(const KktArgs &a, hipStream_t s)
 #define LQRX_FIL_INST_DIAG(NX, M, A0, AK, AN)                                                            \
     template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, true>>(const KktArgs, double *__restrict__);  \
     template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, false>>(const KktArgs, double *__restrict__);
+// direct (no LDS staging) variants, diagonal H
+#define LQRX_FILD_INST(NX, M, A0, AK, AN)                                                                \
+    template __global__ void kkt_fild_kernel<Shape<NX, M, A0, AK, AN, true, true>>(const KktArgs, double *__restrict__);  \
+    template __global__ void kkt_fild_kernel<Shape<NX, M, A0, AK, AN, true, false>>(const KktArgs, double *__restrict__);
 LQRX_FIL_INST(3, 2, 3, 0, 3)
 LQRX_FIL_INST_DIAG(4, 1, 4, 0, 4)
+LQRX_FILD_INST(6, 3, 6, 1, 6)
 #undef LQRX_FIL_INST
 #undef LQRX_FIL_INST_DIAG
+#undef LQRX_FILD_INST
 
 } // namespace fil
 
@@ -1129,34 +1328,42 @@ static bool fil_dispatch(const KktArgs &a, const int32_t *n1, const int32_t *p, 
     const bool diag = a.h_mode == 2, ginv = a.ginv != 0;
 #define LQRX_FIL(NX, M, A0, AK, AN)                                                                      \
     if (nx == NX && m == M && P0 == A0 && PK == AK && PN == AN) {                                        \
-        if (diag && ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true>{});                               \
-        else if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, false, true>{});                                 \
-        else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{});                                           \
+        if (diag && ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true>{}, std::false_type{});                               \
+        else if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, false, true>{}, std::false_type{});                                 \
+        else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{}, std::false_type{});                                           \
         return true;                                                                                     \
     }
 #define LQRX_FIL_DIAG(NX, M, A0, AK, AN)                                                                 \
     if (nx == NX && m == M && P0 == A0 && PK == AK && PN == AN && (diag || !ginv)) {                     \
-        if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true>{});                                       \
-        else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{});                                           \
+        if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true>{}, std::false_type{});                                       \
+        else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{}, std::false_type{});                                           \
+        return true;                                                                                     \
+    }
+#define LQRX_FILD(NX, M, A0, AK, AN)                                                                     \
+    if (nx == NX && m == M && P0 == A0 && PK == AK && PN == AN && (diag || !ginv)) {                     \
+        if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true>{}, std::true_type{});                     \
+        else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{}, std::true_type{});                         \
         return true;                                                                                     \
     }
     LQRX_FIL(3, 2, 3, 0, 3)        // Dubins car (BASELINE cfg3), test/dubins.jl
     LQRX_FIL_DIAG(4, 1, 4, 0, 4)   // cartpole trajectory problem (test/problems.jl:58-88, device SQP)
+    LQRX_FILD(6, 3, 6, 1, 6)       // DoubleIntegrator(3) (test/problems.jl:14-56, test/cholesky_solve.jl)
 #undef LQRX_FIL
 #undef LQRX_FIL_DIAG
+#undef LQRX_FILD
     return false;
 }
 
 bool kkt_fil_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
                     const int32_t *w, hipStream_t s, hipError_t *err)
 {
-    return fil_dispatch(a, n1, p, n2, w, [&](auto shape) { *err = fil::launch<decltype(shape)>(a, s); });
+    return fil_dispatch(a, n1, p, n2, w, [&](auto shape, auto direct) { *err = fil::launch<decltype(shape), decltype(direct)::value>(a, s); });
 }
 
 bool kkt_fil_scratch_bytes(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
                            const int32_t *w, size_t *bytes)
 {
-    return fil_dispatch(a, n1, p, n2, w, [&](auto shape) { *bytes = fil::slab_bytes<decltype(shape)>(a); });
+    return fil_dispatch(a, n1, p, n2, w, [&](auto shape, auto) { *bytes = fil::slab_bytes<decltype(shape)>(a); });
 }
 
 } // namespace lqrx

@@ -132,6 +132,22 @@ struct Cartpole {
     }
 };
 
+// RobotZoo.DoubleIntegrator(D) (test/problems.jl:14-56): x = [q; q̇] ∈ R^{2D}, ẋ = [q̇; u]
+template <int D> struct DoubleIntegrator {
+    static constexpr int NX = 2 * D, NU = D;
+    template <class T> __device__ static void f(const T *x, const T *u, T *out, const double *)
+    {
+        for (int i = 0; i < D; ++i) out[i] = x[D + i], out[D + i] = u[i];
+    }
+};
+
+// a model + the number of rows PK of the linear stage constraint A_s·x_k = b_s on the interior
+// knots 1..N−2 (the LinearConstraint DoubleIntegrator() adds on 2:N−1, problems.jl:40-44;
+// 0 = none).  A_s (PK × NX, column-major) and b_s are shared by the batch.
+template <class Dyn, int PK_> struct Prob : Dyn {
+    static constexpr int PK = PK_;
+};
+
 // RobotDynamics RK3: k1 = f(x)dt, k2 = f(x + k1/2)dt, k3 = f(x − k1 + 2k2)dt,
 // x⁺ = x + (k1 + 4k2 + k3)/6 — generic in the scalar type
 template <class M, class T>
@@ -173,14 +189,31 @@ __device__ __forceinline__ void rk3_jac(const double *x, const double *u, double
 }
 
 template <class M> struct Dims {
-    static constexpr int NX = M::NX, NU = M::NU, W = NX + NU;
+    static constexpr int NX = M::NX, NU = M::NU, W = NX + NU, PK = M::PK;
+    // KKT block rows of knot k: first [C = initial state; D1], interior [D2; C = stage; D1],
+    // last [D2; C = goal]
+    __host__ __device__ static constexpr int rows(int k, int N) { return k == 0 || k == N - 1 ? 2 * NX : 2 * NX + PK; }
     __host__ __device__ static constexpr int64_t nn(int N) { return (int64_t)N * NX + (int64_t)(N - 1) * NU; }
-    __host__ __device__ static constexpr int64_t np_(int N) { return (int64_t)(N + 1) * NX; }
-    // Y: knots 0..N-2 are 2NX × W, the last 2NX × NX
-    __host__ __device__ static constexpr int64_t ny_(int N) { return 2 * NX * W * (int64_t)(N - 1) + 2 * NX * NX; }
-    __device__ static int64_t oy(int k) { return k == 0 ? 0 : (int64_t)NX * k + NX; }   // y / λ blocks
-    __device__ static int64_t om(int k) { return k == 0 ? 0 : (int64_t)NX * k; }        // [λ_{k-1}; μ_k; λ_k]
+    // multipliers = constraint rows: init NX, per interior knot PK + NX, dynamics 0 NX, goal NX
+    __host__ __device__ static constexpr int64_t np_(int N) { return (int64_t)(N + 1) * NX + (int64_t)(N - 2) * PK; }
+    __host__ __device__ static constexpr int64_t ny_(int N)
+    {
+        return 2 * NX * W + (int64_t)(N - 2) * (2 * NX + PK) * W + 2 * NX * NX;
+    }
+    __device__ static int64_t oY(int k) { return k == 0 ? 0 : 2 * NX * W + (int64_t)(k - 1) * (2 * NX + PK) * W; }
+    __device__ static int64_t oy(int k) { return k == 0 ? 0 : 2 * NX + (int64_t)(k - 1) * (PK + NX); }   // y / λ blocks
+    __device__ static int64_t om(int k) { return k == 0 ? 0 : oy(k) - NX; }        // [λ_{k-1}; μ_k; λ_k]
 };
+
+// the stage constraint values A_s·x − b_s (PK rows)
+template <class M> __device__ __forceinline__ void stage_con(const Args &A, const double *x, double *c)
+{
+    for (int r = 0; r < M::PK; ++r) {
+        double v = -A.Sb[r];
+        for (int j = 0; j < M::NX; ++j) v += A.SA[r + M::PK * j] * x[j];
+        c[r] = v;
+    }
+}
 
 // merit pieces of knot k at the point zk (+ a·dk + b·ek): cost and Σ|c| of the constraint
 // values the knot owns (knot 0: initial state + dynamics 0; knot k: dynamics k; last: goal)
@@ -215,6 +248,12 @@ __device__ __forceinline__ void knot_merit(const Args &A, int t, int k, const Kn
         rk3<M>(x, u, A.dt, xn, A.par);
         if (k == 0)
             for (int i = 0; i < NX; ++i) c1 += fabs(x[i] - A.x0[(int64_t)t * NX + i]);
+        if constexpr (M::PK > 0)
+            if (k > 0) {
+                double cs[M::PK > 0 ? M::PK : 1];
+                stage_con<M>(A, x, cs);
+                for (int r = 0; r < M::PK; ++r) c1 += fabs(cs[r]);
+            }
         for (int i = 0; i < NX; ++i) c1 += fabs(xn[i] - p.at(o + W + i));
     } else {
         for (int i = 0; i < NX; ++i) cost += 0.5 * (x[i] - xf[i]) * A.Qf[i] * (x[i] - xf[i]);
@@ -271,12 +310,12 @@ template <class M>
 __device__ void expand_knot(const Args &A, int t, int k, double &cost, double &c1, double &cinf, double &r2)
 {
     using D = Dims<M>;
-    constexpr int NX = M::NX, NU = M::NU, W = NX + NU, R2 = 2 * NX;
+    constexpr int NX = M::NX, NU = M::NU, W = NX + NU, PK = M::PK, RM = 2 * NX + PK;
     const int N = A.N;
     const int64_t NN = D::nn(N), P = D::np_(N);
     const double *z = A.Z + t * NN + (int64_t)W * k;
     const double *xf = A.xf + (int64_t)t * NX;
-    double *Y = A.Y + t * D::ny_(N) + (int64_t)R2 * W * k;
+    double *Y = A.Y + t * D::ny_(N) + D::oY(k);
     double *y = A.y + t * P + D::oy(k);
     double *H = A.H + t * NN + (int64_t)W * k;
     double *g = A.g + t * NN + (int64_t)W * k;
@@ -293,18 +332,27 @@ __device__ void expand_knot(const Args &A, int t, int k, double &cost, double &c
         for (int i = 0; i < NU; ++i) u[i] = z[NX + i];
         double xn[NX], J[NX][W];
         rk3_jac<M>(x, u, A.dt, xn, J, A.par);
-        // rows: k == 0: [C = [I 0] (initial state); D1 = J]; else [D2 = [−I 0]; D1 = J]
-        double Yk[R2][W];
-        for (int i = 0; i < NX; ++i)
-            for (int j = 0; j < W; ++j) {
-                Yk[i][j] = (i == j) ? (k == 0 ? 1.0 : -1.0) : 0.0;
-                Yk[NX + i][j] = J[i][j];
-            }
-        for (int j = 0; j < W; ++j)
-            for (int i = 0; i < R2; ++i) Y[i + R2 * j] = Yk[i][j];
+        // rows: k == 0: [C = [I 0] (initial state); D1 = J]                   (2NX rows)
+        //       else    [D2 = [−I 0]; C = [A_s 0] (stage, PK rows); D1 = J]   (2NX + PK rows)
+        const bool first = (k == 0);
+        const int R = first ? 2 * NX : RM, o1 = first ? NX : NX + PK;   // o1: first row of D1
+        for (int j = 0; j < W; ++j) {
+            double *Yj = Y + (int64_t)R * j;
+            for (int i = 0; i < NX; ++i) Yj[i] = (i == j) ? (first ? 1.0 : -1.0) : 0.0;
+            if constexpr (PK > 0)
+                if (!first)
+                    for (int q = 0; q < PK; ++q) Yj[NX + q] = j < NX ? A.SA[q + PK * j] : 0.0;
+            for (int i = 0; i < NX; ++i) Yj[o1 + i] = J[i][j];
+        }
         int r = 0;
         if (k == 0)
             for (int i = 0; i < NX; ++i) con(x[i] - A.x0[(int64_t)t * NX + i], r++);
+        if constexpr (PK > 0)
+            if (k > 0) {
+                double cs[PK > 0 ? PK : 1];
+                stage_con<M>(A, x, cs);
+                for (int q = 0; q < PK; ++q) con(cs[q], r++);
+            }
         for (int i = 0; i < NX; ++i) con(xn[i] - z[W + i], r++);
         double gk[W];
         for (int i = 0; i < NX; ++i) {
@@ -318,18 +366,23 @@ __device__ void expand_knot(const Args &A, int t, int k, double &cost, double &c
             H[NX + i] = A.R[i];
             cost += 0.5 * u[i] * A.R[i] * u[i];
         }
+        // ∇f + ∇cᵀλ restricted to z_k: g_k + Y_kᵀ m_k, from the block structure
         for (int j = 0; j < W; ++j) {
             g[j] = gk[j];
             double sres = gk[j];
-            for (int i = 0; i < R2; ++i) sres += Yk[i][j] * m[i];
+            if (j < NX) sres += first ? m[j] : -m[j];
+            if constexpr (PK > 0)
+                if (!first && j < NX)
+                    for (int q = 0; q < PK; ++q) sres += A.SA[q + PK * j] * m[NX + q];
+            for (int i = 0; i < NX; ++i) sres += J[i][j] * m[o1 + i];
             r2 += sres * sres;
         }
     } else {
         // last knot: [D2 = −I; C = I (goal)], 2NX × NX
         for (int j = 0; j < NX; ++j)
             for (int i = 0; i < NX; ++i) {
-                Y[i + R2 * j] = (i == j) ? -1.0 : 0.0;
-                Y[NX + i + R2 * j] = (i == j) ? 1.0 : 0.0;
+                Y[i + 2 * NX * j] = (i == j) ? -1.0 : 0.0;
+                Y[NX + i + 2 * NX * j] = (i == j) ? 1.0 : 0.0;
             }
         for (int i = 0; i < NX; ++i) con(x[i] - xf[i], i);
         for (int i = 0; i < NX; ++i) {
@@ -401,6 +454,11 @@ template <class M> __global__ __launch_bounds__(64 * TPB) void sqp_ls1_kernel(co
             int r = 0;
             if (k == 0)
                 for (int i = 0; i < NX; ++i) yk[r++] = x[i] - A.x0[t * NX + i];
+            if constexpr (M::PK > 0)
+                if (k > 0) {
+                    stage_con<M>(A, x, yk);
+                    r += M::PK;
+                }
             for (int i = 0; i < NX; ++i) yk[r++] = xn[i] - p1.at(o + W + i);
         } else {
             for (int i = 0; i < NX; ++i) yk[i] = x[i] - A.xf[t * NX + i];
@@ -485,17 +543,20 @@ bool sqp_model_dims(int model, int *nx, int *nu)
     switch (model) {
     case SQP_DUBINS: *nx = sqp::Dubins::NX, *nu = sqp::Dubins::NU; return true;
     case SQP_CARTPOLE: *nx = sqp::Cartpole::NX, *nu = sqp::Cartpole::NU; return true;
+    case SQP_DI1: *nx = 2, *nu = 1; return true;
+    case SQP_DI2: *nx = 4, *nu = 2; return true;
+    case SQP_DI3: *nx = 6, *nu = 3; return true;
     default: return false;
     }
 }
 
 // the structure tables of the trajectory KKT (ConstraintBlocks, conblocks.jl:403-425):
-// knot 0 (0, NX, NX, NX+NU), interior (NX, 0, NX, NX+NU), last (NX, NX, 0, NX)
-void sqp_structure(int nx, int nu, int N, std::vector<int32_t> &n1, std::vector<int32_t> &p,
+// knot 0 (0, NX, NX, NX+NU), interior (NX, PK, NX, NX+NU), last (NX, NX, 0, NX)
+void sqp_structure(int nx, int nu, int pk, int N, std::vector<int32_t> &n1, std::vector<int32_t> &p,
                    std::vector<int32_t> &n2, std::vector<int32_t> &w)
 {
     n1.assign(N, nx);
-    p.assign(N, 0);
+    p.assign(N, pk);
     n2.assign(N, nx);
     w.assign(N, nx + nu);
     n1[0] = 0;
@@ -505,14 +566,31 @@ void sqp_structure(int nx, int nu, int N, std::vector<int32_t> &n1, std::vector<
     w[N - 1] = nx;
 }
 
+namespace {
+template <class Dyn>
+hipError_t run_pk(const SqpArgs &A, int max_iters, hipStream_t s, int (*kkt)(void *, int, double *), void *ctx,
+                  int *kkt_rc)
+{
+    switch (A.stage_rows) {
+    case 0: return sqp::run<sqp::Prob<Dyn, 0>>(A, max_iters, s, kkt, ctx, kkt_rc);
+    case 1: return sqp::run<sqp::Prob<Dyn, 1>>(A, max_iters, s, kkt, ctx, kkt_rc);
+    case 2: return sqp::run<sqp::Prob<Dyn, 2>>(A, max_iters, s, kkt, ctx, kkt_rc);
+    default: return hipErrorInvalidValue;
+    }
+}
+} // namespace
+
 // Device driver (lqrx_api.cpp validates and calls this).  kkt(ctx, ginv, dz) runs one KKT
 // solve of the trajectory structure on Y, y, H, g → dz, lamn; a negative return stops the loop.
 hipError_t sqp_run(const SqpArgs &A, int max_iters, hipStream_t s, int (*kkt)(void *ctx, int ginv, double *dz),
                    void *ctx, int *kkt_rc)
 {
     switch (A.model) {
-    case SQP_DUBINS: return sqp::run<sqp::Dubins>(A, max_iters, s, kkt, ctx, kkt_rc);
-    case SQP_CARTPOLE: return sqp::run<sqp::Cartpole>(A, max_iters, s, kkt, ctx, kkt_rc);
+    case SQP_DUBINS: return run_pk<sqp::Dubins>(A, max_iters, s, kkt, ctx, kkt_rc);
+    case SQP_CARTPOLE: return run_pk<sqp::Cartpole>(A, max_iters, s, kkt, ctx, kkt_rc);
+    case SQP_DI1: return run_pk<sqp::DoubleIntegrator<1>>(A, max_iters, s, kkt, ctx, kkt_rc);
+    case SQP_DI2: return run_pk<sqp::DoubleIntegrator<2>>(A, max_iters, s, kkt, ctx, kkt_rc);
+    case SQP_DI3: return run_pk<sqp::DoubleIntegrator<3>>(A, max_iters, s, kkt, ctx, kkt_rc);
     default: return hipErrorInvalidValue;
     }
 }

@@ -53,10 +53,10 @@ class TrajSqpDesc(C.Structure):
     """Mirror of ``lqrx_sqp_desc``."""
 
     _fields_ = [
-        ("model", C.c_int32), ("N", C.c_int32), ("max_iters", C.c_int32), ("reserved", C.c_int32),
+        ("model", C.c_int32), ("N", C.c_int32), ("max_iters", C.c_int32), ("stage_rows", C.c_int32),
         ("batch", C.c_int64), ("dt", C.c_double), ("Q", C.c_double * 8), ("R", C.c_double * 8),
         ("Qf", C.c_double * 8), ("params", C.c_double * 4), ("mu", C.c_double),
-        ("tol_p", C.c_double), ("tol_d", C.c_double),
+        ("tol_p", C.c_double), ("tol_d", C.c_double), ("stage_A", C.c_double * 32), ("stage_b", C.c_double * 4),
     ]
 
 

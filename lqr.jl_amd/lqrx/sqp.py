@@ -1,7 +1,8 @@
 """Batched trajectory-optimisation SQP on the device (SURVEY.md §8(f) ranks 2–3) — host
 mirror of the reference's CholeskySolver outer loop around the KKT path, for the reference's
-test models: the Dubins car (test/dubins_sqp.jl, BASELINE cfg3) and the cartpole
-(test/problems.jl:58-88 Cartpole(), test/cartpole.jl).
+test models: the Dubins car (test/dubins_sqp.jl, BASELINE cfg3), the cartpole
+(test/problems.jl:58-88 Cartpole(), test/cartpole.jl) and the double integrator with its
+interior-knot linear constraint (test/problems.jl:14-56 DoubleIntegrator(D)).
 
 Reference (Julia, /root/reference):
   solve!/step!: ≤ 10 steps, convergence before each step   src/cholesky_solver.jl:109-153
@@ -20,13 +21,14 @@ import numpy as np
 
 from . import _lib
 
-__all__ = ["SQPProblem", "DubinsSQP", "CartpoleSQP", "sqp_solve", "sqp_solve_device", "dubins_sqp_solve",
+__all__ = ["SQPProblem", "DubinsSQP", "CartpoleSQP", "DoubleIntegratorSQP", "sqp_solve", "sqp_solve_device", "dubins_sqp_solve",
            "dubins_sqp_solve_device", "CONVERGED", "LIMIT", "LS_FAILED", "MODEL_DUBINS", "MODEL_CARTPOLE",
            "model_dims", "num_vars", "num_multipliers", "cartpole_rollout_guess"]
 
 CONVERGED, LIMIT, LS_FAILED = 0, 1, 2
 MODEL_DUBINS, MODEL_CARTPOLE = 0, 1           # LQRX_MODEL_*
-_DIMS = {MODEL_DUBINS: (3, 2), MODEL_CARTPOLE: (4, 1)}
+MODEL_DOUBLE_INTEGRATOR = {1: 2, 2: 3, 3: 4}  # D → LQRX_MODEL_DOUBLE_INTEGRATOR{D}
+_DIMS = {MODEL_DUBINS: (3, 2), MODEL_CARTPOLE: (4, 1), 2: (2, 1), 3: (4, 2), 4: (6, 3)}
 CARTPOLE_PARAMS = (1.0, 0.2, 0.5, 9.81)       # RobotZoo.Cartpole(): mc, mp, l, g
 
 
@@ -43,9 +45,9 @@ def num_vars(N: int, model: int = MODEL_DUBINS) -> int:
     return N * n + (N - 1) * m
 
 
-def num_multipliers(N: int, model: int = MODEL_DUBINS) -> int:
-    """initial state + N−1 dynamics + goal, n rows each."""
-    return model_dims(model)[0] * (N + 1)
+def num_multipliers(N: int, model: int = MODEL_DUBINS, stage_rows: int = 0) -> int:
+    """initial state + N−1 dynamics + goal, n rows each, + the stage rows of knots 2..N−1."""
+    return model_dims(model)[0] * (N + 1) + stage_rows * (N - 2)
 
 
 @dataclass
@@ -64,6 +66,12 @@ class SQPProblem:
     max_iters: int = 10        # cholesky_solver.jl:111
     tol_p: float = 1e-5        # :131-132
     tol_d: float = 1e-5
+    stage_A: tuple = ()        # A_s (stage_rows × n) rows, shared by the batch; () = none
+    stage_b: tuple = ()
+
+    @property
+    def stage_rows(self) -> int:
+        return len(self.stage_b)
 
     @property
     def n(self) -> int:
@@ -78,8 +86,11 @@ class SQPProblem:
         if len(self.Q) != n or len(self.Qf) != n or len(self.R) != m:
             raise ValueError(f"Q, Qf need {n} entries and R {m} for model {self.model}")
         pad = lambda v: (C.c_double * 8)(*v)
-        return _lib.TrajSqpDesc(self.model, self.N, self.max_iters, 0, batch, self.dt, pad(self.Q), pad(self.R),
-                                pad(self.Qf), (C.c_double * 4)(*self.params), self.mu, self.tol_p, self.tol_d)
+        pk = self.stage_rows
+        SA = np.asarray(self.stage_A, float).reshape(pk, n) if pk else np.zeros((0, n))
+        return _lib.TrajSqpDesc(self.model, self.N, self.max_iters, pk, batch, self.dt, pad(self.Q), pad(self.R),
+                                pad(self.Qf), (C.c_double * 4)(*self.params), self.mu, self.tol_p, self.tol_d,
+                                (C.c_double * 32)(*SA.T.ravel()), (C.c_double * 4)(*self.stage_b))
 
 
 def DubinsSQP(N: int, dt: float, Q=(1e-2,) * 3, R=(1e-1,) * 2, Qf=(100.0,) * 3, mu=1.0, max_iters=10,
@@ -93,6 +104,22 @@ def CartpoleSQP(N: int = 101, tf: float = 5.0, Q=(1e-2,) * 4, R=(1e-1,), Qf=(100
     """Cartpole() of test/problems.jl:58-88: Q = 1e-2·I, R = 1e-1·I, Qf = 100·I, dt = tf/(N−1)."""
     return SQPProblem(MODEL_CARTPOLE, N, tf / (N - 1), tuple(Q), tuple(R), tuple(Qf), tuple(params), mu,
                       max_iters, tol_p, tol_d)
+
+
+def DoubleIntegratorSQP(D: int = 3, N: int = 101, stage_A=None, stage_b=None, tf: float = 2.0, mu=10.0,
+                        max_iters=10, tol_p=1e-5, tol_d=1e-5) -> SQPProblem:
+    """DoubleIntegrator(D, N) of test/problems.jl:14-56: Q = diag(10·1_D, 1_D), R = 0.1·I,
+    Qf = 10Q, dt = (N−1)/tf as the reference writes it (:19), and the planar LinearConstraint
+    A_s x = b_s (p = max(D−2, 1) rows; the reference draws A_s = [rand(p,D) rand(p,D)], b = 0)
+    on knots 2:N−1.  x0 = [1_D; 0_D] and xf = 0 are the solve's per-trajectory inputs."""
+    Q = (10.0,) * D + (1.0,) * D
+    p = max(D - 2, 1)
+    if stage_A is None:
+        stage_A = np.random.default_rng(1).random((p, 2 * D))
+    stage_A = np.asarray(stage_A, float)
+    stage_b = np.zeros(stage_A.shape[0]) if stage_b is None else np.asarray(stage_b, float)
+    return SQPProblem(MODEL_DOUBLE_INTEGRATOR[D], N, (N - 1) / tf, Q, (0.1,) * D, tuple(10.0 * q for q in Q),
+                      (0.0,) * 4, mu, max_iters, tol_p, tol_d, tuple(stage_A.ravel()), tuple(stage_b))
 
 
 def _ptr(a):
@@ -109,7 +136,7 @@ def sqp_solve(prob: SQPProblem, Z0, x0, xf) -> dict:
         raise ValueError(f"Z0 has {Z.shape[1]} columns, the problem {num_vars(prob.N, prob.model)}")
     x0 = np.ascontiguousarray(np.broadcast_to(x0, (bt, n)), dtype=np.float64)
     xf = np.ascontiguousarray(np.broadcast_to(xf, (bt, n)), dtype=np.float64)
-    lam = np.zeros((bt, num_multipliers(prob.N, prob.model)))
+    lam = np.zeros((bt, num_multipliers(prob.N, prob.model, prob.stage_rows)))
     it = np.zeros(bt, np.int32)
     st = np.zeros(bt, np.int32)
     _lib.check(lib.lqrx_sqp_solve_host(C.byref(prob.desc(bt)), _ptr(Z), _ptr(x0), _ptr(xf), _ptr(lam), _ptr(it),

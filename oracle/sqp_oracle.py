@@ -64,8 +64,14 @@ class Model:
         self.name, self.nx, self.nu, self.f, self.model_id, self.params = name, nx, nu, f, model_id, params
 
 
+def double_integrator(D):
+    """RobotZoo.DoubleIntegrator(D): x = [q; q̇], ẋ = [q̇; u]."""
+    return lambda x, u: np.concatenate([x[D:2 * D], u])
+
+
 DUBINS = Model("dubins", 3, 2, dubins, 0)
 CARTPOLE = Model("cartpole", 4, 1, cartpole, 1, CARTPOLE_PARAMS)
+DOUBLE_INTEGRATOR = {D: Model(f"double_integrator{D}", 2 * D, D, double_integrator(D), 1 + D) for D in (1, 2, 3)}
 
 
 def rk3(x, u, dt, model=DUBINS):
@@ -102,14 +108,24 @@ def rollout(model, x0, U, dt):
 class TrajSQP:
     """One trajectory's NLP, variables in the reference's order z = [x₁; u₁; …; x_{N-1}; u_{N-1}; x_N]."""
 
-    def __init__(self, N, dt, Q, R, Qf, x0, xf, mu=1.0, model=DUBINS):
+    def __init__(self, N, dt, Q, R, Qf, x0, xf, mu=1.0, model=DUBINS, stage=None):
+        """stage = (A_s, b_s): the linear constraint A_s x_k = b_s on the interior knots
+        k = 2..N−1 (1-based; DoubleIntegrator()'s LinearConstraint, problems.jl:40-44)."""
         self.model = model
         self.nx, self.nu = model.nx, model.nu
         self.N, self.dt, self.mu = N, dt, mu
         self.Q, self.R, self.Qf = (np.asarray(v, float) for v in (Q, R, Qf))
         self.x0, self.xf = np.asarray(x0, float), np.asarray(xf, float)
+        if stage is None:
+            stage = (np.zeros((0, self.nx)), np.zeros(0))
+        self.SA, self.Sb = np.asarray(stage[0], float).reshape(-1, self.nx), np.asarray(stage[1], float)
+        self.pk = self.SA.shape[0]
         self.NN = N * self.nx + (N - 1) * self.nu
-        self.P = (N + 1) * self.nx
+        self.P = (N + 1) * self.nx + (N - 2) * self.pk
+
+    def oy(self, k):
+        """start of knot k's constraint block [c_k; d_k] (the KKT y / λ order)."""
+        return 0 if k == 0 else 2 * self.nx + (k - 1) * (self.pk + self.nx)
 
     def split(self, z):
         NX, NU = self.nx, self.nu
@@ -139,21 +155,26 @@ class TrajSQP:
         return np.concatenate([np.concatenate([self.Q, self.R])] * (self.N - 1) + [self.Qf])
 
     def c(self, z):
+        """[x₁ − x0; dyn₁; (A_s x_k − b_s; dyn_k) for k = 2..N−1; x_N − xf]"""
         X, U = self.split(z)
         v = [X[0] - self.x0]
         for k in range(self.N - 1):
+            if k > 0:
+                v.append(self.SA @ X[k] - self.Sb)
             v.append(rk3(X[k], U[k], self.dt, self.model) - X[k + 1])
         v.append(X[-1] - self.xf)
         return np.concatenate(v)
 
     def jac(self, z):
         X, U = self.split(z)
-        NX = self.nx
+        NX, PK = self.nx, self.pk
         A = np.zeros((self.P, self.NN))
         w = NX + self.nu
         A[:NX, :NX] = np.eye(NX)
         for k in range(self.N - 1):
-            r = NX * (k + 1)
+            r = NX if k == 0 else self.oy(k) + PK          # dynamics rows of knot k
+            if k > 0:
+                A[self.oy(k):self.oy(k) + PK, k * w:k * w + NX] = self.SA
             A[r:r + NX, k * w:(k + 1) * w] = rk3_jac(X[k], U[k], self.dt, self.model)
             A[r:r + NX, (k + 1) * w:(k + 1) * w + NX] = -np.eye(NX)
         A[-NX:, (self.N - 1) * w:] = np.eye(NX)
@@ -216,6 +237,26 @@ def cartpole_problem(N, mu=1.0, x0=(0.0, 0.0, 0.0, 0.0), xf=(0.0, np.pi, 0.0, 0.
     return p, z
 
 
+def double_integrator_problem(D=3, N=101, mu=1.0, seed=1, x0=None, xf=None):
+    """DoubleIntegrator(D, N) of test/problems.jl:14-56: Q = diag(10·1_D, 1_D), R = 0.1·I,
+    Qf = 10Q, x0 = [1_D; 0_D], xf = 0, dt = (N−1)/tf with tf = 2 (as the reference writes it,
+    :19), the planar LinearConstraint A = [rand(p,D) rand(p,D)], b = 0, p = max(D−2, 1) on
+    knots 2:N−1 (Julia's rand stream is not reproducible here: A from a seeded numpy draw) and
+    the goal.  Initial guess: zeros (the reference's Problem holds no trajectory for it).
+    Returns (TrajSQP, z0)."""
+    model = DOUBLE_INTEGRATOR[D]
+    tf = 2.0
+    dt = (N - 1) / tf
+    p = max(D - 2, 1)
+    rng = np.random.default_rng(seed)
+    SA = rng.random((p, 2 * D))
+    Q = [10.0] * D + [1.0] * D
+    x0 = np.concatenate([np.ones(D), np.zeros(D)]) if x0 is None else x0
+    xf = np.zeros(2 * D) if xf is None else xf
+    prob = TrajSQP(N, dt, Q, [0.1] * D, [10.0 * q for q in Q], x0, xf, mu, model, (SA, np.zeros(p)))
+    return prob, np.zeros(prob.NN)
+
+
 def solve(prob: TrajSQP, z0, iters=10, tol_p=1e-5, tol_d=1e-5):
     """CholeskySolver.solve! loop (cholesky_solver.jl:109-153).  Returns dict z, lam, iters
     (steps taken), status (0 converged, 1 iteration limit, 2 line search failed), hist
@@ -260,14 +301,15 @@ def assemble(prob: TrajSQP, z):
     126-132), cut from the dense ∇c, c, ∇²f, ∇f above.  Knot k's rows are the constraints
     [λ_{k-1}; μ_k; λ_k] = c[mk : mk+2n], mk = 0 (k = 0) or n·k; its columns are z_k."""
     A, c, g, h = prob.jac(z), prob.c(z), prob.grad(z), prob.hess_diag()
-    N, NX, W = prob.N, prob.nx, prob.nx + prob.nu
+    N, NX, W, PK = prob.N, prob.nx, prob.nx + prob.nu, prob.pk
     Y, y, H, G = [], [], [], []
     for k in range(N):
         w = W if k < N - 1 else NX
-        mk = 0 if k == 0 else NX * k
-        Y.append(A[mk:mk + 2 * NX, W * k:W * k + w].T.ravel())     # column-major
-        oy = 0 if k == 0 else NX * k + NX
-        y.append(c[oy:oy + (2 * NX if k == 0 else NX)])
+        rows = 2 * NX if k in (0, N - 1) else 2 * NX + PK
+        mk = 0 if k == 0 else prob.oy(k) - NX
+        Y.append(A[mk:mk + rows, W * k:W * k + w].T.ravel())     # column-major
+        oy = prob.oy(k)
+        y.append(c[oy:oy + (2 * NX if k == 0 else NX if k == N - 1 else PK + NX)])
         H.append(h[W * k:W * k + w])
         G.append(g[W * k:W * k + w])
     return tuple(np.concatenate(v) for v in (Y, y, H, G))

@@ -69,7 +69,7 @@ def test_sqp_desc_validation(lqrx):
 
     lib = lqrx.load()
     for field, val in (("N", 1), ("dt", 0.0), ("max_iters", -1), ("mu", -1.0), ("batch", -1), ("model", 7),
-                       ("reserved", 1)):
+                       ("stage_rows", 3)):
         d = Q.DubinsSQP(11, 0.3).desc(4)
         setattr(d, field, val)
         assert lib.lqrx_sqp_solve(C.byref(d), *([None] * 6), None) == -1, field
@@ -90,10 +90,17 @@ def test_sqp_desc_validation(lqrx):
     old.R[1] = 1.0
     old.batch = 0
     assert lib.lqrx_dubins_sqp_solve(C.byref(old), *([None] * 6), None) == 0
+    d = Q.DoubleIntegratorSQP(3, 11).desc(2)
+    d.stage_rows = 3                                                    # > 2
+    assert lib.lqrx_sqp_solve(C.byref(d), *([None] * 6), None) == -1
+    d = Q.DoubleIntegratorSQP(3, 11).desc(2)
+    d.stage_A[0] = float("nan")
+    assert lib.lqrx_sqp_solve(C.byref(d), *([None] * 6), None) == -1
     nx, nu = C.c_int32(), C.c_int32()
     assert lib.lqrx_sqp_model_dims(1, C.byref(nx), C.byref(nu)) == 0 and (nx.value, nu.value) == (4, 1)
     assert lib.lqrx_sqp_model_dims(0, C.byref(nx), C.byref(nu)) == 0 and (nx.value, nu.value) == (3, 2)
-    assert lib.lqrx_sqp_model_dims(2, C.byref(nx), C.byref(nu)) == -1
+    assert lib.lqrx_sqp_model_dims(4, C.byref(nx), C.byref(nu)) == 0 and (nx.value, nu.value) == (6, 3)
+    assert lib.lqrx_sqp_model_dims(5, C.byref(nx), C.byref(nu)) == -1
 
 
 # ---------------------------------------------------------------- cartpole (problems.jl:58-88)
@@ -230,6 +237,74 @@ def test_sqp_gpu_line_search_paths(lqrx, gpu_ok, N, mu):
            if got["status"][b] != r["status"] or got["iters"][b] != r["iters"]
            or np.abs(got["z"][b] - r["z"]).max() > 1e-9 * np.abs(r["z"]).max()]
     assert not bad, bad
+
+
+# ---------------------------------------------------------------- DoubleIntegrator (problems.jl:14-56)
+def _double_integrator(D, N, mu, seed, batch):
+    """DoubleIntegrator(D, N) per trajectory, x0 = [1_D; 0_D] for trajectory 0 and perturbed
+    for the others; the shared stage matrix of lqrx.sqp.DoubleIntegratorSQP."""
+    import lqrx.sqp as Q
+
+    prob = Q.DoubleIntegratorSQP(D, N, mu=mu)
+    SA = np.asarray(prob.stage_A).reshape(prob.stage_rows, 2 * D)
+    rng = np.random.default_rng(seed)
+    probs, Z0, x0s, xfs = [], [], [], []
+    for b in range(batch):
+        x0 = np.concatenate([np.ones(D), np.zeros(D)]) + (0.2 * rng.standard_normal(2 * D) if b else 0.0)
+        p, z0 = S.double_integrator_problem(D, N, mu=mu, x0=x0)
+        p.SA = SA
+        probs.append(p), Z0.append(z0 + (0.1 * rng.standard_normal(z0.shape) if b % 2 else 0.0))
+        x0s.append(x0), xfs.append(np.zeros(2 * D))
+    return prob, probs, np.stack(Z0), np.stack(x0s), np.stack(xfs)
+
+
+@pytest.mark.parametrize("D,N", [(2, 12), (3, 21)])
+def test_double_integrator_assembly_matches_kkt_oracle(D, N):
+    """The stage-constrained assembly (Y_k = [D2; C; D1] with C = A_s on knots 2..N−1) fed to
+    the KAT-pinned block KKT oracle on the DoubleIntegrator structure reproduces the dense
+    Newton step — the structure test/cholesky_solve.jl pins (its problem)."""
+    import lqrx.kkt as K
+
+    _, probs, Z0, _, _ = _double_integrator(D, N, 10.0, 0, 2)
+    st = K.double_integrator_structure(D, N)
+    sto = orc.KktStructure(2 * D, D, N, st.p)
+    rng = np.random.default_rng(2)
+    for b, p in enumerate(probs):
+        z = Z0[b] + 0.1 * rng.standard_normal(Z0.shape[1])
+        dz, lam = p.newton(z)
+        Y, y, H, g = S.assemble(p, z)
+        r = orc.kkt_solve_batch(sto, 1, Y[None], y[None], H[None], g[None], h_mode=2, ginv=1, nthreads=1)
+        assert np.abs(r["dz"].ravel() - dz).max() <= 1e-9 * np.abs(dz).max()
+        assert np.abs(r["lam"].ravel() - lam).max() <= 1e-8 * np.abs(lam).max()
+
+
+def test_double_integrator_oracle_behaviour():
+    """A linear-quadratic problem: with μ = 10 the first full Newton step is the optimum
+    (converged at the next check); with μ = 1 the L1 merit is inexact and the line search fails."""
+    _, probs, Z0, _, _ = _double_integrator(3, 21, 10.0, 1, 2)
+    for p, z0 in zip(probs, Z0):
+        r = S.solve(p, z0)
+        assert r["status"] == 0 and r["iters"] == 1
+    _, probs, Z0, _, _ = _double_integrator(3, 21, 1.0, 1, 1)
+    assert S.solve(probs[0], Z0[0])["status"] == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,N,mu,batch", [(3, 101, 10.0, 4), (2, 12, 10.0, 67), (3, 21, 1.0, 3)])
+def test_double_integrator_sqp_gpu_parity(lqrx, gpu_ok, D, N, mu, batch):
+    """Device SQP with the interior-knot linear constraint (stage rows in the KKT blocks, the
+    generic KKT kernel) against the oracle: status, steps, z, λ (relative 1e-8: dt = (N−1)/tf
+    as the reference writes it makes the D = 3, N = 101 system ill-conditioned)."""
+    import lqrx.sqp as Q
+
+    prob, probs, Z0, x0, xf = _double_integrator(D, N, mu, 5, batch)
+    got = Q.sqp_solve(prob, Z0, x0, xf)
+    for b in sorted({0, 1, batch // 2, batch - 1}):
+        r = S.solve(probs[b], Z0[b])
+        assert got["status"][b] == r["status"] and got["iters"][b] == r["iters"], (b, got["status"][b], r["status"])
+        assert np.abs(got["z"][b] - r["z"]).max() <= 1e-8 * np.abs(r["z"]).max()
+        if r["iters"]:
+            assert np.abs(got["lam"][b] - r["lam"]).max() <= 1e-8 * np.abs(r["lam"]).max()
 
 
 def _cartpole_gpu(N, mu, seed, batch, goal, tf, iters=10):
