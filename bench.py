@@ -494,6 +494,23 @@ def main():
                         "alg_bytes_per_launch": ab, "min_traffic_bytes_per_launch": min_traffic,
                         "min_traffic_frac": min_traffic / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                         "fp64_tflops": achieved, "fp64_frac": achieved / peak}
+            elif n <= 4 and m <= 4:
+                # n ≤ 4 (cfg2 cartpole): AI ≈ 6 flop/B is below the ridge, so the roofline is
+                # HBM — but the launch is latency-bound: 4 (quad) or 1 (lane) lanes per
+                # trajectory give B·lanes/64 waves, at most one per CU for B ≤ 16384, each
+                # running a serial N-knot chain; report that beside the HBM fraction
+                ab = dp_bytes_per_traj(n, m, N, 8 if f64 else 4, False) * bt
+                hbm = ab / (kern_ms * 1e-3) / 1e9
+                kname = _dp_kernel_name(n, m, bt, False)
+                waves = -(-bt * (4 if kname == "dp_quad_kernel" else 1) // 64)
+                roof = {"bound": "hbm", "achieved": hbm, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": hbm / PEAK_HBM_GBS, "traffic": traffic, "kernel": kname,
+                        "kernel_ms": kern_ms, "alg_bytes_per_launch": ab,
+                        "fp64_tflops": achieved, "fp64_frac": achieved / peak,
+                        "latency_bound": {"waves": waves, "cus": 256, "waves_per_cu": waves / 256,
+                                          "knot_chain_us": kern_ms * 1e3 / N,
+                                          "note": "one serial N-knot chain per wave; the chip holds "
+                                                  "the whole batch at <= 1 wave per CU"}}
             headline = (n, m, N, bt, args.dtype) == (32, 16, 256, 65536, "f64") and not args.tv
             if args.workload == "cartpole":
                 metric = f"LQR trajectories/sec (Riccati bwd+fwd), cartpole n=4 m=1 N={N} B={bt}"

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define LQRX_ABI_VERSION 1
+#define LQRX_ABI_VERSION 2   /* 2: layout 1, lqrx_sqp_* (models, stage constraints) */
 
 #define LQRX_F64 0
 #define LQRX_F32 1

@@ -158,6 +158,46 @@ function ls_solve!(U::Matrix{Float64}, X::Matrix{Float64}, info::Vector{Int32},
     return check(rc)
 end
 
-export LQRProblem, LQRSolution, LQRBatch, DPSolver, solve!, kkt_solve!, ls_solve!
+# ---- trajectory SQP: lqrx_sqp_desc ----
+struct SqpDesc
+    model::Int32; N::Int32; max_iters::Int32; stage_rows::Int32
+    batch::Int64
+    dt::Float64
+    Q::NTuple{8,Float64}; R::NTuple{8,Float64}; Qf::NTuple{8,Float64}; params::NTuple{4,Float64}
+    mu::Float64; tol_p::Float64; tol_d::Float64
+    stage_A::NTuple{32,Float64}; stage_b::NTuple{4,Float64}
+end
+const MODEL_DUBINS, MODEL_CARTPOLE = Int32(0), Int32(1)
+model_double_integrator(D) = Int32(1 + D)
+pad(v, n) = ntuple(i -> i <= length(v) ? Float64(v[i]) : 0.0, n)
+
+"""
+    sqp_solve!(Z, lam, iters, status, x0, xf; model, N, dt, Q, R, Qf, params=(), mu=1,
+               max_iters=10, tol_p=1e-5, tol_d=1e-5, stage_A=zeros(0,0), stage_b=Float64[])
+
+CholeskySolver.solve! (src/cholesky_solver.jl:109-164) with the L1-merit line search of
+test/dubins_sqp.jl:74-97 for a batch of trajectory problems of one model (Dubins car,
+cartpole, DoubleIntegrator(D)); Z (N·n + (N−1)·m, batch) in/out, x0/xf (n, batch),
+Q/R/Qf the diagonals of the LQRObjective, stage_A/stage_b the LinearConstraint of
+DoubleIntegrator() on knots 2:N−1 (test/problems.jl:40-44).
+"""
+function sqp_solve!(Z::Matrix{Float64}, lam::Matrix{Float64}, iters::Vector{Int32},
+                    status::Vector{Int32}, x0::Matrix{Float64}, xf::Matrix{Float64};
+                    model::Integer, N::Integer, dt::Real, Q, R, Qf, params=(), mu::Real=1.0,
+                    max_iters::Integer=10, tol_p::Real=1e-5, tol_d::Real=1e-5,
+                    stage_A::Matrix{Float64}=zeros(0, 0), stage_b::Vector{Float64}=Float64[])
+    d = Ref(SqpDesc(model, N, max_iters, length(stage_b), size(Z, 2), dt, pad(Q, 8), pad(R, 8),
+                    pad(Qf, 8), pad(params, 4), mu, tol_p, tol_d, pad(vec(stage_A), 32),
+                    pad(stage_b, 4)))
+    GC.@preserve Z lam iters status x0 xf begin
+        rc = ccall((:lqrx_sqp_solve_host, liblqrx), Cint,
+                   (Ref{SqpDesc}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                    Ptr{Int32}, Ptr{Int32}),
+                   d, Z, x0, xf, lam, iters, status)
+    end
+    return check(rc)
+end
+
+export LQRProblem, LQRSolution, LQRBatch, DPSolver, solve!, kkt_solve!, ls_solve!, sqp_solve!
 
 end # module

@@ -18,7 +18,7 @@ def test_exports_every_header_symbol(lqrx):
 
 
 def test_abi_version(lqrx):
-    assert lqrx.load().lqrx_abi_version() == 1
+    assert lqrx.load().lqrx_abi_version() == 2
 
 
 @pytest.mark.parametrize("field,val,code", [("n", 0, -1), ("m", 0, -1), ("N", 1, -1),
