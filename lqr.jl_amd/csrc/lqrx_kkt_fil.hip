@@ -32,7 +32,9 @@ namespace lqrx {
 namespace fil {
 
 #ifndef LQRX_FIL_ABL
-#define LQRX_FIL_ABL 0   // ablation builds for tools/ only (1: forward sweep alone)
+#define LQRX_FIL_ABL 0   // ablation builds for tools/ only (bits: 1 forward sweep alone, 2 Schur
+                         // from one column, 4 no F̃ recompute, 8 primal without Yᵀm, 16 no
+                         // hand-placed VMEM waits, 32 no forward slab stores)
 #endif
 #ifndef LQRX_FIL_N12
 #define LQRX_FIL_N12 1   // 12-byte LDS-DMA pieces for the short chunks (0: dwords only)
@@ -319,6 +321,15 @@ __device__ __forceinline__ void bstore(double v, rsrc_t r, uint32_t vo, uint32_t
 {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2_t, v), r, vo, so, 0);
 }
+// the forward sweep's slab stores (an ablation build can drop them)
+__device__ __forceinline__ void sstore(double v, rsrc_t r, uint32_t vo, uint32_t so)
+{
+#if LQRX_FIL_ABL & 32
+    (void)v, (void)r, (void)vo, (void)so;
+#else
+    bstore(v, r, vo, so);
+#endif
+}
 __device__ __forceinline__ double bload(rsrc_t r, uint32_t vo, uint32_t so)
 {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
@@ -328,7 +339,12 @@ __device__ __forceinline__ double bload(rsrc_t r, uint32_t vo, uint32_t so)
 template <int N> __device__ __forceinline__ void vm_wait()
 {
     constexpr int n = N > 63 ? 63 : (N < 0 ? 0 : N);
+#if LQRX_FIL_ABL & 16
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // ablation: no VMEM waits (wrong results)
+    (void)n;
+#else
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(n) : "memory");
+#endif
 }
 
 // ------------------------------------------------------------------ small dense kernels
@@ -417,7 +433,7 @@ __device__ __forceinline__ bool compute_shur(Shur<C> &s, const double (&Y)[S::te
     if constexpr (!S::GINV || S::HDIAG) {
         // stream Y column by column: S += y_j h_j y_jᵀ, r += y_j h_j g_j  (h = 1/H_jj)
 #pragma unroll
-        for (int j = 0; j < W; ++j) {
+        for (int j = 0; j < ((LQRX_FIL_ABL & 2) ? 1 : W); ++j) {
             double v[R], vh[R];
 #pragma unroll
             for (int i = 0; i < R; ++i) v[i] = Y[i + j * R];
@@ -590,23 +606,23 @@ __device__ __forceinline__ void factor_knot(int k, const Shur<C> &sc, const doub
 #pragma unroll
     for (int i = 0; i < ps; ++i)
 #pragma unroll
-        for (int j = i; j < ps; ++j) bstore(Bm[i][j], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
+        for (int j = i; j < ps; ++j) sstore(Bm[i][j], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
 #pragma unroll
     for (int i = 0; i < p2; ++i)
 #pragma unroll
-        for (int j = i; j < p2; ++j) bstore(Cm[i][j], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
+        for (int j = i; j < p2; ++j) sstore(Cm[i][j], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
 #pragma unroll
     for (int i = 0; i < p1; ++i)
 #pragma unroll
-        for (int j = 0; j < ps; ++j) bstore(D[i][j], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
+        for (int j = 0; j < ps; ++j) sstore(D[i][j], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
 #pragma unroll
     for (int i = 0; i < ps; ++i)
 #pragma unroll
-        for (int j = 0; j < p2; ++j) bstore(E[i][j], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
+        for (int j = 0; j < p2; ++j) sstore(E[i][j], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
 #pragma unroll
-    for (int i = 0; i < ps; ++i) bstore(mu[i], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
+    for (int i = 0; i < ps; ++i) sstore(mu[i], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
 #pragma unroll
-    for (int i = 0; i < p2; ++i) bstore(la[i], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
+    for (int i = 0; i < p2; ++i) sstore(la[i], make_rsrc(c.bS), c.vS, slab_so<S>(k, f++));
     // carry C̃_k, λ_k to knot k+1
     if constexpr (p2 > 0) {
 #pragma unroll
@@ -707,7 +723,12 @@ __device__ __forceinline__ void recompute_Ft(double (&Fo)[Z(Cn::P1)][Z(Cn::P2)],
                                              const double (&H)[S::template LH<Cn>()])
 {
     constexpr int R = Cn::R, W = Cn::W, p1 = Cn::P1, p2 = Cn::P2, O1 = Cn::O1, O2 = Cn::O2;
-    if constexpr (p1 > 0 && p2 > 0) {
+    if constexpr ((LQRX_FIL_ABL & 4) && p1 > 0 && p2 > 0) {
+#pragma unroll
+        for (int i = 0; i < p1; ++i)
+#pragma unroll
+            for (int i2 = 0; i2 < p2; ++i2) Fo[i][i2] = Y[i + i2] * Ua[0][0];
+    } else if constexpr (p1 > 0 && p2 > 0) {
 #pragma unroll
         for (int i = 0; i < p1; ++i)
 #pragma unroll
@@ -848,6 +869,10 @@ __device__ __forceinline__ void primal_knot(const Ctx<S> &c, int k, const SlabV<
 #pragma unroll
     for (int j = 0; j < W; ++j) {
         double s = 0.0;
+        if constexpr (LQRX_FIL_ABL & 8) {
+            z[j] = Y[j] * (C::P2 ? v.la[0] : 1.0);
+            continue;
+        }
 #pragma unroll
         for (int i = 0; i < C::P2; ++i) s = fma(Y[(C::O2 + i) + j * R], v.la[i], s);   // D1ᵀλ_k
 #pragma unroll
@@ -992,7 +1017,7 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
         factor_knot<S, L, NoCls>(N - 1, sL, yL, none, cy, c, info);
     }
 
-#if LQRX_FIL_ABL == 1
+#if LQRX_FIL_ABL & 1
     // ablation (tools only): forward sweep alone
     if (a.info && c.live) a.info[t0 + c.lane] = info;
     return;
