@@ -198,6 +198,9 @@ def main():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     ap.add_argument("--kkt-structure", choices=["dubins", "di"], default="dubins",
                     help="kkt workload: Dubins (configs[2]) or DoubleIntegrator(3,N) (test/problems.jl)")
+    ap.add_argument("--kkt-layout", type=int, choices=[0, 1], default=0,
+                    help="kkt workload: ABI layout 0 (per trajectory, the reference's blocks) or 1 "
+                         "(batch fastest, SoA)")
     ap.add_argument("--sqp-model", choices=["dubins", "cartpole"], default="dubins",
                     help="sqp workload: Dubins car (test/dubins_sqp.jl, mu 10, N 101) or the swing-up "
                          "Cartpole() of test/problems.jl:58-88 (mu 1, N 101, tf 5)")
@@ -311,15 +314,18 @@ def main():
         import lqrx.kkt as K
         st = kkt_structure(args.kkt_structure, N)
         pb = K.random_kkt(st, bt, seed=args.seed + rank, h_mode=K.H_DIAG)
-        t = {k: torch.from_numpy(getattr(pb, k).ravel()).to(dev) for k in ("Y", "y", "H", "g")}
+        kl = args.kkt_layout
+        # layout 1: the same data as [element][batch] (transposed on the device, untimed)
+        t = {k: (torch.from_numpy(getattr(pb, k)).to(dev).t().contiguous().view(-1) if kl else
+                 torch.from_numpy(getattr(pb, k).ravel()).to(dev)) for k in ("Y", "y", "H", "g")}
         t["batch"] = bt
         # caller-owned workspace (lqrx_kkt_solve_ws): a step is the kernel alone, as a serving
         # loop would run it (the pool path adds ~0.05 ms of stream-ordered alloc/free per call)
-        ws = torch.empty(K.workspace_size(st, bt, K.H_DIAG, 1), dtype=torch.uint8, device=dev)
-        out = K.kkt_solve_device(st, t, K.H_DIAG, 1, stream=sh, workspace=ws)
+        ws = torch.empty(K.workspace_size(st, bt, K.H_DIAG, 1, kl), dtype=torch.uint8, device=dev)
+        out = K.kkt_solve_device(st, t, K.H_DIAG, 1, stream=sh, workspace=ws, layout=kl)
 
         def step():
-            K.kkt_solve_device(st, t, K.H_DIAG, 1, stream=sh, out=out, workspace=ws)
+            K.kkt_solve_device(st, t, K.H_DIAG, 1, stream=sh, out=out, workspace=ws, layout=kl)
 
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -338,7 +344,9 @@ def main():
     if rank == 0 and args.workload in ("dp", "cartpole", "kkt"):
         thr = max(1, min(16, os.cpu_count() or 1))
         if args.workload == "kkt":
-            sampled = check_kkt_sample(out, pb, st, _sample_index(bt), bt, thr)
+            o = out if not args.kkt_layout else \
+                {k: out[k].view(-1, bt).t().contiguous().view(-1) for k in ("dz", "lam")}
+            sampled = check_kkt_sample(o, pb, st, _sample_index(bt), bt, thr)
         else:   # (a --tv run repeats the time-invariant draw per knot: same oracle problem)
             sampled = check_dp_sample(out, chk_sub, chk_idx, n, m, N, bt,
                                       1e-10 if f64 else 1e-4, thr)
@@ -440,7 +448,7 @@ def main():
             alg_bytes = (sY + sy + sH + sg + sg + sy) * 8 * bt     # inputs + dz + λ
             achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
             traffic = None
-            key = f"kkt_{args.kkt_structure}_N{N}_B{bt}_f64"
+            key = f"kkt_{args.kkt_structure}_N{N}_B{bt}_f64" + ("_soa" if args.kkt_layout else "")
             if os.path.exists(args.traffic_json):
                 try:
                     traffic = json.load(open(args.traffic_json)).get(key, {}).get("hbm_bytes_per_launch")
@@ -455,7 +463,8 @@ def main():
                     "alg_bytes_per_traj": alg_bytes / bt}
             if args.kkt_structure == "dubins":
                 metric = "KKT solves/sec (Dubins n=3 m=2 N=101 block-tridiagonal _solve!)"
-                workload = "Dubins constrained KKT inner solve (BASELINE.json configs[2])"
+                workload = "Dubins constrained KKT inner solve (BASELINE.json configs[2])" + \
+                    (", ABI layout 1 (batch-fastest SoA)" if args.kkt_layout else "")
             else:
                 metric = f"KKT solves/sec (DoubleIntegrator(3,{N}) n=6 m=3 block-tridiagonal _solve!)"
                 workload = "DoubleIntegrator KKT structure of test/cholesky_solve.jl (non-baseline)"

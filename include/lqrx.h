@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define LQRX_ABI_VERSION 2   /* 2: layout 1, lqrx_sqp_* (models, stage constraints) */
+#define LQRX_ABI_VERSION 2   /* 2: layout 1 (DP, KKT), lqrx_sqp_* (models, stage constraints) */
 
 #define LQRX_F64 0
 #define LQRX_F32 1
@@ -132,7 +132,14 @@ typedef struct lqrx_kkt_desc {
     const int32_t *w;   /* [N]                                                      */
     int32_t h_mode;     /* 0 dense, 1 block-diagonal, 2 diagonal                    */
     int32_t ginv;       /* 1 = _solve!;  0 = second-order-correction variant        */
-    int32_t layout;     /* 0 = per-trajectory packed, batch slowest                 */
+    int32_t layout;     /* 0 = per-trajectory packed, batch slowest: element e of
+                           trajectory t's packed array (Y, y, H, g, dz, lam) at
+                           [t·len + e];  1 = batch fastest (SoA) at [e·batch + t] —
+                           a wave's 64 trajectories read each element as one 512-B
+                           row.  Layout 1 is served by the compile-time shapes only
+                           (Dubins (3,2,3,0,3) every h_mode; cartpole (4,1,4,0,4)
+                           diagonal H / SOC; N >= 4; arrays < 2 GiB), else
+                           LQRX_ERR_UNSUPPORTED                                       */
     int32_t reserved;
 } lqrx_kkt_desc;
 

@@ -296,7 +296,8 @@ int kkt_layout(const lqrx_kkt_desc *d, KktLayout &L)
     if (!d->n1 || !d->p || !d->n2 || !d->w) return set_err(-1, "block-size arrays are NULL");
     if (d->h_mode < 0 || d->h_mode > 2) return set_err(-1, "desc.h_mode must be 0, 1 or 2");
     if (d->ginv != 0 && d->ginv != 1) return set_err(-1, "desc.ginv must be 0 or 1");
-    if (d->layout != 0) return set_err(LQRX_ERR_UNSUPPORTED, "desc.layout must be 0");
+    if (d->layout != 0 && d->layout != 1)
+        return set_err(-1, "desc.layout must be 0 (per trajectory) or 1 (batch fastest) (got %d)", d->layout);
     L.meta.assign((size_t)d->N * 8, 0);
     for (int k = 0; k < d->N; ++k) {
         int n1 = d->n1[k], p = d->p[k], n2 = d->n2[k], w = d->w[k];
@@ -323,6 +324,9 @@ int kkt_layout(const lqrx_kkt_desc *d, KktLayout &L)
         L.max_p2 = std::max(L.max_p2, n2);
     }
     if (L.sY > INT32_MAX) return set_err(LQRX_ERR_UNSUPPORTED, "trajectory too large");
+    // layout 1: every array's element rows are addressed with 32-bit byte offsets
+    if (d->layout == 1 && std::max(std::max(L.sY, L.sy), std::max(L.sH, L.sg)) * d->batch * 8 > INT32_MAX)
+        return set_err(LQRX_ERR_UNSUPPORTED, "layout 1: arrays above 2 GiB (split the batch)");
     return 0;
 }
 // Per-device cache of uploaded structure tables (process-wide, mutex-guarded), keyed on the
@@ -407,6 +411,7 @@ lqrx::KktArgs kkt_args(const lqrx_kkt_desc *d, const KktLayout &L)
     a.max_p1 = L.max_p1; a.max_ps = L.max_ps; a.max_p2 = L.max_p2;
     static const int force_lane = [] { const char *v = std::getenv("LQRX_KKT_FORCE_LANE"); return v && *v == '1'; }();
     a.force_lane = force_lane;
+    a.layout = d->layout;
     return a;
 }
 // LQRX_KKT_GENERIC=1 forces the generic (runtime-shaped) kernel, for A/B checks
@@ -481,7 +486,14 @@ int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const v
         a.ws_bytes = ws_bytes;
     }
     static const int debug_meta = [] { const char *v = std::getenv("LQRX_DEBUG_META"); return v && *v == '1'; }();
-    if (a.force_lane || kkt_force_generic() || !lqrx::kkt_fil_launch(a, d->n1, d->p, d->n2, d->w, s, &e))
+    if (d->layout == 1) {
+        // batch-fastest inputs are served by the compile-time-shaped kernel only
+        if (!lqrx::kkt_fil_launch(a, d->n1, d->p, d->n2, d->w, s, &e)) {
+            if (meta_tmp) (void)lqrx::scratch_free(meta_tmp, s);
+            return set_err(LQRX_ERR_UNSUPPORTED, "layout 1 needs a compile-time KKT shape (Dubins; cartpole with "
+                                                 "diagonal H) and N >= 4");
+        }
+    } else if (a.force_lane || kkt_force_generic() || !lqrx::kkt_fil_launch(a, d->n1, d->p, d->n2, d->w, s, &e))
         e = lqrx::kkt_launch(a, s);
     if (meta_tmp) (void)lqrx::scratch_free(meta_tmp, s);   // stream-ordered after the launch
     if (debug_meta) {

@@ -40,6 +40,7 @@ struct KktArgs {
     int64_t sY, sy, sH, sg, sl; // per-trajectory strides (elements)
     int maxw, maxrows, max_p1, max_ps, max_p2;
     int force_lane; // debug: LQRX_KKT_FORCE_LANE=1 selects the register-only kernel
+    int layout;     // 0 per-trajectory packed; 1 batch fastest (compile-time shapes only)
     void *ws;         // caller's device workspace (lqrx_kkt_solve_ws) or NULL: library pool
     size_t ws_bytes;
 };

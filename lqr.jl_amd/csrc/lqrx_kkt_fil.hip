@@ -49,9 +49,11 @@ template <int P1_, int PS_, int P2_, int W_> struct Cls {
 };
 using NoCls = Cls<0, 0, 0, 0>;
 
-template <int NX_, int M_, int P0_, int PK_, int PN_, bool HDIAG_, bool GINV_> struct Shape {
+// SOA = ABI layout 1 (batch fastest): element e of a trajectory's packed array at [e·batch + t],
+// so the 64 trajectories of a wave read one element as a contiguous 512-B row
+template <int NX_, int M_, int P0_, int PK_, int PN_, bool HDIAG_, bool GINV_, bool SOA_ = false> struct Shape {
     static constexpr int NX = NX_, M = M_;
-    static constexpr bool HDIAG = HDIAG_, GINV = GINV_;
+    static constexpr bool HDIAG = HDIAG_, GINV = GINV_, SOA = SOA_;
     using F = Cls<0, P0_, NX_, NX_ + M_>;
     using I = Cls<NX_, PK_, NX_, NX_ + M_>;
     using L = Cls<NX_, PN_, 0, NX_>;
@@ -63,13 +65,19 @@ template <int NX_, int M_, int P0_, int PK_, int PN_, bool HDIAG_, bool GINV_> s
     // knot offset and the trajectory stride are even); the short y/H/g chunks in dwords
     static constexpr bool WIDE_Y = (LY<F>() % 2 == 0) && (LY<I>() % 2 == 0) && (LY<L>() % 2 == 0);
     static constexpr int nsplit(int L) { return LQRX_FIL_N12 ? (8 * L) / 12 + ((8 * L) % 12) / 4 : 2 * L; }   // = Split<L>::instrs
+    // SOA: one 16-B-per-lane DMA moves two element rows (2 × 64 doubles)
+    static constexpr int rows2(int L) { return (L + 1) / 2; }
     template <class C> static constexpr int Dmin()   // DMA instructions of a forward restage
     {
+        if constexpr (SOA)
+            return C::none ? 0 : rows2(LY<C>()) + rows2(Ly<C>()) + (GINV ? rows2(LH<C>()) + rows2(Lg<C>()) : 0);
         return C::none ? 0 : (WIDE_Y ? LY<C>() / 2 : 2 * LY<C>()) + nsplit(Ly<C>()) +
                                  (GINV ? nsplit(LH<C>()) + nsplit(Lg<C>()) : 0);
     }
     template <class C> static constexpr int Dbwd()   // … of a backward restage (no y)
     {
+        if constexpr (SOA)
+            return C::none ? 0 : rows2(LY<C>()) + (GINV ? rows2(LH<C>()) + rows2(Lg<C>()) : 0);
         return C::none ? 0 : (WIDE_Y ? LY<C>() / 2 : 2 * LY<C>()) + (GINV ? nsplit(LH<C>()) + nsplit(Lg<C>()) : 0);
     }
     template <int A, int B, int C> static constexpr int mx3() { return A > B ? (A > C ? A : C) : (B > C ? B : C); }
@@ -78,8 +86,12 @@ template <int NX_, int M_, int P0_, int PK_, int PN_, bool HDIAG_, bool GINV_> s
     static constexpr int LHm = mx3<LH<F>(), LH<I>(), LH<L>()>();
     static constexpr int Lgm = mx3<Lg<F>(), Lg<I>(), Lg<L>()>();
     // staging buffer (bytes): Y image (16-B pieces, dense) | y | H | g split images
-    static constexpr int sb(int L) { return LQRX_FIL_N12 ? 16 * ((8 * L) / 12) + 4 * (((8 * L) % 12) / 4) : 8 * L; }
-    static constexpr int OFF_y = 64 * 8 * LYm;
+    // (SOA: [element row][64 lanes] images, rows rounded up to even — the DMA moves row pairs)
+    static constexpr int sb(int L)
+    {
+        return SOA ? 8 * (2 * rows2(L)) : LQRX_FIL_N12 ? 16 * ((8 * L) / 12) + 4 * (((8 * L) % 12) / 4) : 8 * L;
+    }
+    static constexpr int OFF_y = 64 * (SOA ? sb(LYm) : 8 * LYm);
     static constexpr int OFF_H = OFF_y + 64 * mx3<sb(Ly<F>()), sb(Ly<I>()), sb(Ly<L>())>();
     static constexpr int OFF_g = OFF_H + 64 * mx3<sb(LH<F>()), sb(LH<I>()), sb(LH<L>())>();
     static constexpr int BUF_BYTES = OFF_g + 64 * mx3<sb(Lg<F>()), sb(Lg<I>()), sb(Lg<L>())>();
@@ -244,17 +256,34 @@ template <int L, bool WIDE> __device__ __forceinline__ void load_Y(uint32_t lds_
     }
 }
 
-// staging buffer views (lane-linear [t][L] images)
+// reader of an SOA image ([element][64 lanes]): element j of this lane's chunk — consecutive
+// lanes read consecutive doubles (no bank conflicts)
+template <int L> struct SImgS {
+    uint32_t base;
+    int lane;
+    __device__ __forceinline__ double operator[](int j) const { return *(lds_d *)(size_t)(base + (j * 64 + lane) * 8); }
+    __device__ __forceinline__ void load(double (&out)[L]) const
+    {
+#pragma unroll
+        for (int j = 0; j < L; ++j) out[j] = (*this)[j];
+    }
+};
+
+// staging buffer views (lane-linear [t][L] images; SOA: [element][64] images)
 template <class S> struct Buf {
     double *base;
     __device__ const double *Y(int lane, int L) const { return base + lane * L; }
     __device__ uint32_t lds() const { return (uint32_t)(size_t)(lptr_t)base; }
-    template <int L> __device__ SImg<L> y(int lane) const { return SImg<L>{lds() + S::OFF_y, lane}; }
-    template <int L> __device__ SImg<L> H(int lane) const { return SImg<L>{lds() + S::OFF_H, lane}; }
-    template <int L> __device__ SImg<L> g(int lane) const { return SImg<L>{lds() + S::OFF_g, lane}; }
+    template <int L> using Img = typename std::conditional<S::SOA, SImgS<L>, SImg<L>>::type;
+    template <int L> __device__ Img<L> y(int lane) const { return Img<L>{lds() + S::OFF_y, lane}; }
+    template <int L> __device__ Img<L> H(int lane) const { return Img<L>{lds() + S::OFF_H, lane}; }
+    template <int L> __device__ Img<L> g(int lane) const { return Img<L>{lds() + S::OFF_g, lane}; }
     template <class C> __device__ void ld_Y(int lane, double (&v)[S::template LY<C>()]) const
     {
-        load_Y<S::template LY<C>(), S::WIDE_Y>(lds(), lane, v);
+        if constexpr (S::SOA)
+            SImgS<S::template LY<C>()>{lds(), lane}.load(v);
+        else
+            load_Y<S::template LY<C>(), S::WIDE_Y>(lds(), lane, v);
     }
     template <class C> __device__ void ld_H(int lane, double (&v)[S::template LH<C>()]) const { H<S::template LH<C>()>(lane).load(v); }
     template <class C> __device__ void ld_g(int lane, double (&v)[S::template Lg<C>()]) const { g<S::template Lg<C>()>(lane).load(v); }
@@ -268,6 +297,20 @@ template <class S> struct Ctx {
     int lane, nlive;
     bool live;
     uint32_t vS, vdz, vlam;                        // per-lane byte offsets: slab, dz, lam
+    uint32_t vsoa = 0, rowb = 0;                   // SOA: lane's row-pair offset, bytes per element row
+    uint32_t limY = 0, limy = 0, limH = 0, limg = 0; // SOA: bytes from the wave base to each array's end
+    // SOA: L element rows from row r0 of one array, as (L+1)/2 row-pair DMAs (lane l → row
+    // 2i + l/32, trajectories 2(l mod 32), +1).  Reads past the array's end (dead lanes of the
+    // last wave, the odd row of the last pair) are out of the resource's range and return 0.
+    template <int L>
+    __device__ __forceinline__ void soa_issue(const double *base, uint32_t lim, int64_t r0, double *lds) const
+    {
+        const u4_t r = make_rsrc4n(base, lim);
+        const uint32_t l0 = lds_addr(lds), v0 = vsoa + (uint32_t)r0 * rowb;
+        // (the row offset rides in the VGPR offset: the buffer range check does not cover soffset)
+#pragma unroll
+        for (int i = 0; i < S::rows2(L); ++i) dma_lds<16>(r, v0 + 2u * (uint32_t)i * rowb, 0u, l0 + 1024u * i);
+    }
     Pat<S::template LY<I>(), S::WIDE_Y> pY;
     PatS<S::template Ly<I>()> py;
     PatS<S::template LH<I>()> pH;
@@ -277,6 +320,15 @@ template <class S> struct Ctx {
     __device__ __forceinline__ void stage_I(int k, double *buf, bool fwd) const
     {
         using O = Off<S>;
+        if constexpr (S::SOA) {
+            soa_issue<S::template LY<I>()>(bY, limY, O::Y(k), buf);
+            if (fwd) soa_issue<S::template Ly<I>()>(by, limy, O::y(k), buf + S::OFF_y / 8);
+            if constexpr (S::GINV) {
+                soa_issue<S::template LH<I>()>(bH, limH, O::H(k), buf + S::OFF_H / 8);
+                soa_issue<S::template Lg<I>()>(bg, limg, O::g(k), buf + S::OFF_g / 8);
+            }
+            return;
+        }
         pY.issue(make_rsrc4(bY), O::Y(k), buf);
         if (fwd) py.issue(make_rsrc4(by), O::y(k), buf + S::OFF_y / 8);
         if constexpr (S::GINV) {
@@ -289,6 +341,15 @@ template <class S> struct Ctx {
     __device__ __forceinline__ void stage(const KktArgs &a, int k, double *buf, bool fwd) const
     {
         using O = Off<S>;
+        if constexpr (S::SOA) {
+            soa_issue<S::template LY<C>()>(bY, limY, O::Y(k), buf);
+            if (fwd) soa_issue<S::template Ly<C>()>(by, limy, O::y(k), buf + S::OFF_y / 8);
+            if constexpr (S::GINV) {
+                soa_issue<S::template LH<C>()>(bH, limH, O::H(k), buf + S::OFF_H / 8);
+                soa_issue<S::template Lg<C>()>(bg, limg, O::g(k), buf + S::OFF_g / 8);
+            }
+            return;
+        }
         Pat<S::template LY<C>(), S::WIDE_Y> qY;
         qY.init(a.sY, lane, nlive);
         qY.issue(make_rsrc4(bY), O::Y(k), buf);
@@ -901,9 +962,14 @@ __device__ __forceinline__ void primal_knot(const Ctx<S> &c, int k, const SlabV<
         }
     }
     if (c.live) {
-        const uint32_t so = (uint32_t)(Off<S>::g(k) * 8);
+        if constexpr (S::SOA) {                                   // coalesced 512-B rows
 #pragma unroll
-        for (int j = 0; j < W; ++j) bstore(-z[j], make_rsrc(c.bdz), c.vdz + 8 * j, so);
+            for (int j = 0; j < W; ++j) bstore(-z[j], make_rsrc(c.bdz), c.vdz, (uint32_t)(Off<S>::g(k) + j) * c.rowb);
+        } else {
+            const uint32_t so = (uint32_t)(Off<S>::g(k) * 8);
+#pragma unroll
+            for (int j = 0; j < W; ++j) bstore(-z[j], make_rsrc(c.bdz), c.vdz + 8 * j, so);
+        }
     }
 }
 
@@ -911,6 +977,14 @@ template <class S, class C>
 __device__ __forceinline__ void store_lam(const Ctx<S> &c, int k, const SlabV<C> &v)
 {
     if (!c.live) return;
+    if constexpr (S::SOA) {
+        const uint32_t r0 = (uint32_t)Off<S>::y(k);
+#pragma unroll
+        for (int i = 0; i < C::PS; ++i) bstore(v.mu[i], make_rsrc(c.blam), c.vlam, (r0 + i) * c.rowb);
+#pragma unroll
+        for (int i = 0; i < C::P2; ++i) bstore(v.la[i], make_rsrc(c.blam), c.vlam, (r0 + C::PS + i) * c.rowb);
+        return;
+    }
     const uint32_t so = (uint32_t)(Off<S>::y(k) * 8);
 #pragma unroll
     for (int i = 0; i < C::PS; ++i) bstore(v.mu[i], make_rsrc(c.blam), c.vlam + 8 * i, so);
@@ -946,20 +1020,39 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     c.lane = threadIdx.x;
     c.nlive = (int)(a.batch - t0 < 64 ? a.batch - t0 : 64);
     c.live = c.lane < c.nlive;
-    c.bY = a.Y + t0 * a.sY;
-    c.by = a.y + t0 * a.sy;
-    c.bH = a.H + t0 * a.sH;
-    c.bg = a.g + t0 * a.sg;
-    c.bdz = a.dz + t0 * a.sg;
-    c.blam = a.lam + t0 * a.sl;
     c.bS = scratch + (int64_t)blockIdx.x * N * S::SLOT * 64;
     c.vS = 8u * c.lane;
-    c.vdz = (uint32_t)(c.lane * a.sg * 8);
-    c.vlam = (uint32_t)(c.lane * a.sl * 8);
-    c.pY.init(a.sY, c.lane, c.nlive);
-    c.py.init(a.sy, c.lane, c.nlive);
-    c.pH.init(a.sH, c.lane, c.nlive);
-    c.pg.init(a.sg, c.lane, c.nlive);
+    if constexpr (S::SOA) {
+        // wave bases at trajectory t0 of element row 0; a lane past the batch end reads the
+        // next row's first trajectories (or past the array: buffer bounds return 0) — its
+        // results are never stored
+        c.bY = a.Y + t0;
+        c.by = a.y + t0;
+        c.bH = a.H + t0;
+        c.bg = a.g + t0;
+        c.bdz = a.dz + t0;
+        c.blam = a.lam + t0;
+        c.rowb = (uint32_t)(a.batch * 8);
+        c.limY = (uint32_t)((a.sY * a.batch - t0) * 8);
+        c.limy = (uint32_t)((a.sy * a.batch - t0) * 8);
+        c.limH = (uint32_t)((a.sH * a.batch - t0) * 8);
+        c.limg = (uint32_t)((a.sg * a.batch - t0) * 8);
+        c.vsoa = (uint32_t)(((c.lane >> 5) * a.batch + 2 * (c.lane & 31)) * 8);
+        c.vdz = c.vlam = 8u * c.lane;
+    } else {
+        c.bY = a.Y + t0 * a.sY;
+        c.by = a.y + t0 * a.sy;
+        c.bH = a.H + t0 * a.sH;
+        c.bg = a.g + t0 * a.sg;
+        c.bdz = a.dz + t0 * a.sg;
+        c.blam = a.lam + t0 * a.sl;
+        c.vdz = (uint32_t)(c.lane * a.sg * 8);
+        c.vlam = (uint32_t)(c.lane * a.sl * 8);
+        c.pY.init(a.sY, c.lane, c.nlive);
+        c.py.init(a.sy, c.lane, c.nlive);
+        c.pH.init(a.sH, c.lane, c.nlive);
+        c.pg.init(a.sg, c.lane, c.nlive);
+    }
     int info = 0;
 
     // ---------------- forward ----------------
@@ -1316,14 +1409,16 @@ hipError_t launch(const KktArgs &a, hipStream_t s)
 
 // Explicit instantiations of every dispatched shape: this compiler has dropped the host stub
 // of an implicitly instantiated kernel template launched from a conditional (link error).
-#define LQRX_FIL_INST(NX, M, A0, AK, AN)                                                                 \
-    template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, true>>(const KktArgs, double *__restrict__);  \
-    template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, false, true>>(const KktArgs, double *__restrict__); \
-    template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, false>>(const KktArgs, double *__restrict__);
+#define LQRX_FIL_INST1(NX, M, A0, AK, AN, SOA)                                                          \
+    template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, true, SOA>>(const KktArgs, double *__restrict__);  \
+    template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, false, true, SOA>>(const KktArgs, double *__restrict__); \
+    template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, false, SOA>>(const KktArgs, double *__restrict__);
+#define LQRX_FIL_INST(NX, M, A0, AK, AN) LQRX_FIL_INST1(NX, M, A0, AK, AN, false) LQRX_FIL_INST1(NX, M, A0, AK, AN, true)
 // diagonal-H variants only (the dense-H staging ring of these shapes exceeds 160 KB of LDS)
-#define LQRX_FIL_INST_DIAG(NX, M, A0, AK, AN)                                                            \
-    template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, true>>(const KktArgs, double *__restrict__);  \
-    template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, false>>(const KktArgs, double *__restrict__);
+#define LQRX_FIL_INST_DIAG1(NX, M, A0, AK, AN, SOA)                                                     \
+    template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, true, SOA>>(const KktArgs, double *__restrict__);  \
+    template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, false, SOA>>(const KktArgs, double *__restrict__);
+#define LQRX_FIL_INST_DIAG(NX, M, A0, AK, AN) LQRX_FIL_INST_DIAG1(NX, M, A0, AK, AN, false) LQRX_FIL_INST_DIAG1(NX, M, A0, AK, AN, true)
 // direct (no LDS staging) variants, diagonal H
 #define LQRX_FILD_INST(NX, M, A0, AK, AN)                                                                \
     template __global__ void kkt_fild_kernel<Shape<NX, M, A0, AK, AN, true, true>>(const KktArgs, double *__restrict__);  \
@@ -1332,7 +1427,9 @@ LQRX_FIL_INST(3, 2, 3, 0, 3)
 LQRX_FIL_INST_DIAG(4, 1, 4, 0, 4)
 LQRX_FILD_INST(6, 3, 6, 1, 6)
 #undef LQRX_FIL_INST
+#undef LQRX_FIL_INST1
 #undef LQRX_FIL_INST_DIAG
+#undef LQRX_FIL_INST_DIAG1
 #undef LQRX_FILD_INST
 
 } // namespace fil
@@ -1350,22 +1447,30 @@ static bool fil_dispatch(const KktArgs &a, const int32_t *n1, const int32_t *p, 
     if (n1[0] != 0 || w[N - 1] != nx || n2[N - 1] != 0 || n1[N - 1] != nx) return false;
     for (int k = 1; k < N - 1; ++k)
         if (n1[k] != nx || n2[k] != nx || p[k] != PK || w[k] != nx + m) return false;
-    const bool diag = a.h_mode == 2, ginv = a.ginv != 0;
+    const bool diag = a.h_mode == 2, ginv = a.ginv != 0, soa = a.layout == 1;
+#define LQRX_FIL_SEL(NX, M, A0, AK, AN, SOA)                                                             \
+    if (diag && ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true, SOA>{}, std::false_type{});           \
+    else if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, false, true, SOA>{}, std::false_type{});             \
+    else fn(fil::Shape<NX, M, A0, AK, AN, true, false, SOA>{}, std::false_type{});
 #define LQRX_FIL(NX, M, A0, AK, AN)                                                                      \
     if (nx == NX && m == M && P0 == A0 && PK == AK && PN == AN) {                                        \
-        if (diag && ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true>{}, std::false_type{});                               \
-        else if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, false, true>{}, std::false_type{});                                 \
-        else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{}, std::false_type{});                                           \
+        if (soa) { LQRX_FIL_SEL(NX, M, A0, AK, AN, true) }                                               \
+        else { LQRX_FIL_SEL(NX, M, A0, AK, AN, false) }                                                  \
         return true;                                                                                     \
     }
 #define LQRX_FIL_DIAG(NX, M, A0, AK, AN)                                                                 \
     if (nx == NX && m == M && P0 == A0 && PK == AK && PN == AN && (diag || !ginv)) {                     \
-        if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true>{}, std::false_type{});                                       \
-        else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{}, std::false_type{});                                           \
+        if (soa) {                                                                                       \
+            if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true, true>{}, std::false_type{});          \
+            else fn(fil::Shape<NX, M, A0, AK, AN, true, false, true>{}, std::false_type{});              \
+        } else {                                                                                         \
+            if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true>{}, std::false_type{});                \
+            else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{}, std::false_type{});                    \
+        }                                                                                                \
         return true;                                                                                     \
     }
 #define LQRX_FILD(NX, M, A0, AK, AN)                                                                     \
-    if (nx == NX && m == M && P0 == A0 && PK == AK && PN == AN && (diag || !ginv)) {                     \
+    if (nx == NX && m == M && P0 == A0 && PK == AK && PN == AN && (diag || !ginv) && !soa) {             \
         if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true>{}, std::true_type{});                     \
         else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{}, std::true_type{});                         \
         return true;                                                                                     \
@@ -1374,6 +1479,7 @@ static bool fil_dispatch(const KktArgs &a, const int32_t *n1, const int32_t *p, 
     LQRX_FIL_DIAG(4, 1, 4, 0, 4)   // cartpole trajectory problem (test/problems.jl:58-88, device SQP)
     LQRX_FILD(6, 3, 6, 1, 6)       // DoubleIntegrator(3) (test/problems.jl:14-56, test/cholesky_solve.jl)
 #undef LQRX_FIL
+#undef LQRX_FIL_SEL
 #undef LQRX_FIL_DIAG
 #undef LQRX_FILD
     return false;

@@ -52,6 +52,17 @@ __device__ __forceinline__ void stage_chunk(const double *X, int64_t s, int64_t 
 // a raw buffer descriptor (stride 0, full 31-bit range, gfx9 dword-3 format bits) as four
 // SGPRs, for the inline-asm LDS-DMA below
 typedef uint32_t u4_t __attribute__((ext_vector_type(4)));
+// raw buffer resource with an explicit size: loads at offsets ≥ bytes return 0 (no access)
+__device__ __forceinline__ u4_t make_rsrc4n(const void *base, uint32_t bytes)
+{
+    const uint64_t a = (uint64_t)base;
+    u4_t r;
+    r.x = (uint32_t)a;
+    r.y = (uint32_t)(a >> 32) & 0xffffu;
+    r.z = bytes;
+    r.w = 0x00020000u;
+    return r;
+}
 __device__ __forceinline__ u4_t make_rsrc4(const void *base)
 {
     const uint64_t a = (uint64_t)base;

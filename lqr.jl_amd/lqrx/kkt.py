@@ -50,10 +50,10 @@ class KktStructure:
         sg = int(np.sum(self.w))
         return sY, sy, sH, sg
 
-    def desc(self, batch, h_mode, ginv):
+    def desc(self, batch, h_mode, ginv, layout=0):
         arrs = [np.ascontiguousarray(a, dtype=np.int32) for a in (self.n1, self.p, self.n2, self.w)]
         ptr = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32))
-        d = _lib.KktDesc(self.N, _lib.F64, batch, *[ptr(a) for a in arrs], h_mode, ginv, 0, 0)
+        d = _lib.KktDesc(self.N, _lib.F64, batch, *[ptr(a) for a in arrs], h_mode, ginv, layout, 0)
         d._keep = arrs  # keep the arrays alive with the descriptor
         return d
 
@@ -152,20 +152,24 @@ def _ptr(a):
     return a.ctypes.data_as(C.c_void_p)
 
 
-def kkt_solve(pb: KktProblem, ginv: int = 1):
+def kkt_solve(pb: KktProblem, ginv: int = 1, layout: int = 0):
     """Batched _solve! via lqrx_kkt_solve_host.  Returns dict dz (batch, NN), lam
-    (batch, P), info (batch,), rc."""
+    (batch, P), info (batch,), rc.  layout=1 hands the library batch-fastest (SoA) copies
+    ([element][batch]) and transposes the outputs back — same results."""
     lib = _lib.load()
     st, bt = pb.st, pb.batch
     sY, sy, sH, sg = st.sizes(pb.h_mode)
-    d = st.desc(bt, pb.h_mode, ginv)
-    f = lambda a: np.ascontiguousarray(a, dtype=np.float64)
+    d = st.desc(bt, pb.h_mode, ginv, layout)
+    f = (lambda a: np.ascontiguousarray(np.asarray(a, dtype=np.float64).T)) if layout == 1 else \
+        (lambda a: np.ascontiguousarray(a, dtype=np.float64))
     Y, y, H, g = f(pb.Y), f(pb.y), f(pb.H), f(pb.g)
-    dz = np.zeros((bt, sg))
-    lam = np.zeros((bt, sy))
+    dz = np.zeros((sg, bt) if layout == 1 else (bt, sg))
+    lam = np.zeros((sy, bt) if layout == 1 else (bt, sy))
     info = np.zeros(bt, np.int32)
     rc = _lib.check(lib.lqrx_kkt_solve_host(C.byref(d), _ptr(Y), _ptr(y), _ptr(H), _ptr(g),
                                             _ptr(dz), _ptr(lam), _ptr(info)))
+    if layout == 1:
+        dz, lam = np.ascontiguousarray(dz.T), np.ascontiguousarray(lam.T)
     return dict(dz=dz, lam=lam, info=info, rc=rc)
 
 
@@ -174,19 +178,20 @@ def second_order_correction(pb: KktProblem):
     return kkt_solve(pb, ginv=0)
 
 
-def workspace_size(st: KktStructure, batch: int, h_mode: int, ginv: int = 1) -> int:
+def workspace_size(st: KktStructure, batch: int, h_mode: int, ginv: int = 1, layout: int = 0) -> int:
     """Bytes of device workspace lqrx_kkt_solve_ws needs (lqrx_kkt_workspace_size)."""
     lib = _lib.load()
     n = C.c_size_t(0)
-    _lib.check(lib.lqrx_kkt_workspace_size(C.byref(st.desc(batch, h_mode, ginv)), C.byref(n)))
+    _lib.check(lib.lqrx_kkt_workspace_size(C.byref(st.desc(batch, h_mode, ginv, layout)), C.byref(n)))
     return n.value
 
 
 def kkt_solve_device(st: KktStructure, t: dict, h_mode: int, ginv: int = 1,
-                     stream: int | None = None, out: dict | None = None, workspace=None) -> dict:
-    """Device-pointer entry on torch tensors (flat, ABI layout): t has Y, y, H, g, batch.
-    `workspace` (a device uint8 tensor of >= workspace_size() bytes) selects lqrx_kkt_solve_ws:
-    no allocation inside the call."""
+                     stream: int | None = None, out: dict | None = None, workspace=None,
+                     layout: int = 0) -> dict:
+    """Device-pointer entry on torch tensors (flat, ABI layout `layout`): t has Y, y, H, g,
+    batch.  `workspace` (a device uint8 tensor of >= workspace_size() bytes) selects
+    lqrx_kkt_solve_ws: no allocation inside the call."""
     import torch
 
     lib = _lib.load()
@@ -197,7 +202,7 @@ def kkt_solve_device(st: KktStructure, t: dict, h_mode: int, ginv: int = 1,
         out = dict(dz=torch.empty(bt * sg, dtype=torch.float64, device=dev),
                    lam=torch.empty(bt * sy, dtype=torch.float64, device=dev),
                    info=torch.empty(bt, dtype=torch.int32, device=dev))
-    d = st.desc(bt, h_mode, ginv)
+    d = st.desc(bt, h_mode, ginv, layout)
     p = lambda x: C.c_void_p(x.data_ptr())
     args = [C.byref(d), p(t["Y"]), p(t["y"]), p(t["H"]), p(t["g"]), p(out["dz"]), p(out["lam"]),
             p(out["info"])]

@@ -70,6 +70,12 @@ def test_kkt_validation(lqrx):
     st2.n1[2] = 2            # breaks the A ≡ previous-C aliasing (n1[k] == n2[k-1])
     d2 = st2.desc(4, 2, 1)
     assert lqrx.load().lqrx_kkt_solve(C.byref(d2), *([None] * 7), None) == -1
+    d3 = st.desc(4, 2, 1, layout=2)                      # layouts: 0, 1
+    assert lqrx.load().lqrx_kkt_solve(C.byref(d3), *([None] * 7), None) == -1
+    d4 = st.desc(4, 2, 1, layout=1)                      # SoA is valid: first NULL is Y
+    assert lqrx.load().lqrx_kkt_solve(C.byref(d4), *([None] * 7), None) == -2
+    big = K.dubins_structure(101).desc(1 << 20, 2, 1, layout=1)   # Y rows past 2 GiB
+    assert lqrx.load().lqrx_kkt_solve(C.byref(big), *([None] * 7), None) == lqrx._lib.ERR_UNSUPPORTED
 
 
 def test_kkt_sizes(lqrx):

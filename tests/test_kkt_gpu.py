@@ -159,3 +159,44 @@ def test_kkt_meta_cache_overflow(lqrx, gpu_ok):
     r = subprocess.run([sys.executable, os.path.join(here, "_kkt_meta_overflow.py")], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("model,N,batch", [("dubins", 4, 1), ("dubins", 5, 130), ("dubins", 101, 16384 + 3),
+                                           ("cartpole", 7, 70), ("cartpole", 101, 4096 + 5)])
+@pytest.mark.parametrize("h_mode,ginv", [(2, 1), (0, 1), (1, 1), (2, 0)])
+def test_kkt_layout1_soa(lqrx, gpu_ok, model, N, batch, h_mode, ginv):
+    """ABI layout 1 (batch fastest: element e of trajectory t at [e·batch + t]) on the
+    compile-time-shaped kernel: bit-identical to layout 0 (same arithmetic, only the staging
+    differs: 512-B element rows instead of per-trajectory chunks) and within 1e-10 of the
+    oracle; ragged last waves (dead lanes read past the arrays' ends, bounds-checked to 0)."""
+    import lqrx.kkt as K
+
+    st = K.dubins_structure(N) if model == "dubins" else K.trajectory_structure(4, 1, N)
+    if model == "cartpole" and h_mode != 2 and ginv:
+        pb = K.random_kkt(st, 2, seed=1, h_mode=h_mode)            # dense H: no SoA shape
+        with pytest.raises(K._lib.LqrxError) as e:
+            K.kkt_solve(pb, ginv=ginv, layout=1)
+        assert e.value.code == K._lib.ERR_UNSUPPORTED
+        return
+    pb = K.random_kkt(st, batch, seed=11 * N + h_mode, h_mode=h_mode)
+    got1 = K.kkt_solve(pb, ginv=ginv, layout=1)
+    got0 = K.kkt_solve(pb, ginv=ginv, layout=0)
+    assert got1["rc"] == 0 and (got1["info"] == got0["info"]).all()
+    assert np.array_equal(got1["dz"], got0["dz"]) and np.array_equal(got1["lam"], got0["lam"])
+    idx = np.unique(np.linspace(0, batch - 1, min(batch, 64)).round().astype(int))
+    sub = K.KktProblem(st, len(idx), h_mode, pb.Y[idx], pb.y[idx], pb.H[idx], pb.g[idx])
+    ref = _ref(st, sub, ginv)
+    assert rel(got1["dz"][idx], ref["dz"].reshape(len(idx), -1)) <= TOL
+    assert rel(got1["lam"][idx], ref["lam"].reshape(len(idx), -1)) <= TOL
+
+
+def test_kkt_layout1_unsupported_shapes(lqrx, gpu_ok):
+    """Layout 1 is served by the compile-time shapes only: the generic structures (here
+    DoubleIntegrator(2, 12)) and N < 4 return LQRX_ERR_UNSUPPORTED."""
+    import lqrx.kkt as K
+
+    for st in (K.double_integrator_structure(2, 12), K.dubins_structure(3)):
+        pb = K.random_kkt(st, 3, seed=2, h_mode=K.H_DIAG)
+        with pytest.raises(K._lib.LqrxError) as e:
+            K.kkt_solve(pb, layout=1)
+        assert e.value.code == K._lib.ERR_UNSUPPORTED
