@@ -137,8 +137,9 @@ typedef struct lqrx_kkt_desc {
                            [t·len + e];  1 = batch fastest (SoA) at [e·batch + t] —
                            a wave's 64 trajectories read each element as one 512-B
                            row.  Layout 1 is served by the compile-time shapes only
-                           (Dubins (3,2,3,0,3) every h_mode; cartpole (4,1,4,0,4)
-                           diagonal H / SOC; N >= 4; arrays < 2 GiB), else
+                           (Dubins (3,2,3,0,3) every h_mode; cartpole (4,1,4,0,4),
+                           DoubleIntegrator(2)/(3) (4,2,4,1,4)/(6,3,6,1,6) diagonal
+                           H / SOC; N >= 4; arrays < 2 GiB), else
                            LQRX_ERR_UNSUPPORTED                                       */
     int32_t reserved;
 } lqrx_kkt_desc;

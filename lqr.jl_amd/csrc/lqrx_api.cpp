@@ -490,8 +490,8 @@ int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const v
         // batch-fastest inputs are served by the compile-time-shaped kernel only
         if (!lqrx::kkt_fil_launch(a, d->n1, d->p, d->n2, d->w, s, &e)) {
             if (meta_tmp) (void)lqrx::scratch_free(meta_tmp, s);
-            return set_err(LQRX_ERR_UNSUPPORTED, "layout 1 needs a compile-time KKT shape (Dubins; cartpole with "
-                                                 "diagonal H) and N >= 4");
+            return set_err(LQRX_ERR_UNSUPPORTED, "layout 1 needs a compile-time KKT shape (Dubins; cartpole, "
+                                                 "DoubleIntegrator(2|3) with diagonal H) and N >= 4");
         }
     } else if (a.force_lane || kkt_force_generic() || !lqrx::kkt_fil_launch(a, d->n1, d->p, d->n2, d->w, s, &e))
         e = lqrx::kkt_launch(a, s);

@@ -1201,20 +1201,33 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
 // offsets, no LDS): a lane streams a contiguous chunk per knot, its 64 neighbours the chunks
 // of the next trajectories; L2 absorbs the partial lines.  Same operation order as the staged
 // kernel, so the two agree bit for bit on a shape both serve.
+// element e of trajectory t's packed array (length len) starting at offset off: layout 0
+// [t·len + off + e], layout 1 [(off + e)·batch + t] — one coalesced 512-B row per element for
+// the wave, loaded with the row offset in the scalar offset (32-bit, uniform) and the lane's
+// trajectory in the vector offset (dead lanes hold the last live trajectory: always in range)
+template <class S>
+__device__ __forceinline__ double gld(const double *base, int64_t t, int64_t len, int64_t off, int e, int64_t batch)
+{
+    if constexpr (S::SOA) {
+        const int64_t t0 = (int64_t)blockIdx.x * 64;
+        return bload(make_rsrc(base + t0), (uint32_t)(t - t0) * 8u, (uint32_t)((off + e) * batch * 8));
+    } else {
+        return base[t * len + off + e];
+    }
+}
+
 template <class S, class C> struct GIn {          // knot k's inputs (class C) of one trajectory
     double Y[S::template LY<C>()], H[S::template LH<C>()], g[S::template Lg<C>()];
     __device__ __forceinline__ void load(const KktArgs &a, int64_t t, int k)
     {
         using O = Off<S>;
-        const double *Yp = a.Y + t * a.sY + O::Y(k);
 #pragma unroll
-        for (int e = 0; e < S::template LY<C>(); ++e) Y[e] = Yp[e];
+        for (int e = 0; e < S::template LY<C>(); ++e) Y[e] = gld<S>(a.Y, t, a.sY, O::Y(k), e, a.batch);
         if constexpr (S::GINV) {
-            const double *Hp = a.H + t * a.sH + O::H(k), *gp = a.g + t * a.sg + O::g(k);
 #pragma unroll
-            for (int e = 0; e < S::template LH<C>(); ++e) H[e] = Hp[e];
+            for (int e = 0; e < S::template LH<C>(); ++e) H[e] = gld<S>(a.H, t, a.sH, O::H(k), e, a.batch);
 #pragma unroll
-            for (int e = 0; e < S::template Lg<C>(); ++e) g[e] = gp[e];
+            for (int e = 0; e < S::template Lg<C>(); ++e) g[e] = gld<S>(a.g, t, a.sg, O::g(k), e, a.batch);
         }
     }
     __device__ __forceinline__ const KnotIn<S, C> &as_in() const { return *reinterpret_cast<const KnotIn<S, C> *>(this); }
@@ -1232,8 +1245,9 @@ __device__ __forceinline__ void shur_part(Shur<C> &sc, const KktArgs &a, int64_t
     static_assert(!S::GINV || S::HDIAG, "direct kernel: diagonal H or the SOC variant");
     constexpr int R = C::R, W = C::W, p1 = C::P1;
     constexpr int lo = 0, hi = HEAD ? p1 : R;                     // rows i in [lo, hi)
-    const double *Yp = a.Y + t * a.sY + Off<S>::Y(k);
-    const double *Hp = a.H + t * a.sH + Off<S>::H(k), *gp = a.g + t * a.sg + Off<S>::g(k);
+    auto Yp = [&](int e) { return gld<S>(a.Y, t, a.sY, Off<S>::Y(k), e, a.batch); };
+    auto Hp = [&](int e) { return gld<S>(a.H, t, a.sH, Off<S>::H(k), e, a.batch); };
+    auto gp = [&](int e) { return gld<S>(a.g, t, a.sg, Off<S>::g(k), e, a.batch); };
     auto want = [](int i, int i2) { return HEAD ? (i < p1 && i2 < p1) : !(i < p1 && i2 < p1); };
 #pragma unroll
     for (int i = lo; i < hi; ++i) {
@@ -1247,10 +1261,10 @@ __device__ __forceinline__ void shur_part(Shur<C> &sc, const KktArgs &a, int64_t
         double v[R], vh[R];
 #pragma unroll
         for (int i = 0; i < R; ++i)
-            if (!HEAD || i < p1) v[i] = Yp[i + j * R];
+            if (!HEAD || i < p1) v[i] = Yp(i + j * R);
         if constexpr (S::GINV) {
-            const double h = rcp_nr2(Hp[j]);                      // block_cholesky.jl:86 inv
-            const double gh = gp[j];
+            const double h = rcp_nr2(Hp(j));                      // block_cholesky.jl:86 inv
+            const double gh = gp(j);
 #pragma unroll
             for (int i = lo; i < hi; ++i) {
                 vh[i] = v[i] * h;
@@ -1271,9 +1285,8 @@ __device__ __forceinline__ void shur_part(Shur<C> &sc, const KktArgs &a, int64_t
 template <class S, class C>
 __device__ __forceinline__ void y_direct(double (&yc)[Z(C::PS + C::P2)], const KktArgs &a, int64_t t, int k)
 {
-    const double *yp = a.y + t * a.sy + Off<S>::y(k);
 #pragma unroll
-    for (int i = 0; i < C::PS + C::P2; ++i) yc[i] = yp[i];
+    for (int i = 0; i < C::PS + C::P2; ++i) yc[i] = gld<S>(a.y, t, a.sy, Off<S>::y(k), i, a.batch);
 }
 
 template <class S>
@@ -1289,12 +1302,19 @@ __global__ __launch_bounds__(64) void kkt_fild_kernel(const KktArgs a, double *_
     c.nlive = (int)(a.batch - t0 < 64 ? a.batch - t0 : 64);
     c.live = c.lane < c.nlive;
     const int64_t t = t0 + (c.live ? c.lane : c.nlive - 1);     // dead lanes re-read a live one
-    c.bdz = a.dz + t0 * a.sg;
-    c.blam = a.lam + t0 * a.sl;
     c.bS = scratch + (int64_t)blockIdx.x * N * S::SLOT * 64;
     c.vS = 8u * c.lane;
-    c.vdz = (uint32_t)(c.lane * a.sg * 8);
-    c.vlam = (uint32_t)(c.lane * a.sl * 8);
+    if constexpr (S::SOA) {
+        c.bdz = a.dz + t0;
+        c.blam = a.lam + t0;
+        c.rowb = (uint32_t)(a.batch * 8);
+        c.vdz = c.vlam = 8u * c.lane;
+    } else {
+        c.bdz = a.dz + t0 * a.sg;
+        c.blam = a.lam + t0 * a.sl;
+        c.vdz = (uint32_t)(c.lane * a.sg * 8);
+        c.vlam = (uint32_t)(c.lane * a.sl * 8);
+    }
     int info = 0;
 
     // ---------------- forward ----------------
@@ -1420,17 +1440,20 @@ hipError_t launch(const KktArgs &a, hipStream_t s)
     template __global__ void kkt_fil_kernel<Shape<NX, M, A0, AK, AN, true, false, SOA>>(const KktArgs, double *__restrict__);
 #define LQRX_FIL_INST_DIAG(NX, M, A0, AK, AN) LQRX_FIL_INST_DIAG1(NX, M, A0, AK, AN, false) LQRX_FIL_INST_DIAG1(NX, M, A0, AK, AN, true)
 // direct (no LDS staging) variants, diagonal H
-#define LQRX_FILD_INST(NX, M, A0, AK, AN)                                                                \
-    template __global__ void kkt_fild_kernel<Shape<NX, M, A0, AK, AN, true, true>>(const KktArgs, double *__restrict__);  \
-    template __global__ void kkt_fild_kernel<Shape<NX, M, A0, AK, AN, true, false>>(const KktArgs, double *__restrict__);
+#define LQRX_FILD_INST1(NX, M, A0, AK, AN, SOA)                                                          \
+    template __global__ void kkt_fild_kernel<Shape<NX, M, A0, AK, AN, true, true, SOA>>(const KktArgs, double *__restrict__);  \
+    template __global__ void kkt_fild_kernel<Shape<NX, M, A0, AK, AN, true, false, SOA>>(const KktArgs, double *__restrict__);
+#define LQRX_FILD_INST(NX, M, A0, AK, AN) LQRX_FILD_INST1(NX, M, A0, AK, AN, false) LQRX_FILD_INST1(NX, M, A0, AK, AN, true)
 LQRX_FIL_INST(3, 2, 3, 0, 3)
 LQRX_FIL_INST_DIAG(4, 1, 4, 0, 4)
 LQRX_FILD_INST(6, 3, 6, 1, 6)
+LQRX_FILD_INST(4, 2, 4, 1, 4)
 #undef LQRX_FIL_INST
 #undef LQRX_FIL_INST1
 #undef LQRX_FIL_INST_DIAG
 #undef LQRX_FIL_INST_DIAG1
 #undef LQRX_FILD_INST
+#undef LQRX_FILD_INST1
 
 } // namespace fil
 
@@ -1470,14 +1493,20 @@ static bool fil_dispatch(const KktArgs &a, const int32_t *n1, const int32_t *p, 
         return true;                                                                                     \
     }
 #define LQRX_FILD(NX, M, A0, AK, AN)                                                                     \
-    if (nx == NX && m == M && P0 == A0 && PK == AK && PN == AN && (diag || !ginv) && !soa) {             \
-        if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true>{}, std::true_type{});                     \
-        else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{}, std::true_type{});                         \
+    if (nx == NX && m == M && P0 == A0 && PK == AK && PN == AN && (diag || !ginv)) {                     \
+        if (soa) {                                                                                       \
+            if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true, true>{}, std::true_type{});           \
+            else fn(fil::Shape<NX, M, A0, AK, AN, true, false, true>{}, std::true_type{});               \
+        } else {                                                                                         \
+            if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true>{}, std::true_type{});                 \
+            else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{}, std::true_type{});                     \
+        }                                                                                                \
         return true;                                                                                     \
     }
     LQRX_FIL(3, 2, 3, 0, 3)        // Dubins car (BASELINE cfg3), test/dubins.jl
     LQRX_FIL_DIAG(4, 1, 4, 0, 4)   // cartpole trajectory problem (test/problems.jl:58-88, device SQP)
     LQRX_FILD(6, 3, 6, 1, 6)       // DoubleIntegrator(3) (test/problems.jl:14-56, test/cholesky_solve.jl)
+    LQRX_FILD(4, 2, 4, 1, 4)       // DoubleIntegrator(2)
 #undef LQRX_FIL
 #undef LQRX_FIL_SEL
 #undef LQRX_FIL_DIAG

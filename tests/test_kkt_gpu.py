@@ -162,17 +162,20 @@ def test_kkt_meta_cache_overflow(lqrx, gpu_ok):
 
 
 @pytest.mark.parametrize("model,N,batch", [("dubins", 4, 1), ("dubins", 5, 130), ("dubins", 101, 16384 + 3),
-                                           ("cartpole", 7, 70), ("cartpole", 101, 4096 + 5)])
+                                           ("cartpole", 7, 70), ("cartpole", 101, 4096 + 5),
+                                           ("di3", 4, 70), ("di3", 101, 1000), ("di2", 12, 67)])
 @pytest.mark.parametrize("h_mode,ginv", [(2, 1), (0, 1), (1, 1), (2, 0)])
 def test_kkt_layout1_soa(lqrx, gpu_ok, model, N, batch, h_mode, ginv):
     """ABI layout 1 (batch fastest: element e of trajectory t at [e·batch + t]) on the
-    compile-time-shaped kernel: bit-identical to layout 0 (same arithmetic, only the staging
-    differs: 512-B element rows instead of per-trajectory chunks) and within 1e-10 of the
-    oracle; ragged last waves (dead lanes read past the arrays' ends, bounds-checked to 0)."""
+    compile-time-shaped kernels (LDS-staged Dubins / cartpole, direct DoubleIntegrator(2, 3)):
+    bit-identical to layout 0 (same arithmetic, only the staging differs: 512-B element rows
+    instead of per-trajectory chunks) and within 1e-10 of the oracle; ragged last waves (dead
+    lanes read past the arrays' ends, bounds-checked to 0)."""
     import lqrx.kkt as K
 
-    st = K.dubins_structure(N) if model == "dubins" else K.trajectory_structure(4, 1, N)
-    if model == "cartpole" and h_mode != 2 and ginv:
+    st = {"dubins": lambda: K.dubins_structure(N), "cartpole": lambda: K.trajectory_structure(4, 1, N),
+          "di3": lambda: K.double_integrator_structure(3, N), "di2": lambda: K.double_integrator_structure(2, N)}[model]()
+    if model != "dubins" and h_mode != 2 and ginv:
         pb = K.random_kkt(st, 2, seed=1, h_mode=h_mode)            # dense H: no SoA shape
         with pytest.raises(K._lib.LqrxError) as e:
             K.kkt_solve(pb, ginv=ginv, layout=1)
@@ -191,11 +194,11 @@ def test_kkt_layout1_soa(lqrx, gpu_ok, model, N, batch, h_mode, ginv):
 
 
 def test_kkt_layout1_unsupported_shapes(lqrx, gpu_ok):
-    """Layout 1 is served by the compile-time shapes only: the generic structures (here
-    DoubleIntegrator(2, 12)) and N < 4 return LQRX_ERR_UNSUPPORTED."""
+    """Layout 1 is served by the compile-time shapes only: other structures (here n = 5, m = 2)
+    and N < 4 return LQRX_ERR_UNSUPPORTED."""
     import lqrx.kkt as K
 
-    for st in (K.double_integrator_structure(2, 12), K.dubins_structure(3)):
+    for st in (K.trajectory_structure(5, 2, 12), K.dubins_structure(3)):
         pb = K.random_kkt(st, 3, seed=2, h_mode=K.H_DIAG)
         with pytest.raises(K._lib.LqrxError) as e:
             K.kkt_solve(pb, layout=1)
