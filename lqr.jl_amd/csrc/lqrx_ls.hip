@@ -35,6 +35,10 @@ constexpr int LS_BIG_MAX_NM = 1024; // H in global scratch (the "big" path): blo
 constexpr int LS_PB = 16;           // big path: max panel rows factored in LDS per pass (the host
                                     // halves it until the panel fits the LDS budget)
 constexpr size_t LS_LDS_CAP = 163840;
+#ifndef LQRX_LS_PNL
+#define LQRX_LS_PNL 4
+#endif
+constexpr int LS_PNL = LQRX_LS_PNL;  // LDS path: potrf panel rows per barrier pair
 
 // order one wave's LDS accesses across lanes (a wave executes LDS ops in order; this stops
 // the compiler from moving them across and waits for the writes)
@@ -370,57 +374,85 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
         __syncthreads();
     }
     } else {
-    // ---- potrf 'U' (:181): right-looking, one barrier per pivot.  Step j updates the trailing
-    // upper triangle with the unscaled row j (H[i,k] −= H[j,i]·H[j,k]/d_j) and scales row j−1
-    // (read by nobody in step j); info = first non-positive pivot.  Waves own rows (4 per
-    // pass, sharing each loaded H[j,k]), lanes columns: every LDS access is row-contiguous.
-    double dprev = 1.0;
-    for (int j = 0; j < Nm; ++j) {
-        const double d = H[up(j, j, Nm)];
-        if (!(d > 0.0)) {   // uniform: every thread reads the same LDS word
-            ls_fail(gU, gX, ginfo, b, n, m, N, j + 1);
-            return;
-        }
-        const double rinv = rcp_nr2(d);
-        if (j > 0) {
-            const double rdp = rsqrt_nr(dprev);
-            const int rb = rbase(j - 1, Nm);
-            for (int k = j + tid; k < Nm; k += LS_THREADS) H[rb + k] *= rdp;
-            if (tid == 0) {
-                H[rb + j - 1] = dprev * rdp;
-                dinv[j - 1] = rdp;
+    // ---- potrf 'U' (:181): blocked right-looking with LS_PNL-row panels and one-panel
+    // lookahead, one barrier per panel instead of one per pivot.  While waves 1..3 apply panel
+    // p's rank-pr update H[i,k] −= Σ_u U[u,i]·U[u,k] (u in pivot order) to the trailing rows
+    // past panel p+1 (4 rows per wave pass sharing each loaded panel column, lanes over
+    // columns), wave 0 applies it to panel p+1's rows and factors that panel (pivot by pivot,
+    // rows scaled to U at once, in-panel updates; wave-level ordering only).  info = first
+    // non-positive pivot.
+    auto factor_panel = [&](int j0, int pr) {           // wave 0 only
+        for (int u = 0; u < pr; ++u) {
+            const int j = j0 + u, rj = rbase(j, Nm);
+            const double d = H[rj + j];
+            if (!(d > 0.0)) {      // wave-uniform: every lane reads the same LDS word
+                if (lane == 0) *flag = j + 1;
+                return;
             }
+            const double rd = rsqrt_nr(d);
+            for (int k = j + 1 + lane; k < Nm; k += 64) H[rj + k] *= rd;
+            if (lane == 0) {
+                H[rj + j] = d * rd;
+                dinv[j] = rd;
+            }
+            wave_sync();
+            for (int v = j + 1; v < j0 + pr; ++v) {
+                const double ujv = H[rj + v];
+                const int rv = rbase(v, Nm);
+                for (int k = v + lane; k < Nm; k += 64) H[rv + k] = fma(-ujv, H[rj + k], H[rv + k]);
+            }
+            wave_sync();
         }
-        const int rj = rbase(j, Nm);
-        for (int i0 = j + 1 + 4 * wave; i0 < Nm; i0 += 4 * (LS_THREADS / 64)) {
-            double hi[4];
+    };
+    // rows [ia, Nm) −= panel (rows j0..j0+pr−1), by nw waves starting at wave w0; rows ≥ ib skipped
+    auto rank_update = [&](int j0, int pr, int ia, int ib, int w0, int nw) {
+        int rp[LS_PNL];
+#pragma unroll
+        for (int u = 0; u < LS_PNL; ++u) rp[u] = u < pr ? rbase(j0 + u, Nm) : 0;
+        for (int i0 = ia + 4 * (wave - w0); i0 < ib; i0 += 4 * nw) {
+            double ui[4][LS_PNL];
             int rb[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const bool ok = i0 + u < Nm;
-                hi[u] = ok ? H[rj + i0 + u] * rinv : 0.0;
-                rb[u] = ok ? rbase(i0 + u, Nm) : 0;
+            for (int q = 0; q < 4; ++q) {
+                const bool ok = i0 + q < ib;
+                rb[q] = ok ? rbase(i0 + q, Nm) : 0;
+#pragma unroll
+                for (int u = 0; u < LS_PNL; ++u) ui[q][u] = (ok && u < pr) ? H[rp[u] + i0 + q] : 0.0;
             }
             for (int k = i0 + lane; k < Nm; k += 64) {
-                const double hjk = H[rj + k];
-                double h[4];
+                double hp[LS_PNL];
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (i0 + u <= k) h[u] = H[rb[u] + k];
+                for (int u = 0; u < LS_PNL; ++u) hp[u] = u < pr ? H[rp[u] + k] : 0.0;
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (i0 + u <= k) H[rb[u] + k] = fma(-hi[u], hjk, h[u]);
+                for (int q = 0; q < 4; ++q)
+                    if (i0 + q < ib && i0 + q <= k) {
+                        double v = H[rb[q] + k];
+#pragma unroll
+                        for (int u = 0; u < LS_PNL; ++u) v = fma(-ui[q][u], hp[u], v);
+                        H[rb[q] + k] = v;
+                    }
             }
         }
-        dprev = d;
+    };
+    if (wave == 0) factor_panel(0, Nm < LS_PNL ? Nm : LS_PNL);
+    __syncthreads();
+    for (int j0 = 0; j0 < Nm; j0 += LS_PNL) {
+        if (*flag) {            // uniform
+            ls_fail(gU, gX, ginfo, b, n, m, N, *flag);
+            return;
+        }
+        const int pr = Nm - j0 < LS_PNL ? Nm - j0 : LS_PNL, n0 = j0 + pr;
+        if (n0 >= Nm) break;
+        const int pr2 = Nm - n0 < LS_PNL ? Nm - n0 : LS_PNL;
+        if (wave == 0) {
+            rank_update(j0, pr, n0, n0 + pr2, 0, 1);
+            wave_sync();
+            factor_panel(n0, pr2);
+        } else {
+            rank_update(j0, pr, n0 + pr2, Nm, 1, LS_THREADS / 64 - 1);
+        }
         __syncthreads();
     }
-    if (tid == 0) {
-        const double rdp = rsqrt_nr(dprev);
-        H[up(Nm - 1, Nm - 1, Nm)] = dprev * rdp;
-        dinv[Nm - 1] = rdp;
-    }
-    __syncthreads();
     }
     // ---- potrs 'U' (:182): Uᵀz = y, then U x = z — wave 0, y held in registers (lane l owns
     // y[l + 64 s]), the pivot broadcast by readlane: no barriers in the 2·Nm-step chain
