@@ -24,6 +24,7 @@ bench cfg4 --cpu-seconds ${CPUS:-10}
 bench cfg5 --n 64 --m 32 --N 512 --batch 8192 --dtype f32 --no-cpu-baseline
 bench kkt --workload kkt --steps 20 --warmup 20 --cpu-seconds 6
 bench kkt_di --workload kkt --kkt-structure di --steps 20 --warmup 20 --cpu-seconds 6
+bench kkt_soa --workload kkt --kkt-layout 1 --steps 20 --warmup 20 --cpu-seconds 6
 bench cartpole --workload cartpole --steps 20 --warmup 20 --cpu-seconds 6
 bench tv --tv --no-cpu-baseline
 bench ls --workload ls --steps 10 --warmup 5 --cpu-seconds 4
@@ -38,6 +39,7 @@ prof() {  # name, args...
 }
 prof cfg4 --steps 5 --warmup 1
 prof kkt --workload kkt --steps 20 --warmup 20
+prof kkt_soa --workload kkt --kkt-layout 1 --steps 20 --warmup 20
 prof cartpole --workload cartpole --steps 20 --warmup 20
 prof tv --tv --steps 3 --warmup 1
 prof ls --workload ls --steps 5 --warmup 2
