@@ -186,7 +186,7 @@ template <typename T, int NT, int MT> struct DpCfg {
 
 // Forward rollout  dynamic_programming.jl:66-70 :  u_k = −K_k x_k ; x_{k+1} = A x_k + B u_k.
 // K_k is streamed back from global (written by the backward sweep of this same wave),
-// DEPTH knots ahead, straight into registers in the u-phase's lane layout.
+// DEPTH knots ahead, 64 lanes × KPL coalesced elements per knot, staged through LDS.
 // Dot products are split over the wave: u_i by SU = 64/MP lanes (i = lane % MP), x'_i by
 // SX = 64/NP lanes (i = lane % NP), partial sums combined with xor-shuffles.
 template <typename T, int NT, int MT, int DEPTH, bool TV = false>
@@ -206,7 +206,7 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
     const T *__restrict__ Bg = (const T *)a.B + (size_t)b * n * m * (TV && a.tv_AB ? N - 1 : 1);
     T *__restrict__ Xg = (T *)a.X + (size_t)b * (size_t)N * n;
     T *__restrict__ Ug = (T *)a.U + (size_t)b * (size_t)(N - 1) * m;
-    T *xs = lds + MP * NP, *us = xs + NP;
+    T *Ks = lds, *xs = lds + MP * NP, *us = xs + NP;
 
     const int iu = lane % MP, hu = lane / MP;   // u row, column part
     const int ix = lane % NP, hx = lane / NP;   // x row, column part
@@ -235,19 +235,12 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
     if (lane < MP) us[lane] = (T)0;
     if (lane < n) Xg[lane] = x0[lane];
 
-    // K_kk straight into the u-phase's lane layout (lane (iu, hu) holds K[iu][hu·JU + t]):
-    // for each t the 64 lanes read SU runs of MP consecutive elements — no LDS staging
-    T ring[DEPTH][JU];
-    auto issue = [&](int kk, T(&dst)[JU]) {
-        // knot base uniform (scalar), the lane's element a 32-bit offset formed at its use
-        // (laundered: hoisted out of the knot loop, JU 64-bit addresses would be live)
-        const T *Kk = Kg + (size_t)(kk - 1) * mn;
-        uint32_t off = (uint32_t)(iu + hu * JU * m);
-        asm volatile("" : "+v"(off));
+    T ring[DEPTH][KPL];
+    auto issue = [&](int kk, T(&dst)[KPL]) {
 #pragma unroll
-        for (int t = 0; t < JU; ++t) {
-            const int j = hu * JU + t;
-            dst[t] = (kk <= N - 1 && iu < m && j < n) ? Kk[off + (uint32_t)(t * m)] : (T)0;
+        for (int s = 0; s < KPL; ++s) {
+            size_t e = (size_t)lane + 64 * s;
+            dst[s] = (kk <= N - 1 && e < mn) ? Kg[(size_t)(kk - 1) * mn + e] : (T)0;
         }
     };
 #pragma unroll
@@ -259,18 +252,24 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
         for (int d = 0; d < DEPTH; ++d) {
             const int k = k0 + d;
             if (k <= N - 1) {
+#pragma unroll
+                for (int s = 0; s < KPL; ++s) {
+                    size_t e = (size_t)lane + 64 * s;
+                    if (e < mn) Ks[e] = ring[d][s];
+                }
+                issue(k + DEPTH, ring[d]);
                 if constexpr (TV) {
                     if (k + 1 <= N - 1) load_rows(k + 1, arow_n, brow_n);   // next knot's rows
                 }
+                __syncthreads();
                 // u_i = −Σ_j K[i][j] x_j   (dynamic_programming.jl:68)
                 T s0 = 0, s1 = 0;
 #pragma unroll
                 for (int t = 0; t < JU; t += 2) {
                     int j0 = hu * JU + t, j1 = j0 + 1;
-                    if (j0 < n) s0 = fma(ring[d][t], xs[j0], s0);
-                    if (t + 1 < JU && j1 < n) s1 = fma(ring[d][t + 1], xs[j1], s1);
+                    if (j0 < n) s0 = fma(Ks[iu + j0 * m], xs[j0], s0);
+                    if (t + 1 < JU && j1 < n) s1 = fma(Ks[iu + j1 * m], xs[j1], s1);
                 }
-                issue(k + DEPTH, ring[d]);                 // slot consumed: refill DEPTH knots ahead
                 T su = s0 + s1;
 #pragma unroll
                 for (int o = MP; o < 64; o <<= 1) su += __shfl_xor(su, o);
