@@ -429,7 +429,7 @@ size_t kkt_ws_bytes(const lqrx_kkt_desc *d, const lqrx::KktArgs &a)
 }
 int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const void *H, const void *g,
                    void *dz, void *lam, int32_t *info, void *ws, size_t ws_bytes, void *stream,
-                   bool null_sync = true);
+                   bool null_sync = true, const int32_t *sel = nullptr, const int32_t *nsel = nullptr);
 } // namespace
 
 extern "C" int lqrx_kkt_workspace_size(const lqrx_kkt_desc *d, size_t *bytes)
@@ -458,7 +458,8 @@ extern "C" int lqrx_kkt_solve_ws(const lqrx_kkt_desc *d, const void *Y, const vo
 
 namespace {
 int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const void *H, const void *g,
-                   void *dz, void *lam, int32_t *info, void *ws, size_t ws_bytes, void *stream, bool null_sync)
+                   void *dz, void *lam, int32_t *info, void *ws, size_t ws_bytes, void *stream, bool null_sync,
+                   const int32_t *sel, const int32_t *nsel)
 {
     KktLayout L;
     int st = kkt_layout(d, L);
@@ -478,6 +479,13 @@ int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const v
     lqrx::KktArgs a = kkt_args(d, L);
     a.Y = (const double *)Y; a.y = (const double *)y; a.H = (const double *)H; a.g = (const double *)g;
     a.dz = (double *)dz; a.lam = (double *)lam; a.info = info; a.meta = dmeta;
+    // a trajectory subset (internal, SQP): per-lane offsets of the selected trajectories are
+    // 32-bit in the layout-0 kernel
+    if (sel && nsel && d->layout == 0 &&
+        std::max(std::max(L.sY, L.sy), std::max(L.sH, L.sg)) * d->batch * 8 <= INT32_MAX) {
+        a.sel = sel;
+        a.nsel = nsel;
+    }
     if (ws) {
         const size_t need = kkt_ws_bytes(d, a);
         if (ws_bytes < need)
@@ -687,12 +695,12 @@ struct SqpKkt {
     hipStream_t s;
 };
 
-int sqp_kkt(void *ctx, int ginv, double *dz)
+int sqp_kkt(void *ctx, int ginv, double *dz, const int32_t *sel, const int32_t *nsel)
 {
     SqpKkt &c = *(SqpKkt *)ctx;
     c.kd.ginv = ginv;
     return kkt_solve_impl(&c.kd, c.Y, c.y, c.H, c.g, dz, ginv ? c.lamn : c.lams, c.info, c.ws, c.ws_bytes, c.s,
-                          /*null_sync=*/false);
+                          /*null_sync=*/false, sel, nsel);
 }
 } // namespace
 
@@ -740,7 +748,8 @@ extern "C" int lqrx_sqp_solve(const lqrx_sqp_desc *d, double *Z, const double *x
     const size_t oY = take(B * sY * 8), oy = take(B * sy * 8), oH = take(B * sH * 8), og = take(B * sg * 8),
                  odz = take(B * NN * 8), olamn = take(B * P * 8), odzs = take(B * NN * 8), olams = take(B * P * 8),
                  ophi = take(B * 8), odphi = take(B * 8), osoc = take(B * 4),
-                 oact = take(4), oinfo = take(B * 4), ows = take(std::max(ws0, ws1));
+                 oact = take(4), oinfo = take(B * 4), ows = take(std::max(ws0, ws1)),
+                 osel = take(B * 4), onsel = take(4);
     void *blk = nullptr;
     hipError_t e = lqrx::scratch_alloc(&blk, off, s);
     if (e != hipSuccess) return hip_err(e, "sqp scratch");
@@ -757,6 +766,7 @@ extern "C" int lqrx_sqp_solve(const lqrx_sqp_desc *d, double *Z, const double *x
     A.dz = (double *)(b + odz); A.lamn = (double *)(b + olamn); A.dzs = (double *)(b + odzs);
     A.phi0 = (double *)(b + ophi); A.dphi = (double *)(b + odphi);
     A.need_soc = (int32_t *)(b + osoc); A.n_active = (int32_t *)(b + oact);
+    A.sel = (int32_t *)(b + osel); A.nsel = (int32_t *)(b + onsel);
     c.Y = A.Y; c.y = A.y; c.H = A.H; c.g = A.g; c.lamn = A.lamn; c.lams = (double *)(b + olams);
     c.info = (int32_t *)(b + oinfo); c.ws = b + ows; c.ws_bytes = std::max(ws0, ws1); c.s = s;
     int kkt_rc = 0;

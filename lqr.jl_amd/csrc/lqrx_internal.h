@@ -41,6 +41,9 @@ struct KktArgs {
     int maxw, maxrows, max_p1, max_ps, max_p2;
     int force_lane; // debug: LQRX_KKT_FORCE_LANE=1 selects the register-only kernel
     int layout;     // 0 per-trajectory packed; 1 batch fastest (compile-time shapes only)
+    // internal (SQP): solve only the trajectories sel[0 .. *nsel) (device arrays; layout-0
+    // LDS-staged kernel only — the other kernels solve the whole batch, which is also correct)
+    const int32_t *sel, *nsel;
     void *ws;         // caller's device workspace (lqrx_kkt_solve_ws) or NULL: library pool
     size_t ws_bytes;
 };
@@ -98,9 +101,12 @@ struct SqpArgs {
     double *phi0, *dphi;              // B
     int32_t *need_soc;                // B
     int32_t *n_active;                // 1
+    int32_t *sel, *nsel;              // B, 1: the trajectories the next KKT solve needs
 };
-hipError_t sqp_run(const SqpArgs &A, int max_iters, hipStream_t s, int (*kkt)(void *ctx, int ginv, double *dz),
-                   void *ctx, int *kkt_rc);
+// kkt(ctx, ginv, dz, sel, nsel): one KKT solve of the trajectories sel[0 .. *nsel)
+hipError_t sqp_run(const SqpArgs &A, int max_iters, hipStream_t s,
+                   int (*kkt)(void *ctx, int ginv, double *dz, const int32_t *sel, const int32_t *nsel), void *ctx,
+                   int *kkt_rc);
 void sqp_structure(int nx, int nu, int pk, int N, std::vector<int32_t> &n1, std::vector<int32_t> &p,
                    std::vector<int32_t> &n2, std::vector<int32_t> &w);
 bool sqp_model_dims(int model, int *nx, int *nu);

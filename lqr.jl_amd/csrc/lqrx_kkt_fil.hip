@@ -134,7 +134,8 @@ template <int L, bool WIDE> struct Pat {
     static constexpr int unit = WIDE ? 16 : 4;
     static constexpr int per = L * 8 / unit;
     uint32_t vo[per > 0 ? per : 1];
-    __device__ __forceinline__ void init(int64_t s, int lane, int nlive)
+    // sel (optional): the wave's trajectories are sel[0..nlive) instead of 0..nlive-1
+    __device__ __forceinline__ void init(int64_t s, int lane, int nlive, const int32_t *sel = nullptr)
     {
 #pragma unroll
         for (int i = 0; i < per; ++i) {
@@ -142,6 +143,7 @@ template <int L, bool WIDE> struct Pat {
             uint32_t tr = p / (uint32_t)per;
             const uint32_t e = p - tr * (uint32_t)per;
             tr = tr < (uint32_t)nlive ? tr : (uint32_t)(nlive - 1);
+            if (sel) tr = (uint32_t)sel[tr];
             vo[i] = tr * (uint32_t)(s * 8) + e * (uint32_t)unit;
         }
     }
@@ -168,7 +170,7 @@ template <int L> struct Split {
 template <int L> struct PatS {
     using SP = Split<L>;
     uint32_t voA[SP::n12 > 0 ? SP::n12 : 1], voB[SP::n4 > 0 ? SP::n4 : 1];
-    __device__ __forceinline__ void init(int64_t s, int lane, int nlive)
+    __device__ __forceinline__ void init(int64_t s, int lane, int nlive, const int32_t *sel = nullptr)
     {
         const uint32_t sb = (uint32_t)(s * 8);
 #pragma unroll
@@ -177,6 +179,7 @@ template <int L> struct PatS {
             uint32_t tr = p / (uint32_t)(SP::n12 > 0 ? SP::n12 : 1);
             const uint32_t e = p - tr * (uint32_t)(SP::n12 > 0 ? SP::n12 : 1);
             tr = tr < (uint32_t)nlive ? tr : (uint32_t)(nlive - 1);
+            if (sel) tr = (uint32_t)sel[tr];
             voA[i] = tr * sb + 12u * e;
         }
 #pragma unroll
@@ -185,6 +188,7 @@ template <int L> struct PatS {
             uint32_t tr = p / (uint32_t)(SP::n4 > 0 ? SP::n4 : 1);
             const uint32_t e = p - tr * (uint32_t)(SP::n4 > 0 ? SP::n4 : 1);
             tr = tr < (uint32_t)nlive ? tr : (uint32_t)(nlive - 1);
+            if (sel) tr = (uint32_t)sel[tr];
             voB[i] = tr * sb + 12u * SP::n12 + 4u * e;
         }
     }
@@ -297,6 +301,7 @@ template <class S> struct Ctx {
     int lane, nlive;
     bool live;
     uint32_t vS, vdz, vlam;                        // per-lane byte offsets: slab, dz, lam
+    const int32_t *sel = nullptr;                  // layout 0, selected trajectories (a.sel + t0) or null
     uint32_t vsoa = 0, rowb = 0;                   // SOA: lane's row-pair offset, bytes per element row
     uint32_t limY = 0, limy = 0, limH = 0, limg = 0; // SOA: bytes from the wave base to each array's end
     // SOA: L element rows from row r0 of one array, as (L+1)/2 row-pair DMAs (lane l → row
@@ -351,19 +356,19 @@ template <class S> struct Ctx {
             return;
         }
         Pat<S::template LY<C>(), S::WIDE_Y> qY;
-        qY.init(a.sY, lane, nlive);
+        qY.init(a.sY, lane, nlive, sel);
         qY.issue(make_rsrc4(bY), O::Y(k), buf);
         if (fwd) {
             PatS<S::template Ly<C>()> qy;
-            qy.init(a.sy, lane, nlive);
+            qy.init(a.sy, lane, nlive, sel);
             qy.issue(make_rsrc4(by), O::y(k), buf + S::OFF_y / 8);
         }
         if constexpr (S::GINV) {
             PatS<S::template LH<C>()> qH;
-            qH.init(a.sH, lane, nlive);
+            qH.init(a.sH, lane, nlive, sel);
             qH.issue(make_rsrc4(bH), O::H(k), buf + S::OFF_H / 8);
             PatS<S::template Lg<C>()> qg;
-            qg.init(a.sg, lane, nlive);
+            qg.init(a.sg, lane, nlive, sel);
             qg.issue(make_rsrc4(bg), O::g(k), buf + S::OFF_g / 8);
         }
     }
@@ -1018,10 +1023,17 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     const int64_t t0 = (int64_t)blockIdx.x * 64;
     Ctx<S> c;
     c.lane = threadIdx.x;
-    c.nlive = (int)(a.batch - t0 < 64 ? a.batch - t0 : 64);
+    // a.sel (layout 0): wave w solves the trajectories sel[64w ..) of the *nsel selected ones
+    // (the SQP's second-order-correction subset); waves past the end leave at once (uniform)
+    const int64_t nb = (!S::SOA && a.sel) ? (int64_t)*a.nsel : a.batch;
+    if (t0 >= nb) return;
+    c.nlive = (int)(nb - t0 < 64 ? nb - t0 : 64);
     c.live = c.lane < c.nlive;
     c.bS = scratch + (int64_t)blockIdx.x * N * S::SLOT * 64;
     c.vS = 8u * c.lane;
+    if constexpr (!S::SOA) {
+        if (a.sel) c.sel = a.sel + t0;
+    }
     if constexpr (S::SOA) {
         // wave bases at trajectory t0 of element row 0; a lane past the batch end reads the
         // next row's first trajectories (or past the array: buffer bounds return 0) — its
@@ -1040,18 +1052,20 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
         c.vsoa = (uint32_t)(((c.lane >> 5) * a.batch + 2 * (c.lane & 31)) * 8);
         c.vdz = c.vlam = 8u * c.lane;
     } else {
-        c.bY = a.Y + t0 * a.sY;
-        c.by = a.y + t0 * a.sy;
-        c.bH = a.H + t0 * a.sH;
-        c.bg = a.g + t0 * a.sg;
-        c.bdz = a.dz + t0 * a.sg;
-        c.blam = a.lam + t0 * a.sl;
-        c.vdz = (uint32_t)(c.lane * a.sg * 8);
-        c.vlam = (uint32_t)(c.lane * a.sl * 8);
-        c.pY.init(a.sY, c.lane, c.nlive);
-        c.py.init(a.sy, c.lane, c.nlive);
-        c.pH.init(a.sH, c.lane, c.nlive);
-        c.pg.init(a.sg, c.lane, c.nlive);
+        const int64_t tb = c.sel ? 0 : t0;                 // base trajectory of the wave's arrays
+        const int64_t tl = c.sel ? (int64_t)c.sel[c.live ? c.lane : c.nlive - 1] : c.lane;
+        c.bY = a.Y + tb * a.sY;
+        c.by = a.y + tb * a.sy;
+        c.bH = a.H + tb * a.sH;
+        c.bg = a.g + tb * a.sg;
+        c.bdz = a.dz + tb * a.sg;
+        c.blam = a.lam + tb * a.sl;
+        c.vdz = (uint32_t)(tl * a.sg * 8);
+        c.vlam = (uint32_t)(tl * a.sl * 8);
+        c.pY.init(a.sY, c.lane, c.nlive, c.sel);
+        c.py.init(a.sy, c.lane, c.nlive, c.sel);
+        c.pH.init(a.sH, c.lane, c.nlive, c.sel);
+        c.pg.init(a.sg, c.lane, c.nlive, c.sel);
     }
     int info = 0;
 
@@ -1112,7 +1126,7 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
 
 #if LQRX_FIL_ABL & 1
     // ablation (tools only): forward sweep alone
-    if (a.info && c.live) a.info[t0 + c.lane] = info;
+    if (a.info && c.live) a.info[c.sel ? (int64_t)c.sel[c.lane] : t0 + c.lane] = info;
     return;
 #endif
     // ---------------- backward + primal recovery ----------------

@@ -502,6 +502,21 @@ __global__ __launch_bounds__(256) void sqp_init_kernel(const Args A, int64_t P)
     }
 }
 
+// sel ← the trajectories with gate[t] == val (any order: every trajectory's KKT solve is
+// independent of which wave runs it), *nsel ← their count; one atomic per wave
+__global__ __launch_bounds__(256) void sqp_select_kernel(const int32_t *gate, int32_t val, int64_t B, int32_t *sel,
+                                                         int32_t *nsel)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool on = t < B && gate[t] == val;
+    const uint64_t m = __ballot(on);
+    const int lane = threadIdx.x & 63;
+    int32_t base = 0;
+    if (lane == 0 && m) base = atomicAdd(nsel, (int32_t)__popcll(m));
+    base = __shfl(base, 0, 64);
+    if (on) sel[base + (int32_t)__popcll(m & ((1ull << lane) - 1))] = (int32_t)t;
+}
+
 __global__ __launch_bounds__(256) void sqp_finish_kernel(const Args A)
 {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -510,9 +525,19 @@ __global__ __launch_bounds__(256) void sqp_finish_kernel(const Args A)
 
 static dim3 grid_for(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 
+using KktFn = int (*)(void *ctx, int ginv, double *dz, const int32_t *sel, const int32_t *nsel);
+
+// sel ← {t : gate[t] == val}
+static hipError_t select(const SqpArgs &A, const int32_t *gate, int32_t val, hipStream_t s)
+{
+    hipError_t e = hipMemsetAsync(A.nsel, 0, sizeof(int32_t), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(sqp_select_kernel, grid_for(A.B), dim3(256), 0, s, gate, val, A.B, A.sel, A.nsel);
+    return hipGetLastError();
+}
+
 template <class M>
-hipError_t run(const SqpArgs &A, int max_iters, hipStream_t s, int (*kkt)(void *ctx, int ginv, double *dz), void *ctx,
-               int *kkt_rc)
+hipError_t run(const SqpArgs &A, int max_iters, hipStream_t s, KktFn kkt, void *ctx, int *kkt_rc)
 {
     const int64_t BP = A.B * Dims<M>::np_(A.N);
     hipLaunchKernelGGL(sqp_init_kernel, grid_for(BP > A.B ? BP : A.B), dim3(256), 0, s, A, Dims<M>::np_(A.N));
@@ -526,9 +551,13 @@ hipError_t run(const SqpArgs &A, int max_iters, hipStream_t s, int (*kkt)(void *
             (e = hipStreamSynchronize(s)) != hipSuccess)
             return e;
         if (h_active == 0) break;
-        if ((*kkt_rc = kkt(ctx, 1, A.dz)) < 0) return hipSuccess;
+        // Newton step for the still-active trajectories, SOC for those whose full step failed
+        // the Armijo test (usually a few): the KKT kernel runs the selected subset only
+        if ((e = select(A, A.status, ACTIVE, s)) != hipSuccess) return e;
+        if ((*kkt_rc = kkt(ctx, 1, A.dz, A.sel, A.nsel)) < 0) return hipSuccess;
         hipLaunchKernelGGL(sqp_ls1_kernel<M>, gw, bw, 0, s, A);
-        if ((*kkt_rc = kkt(ctx, 0, A.dzs)) < 0) return hipSuccess;
+        if ((e = select(A, A.need_soc, 1, s)) != hipSuccess) return e;
+        if ((*kkt_rc = kkt(ctx, 0, A.dzs, A.sel, A.nsel)) < 0) return hipSuccess;
         hipLaunchKernelGGL(sqp_ls2_kernel<M>, gw, bw, 0, s, A);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
@@ -568,8 +597,7 @@ void sqp_structure(int nx, int nu, int pk, int N, std::vector<int32_t> &n1, std:
 
 namespace {
 template <class Dyn>
-hipError_t run_pk(const SqpArgs &A, int max_iters, hipStream_t s, int (*kkt)(void *, int, double *), void *ctx,
-                  int *kkt_rc)
+hipError_t run_pk(const SqpArgs &A, int max_iters, hipStream_t s, sqp::KktFn kkt, void *ctx, int *kkt_rc)
 {
     switch (A.stage_rows) {
     case 0: return sqp::run<sqp::Prob<Dyn, 0>>(A, max_iters, s, kkt, ctx, kkt_rc);
@@ -582,8 +610,7 @@ hipError_t run_pk(const SqpArgs &A, int max_iters, hipStream_t s, int (*kkt)(voi
 
 // Device driver (lqrx_api.cpp validates and calls this).  kkt(ctx, ginv, dz) runs one KKT
 // solve of the trajectory structure on Y, y, H, g → dz, lamn; a negative return stops the loop.
-hipError_t sqp_run(const SqpArgs &A, int max_iters, hipStream_t s, int (*kkt)(void *ctx, int ginv, double *dz),
-                   void *ctx, int *kkt_rc)
+hipError_t sqp_run(const SqpArgs &A, int max_iters, hipStream_t s, sqp::KktFn kkt, void *ctx, int *kkt_rc)
 {
     switch (A.model) {
     case SQP_DUBINS: return run_pk<sqp::Dubins>(A, max_iters, s, kkt, ctx, kkt_rc);
