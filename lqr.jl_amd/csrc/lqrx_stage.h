@@ -80,25 +80,27 @@ __device__ __forceinline__ u4_t make_rsrc4(const void *base)
 // builtin it makes EVERY later LDS read wait for it (vmcnt(0) before the first read of the
 // knot staged two steps earlier) — which defeats the ring's prefetch entirely.  Issued here the
 // DMA is invisible to that pass: completion is tracked by hand (vm_wait<N>, which counts these
-// like any vector-memory op), the "memory" clobber keeps LDS accesses from moving across it,
-// and M0 is restored for the compiler (M0 is reserved: a clobber of it is not honoured).
+// like any vector-memory op) and the "memory" clobber keeps LDS accesses from moving across it.
+// M0 is set and NOT restored: M0 is reserved (a clobber of it is not honoured), and the
+// kernels including this header leave it unused outside these blocks — which
+// tests/test_isa_guards.py checks on the compiled gfx950 assembly (the round-1 save/restore
+// pair per DMA cost 4–8 % of the KKT kernel in its latency-bound regimes).
 template <int BYTES>
 __device__ __forceinline__ void dma_lds(u4_t r, uint32_t vo, uint32_t so, uint32_t lds)
 {
-    uint32_t keep;
     if constexpr (BYTES == 16)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, %4 offen lds\n\t"
-                     "s_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(vo), "s"(lds), "s"(r), "s"(so) : "memory");
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %2, %3 offen lds" ::"v"(vo), "s"(lds),
+                     "s"(r), "s"(so)
+                     : "memory");
     else if constexpr (BYTES == 12)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx3 %1, %3, %4 offen lds\n\t"
-                     "s_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(vo), "s"(lds), "s"(r), "s"(so) : "memory");
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx3 %0, %2, %3 offen lds" ::"v"(vo), "s"(lds),
+                     "s"(r), "s"(so)
+                     : "memory");
     else {
         static_assert(BYTES == 4, "LDS-DMA piece of 4, 12 or 16 bytes");
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %1, %3, %4 offen lds\n\t"
-                     "s_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(vo), "s"(lds), "s"(r), "s"(so) : "memory");
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dword %0, %2, %3 offen lds" ::"v"(vo), "s"(lds),
+                     "s"(r), "s"(so)
+                     : "memory");
     }
 }
 __device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(size_t)(lptr_t)p; }
