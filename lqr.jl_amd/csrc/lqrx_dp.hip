@@ -43,6 +43,15 @@
 #ifndef LQRX_DP_TVABL
 #define LQRX_DP_TVABL 0     // ablation (tools only): re-read knot-1 inputs, see the kernel
 #endif
+#ifndef LQRX_DP_TVAD
+#define LQRX_DP_TVAD 1      // time-varying rollout: knots of A_k/B_k row prefetch (A/B builds)
+#endif
+#ifndef LQRX_DP_KD
+#define LQRX_DP_KD 4        // rollout: knots of K_k prefetch (A/B builds)
+#endif
+#ifndef LQRX_DP_TVKD
+#define LQRX_DP_TVKD 4      // time-varying rollout: knots of K_k prefetch (A/B builds)
+#endif
 #ifndef LQRX_DP_TVWAIT
 #define LQRX_DP_TVWAIT 0
 #endif
@@ -210,7 +219,9 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
 
     const int iu = lane % MP, hu = lane / MP;   // u row, column part
     const int ix = lane % NP, hx = lane / NP;   // x row, column part
-    T arow[JX], brow[PX], arow_n[TV ? JX : 1], brow_n[TV ? PX : 1];
+    // TV: A_k, B_k rows are prefetched AD knots ahead (a ring rotated by register moves)
+    constexpr int AD = TV ? LQRX_DP_TVAD : 1;
+    T arow[JX], brow[PX], arow_n[AD][TV ? JX : 1], brow_n[AD][TV ? PX : 1];
     auto load_rows = [&](int kk, T *ar, T *br) {   // row ix of A_kk, B_kk (this lane's part)
         const T *Ak = Ag + (int64_t)(kk - 1) * sA, *Bk = Bg + (int64_t)(kk - 1) * sB;
         // per-knot (TV) loads: lane-derived offsets are laundered and kept 32-bit, so they
@@ -230,6 +241,11 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
         }
     };
     load_rows(1, arow, brow);
+    if constexpr (TV) {
+#pragma unroll
+        for (int d = 0; d + 1 < AD; ++d)
+            if (2 + d <= N - 1) load_rows(2 + d, arow_n[d], brow_n[d]);
+    }
     const T *x0 = (const T *)a.x0 + (size_t)b * n;
     if (lane < NP) xs[lane] = (lane < n) ? x0[lane] : (T)0;
     if (lane < MP) us[lane] = (T)0;
@@ -259,7 +275,7 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
                 }
                 issue(k + DEPTH, ring[d]);
                 if constexpr (TV) {
-                    if (k + 1 <= N - 1) load_rows(k + 1, arow_n, brow_n);   // next knot's rows
+                    if (k + AD <= N - 1) load_rows(k + AD, arow_n[AD - 1], brow_n[AD - 1]);   // AD knots ahead
                 }
                 __syncthreads();
                 // u_i = −Σ_j K[i][j] x_j   (dynamic_programming.jl:68)
@@ -297,9 +313,16 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
                 }
                 if constexpr (TV) {
 #pragma unroll
-                    for (int t = 0; t < JX; ++t) arow[t] = arow_n[t];
+                    for (int t = 0; t < JX; ++t) arow[t] = arow_n[0][t];
 #pragma unroll
-                    for (int t = 0; t < PX; ++t) brow[t] = brow_n[t];
+                    for (int t = 0; t < PX; ++t) brow[t] = brow_n[0][t];
+#pragma unroll
+                    for (int d = 0; d + 1 < AD; ++d) {
+#pragma unroll
+                        for (int t = 0; t < JX; ++t) arow_n[d][t] = arow_n[d + 1][t];
+#pragma unroll
+                        for (int t = 0; t < PX; ++t) brow_n[d][t] = brow_n[d + 1][t];
+                    }
                 }
                 __syncthreads();
             }
@@ -486,7 +509,7 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        dp_rollout<T, NT, MT, 4, TV>(a, b, lds, lane);
+        dp_rollout<T, NT, MT, TV ? LQRX_DP_TVKD : LQRX_DP_KD, TV>(a, b, lds, lane);
     }
 }
 
