@@ -27,6 +27,16 @@
 #include <cmath>
 #include <vector>
 
+#ifndef LQRX_SQP_YSTAGE
+#define LQRX_SQP_YSTAGE 1   // stage the expand kernel's Y blocks through LDS (0: direct stores, A/B)
+#endif
+#ifndef LQRX_SQP_ETPB
+#define LQRX_SQP_ETPB 1     // expand kernel: waves (trajectories) per workgroup (A/B: 1 ≥ 2 > 4)
+#endif
+#ifndef LQRX_SQP_EWAVES
+#define LQRX_SQP_EWAVES 1   // expand kernel: minimum waves per SIMD the register allocation targets
+#endif
+
 namespace lqrx {
 namespace sqp {
 
@@ -306,8 +316,10 @@ template <class M> __device__ void accept(const Args &A, int64_t t, const KnotPt
 // Σ|c|, max|c|, ‖g_k + Y_kᵀ m_k‖² with m_k = [λ_{k-1}; μ_k; λ_k] the multipliers of the
 // last Newton step (calc_residual!, cholesky_solver.jl:201-236).  Then the wave's check:
 // ‖c‖∞ < tol_p and ‖∇f + ∇cᵀλ‖₂ < tol_d → converged (cholesky_solver.jl:129-137).
+// Y_k goes to `Y` (the wave's LDS image of its 64 knots' blocks when staged, else HBM)
 template <class M>
-__device__ void expand_knot(const Args &A, int t, int k, double &cost, double &c1, double &cinf, double &r2)
+__device__ __forceinline__ void expand_knot(const Args &A, int t, int k, double *Y, double &cost, double &c1,
+                                            double &cinf, double &r2)
 {
     using D = Dims<M>;
     constexpr int NX = M::NX, NU = M::NU, W = NX + NU, PK = M::PK, RM = 2 * NX + PK;
@@ -315,7 +327,6 @@ __device__ void expand_knot(const Args &A, int t, int k, double &cost, double &c
     const int64_t NN = D::nn(N), P = D::np_(N);
     const double *z = A.Z + t * NN + (int64_t)W * k;
     const double *xf = A.xf + (int64_t)t * NX;
-    double *Y = A.Y + t * D::ny_(N) + D::oY(k);
     double *y = A.y + t * P + D::oy(k);
     double *H = A.H + t * NN + (int64_t)W * k;
     double *g = A.g + t * NN + (int64_t)W * k;
@@ -396,13 +407,44 @@ __device__ void expand_knot(const Args &A, int t, int k, double &cost, double &c
     }
 }
 
-template <class M> __global__ __launch_bounds__(64 * TPB) void sqp_expand_kernel(const Args A)
+// The 64 knots a wave expands at once own one contiguous run of Y (consecutive knot blocks,
+// Dims::oY).  Written lane-per-knot, every store instruction touches 64 blocks RM·W·8 bytes
+// apart; staged, the blocks are built in the wave's LDS image and the run is copied out in
+// 512-B rows.  Staged when the image fits 20 KB per wave.
+template <class M> constexpr int yimg_doubles() { return 64 * (2 * M::NX + M::PK) * (M::NX + M::NU); }
+template <class M> constexpr bool y_staged() { return LQRX_SQP_YSTAGE && yimg_doubles<M>() * 8 <= 20480; }
+constexpr int ETPB = LQRX_SQP_ETPB;                       // trajectories (waves) per expand workgroup
+
+__device__ inline void wave_sync()
 {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+template <class M> __global__ __launch_bounds__(64 * ETPB, LQRX_SQP_EWAVES) void sqp_expand_kernel(const Args A)
+{
+    using D = Dims<M>;
+    constexpr bool ST = y_staged<M>();
+    __shared__ double yimg[ST ? ETPB * yimg_doubles<M>() : 1];
     const int lane = threadIdx.x & 63;
-    const int64_t t = (int64_t)blockIdx.x * TPB + (threadIdx.x >> 6);
+    const int64_t t = (int64_t)blockIdx.x * ETPB + (threadIdx.x >> 6);
     if (t >= A.B || A.status[t] != ACTIVE) return;                 // wave-uniform
     double cost = 0.0, c1 = 0.0, cinf = 0.0, r2 = 0.0;
-    for (int k = lane; k < A.N; k += 64) expand_knot<M>(A, (int)t, k, cost, c1, cinf, r2);
+    const int N = A.N;
+    double *Yt = A.Y + t * D::ny_(N);
+    double *yw = yimg + (ST ? (threadIdx.x >> 6) * yimg_doubles<M>() : 0);
+    for (int kb = 0; kb < N; kb += 64) {
+        const int k = kb + lane;
+        const int64_t e0 = D::oY(kb);
+        if (k < N) expand_knot<M>(A, (int)t, k, ST ? yw + (D::oY(k) - e0) : Yt + D::oY(k), cost, c1, cinf, r2);
+        if constexpr (ST) {
+            const int64_t e1 = kb + 64 < N ? D::oY(kb + 64) : D::ny_(N);
+            wave_sync();
+            for (int64_t i = lane; i < e1 - e0; i += 64) Yt[e0 + i] = yw[i];
+            wave_sync();
+        }
+    }
     const double f = wave_sum(cost), cs = wave_sum(c1), cm = wave_max(cinf), rs = wave_sum(r2);
     if (lane != 0) return;
     if (cm < A.tol_p && sqrt(rs) < A.tol_d) {
@@ -545,8 +587,9 @@ hipError_t run(const SqpArgs &A, int max_iters, hipStream_t s, KktFn kkt, void *
     for (int it = 0; it < max_iters; ++it) {
         hipError_t e = hipMemsetAsync(A.n_active, 0, sizeof(int32_t), s);
         if (e != hipSuccess) return e;
+        const dim3 ge((unsigned)((A.B + ETPB - 1) / ETPB)), be(64 * ETPB);
         const dim3 gw((unsigned)((A.B + TPB - 1) / TPB)), bw(64 * TPB);
-        hipLaunchKernelGGL(sqp_expand_kernel<M>, gw, bw, 0, s, A);
+        hipLaunchKernelGGL(sqp_expand_kernel<M>, ge, be, 0, s, A);
         if ((e = hipMemcpyAsync(&h_active, A.n_active, sizeof(int32_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
             (e = hipStreamSynchronize(s)) != hipSuccess)
             return e;

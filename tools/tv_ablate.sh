@@ -1,18 +1,24 @@
 #!/bin/bash
-# Build (here, on the CPU) liblqrx variants whose time-varying DP kernel drops one source of
-# work each, for the A/B of DESIGN.md §3.1 (VAR_TV).  Run the bench on each with LQRX_LIB.
+# Build (here, on the CPU) liblqrx variants for A/B runs (tools/gpu_tvabl.sh runs the bench on
+# each with LQRX_LIB).  One source (SRC, default lqrx_dp.hip) is rebuilt with extra defines; the
+# others are linked from the in-tree build.  Arguments: name:defines ...  Defaults (SRC =
+# lqrx_dp.hip): the time-varying DP ablation of profiles/r02/dp_tv_ablation_r02.txt —
 #   TVABL bit 1: Q_k re-read from knot 1 (cache-resident); bit 2: A_k/B_k/R_k likewise
-#   TVEXTRA 4: no rollout (VAR_NOROLL)
+#   TVEXTRA 4: no rollout (VAR_NOROLL);  TVKD / TVAD: rollout prefetch depths
 set -e
 cd "$(dirname "$0")/../lqr.jl_amd/csrc"
-OBJS="build/lqrx_dp_lane.hip.o build/lqrx_layout.hip.o build/lqrx_kkt.hip.o build/lqrx_kkt_fil.hip.o build/lqrx_sqp.hip.o build/lqrx_ls.hip.o build/lqrx_api.cpp.o"
+SRC=${SRC:-lqrx_dp.hip}
+OBJS=""
+for f in lqrx_dp.hip lqrx_dp_lane.hip lqrx_layout.hip lqrx_kkt.hip lqrx_kkt_fil.hip lqrx_sqp.hip lqrx_ls.hip lqrx_api.cpp; do
+  [ $f = $SRC ] || OBJS="$OBJS build/$f.o"
+done
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -I../../include -munsafe-fp-atomics"
 mk() {  # name, defines
-  /opt/rocm/bin/hipcc $FL $2 -c lqrx_dp.hip -o build/dp_$1.o
-  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../../tools/abl/liblqrx_$1.so build/dp_$1.o $OBJS -lpthread
+  /opt/rocm/bin/hipcc $FL $2 -c $SRC -o build/abl_$1.o
+  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../../tools/abl/liblqrx_$1.so build/abl_$1.o $OBJS -lpthread
 }
-#   TVKD / TVAD: rollout prefetch depth (knots) of K_k and of the A_k/B_k rows
 if [ $# -eq 0 ]; then set -- q:-DLQRX_DP_TVABL=1 abr:-DLQRX_DP_TVABL=2 all:-DLQRX_DP_TVABL=3 \
     noroll:-DLQRX_DP_TVEXTRA=4 "noroll_all:-DLQRX_DP_TVEXTRA=4 -DLQRX_DP_TVABL=3"; fi
+mkdir -p ../../tools/abl
 for v in "$@"; do mk "${v%%:*}" "${v#*:}" & done   # name:defines
 wait
