@@ -38,7 +38,8 @@
 extern "C" {
 #endif
 
-#define LQRX_ABI_VERSION 2   /* 2: layout 1 (DP, KKT), lqrx_sqp_* (models, stage constraints) */
+#define LQRX_ABI_VERSION 3   /* 2: layout 1 (DP, KKT), lqrx_sqp_* (models, stage constraints);
+                                3: lqrx_dp_solve_linear[_host] (linear cost terms) */
 
 #define LQRX_F64 0
 #define LQRX_F32 1
@@ -98,6 +99,39 @@ int lqrx_dp_solve(const lqrx_dp_desc *desc, const void *A, const void *B, const 
 int lqrx_dp_solve_host(const lqrx_dp_desc *desc, const void *A, const void *B, const void *Q,
                        const void *R, const void *Qf, const void *x0, void *K, void *P,
                        void *X, void *U, int32_t *info);
+
+/* ------------------------------------------------------------------------------------
+ * DP path with linear cost terms — SURVEY §8(f) rank 1 ("time-varying LQR … and cost
+ * linear terms"), an extension of the reference LQRProblem (lqr_problem.jl:1-11 has no
+ * linear terms).  Stage cost ½xᵀQx + qᵀx + ½uᵀRu + rᵀu, terminal ½xᵀQf x + qfᵀx; the
+ * value function gains a linear part V_k(x) = ½xᵀP_k x + p_kᵀx and the policy a
+ * feedforward: u_k = −K_k x_k − d_k.  In the reference's op order (oracle/lqr_oracle.c
+ * oracle_dp_solve_one_lin): d_k = E⁻¹(r_k + Bᵀp_{k+1}) is one more right-hand side of
+ * chol_solve! (dynamic_programming.jl:42), p_k = q_k + Aᵀp_{k+1} − APB·d_k follows :51.
+ * Same descriptor, inputs and outputs as lqrx_dp_solve plus:
+ *   q   n·batch, or n·(N−1)·batch when knot_stride_QR = 1 (knot k at k−1, like Q)
+ *   r   m·batch, or m·(N−1)·batch when knot_stride_QR = 1
+ *   qf  n·batch
+ *   d   out: m·(N−1)·batch   feedforward d_k, k = 1..N−1
+ *   p   out: n·batch (p_mode 0: p_1) or n·N·batch (p_mode 1: p_k, p_N = qf)
+ * layout 1 applies to these arrays as well.  All zero q, r, qf give the lqrx_dp_solve
+ * results (with d = 0, p = 0).
+ * ------------------------------------------------------------------------------------ */
+typedef struct lqrx_dp_linear {
+    const void *q, *r, *qf; /* linear cost terms (inputs)        */
+    void *d, *p;            /* feedforward, linear cost-to-go (outputs) */
+} lqrx_dp_linear;
+
+int lqrx_dp_solve_linear(const lqrx_dp_desc *desc, const void *A, const void *B,
+                         const void *Q, const void *R, const void *Qf, const void *x0,
+                         const lqrx_dp_linear *lin, void *K, void *P, void *X, void *U,
+                         int32_t *info, void *stream);
+
+/* host pointers in lin and everywhere else: H2D, solve, D2H, synchronous */
+int lqrx_dp_solve_linear_host(const lqrx_dp_desc *desc, const void *A, const void *B,
+                              const void *Q, const void *R, const void *Qf, const void *x0,
+                              const lqrx_dp_linear *lin, void *K, void *P, void *X, void *U,
+                              int32_t *info);
 
 /* ------------------------------------------------------------------------------------
  * KKT path: one inner solve of CholeskySolver._solve!(solver)

@@ -97,6 +97,37 @@ function solve!(sol::LQRSolution{T}, prob::LQRProblem{n,m,T}) where {n,m,T}
     solve!(sol, DPSolver(b), b)
 end
 
+# ---- linear cost terms (lqrx_dp_linear; SURVEY §8(f) rank 1, no upstream counterpart) ----
+struct DpLinear
+    q::Ptr{Cvoid}; r::Ptr{Cvoid}; qf::Ptr{Cvoid}
+    d::Ptr{Cvoid}; p::Ptr{Cvoid}
+end
+
+"""
+    solve_linear!(sol, d, p, solver, prob, q, r, qf)
+
+Batched DP with stage cost ½xᵀQx + qᵀx + ½uᵀRu + rᵀu and terminal ½xᵀQf x + qfᵀx
+(q: n×batch, r: m×batch, qf: n×batch).  Outputs as solve! plus the feedforward
+d (m×(N-1)×batch, u_k = −K_k x_k − d_k) and the linear cost-to-go p (n×batch = p₁, or
+n×N×batch with all_P).  lqrx_dp_solve_linear_host.
+"""
+function solve_linear!(sol::LQRSolution{T}, d::Array{T,3}, p::Array{T}, solver::DPSolver{T},
+                       prob::LQRBatch{T}, q::Matrix{T}, r::Matrix{T}, qf::Matrix{T}) where T
+    n, m, N = solver.n, solver.m, solver.N
+    batch = size(prob.A, 3)
+    all_P = ndims(sol.P) == 4
+    desc = Ref(DpDesc(n, m, N, dtypecode(T), batch, 0, all_P ? 1 : 0, 0, 0))
+    GC.@preserve prob sol d p q r qf begin
+        lin = Ref(DpLinear(pointer(q), pointer(r), pointer(qf), pointer(d), pointer(p)))
+        rc = ccall((:lqrx_dp_solve_linear_host, liblqrx), Cint,
+                   (Ref{DpDesc}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ref{DpLinear},
+                    Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{Int32}),
+                   desc, prob.A, prob.B, prob.Q, prob.R, prob.Qf, prob.x0, lin,
+                   sol.K, sol.P, sol.X, sol.U, sol.info)
+    end
+    return check(rc)
+end
+
 # ---- KKT: lqrx_kkt_desc ----
 struct KktDesc
     N::Int32; dtype::Int32

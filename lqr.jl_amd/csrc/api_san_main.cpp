@@ -59,6 +59,15 @@ int main()
     CHECK(lqrx_dp_solve(&b, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, info, nullptr) < 0);
     CHECK(lqrx_dp_solve(&d, dummy, nullptr, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, info, nullptr) == -3);
     CHECK(lqrx_dp_solve(&d, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, nullptr, dummy, info, nullptr) == -10);
+    // linear cost terms: lin (argument 8) and its pointers validated before any device work
+    CHECK(lqrx_dp_solve_linear(&d, dummy, dummy, dummy, dummy, dummy, dummy, nullptr, dummy, dummy, dummy, dummy, info, nullptr) == -8);
+    {
+        lqrx_dp_linear ln{dummy, dummy, nullptr, dummy, dummy};
+        CHECK(lqrx_dp_solve_linear(&d, dummy, dummy, dummy, dummy, dummy, dummy, &ln, dummy, dummy, dummy, dummy, info, nullptr) == -8);
+        CHECK(lqrx_dp_solve_linear_host(&d, dummy, dummy, dummy, dummy, dummy, dummy, nullptr, dummy, dummy, dummy, dummy, info) == -8);
+        ln.qf = dummy;
+        CHECK(lqrx_dp_solve_linear(&d, dummy, dummy, dummy, dummy, dummy, dummy, &ln, dummy, nullptr, dummy, dummy, info, nullptr) == -10);
+    }
     b = d; b.batch = 0;                                          // empty batch: nothing to do
     CHECK(lqrx_dp_solve(&b, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr) == 0);
     if (!have_gpu) {                                             // valid call, no device: clean failure

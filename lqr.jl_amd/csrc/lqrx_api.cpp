@@ -137,14 +137,18 @@ hipError_t dp_launch_soa_staged(const lqrx::DpArgs &a, hipStream_t s)
 {
     const int64_t B = a.batch, n = a.n, m = a.m, N = a.N, es = dsize(a.dtype);
     const int64_t kAB = a.tv_AB ? N - 1 : 1, kQR = a.tv_QR ? N - 1 : 1;
-    const int64_t S_in[6] = {n * n * kAB, n * m * kAB, n * n * kQR, m * m * kQR, n * n, n};
-    const int64_t S_out[4] = {m * n * (N - 1), a.p_all ? n * n * N : n * n, n * N, m * (N - 1)};
-    const void *in[6] = {a.A, a.B, a.Q, a.R, a.Qf, a.x0};
-    void *out[4] = {a.K, a.P, a.X, a.U};
-    size_t off[10], total = 0;
-    for (int i = 0; i < 10; ++i) {
+    // inputs A B Q R Qf x0 [q r qf], outputs K P X U [d p]
+    const int nin = a.lin ? 9 : 6, nout = a.lin ? 6 : 4;
+    const int64_t S_in[9] = {n * n * kAB, n * m * kAB, n * n * kQR, m * m * kQR, n * n, n,
+                             n * kQR, m * kQR, n};
+    const int64_t S_out[6] = {m * n * (N - 1), a.p_all ? n * n * N : n * n, n * N, m * (N - 1),
+                              m * (N - 1), a.p_all ? n * N : n};
+    const void *in[9] = {a.A, a.B, a.Q, a.R, a.Qf, a.x0, a.q, a.r, a.qf};
+    void *out[6] = {a.K, a.P, a.X, a.U, a.d, a.p};
+    size_t off[15], total = 0;
+    for (int i = 0; i < nin + nout; ++i) {
         off[i] = total;
-        total += ((size_t)(i < 6 ? S_in[i] : S_out[i - 6]) * B * es + 255) & ~(size_t)255;
+        total += ((size_t)(i < nin ? S_in[i] : S_out[i - nin]) * B * es + 255) & ~(size_t)255;
     }
     void *blk = nullptr;
     hipError_t e = lqrx::scratch_alloc(&blk, total, s);
@@ -152,16 +156,16 @@ hipError_t dp_launch_soa_staged(const lqrx::DpArgs &a, hipStream_t s)
     char *base = (char *)blk;
     lqrx::DpArgs a0 = a;
     a0.layout = 0;
-    const void **pin[6] = {&a0.A, &a0.B, &a0.Q, &a0.R, &a0.Qf, &a0.x0};
-    void **pout[4] = {&a0.K, &a0.P, &a0.X, &a0.U};
-    for (int i = 0; i < 6 && e == hipSuccess; ++i) {          // [S][B] → [B][S]
+    const void **pin[9] = {&a0.A, &a0.B, &a0.Q, &a0.R, &a0.Qf, &a0.x0, &a0.q, &a0.r, &a0.qf};
+    void **pout[6] = {&a0.K, &a0.P, &a0.X, &a0.U, &a0.d, &a0.p};
+    for (int i = 0; i < nin && e == hipSuccess; ++i) {        // [S][B] → [B][S]
         *pin[i] = base + off[i];
         e = lqrx::batch_transpose(in[i], base + off[i], S_in[i], B, (int)es, s);
     }
-    for (int i = 0; i < 4; ++i) *pout[i] = base + off[6 + i];
+    for (int i = 0; i < nout; ++i) *pout[i] = base + off[nin + i];
     if (e == hipSuccess) e = lqrx::dp_launch(a0, s);
-    for (int i = 0; i < 4 && e == hipSuccess; ++i)            // [B][S] → [S][B]
-        e = lqrx::batch_transpose(base + off[6 + i], out[i], B, S_out[i], (int)es, s);
+    for (int i = 0; i < nout && e == hipSuccess; ++i)         // [B][S] → [S][B]
+        e = lqrx::batch_transpose(base + off[nin + i], out[i], B, S_out[i], (int)es, s);
     hipError_t ef = lqrx::scratch_free(blk, s);
     return e != hipSuccess ? e : ef;
 }
@@ -194,21 +198,37 @@ int lqrx_device_available(void)
     return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
 }
 
-int lqrx_dp_solve(const lqrx_dp_desc *d, const void *A, const void *B, const void *Q,
-                  const void *R, const void *Qf, const void *x0, void *K, void *P, void *X,
-                  void *U, int32_t *info, void *stream)
+}   // extern "C"
+
+namespace {
+// lqrx_dp_solve and lqrx_dp_solve_linear (lin != NULL); argument numbers in error codes
+// follow the calling entry point's signature
+int dp_solve_impl(const lqrx_dp_desc *d, const void *A, const void *B, const void *Q,
+                  const void *R, const void *Qf, const void *x0, const lqrx_dp_linear *lin,
+                  void *K, void *P, void *X, void *U, int32_t *info, void *stream)
 {
     int st = validate_dp(d);
     if (st) return st;
     if (d->batch == 0) return 0;
+    const int o = lin ? 1 : 0;   // lqrx_dp_solve_linear: lin is argument 8, outputs shift by one
     const void *in[6] = {A, B, Q, R, Qf, x0};
     for (int i = 0; i < 6; ++i)
         if (!in[i]) return set_err(-(i + 2), "input pointer %d is NULL", i + 2);
+    if (lin) {
+        const void *lp[5] = {lin->q, lin->r, lin->qf, lin->d, lin->p};
+        static const char *nm[5] = {"q", "r", "qf", "d", "p"};
+        for (int i = 0; i < 5; ++i)
+            if (!lp[i]) return set_err(-8, "lin->%s is NULL", nm[i]);
+    }
     void *out[4] = {K, P, X, U};
     for (int i = 0; i < 4; ++i)
-        if (!out[i]) return set_err(-(i + 8), "output pointer %d is NULL", i + 8);
+        if (!out[i]) return set_err(-(i + 8 + o), "output pointer %d is NULL", i + 8 + o);
 
     lqrx::DpArgs a{};
+    if (lin) {
+        a.lin = 1;
+        a.q = lin->q; a.r = lin->r; a.qf = lin->qf; a.d = lin->d; a.p = lin->p;
+    }
     a.A = A; a.B = B; a.Q = Q; a.R = R; a.Qf = Qf; a.x0 = x0;
     a.K = K; a.P = P; a.X = X; a.U = U; a.info = info;
     a.n = d->n; a.m = d->m; a.N = d->N; a.dtype = d->dtype; a.p_all = d->p_mode;
@@ -238,36 +258,48 @@ int lqrx_dp_solve(const lqrx_dp_desc *d, const void *A, const void *B, const voi
     return 0;
 }
 
-int lqrx_dp_solve_host(const lqrx_dp_desc *d, const void *A, const void *B, const void *Q,
-                       const void *R, const void *Qf, const void *x0, void *K, void *P,
-                       void *X, void *U, int32_t *info)
+int dp_solve_host_impl(const lqrx_dp_desc *d, const void *A, const void *B, const void *Q,
+                       const void *R, const void *Qf, const void *x0, const lqrx_dp_linear *lin,
+                       void *K, void *P, void *X, void *U, int32_t *info)
 {
     int st = validate_dp(d);
     if (st) return st;
     if (d->batch == 0) return 0;
+    const int o = lin ? 1 : 0;
     const size_t s = dsize(d->dtype), bt = (size_t)d->batch;
     const size_t n = d->n, m = d->m, N = d->N;
     const size_t kAB = d->knot_stride_AB ? N - 1 : 1, kQR = d->knot_stride_QR ? N - 1 : 1;
-    const size_t szin[6] = {n * n * kAB, n * m * kAB, n * n * kQR, m * m * kQR, n * n, n};
-    const void *hin[6] = {A, B, Q, R, Qf, x0};
-    const size_t szout[4] = {m * n * (N - 1), d->p_mode ? n * n * N : n * n, n * N, m * (N - 1)};
-    void *hout[4] = {K, P, X, U};
-    DevBuf din[6], dout[4], dinfo;
-    for (int i = 0; i < 6; ++i) {
-        if (!hin[i]) return set_err(-(i + 2), "input pointer %d is NULL", i + 2);
+    const int nin = lin ? 9 : 6, nout = lin ? 6 : 4;
+    const size_t szin[9] = {n * n * kAB, n * m * kAB, n * n * kQR, m * m * kQR, n * n, n,
+                            n * kQR, m * kQR, n};
+    const void *hin[9] = {A, B, Q, R, Qf, x0, lin ? lin->q : nullptr, lin ? lin->r : nullptr,
+                          lin ? lin->qf : nullptr};
+    const size_t szout[6] = {m * n * (N - 1), d->p_mode ? n * n * N : n * n, n * N, m * (N - 1),
+                             m * (N - 1), d->p_mode ? n * N : n};
+    void *hout[6] = {K, P, X, U, lin ? lin->d : nullptr, lin ? lin->p : nullptr};
+    DevBuf din[9], dout[6], dinfo;
+    for (int i = 0; i < nin; ++i) {
+        if (!hin[i]) return set_err(i < 6 ? -(i + 2) : -8, "input pointer %s is NULL",
+                                    i < 6 ? "" : "in lin");
         if ((st = dev_alloc(din[i], szin[i] * s * bt, "hipMalloc input"))) return st;
         hipError_t e = hipMemcpy(din[i].p, hin[i], szin[i] * s * bt, hipMemcpyHostToDevice);
         if (e != hipSuccess) return hip_err(e, "H2D");
     }
-    for (int i = 0; i < 4; ++i) {
-        if (!hout[i]) return set_err(-(i + 8), "output pointer %d is NULL", i + 8);
+    for (int i = 0; i < nout; ++i) {
+        if (!hout[i]) return set_err(i < 4 ? -(i + 8 + o) : -8, "output pointer %s is NULL",
+                                     i < 4 ? "" : "in lin");
         if ((st = dev_alloc(dout[i], szout[i] * s * bt, "hipMalloc output"))) return st;
     }
     if ((st = dev_alloc(dinfo, 4 * bt, "hipMalloc info"))) return st;
-    st = lqrx_dp_solve(d, din[0].p, din[1].p, din[2].p, din[3].p, din[4].p, din[5].p, dout[0].p,
-                       dout[1].p, dout[2].p, dout[3].p, (int32_t *)dinfo.p, nullptr);
+    lqrx_dp_linear dl{};
+    if (lin) {
+        dl.q = din[6].p; dl.r = din[7].p; dl.qf = din[8].p; dl.d = dout[4].p; dl.p = dout[5].p;
+    }
+    st = dp_solve_impl(d, din[0].p, din[1].p, din[2].p, din[3].p, din[4].p, din[5].p,
+                       lin ? &dl : nullptr, dout[0].p, dout[1].p, dout[2].p, dout[3].p,
+                       (int32_t *)dinfo.p, nullptr);
     if (st < 0) return st;
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < nout; ++i) {
         hipError_t e = hipMemcpy(hout[i], dout[i].p, szout[i] * s * bt, hipMemcpyDeviceToHost);
         if (e != hipSuccess) return hip_err(e, "D2H");
     }
@@ -276,6 +308,41 @@ int lqrx_dp_solve_host(const lqrx_dp_desc *d, const void *A, const void *B, cons
         if (e != hipSuccess) return hip_err(e, "D2H info");
     }
     return st;
+}
+} // namespace
+
+extern "C" {
+
+int lqrx_dp_solve(const lqrx_dp_desc *d, const void *A, const void *B, const void *Q,
+                  const void *R, const void *Qf, const void *x0, void *K, void *P, void *X,
+                  void *U, int32_t *info, void *stream)
+{
+    return dp_solve_impl(d, A, B, Q, R, Qf, x0, nullptr, K, P, X, U, info, stream);
+}
+
+int lqrx_dp_solve_host(const lqrx_dp_desc *d, const void *A, const void *B, const void *Q,
+                       const void *R, const void *Qf, const void *x0, void *K, void *P,
+                       void *X, void *U, int32_t *info)
+{
+    return dp_solve_host_impl(d, A, B, Q, R, Qf, x0, nullptr, K, P, X, U, info);
+}
+
+int lqrx_dp_solve_linear(const lqrx_dp_desc *d, const void *A, const void *B, const void *Q,
+                         const void *R, const void *Qf, const void *x0,
+                         const lqrx_dp_linear *lin, void *K, void *P, void *X, void *U,
+                         int32_t *info, void *stream)
+{
+    if (!lin) return set_err(-8, "lin is NULL");
+    return dp_solve_impl(d, A, B, Q, R, Qf, x0, lin, K, P, X, U, info, stream);
+}
+
+int lqrx_dp_solve_linear_host(const lqrx_dp_desc *d, const void *A, const void *B,
+                              const void *Q, const void *R, const void *Qf, const void *x0,
+                              const lqrx_dp_linear *lin, void *K, void *P, void *X, void *U,
+                              int32_t *info)
+{
+    if (!lin) return set_err(-8, "lin is NULL");
+    return dp_solve_host_impl(d, A, B, Q, R, Qf, x0, lin, K, P, X, U, info);
 }
 
 

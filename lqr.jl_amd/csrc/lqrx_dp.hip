@@ -198,7 +198,7 @@ template <typename T, int NT, int MT> struct DpCfg {
 // DEPTH knots ahead, 64 lanes × KPL coalesced elements per knot, staged through LDS.
 // Dot products are split over the wave: u_i by SU = 64/MP lanes (i = lane % MP), x'_i by
 // SX = 64/NP lanes (i = lane % NP), partial sums combined with xor-shuffles.
-template <typename T, int NT, int MT, int DEPTH, bool TV = false>
+template <typename T, int NT, int MT, int DEPTH, bool TV = false, bool LIN = false>
 __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, int lane)
 {
     using C = DpCfg<T, NT, MT>;
@@ -251,7 +251,8 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
     if (lane < MP) us[lane] = (T)0;
     if (lane < n) Xg[lane] = x0[lane];
 
-    T ring[DEPTH][KPL];
+    T ring[DEPTH][KPL], dring[LIN ? DEPTH : 1];   // K_k (+ the feedforward d_k, lane < m)
+    const T *Dg = LIN ? (const T *)a.d + (size_t)b * (size_t)(N - 1) * m : nullptr;
     auto issue = [&](int kk, T(&dst)[KPL]) {
 #pragma unroll
         for (int s = 0; s < KPL; ++s) {
@@ -259,8 +260,14 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
             dst[s] = (kk <= N - 1 && e < mn) ? Kg[(size_t)(kk - 1) * mn + e] : (T)0;
         }
     };
+    auto issue_d = [&](int kk, T &dst) {
+        if constexpr (LIN) dst = (kk <= N - 1 && lane < m) ? Dg[(size_t)(kk - 1) * m + lane] : (T)0;
+    };
 #pragma unroll
-    for (int d = 0; d < DEPTH; ++d) issue(1 + d, ring[d]);
+    for (int d = 0; d < DEPTH; ++d) {
+        issue(1 + d, ring[d]);
+        issue_d(1 + d, dring[LIN ? d : 0]);
+    }
     __syncthreads();
 
     for (int k0 = 1; k0 <= N - 1; k0 += DEPTH) {
@@ -274,6 +281,11 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
                     if (e < mn) Ks[e] = ring[d][s];
                 }
                 issue(k + DEPTH, ring[d]);
+                T dcur = (T)0;
+                if constexpr (LIN) {
+                    dcur = dring[d];
+                    issue_d(k + DEPTH, dring[d]);
+                }
                 if constexpr (TV) {
                     if (k + AD <= N - 1) load_rows(k + AD, arow_n[AD - 1], brow_n[AD - 1]);   // AD knots ahead
                 }
@@ -290,8 +302,9 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
 #pragma unroll
                 for (int o = MP; o < 64; o <<= 1) su += __shfl_xor(su, o);
                 if (lane < m) {
-                    us[lane] = -su;
-                    Ug[(size_t)(k - 1) * m + lane] = -su;
+                    const T u = LIN ? -(su + dcur) : -su;   // u = −K x (− d)
+                    us[lane] = u;
+                    Ug[(size_t)(k - 1) * m + lane] = u;
                 }
                 __syncthreads();
                 // x_{k+1} = A x_k + B u_k   (:69)
@@ -343,7 +356,42 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
 //                knot k-1's A, B, R are loaded into the same registers right after knot k's
 //                last product that reads them (the load hides behind the rest of the knot);
 //                Q_k is loaded from global straight into the P_ accumulators.
-enum : int { VAR_NOSOLVE = 2, VAR_NOROLL = 4, VAR_NOKSTORE = 8, VAR_SWEEPONLY = 16, VAR_TV = 32 };
+//   VAR_LIN    : linear cost terms (lqrx_dp_solve_linear), always with VAR_TV (time-invariant
+//                fields have knot stride 0): d = XᵀG's companion d = Xᵀ(r + Bᵀp) and
+//                p ← q + Aᵀp − Gᵀd (Gᵀ = APB for symmetric P) on the VALU — the vectors
+//                are exchanged through a small LDS image (lin_* helpers below).
+enum : int { VAR_NOSOLVE = 2, VAR_NOROLL = 4, VAR_NOKSTORE = 8, VAR_SWEEPONLY = 16, VAR_TV = 32,
+             VAR_LIN = 64 };
+
+// Vector products with register tiles (VAR_LIN).  A vector v is read from its LDS image in
+// "row layout" (lane l, slot [i][r] = v[16i + Tile::row(l, r)], the rows a C-layout tile's
+// lane holds); Mᵀv is then a per-lane FMA chain over those rows, summed over the four row
+// groups (lanes l, l^16, l^32, l^48), and lands in "column layout": lane l holds
+// (Mᵀv)[16j + (l & 15)] for output tile j.
+template <typename T, int RT>
+__device__ __forceinline__ void lin_rows(T (&v)[RT][4], const T *img, int lane)
+{
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[i][r] = img[16 * i + Tile<T>::row(lane, r)];
+}
+template <typename T, int RT, int CT>
+__device__ __forceinline__ void lin_tn(T (&y)[CT], const typename Tile<T>::acc (&M)[RT][CT], const T (&v)[RT][4])
+{
+#pragma unroll
+    for (int j = 0; j < CT; ++j)
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) y[j] = fma(M[i][j][r], v[i][r], y[j]);
+}
+template <typename T>
+__device__ __forceinline__ T lin_rowsum(T x)
+{
+    x += __shfl_xor(x, 16);
+    return x + __shfl_xor(x, 32);
+}
 
 template <typename T, int NT, int MT, int WAVES, int VAR, bool FULL>
 __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
@@ -351,8 +399,11 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
     using C = DpCfg<T, NT, MT>;
     using acc = typename Tile<T>::acc;
     constexpr int MP = C::MP, CS = C::CS;
-    constexpr bool TV = (VAR & VAR_TV) != 0;
+    constexpr bool TV = (VAR & VAR_TV) != 0, LIN = (VAR & VAR_LIN) != 0;
+    static_assert(!LIN || TV, "linear terms use the time-varying variant");
+    constexpr int NP = C::NP;
     __shared__ T lds[C::LDS_ELEMS];
+    __shared__ T vimg[LIN ? NP + MP : 1];   // p (NP), then w / d (MP)
     // Q (time-invariant, read every knot as the P_ accumulator start) lives in LDS for the
     // horizon: an LDS read per element instead of an L2 round trip per knot
     __shared__ T qimg[TV ? 1 : C::QIMG];
@@ -393,6 +444,21 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
     if (Pall) tiles_store<T, NT, NT>(P, Pall + (size_t)(N - 1) * nn, n, n, n, lane);
     T *Kb = (T *)a.K + (size_t)b * (size_t)(N - 1) * nm;
     int info = 0;
+    // linear terms: q_k, r_k (knot stride with Q, R), outputs d_k and p (p_1 or every p_k)
+    const size_t sq = (LIN && a.tv_QR) ? (size_t)n : 0, sr = (LIN && a.tv_QR) ? (size_t)m : 0;
+    const T *qg = LIN ? (const T *)a.q + (size_t)b * n * kQR : nullptr;
+    const T *rg = LIN ? (const T *)a.r + (size_t)b * m * kQR : nullptr;
+    T *dg = LIN ? (T *)a.d + (size_t)b * (size_t)(N - 1) * m : nullptr;
+    T *pallv = (LIN && a.p_all) ? (T *)a.p + (size_t)b * (size_t)N * n : nullptr;
+    if constexpr (LIN) {
+        const T *qf = (const T *)a.qf + (size_t)b * n;
+        for (int i = lane; i < NP; i += 64) {
+            const T v = i < n ? qf[i] : (T)0;        // p = qf
+            vimg[i] = v;
+            if (pallv && i < n) pallv[(size_t)(N - 1) * n + i] = v;
+        }
+        __syncthreads();
+    }
     acc Xi[MT][MT], Xp[MT][MT], Id[MT][MT];     // E⁻¹ of the last two knots, identity tiles
 #pragma unroll
     for (int i = 0; i < MT; ++i)
@@ -407,6 +473,19 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
 
     for (int k = N - 1; k >= 1; --k) { // :61
         acc PB[NT][MT], E[MT][MT], PA[NT][NT], G[MT][NT], Pn[NT][NT];
+        T qv[LIN ? NT : 1], rv[LIN ? MT : 1];      // column layout, issued ahead of the MFMAs
+        if constexpr (LIN) {
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const int i = 16 * j + tcol(lane);
+                qv[j] = i < n ? qg[(size_t)(k - 1) * sq + i] : (T)0;
+            }
+#pragma unroll
+            for (int j = 0; j < MT; ++j) {
+                const int i = 16 * j + tcol(lane);
+                rv[j] = i < m ? rg[(size_t)(k - 1) * sr + i] : (T)0;
+            }
+        }
         tiles_zero<T, NT, MT>(PB);
         mma_tn<T, NT, NT, MT>(PB, P, Bt);                          // :38 PB = P B
         tiles_zero<T, NT, NT>(PA);
@@ -426,6 +505,20 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
         tiles_zero<T, MT, NT>(G);
         mma_tn<T, NT, MT, NT>(G, Bt, PA);                          // :41 K = B'PA
         mma_tn_lower<T, NT, NT>(Pn, At, PA);                       // :51 Q + A'PA (lower)
+        // linear terms, first half (A_k, B_k still in the tiles): w = r + Bᵀp, Aᵀp partials
+        T w[LIN ? MT : 1], ap[LIN ? NT : 1];
+        if constexpr (LIN) {
+            T prow[NT][4];
+            lin_rows<T, NT>(prow, vimg, lane);
+#pragma unroll
+            for (int j = 0; j < MT; ++j) w[j] = (T)0;
+#pragma unroll
+            for (int j = 0; j < NT; ++j) ap[j] = (T)0;
+            lin_tn<T, NT, MT>(w, Bt, prow);
+            lin_tn<T, NT, NT>(ap, At, prow);
+#pragma unroll
+            for (int j = 0; j < MT; ++j) w[j] = rv[j] + lin_rowsum(w[j]);
+        }
         if constexpr (TV) {
             // knot k's A, B, R are consumed: bring in knot k-1's (lands during the solve)
             if (k > 1) {
@@ -492,6 +585,45 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
             mma_tn<T, MT, MT, NT>(Kt, Xi, G);                          // K = XᵀG = E⁻¹G
             if constexpr ((VAR & VAR_NOKSTORE) == 0)
                 tiles_store<T, MT, NT, FULL>(Kt, Kb + (size_t)(k - 1) * nm, m, n, m, lane);
+            if constexpr (LIN) {
+                // second half: d = Xᵀw (the companion of K = XᵀG) ;  p ← q + Aᵀp − Gᵀd
+                T dv[MT], gd[NT];
+#pragma unroll
+                for (int j = 0; j < MT; ++j) dv[j] = (T)0;
+#pragma unroll
+                for (int j = 0; j < NT; ++j) gd[j] = (T)0;
+#pragma unroll
+                for (int j = 0; j < MT; ++j)
+                    if (lane < 16) vimg[NP + 16 * j + lane] = w[j];
+                __syncthreads();
+                T wrow[MT][4];
+                lin_rows<T, MT>(wrow, vimg + NP, lane);
+                lin_tn<T, MT, MT>(dv, Xi, wrow);
+                __syncthreads();                       // w read by every lane before d lands
+#pragma unroll
+                for (int j = 0; j < MT; ++j) {
+                    dv[j] = lin_rowsum(dv[j]);
+                    const int i = 16 * j + lane;
+                    if (lane < 16) {
+                        vimg[NP + i] = dv[j];
+                        if (i < m) dg[(size_t)(k - 1) * m + i] = dv[j];
+                    }
+                }
+                __syncthreads();
+                T drow[MT][4];
+                lin_rows<T, MT>(drow, vimg + NP, lane);
+                lin_tn<T, MT, NT>(gd, G, drow);
+#pragma unroll
+                for (int j = 0; j < NT; ++j) {
+                    const T pn = qv[j] + lin_rowsum(ap[j]) - lin_rowsum(gd[j]);
+                    const int i = 16 * j + lane;
+                    if (lane < 16) {
+                        vimg[i] = pn;
+                        if (pallv && i < n) pallv[(size_t)(k - 1) * n + i] = pn;
+                    }
+                }
+                __syncthreads();
+            }
         }
         mma_tn_lower<T, MT, NT, true>(Pn, G, Kt);                  // :50-51 − GᵀK (= APB K)
         tiles_symmetrize_lower<T, NT>(Pn, lds, lane);              // P_ exactly symmetric
@@ -503,13 +635,16 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
     }
     if (!a.p_all) tiles_store<T, NT, NT>(P, (T *)a.P + (size_t)b * nn, n, n, n, lane);
     if (a.info && lane == 0) a.info[b] = info;
+    if constexpr (LIN) {
+        if (!a.p_all && lane < n) ((T *)a.p)[(size_t)b * n + lane] = vimg[lane];   // p_1
+    }
 
     if constexpr ((VAR & VAR_NOROLL) == 0) {
         // make this wave's K stores visible to its own (other-lane) rollout loads
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        dp_rollout<T, NT, MT, TV ? LQRX_DP_TVKD : LQRX_DP_KD, TV>(a, b, lds, lane);
+        dp_rollout<T, NT, MT, TV ? LQRX_DP_TVKD : LQRX_DP_KD, TV, LIN>(a, b, lds, lane);
     }
 }
 
@@ -524,6 +659,11 @@ static hipError_t launch_dp_tv(const DpArgs &a, hipStream_t s)
     // 2 waves/SIMD where the time-varying kernel fits 256 registers without spills (tile
     // grids up to 2×1, i.e. n ≤ 32, m ≤ 16 — cfg4's shape), else 1
     constexpr int TVW = LQRX_DP_TVWAVES ? LQRX_DP_TVWAVES : ((NT <= 2 && MT <= 1) ? 2 : 1);
+    // linear cost terms: the extra vectors tip cfg4's 2×1 double grid over 256 VGPRs (72–91
+    // spilled at 2 waves/SIMD), so LIN runs 2 waves/SIMD only on the 1×1 (double) and up
+    // to 2×1 (float) grids
+    constexpr int LW = (NT * MT <= (sizeof(T) == 4 ? 2 : 1)) ? 2 : 1;
+    if (a.lin) return launch_dp<T, NT, MT, LW, VAR_TV | VAR_LIN>(a, s);
     if (a.tv_AB || a.tv_QR) return launch_dp<T, NT, MT, TVW, VAR_TV | LQRX_DP_TVEXTRA>(a, s);
     return launch_dp<T, NT, MT, WAVES, VAR>(a, s);
 }

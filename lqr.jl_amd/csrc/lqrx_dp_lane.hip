@@ -47,9 +47,15 @@ __device__ __forceinline__ void lane_load(T (&D)[RP][CP], const T *__restrict__ 
 
 } // namespace
 
-template <typename T, int NP, int MP, bool TV, bool SOA>
+// LIN (linear cost terms, lqrx_dp_solve_linear; instantiated with TV only — a
+// time-invariant field simply has knot stride 0): p = qf, then per knot
+//   d = E⁻¹(r + Bᵀp)  (the same potrf factor, one more potrs column),
+//   p ← q + Aᵀp − APB·d  (APB = AᵀPB = Gᵀ for symmetric P),
+// and the rollout applies u = −(K x + d).  Reference op order: oracle_dp_solve_one_lin.
+template <typename T, int NP, int MP, bool TV, bool SOA, bool LIN = false>
 __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
 {
+    static_assert(!LIN || TV, "linear terms use the time-varying kernel");
     const int64_t b = (int64_t)blockIdx.x * 64 + threadIdx.x;
     if (b >= a.batch) return;   // no barriers / cross-lane ops below
     const int n = a.n, m = a.m, N = a.N;
@@ -90,11 +96,35 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
     };
     if (Pall) store_P(Pall + (int64_t)(N - 1) * nn * es);
     int info = 0;
+    // linear terms: p (cost-to-go gradient), knot vectors q_k, r_k (stride with Q, R)
+    constexpr int LN = LIN ? NP : 1, LM = LIN ? MP : 1;
+    const int64_t sq = a.tv_QR ? n : 0, sr = a.tv_QR ? m : 0;
+    const T *qb = LIN ? (const T *)a.q + tb(n * kQR) : nullptr;
+    const T *rb = LIN ? (const T *)a.r + tb(m * kQR) : nullptr;
+    T *db = LIN ? (T *)a.d + tb((int64_t)(N - 1) * m) : nullptr;
+    T *pall = (LIN && a.p_all) ? (T *)a.p + tb((int64_t)N * n) : nullptr;
+    T pv[LN], qv[LN], rv[LM], qn[LN], rn[LM];
+    if constexpr (LIN) {
+        const T *qf = (const T *)a.qf + tb(n);
+#pragma unroll
+        for (int i = 0; i < NP; ++i) pv[i] = i < n ? qf[i * es] : (T)0;
+        if (pall) {
+#pragma unroll
+            for (int i = 0; i < NP; ++i)
+                if (i < n) pall[((int64_t)(N - 1) * n + i) * es] = pv[i];
+        }
+    }
     // time-varying: knot k's matrices are prefetched during knot k+1
     constexpr int TN = TV ? NP : 1, TM = TV ? MP : 1;
     T An[TN][TN], Bn[TN][TM], Qn[TN][TN], Rn[TM][TM];
     auto fetch_tv = [&](int k) {
         if (k < 1) return;
+        if constexpr (LIN) {
+#pragma unroll
+            for (int i = 0; i < NP; ++i) qn[i] = i < n ? qb[((int64_t)(k - 1) * sq + i) * es] : (T)0;
+#pragma unroll
+            for (int i = 0; i < MP; ++i) rn[i] = i < m ? rb[((int64_t)(k - 1) * sr + i) * es] : (T)0;
+        }
         if constexpr (tvAB) {
             lane_load<T, NP, NP>(An, Ab + (int64_t)(k - 1) * sA * es, n, n, (T)0, es);
             lane_load<T, NP, MP>(Bn, Bb + (int64_t)(k - 1) * sB * es, n, m, (T)0, es);
@@ -125,6 +155,12 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
             for (int i = 0; i < MP; ++i)
 #pragma unroll
                 for (int j = 0; j < MP; ++j) R[i][j] = Rn[i][j];
+        }
+        if constexpr (LIN) {
+#pragma unroll
+            for (int i = 0; i < NP; ++i) qv[i] = qn[i];
+#pragma unroll
+            for (int i = 0; i < MP; ++i) rv[i] = rn[i];
         }
         if constexpr (TV) fetch_tv(k - 1);
         // P is symmetric: only P[i][j], i ≥ j, is maintained
@@ -211,6 +247,46 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
 #pragma unroll
             for (int i = 0; i < MP; ++i)
                 if (i < m && j < n) Kk[(i + j * m) * es] = K[i][j];
+        if constexpr (LIN) {
+            // d = E⁻¹(r + Bᵀp): the potrs of :30 on one more column
+            T y[MP], dv[MP];
+#pragma unroll
+            for (int i = 0; i < MP; ++i) {
+                T s = (T)0;
+#pragma unroll
+                for (int l = 0; l < NP; ++l) s = fma(B[l][i], pv[l], s);
+                s = rv[i] + s;
+#pragma unroll
+                for (int c = 0; c < i; ++c) s = fma(-L[i][c], y[c], s);
+                y[i] = s * Linv[i];
+            }
+#pragma unroll
+            for (int i = MP - 1; i >= 0; --i) {
+                T s = y[i];
+#pragma unroll
+                for (int c = i + 1; c < MP; ++c) s = fma(-L[c][i], dv[c], s);
+                dv[i] = s * Linv[i];
+            }
+#pragma unroll
+            for (int i = 0; i < MP; ++i)
+                if (i < m) db[((int64_t)(k - 1) * m + i) * es] = dv[i];
+            // p ← q + Aᵀp − APB·d  (APB[i][c] = G[c][i])
+            T pn[NP];
+#pragma unroll
+            for (int i = 0; i < NP; ++i) {
+                T s = (T)0, t = (T)0;
+#pragma unroll
+                for (int l = 0; l < NP; ++l) s = fma(A[l][i], pv[l], s);
+#pragma unroll
+                for (int c = 0; c < MP; ++c) t = fma(G[c][i], dv[c], t);
+                pn[i] = qv[i] + s - t;
+            }
+#pragma unroll
+            for (int i = 0; i < NP; ++i) {
+                pv[i] = pn[i];
+                if (pall && i < n) pall[((int64_t)(k - 1) * n + i) * es] = pv[i];
+            }
+        }
         // :51 P_ = Q + AᵀPA − GᵀK   (lower triangle)
 #pragma unroll
         for (int i = 0; i < NP; ++i)
@@ -227,6 +303,14 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
     }
     if (!a.p_all) store_P((T *)a.P + tb(nn));
     if (a.info) a.info[b] = info;
+    if constexpr (LIN) {
+        if (!a.p_all) {
+            T *p1 = (T *)a.p + tb(n);
+#pragma unroll
+            for (int i = 0; i < NP; ++i)
+                if (i < n) p1[i * es] = pv[i];
+        }
+    }
 
     // forward rollout  :66-70  u_k = −K_k x_k ; x_{k+1} = A_k x_k + B_k u_k
     T *Xb = (T *)a.X + tb((int64_t)N * n), *Ub = (T *)a.U + tb((int64_t)(N - 1) * m);
@@ -242,7 +326,7 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
     // register ring (unrolled by RD so every ring index is static).
     constexpr int RD = TV ? 4 : ((MP * NP <= 8) ? 8 : 4);
     struct Knot {
-        T K[MP][NP], A[TV ? NP : 1][TV ? NP : 1], B[TV ? NP : 1][TV ? MP : 1];
+        T K[MP][NP], A[TV ? NP : 1][TV ? NP : 1], B[TV ? NP : 1][TV ? MP : 1], d[LM];
     };
     Knot ring[RD];
     auto fetch = [&](int k, Knot &d) {
@@ -252,6 +336,10 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
         for (int j = 0; j < NP; ++j)
 #pragma unroll
             for (int i = 0; i < MP; ++i) d.K[i][j] = (i < m && j < n) ? Kk[(i + j * m) * es] : (T)0;
+        if constexpr (LIN) {
+#pragma unroll
+            for (int i = 0; i < MP; ++i) d.d[i] = i < m ? db[((int64_t)(k - 1) * m + i) * es] : (T)0;
+        }
         if constexpr (tvAB) {
             lane_load<T, NP, NP>(d.A, Ab + (int64_t)(k - 1) * sA * es, n, n, (T)0, es);
             lane_load<T, NP, MP>(d.B, Bb + (int64_t)(k - 1) * sB * es, n, m, (T)0, es);
@@ -264,11 +352,13 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
         for (int d = 0; d < RD; ++d) {
             const int k = k0 + d;
             if (k > N - 1) break;
-            T Kc[MP][NP];
+            T Kc[MP][NP], dc[LM];
 #pragma unroll
             for (int j = 0; j < NP; ++j)
 #pragma unroll
                 for (int i = 0; i < MP; ++i) Kc[i][j] = ring[d].K[i][j];
+#pragma unroll
+            for (int i = 0; i < LM; ++i) dc[i] = ring[d].d[i];
             if constexpr (tvAB) {
 #pragma unroll
                 for (int i = 0; i < NP; ++i) {
@@ -285,7 +375,8 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
                 T s = (T)0;
 #pragma unroll
                 for (int j = 0; j < NP; ++j) s = fma(Kc[i][j], x[j], s);
-                u[i] = -s;
+                if constexpr (LIN) u[i] = -(s + dc[i]);   // u = −(K x + d)
+                else u[i] = -s;
                 if (i < m) Ub[((int64_t)(k - 1) * m + i) * es] = u[i];
             }
             T xn[NP];
@@ -550,7 +641,9 @@ static hipError_t launch_lane(const DpArgs &a, hipStream_t s)
 {
     dim3 grid((unsigned)((a.batch + 63) / 64)), block(64);
     const bool tv = a.tv_AB || a.tv_QR, soa = a.layout == 1;
-    if (tv && soa) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, true, true>), grid, block, 0, s, a);
+    if (a.lin && soa) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, true, true, true>), grid, block, 0, s, a);
+    else if (a.lin) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, true, false, true>), grid, block, 0, s, a);
+    else if (tv && soa) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, true, true>), grid, block, 0, s, a);
     else if (tv) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, true, false>), grid, block, 0, s, a);
     else if (soa) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, false, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, false, false>), grid, block, 0, s, a);
@@ -563,7 +656,7 @@ bool dp_lane_supported(int n, int m) { return n >= 1 && m >= 1 && n <= 4 && m <=
 // lane kernel would leave most CUs idle.  LQRX_DP_SMALL=lane|quad overrides (tests).
 static bool use_quad(const DpArgs &a)
 {
-    if (a.tv_AB || a.tv_QR || a.n < 3 || a.n > 4) return false;
+    if (a.tv_AB || a.tv_QR || a.lin || a.n < 3 || a.n > 4) return false;
     const char *e = std::getenv("LQRX_DP_SMALL");
     if (e && e[0] == 'l') return false;
     if (e && e[0] == 'q') return true;

@@ -18,6 +18,12 @@ struct DpArgs {
     int layout;       // 0 = per-trajectory blocks, batch slowest; 1 = batch fastest (SoA):
                       // element e of trajectory b at [e·batch + b] (e = the layout-0 offset
                       // within the trajectory) — native in the n ≤ 4 kernels
+    // linear cost terms (lqrx_dp_solve_linear; lin = 0: the plain reference problem):
+    // q, r per knot with tv_QR (knot stride n / m), qf; outputs d (m per knot), p (n, or
+    // n per knot with p_all)
+    int lin;
+    const void *q, *r, *qf;
+    void *d, *p;
 };
 
 hipError_t dp_launch(const DpArgs &a, hipStream_t s);

@@ -27,6 +27,13 @@ class DpDesc(C.Structure):
     ]
 
 
+class DpLinear(C.Structure):
+    """Mirror of ``lqrx_dp_linear`` (linear cost terms q, r, qf in; d, p out)."""
+
+    _fields_ = [("q", C.c_void_p), ("r", C.c_void_p), ("qf", C.c_void_p),
+                ("d", C.c_void_p), ("p", C.c_void_p)]
+
+
 class KktDesc(C.Structure):
     """Mirror of ``lqrx_kkt_desc``."""
 
@@ -75,6 +82,10 @@ _SIGS = {
     "lqrx_device_available": (C.c_int, []),
     "lqrx_dp_solve": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 10 + [_VP, _VP]),
     "lqrx_dp_solve_host": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 10 + [_VP]),
+    "lqrx_dp_solve_linear": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 6 + [C.POINTER(DpLinear)]
+                             + [_VP] * 4 + [_VP, _VP]),
+    "lqrx_dp_solve_linear_host": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 6
+                                  + [C.POINTER(DpLinear)] + [_VP] * 5),
     "lqrx_kkt_solve": (C.c_int, [C.POINTER(KktDesc)] + [_VP] * 7 + [_VP]),
     "lqrx_kkt_solve_host": (C.c_int, [C.POINTER(KktDesc)] + [_VP] * 7),
     "lqrx_kkt_sizes": (C.c_int, [C.POINTER(KktDesc)] + [C.POINTER(C.c_int64)] * 5),

@@ -6,6 +6,8 @@ Reference surface (Julia, /root/reference/src):
   DPSolver(prob)                                           dynamic_programming.jl:13-23
   LQRSolution (exported, undefined upstream: fields K, X, U as used by :62-69)
   solve!(sol, solver, prob)                                dynamic_programming.jl:54-72
+Extension (no upstream counterpart): linear cost terms q, r, qf on
+LQRProblem / LQRBatch → feedforward d and linear cost-to-go p (lqrx_dp_solve_linear).
 
 Array conventions here: a single problem uses plain (rows, cols) numpy matrices; batches
 use numpy arrays shaped (batch, rows, cols).  The C ABI wants Julia column-major with the
@@ -64,6 +66,11 @@ class LQRProblem:
     u0: np.ndarray | None = None
     tf: float = 1.0
     N: int = 2
+    # linear cost terms (extension): stage ½xᵀQx + qᵀx + ½uᵀRu + rᵀu, terminal + qfᵀx;
+    # q, r time-invariant or with a leading knot axis N-1 (then Q, R must carry one too)
+    q: np.ndarray | None = None
+    r: np.ndarray | None = None
+    qf: np.ndarray | None = None
 
     def size(self):
         n, m = self.B.shape[-2:]
@@ -87,12 +94,17 @@ class LQRSolution:
     U: np.ndarray
     P: np.ndarray
     info: int = 0
+    d: np.ndarray | None = None   # feedforward (linear terms): u_k = −K_k x_k − d_k
+    p: np.ndarray | None = None   # linear cost-to-go p_1 (or every p_k with all_P)
 
     @classmethod
     def of(cls, prob: LQRProblem, all_P: bool = False):
         n, m, N = prob.size()
+        lin = prob.q is not None
         return cls(np.zeros((N - 1, m, n)), np.zeros((N, n)), np.zeros((N - 1, m)),
-                   np.zeros((N, n, n)) if all_P else np.zeros((n, n)))
+                   np.zeros((N, n, n)) if all_P else np.zeros((n, n)),
+                   d=np.zeros((N - 1, m)) if lin else None,
+                   p=(np.zeros((N, n)) if all_P else np.zeros(n)) if lin else None)
 
 
 @dataclass
@@ -124,6 +136,9 @@ class LQRBatch:
     x0: np.ndarray
     N: int
     extra: dict = field(default_factory=dict)
+    q: np.ndarray | None = None    # (batch, n) or (batch, N-1, n) — linear terms (extension)
+    r: np.ndarray | None = None    # (batch, m) or (batch, N-1, m)
+    qf: np.ndarray | None = None   # (batch, n)
 
     @property
     def batch(self):
@@ -140,7 +155,10 @@ class LQRBatch:
     @classmethod
     def of(cls, probs: list[LQRProblem]):
         st = lambda f: np.stack([np.asarray(getattr(p, f), dtype=np.float64) for p in probs])
-        return cls(st("A"), st("B"), st("Q"), st("R"), st("Qf"), st("x0"), probs[0].N)
+        lin = probs[0].q is not None
+        return cls(st("A"), st("B"), st("Q"), st("R"), st("Qf"), st("x0"), probs[0].N,
+                   q=st("q") if lin else None, r=st("r") if lin else None,
+                   qf=st("qf") if lin else None)
 
 
 def _ptr(a: np.ndarray):
@@ -169,13 +187,37 @@ def solve_batch(b: LQRBatch, dtype: int = _lib.F64, all_P: bool = False, layout:
     U = np.zeros(bt * (N - 1) * m, npdt)
     info = np.zeros(bt, np.int32)
     d = _lib.DpDesc(n, m, N, dtype, bt, layout, 1 if all_P else 0, tvAB, tvQR)
-    rc = _lib.check(lib.lqrx_dp_solve_host(C.byref(d), *[_ptr(a) for a in ins], _ptr(x0),
-                                           _ptr(K), _ptr(P), _ptr(X), _ptr(U), _ptr(info)))
+    lin = b.q is not None
+    if lin:   # linear cost terms: lqrx_dp_solve_linear_host
+        if b.r is None or b.qf is None:
+            raise ValueError("linear cost terms need q, r and qf together")
+        kq = N - 1 if tvQR else 1
+        vec = lambda a, w: np.ascontiguousarray(np.asarray(a, dtype=npdt).reshape(bt * kq * w))
+        q, r = vec(b.q, n), vec(b.r, m)
+        qf = np.ascontiguousarray(np.asarray(b.qf, dtype=npdt).reshape(bt * n))
+        if layout == 1:
+            q, r, qf = to_soa(q, bt), to_soa(r, bt), to_soa(qf, bt)
+        dff = np.zeros(bt * (N - 1) * m, npdt)
+        pv = np.zeros(bt * n * (N if all_P else 1), npdt)
+        ln = _lib.DpLinear(_ptr(q).value, _ptr(r).value, _ptr(qf).value, _ptr(dff).value,
+                           _ptr(pv).value)
+        rc = _lib.check(lib.lqrx_dp_solve_linear_host(
+            C.byref(d), *[_ptr(a) for a in ins], _ptr(x0), C.byref(ln), _ptr(K), _ptr(P),
+            _ptr(X), _ptr(U), _ptr(info)))
+    else:
+        rc = _lib.check(lib.lqrx_dp_solve_host(C.byref(d), *[_ptr(a) for a in ins], _ptr(x0),
+                                               _ptr(K), _ptr(P), _ptr(X), _ptr(U), _ptr(info)))
     if layout == 1:
         K, P, X, U = (from_soa(a, bt) for a in (K, P, X, U))
-    return dict(K=from_abi(K, (bt, N - 1, m, n)),
-                P=from_abi(P, (bt, N, n, n) if all_P else (bt, n, n)),
-                X=X.reshape(bt, N, n), U=U.reshape(bt, N - 1, m), info=info, rc=rc)
+        if lin:
+            dff, pv = from_soa(dff, bt), from_soa(pv, bt)
+    out = dict(K=from_abi(K, (bt, N - 1, m, n)),
+               P=from_abi(P, (bt, N, n, n) if all_P else (bt, n, n)),
+               X=X.reshape(bt, N, n), U=U.reshape(bt, N - 1, m), info=info, rc=rc)
+    if lin:
+        out["d"] = dff.reshape(bt, N - 1, m)
+        out["p"] = pv.reshape(bt, N, n) if all_P else pv.reshape(bt, n)
+    return out
 
 
 def solve(sol: LQRSolution, solver: DPSolver, prob: LQRProblem) -> LQRSolution:
@@ -187,6 +229,9 @@ def solve(sol: LQRSolution, solver: DPSolver, prob: LQRProblem) -> LQRSolution:
     sol.U[...] = out["U"][0]
     sol.P[...] = out["P"][0]
     sol.info = int(out["info"][0])
+    if prob.q is not None:
+        sol.d = out["d"][0]
+        sol.p = out["p"][0]
     return sol
 
 
@@ -216,8 +261,9 @@ def dp_solve_device(t: dict, N: int, p_mode: int = 0, stream: int | None = None,
     """Device-pointer entry point on torch tensors already in ABI layout (flat; layout 1 =
     batch fastest, every input and output).
 
-    t: dict with torch tensors A, B, Q, R, Qf, x0 on the GPU and ints n, m, batch.
-    Returns dict of output tensors (K, P, X, U, info).  `stream` is a raw hipStream_t
+    t: dict with torch tensors A, B, Q, R, Qf, x0 on the GPU and ints n, m, batch; with
+    tensors q, r, qf as well it runs lqrx_dp_solve_linear and also returns d and p.
+    Returns dict of output tensors (K, P, X, U, info[, d, p]).  `stream` is a raw hipStream_t
     (torch.cuda.current_stream().cuda_stream); None = the null stream, synchronous.
     """
     import torch
@@ -235,9 +281,20 @@ def dp_solve_device(t: dict, N: int, p_mode: int = 0, stream: int | None = None,
                    info=torch.empty(bt, dtype=torch.int32, device=dev))
     d = _lib.DpDesc(n, m, N, dtype, bt, layout, p_mode, int(t.get("tv_AB", 0)), int(t.get("tv_QR", 0)))
     p = lambda x: C.c_void_p(x.data_ptr())
-    rc = lib.lqrx_dp_solve(C.byref(d), p(t["A"]), p(t["B"]), p(t["Q"]), p(t["R"]), p(t["Qf"]),
-                           p(t["x0"]), p(out["K"]), p(out["P"]), p(out["X"]), p(out["U"]),
-                           p(out["info"]), C.c_void_p(stream) if stream else None)
+    st = C.c_void_p(stream) if stream else None
+    if t.get("q") is not None:
+        if "d" not in out:
+            out["d"] = torch.empty(bt * (N - 1) * m, dtype=tdt, device=dev)
+            out["p"] = torch.empty(bt * n * (N if p_mode else 1), dtype=tdt, device=dev)
+        ln = _lib.DpLinear(t["q"].data_ptr(), t["r"].data_ptr(), t["qf"].data_ptr(),
+                           out["d"].data_ptr(), out["p"].data_ptr())
+        rc = lib.lqrx_dp_solve_linear(C.byref(d), p(t["A"]), p(t["B"]), p(t["Q"]), p(t["R"]),
+                                      p(t["Qf"]), p(t["x0"]), C.byref(ln), p(out["K"]),
+                                      p(out["P"]), p(out["X"]), p(out["U"]), p(out["info"]), st)
+    else:
+        rc = lib.lqrx_dp_solve(C.byref(d), p(t["A"]), p(t["B"]), p(t["Q"]), p(t["R"]), p(t["Qf"]),
+                               p(t["x0"]), p(out["K"]), p(out["P"]), p(out["X"]), p(out["U"]),
+                               p(out["info"]), st)
     _lib.check(rc)
     out["rc"] = rc
     return out

@@ -117,20 +117,40 @@ static void potrs_upper(int n, int nrhs, const double *U, int ldu, double *X, in
  * Returns info: 0, or the (1-based) knot k whose E = R + BᵀPB was not SPD (first met in
  * the backward sweep).  The sweep continues either way, as the reference does.
  */
-int oracle_dp_solve_one_tv(int n, int m, int N, const double *A0, const double *B0,
-                           const double *Q0, const double *R0, const double *Qf,
-                           const double *x0, double *K, double *P, int p_all, double *X,
-                           double *U, int tvAB, int tvQR)
+/*
+ * Linear cost terms (SURVEY §8(f) rank 1 "cost linear terms"; an extension — the reference
+ * LQRProblem has none): stage cost ½xᵀQx + qᵀx + ½uᵀRu + rᵀu, terminal ½xᵀQf x + qfᵀx.
+ * The value function gains a linear part, V_k(x) = ½xᵀP_k x + p_kᵀx, and the policy a
+ * feedforward, u_k = −K_k x_k − d_k.  Restated in the reference's own op order: d is one
+ * more right-hand side of the same chol_solve! (:42, potrs on [B'PA | r + B'p]), and p
+ * follows compute_ctg!'s P_ .= Q + A'PA − APB*K (:51) as p_ .= q + A'p − APB*d.
+ *   q  n (per knot with tvQR: n×(N-1), knot k at slot k-1), r m (idem), qf n
+ *   d  m×(N-1)   d[k] for k = 1..N-1 at slot k-1
+ *   p  n (p_all == 0: p_1) or n×N (p_all: p_k for k = 1..N, p_N = qf)
+ * q == NULL runs the plain reference recursion (r, qf, d, p unused).
+ */
+int oracle_dp_solve_one_lin(int n, int m, int N, const double *A0, const double *B0,
+                            const double *Q0, const double *R0, const double *Qf,
+                            const double *x0, double *K, double *P, int p_all, double *X,
+                            double *U, int tvAB, int tvQR, const double *q0,
+                            const double *r0, const double *qf, double *d, double *p)
 {
     size_t nn = (size_t)n * n, nm = (size_t)n * m, mm = (size_t)m * m;
     double *Pc = malloc(nn * sizeof(double)), *P_ = malloc(nn * sizeof(double));
     double *PA = malloc(nn * sizeof(double)), *PB = malloc(nm * sizeof(double));
     double *APB = malloc(nm * sizeof(double)), *E = malloc(mm * sizeof(double));
     double *T1 = malloc(nn * sizeof(double)), *T2 = malloc(nn * sizeof(double));
+    const int lin = q0 != NULL;
+    double *pc = malloc((size_t)n * sizeof(double)), *p_ = malloc((size_t)n * sizeof(double));
+    double *t1 = malloc((size_t)n * sizeof(double)), *t2 = malloc((size_t)n * sizeof(double));
     int info = 0;
 
     memcpy(Pc, Qf, nn * sizeof(double));                       /* :58  P .= Qf */
     if (p_all) memcpy(P + (size_t)(N - 1) * nn, Qf, nn * sizeof(double));
+    if (lin) {                                                 /* p .= qf */
+        memcpy(pc, qf, (size_t)n * sizeof(double));
+        if (p_all) memcpy(p + (size_t)(N - 1) * n, qf, (size_t)n * sizeof(double));
+    }
 
     for (int k = N - 1; k >= 1; --k) {                        /* :61  k = N-1:-1:1 */
         double *Kk = K + (size_t)(k - 1) * nm;
@@ -149,6 +169,13 @@ int oracle_dp_solve_one_tv(int n, int m, int N, const double *A0, const double *
         int st = oracle_potrf_upper(m, E, m);                  /* :29  potrf!('U',E) */
         if (st && !info) info = k;
         potrs_upper(m, n, E, m, Kk, m);                        /* :30  potrs!('U',E,K) */
+        double *dk = lin ? d + (size_t)(k - 1) * m : NULL;
+        if (lin) {                                             /* d = E⁻¹(r + B'p) */
+            const double *r = r0 + (tvQR ? (size_t)(k - 1) * m : 0);
+            gemm(m, 1, n, 1, B, n, 0, pc, n, dk, m);
+            for (int i = 0; i < m; ++i) dk[i] = r[i] + dk[i];
+            potrs_upper(m, 1, E, m, dk, m);
+        }
         /* compute_ctg!  :50-51 */
         gemm(n, m, n, 1, A, n, 0, PB, n, APB, n);              /* :50  APB .= A'PB */
         gemm(n, n, n, 1, A, n, 0, PA, n, T1, n);               /*      A'PA         */
@@ -156,8 +183,17 @@ int oracle_dp_solve_one_tv(int n, int m, int N, const double *A0, const double *
         for (size_t i = 0; i < nn; ++i) P_[i] = Q[i] + T1[i] - T2[i]; /* :51 */
         memcpy(Pc, P_, nn * sizeof(double));                   /* :63  P .= P_ */
         if (p_all) memcpy(P + (size_t)(k - 1) * nn, Pc, nn * sizeof(double));
+        if (lin) {                                             /* p_ .= q + A'p − APB*d */
+            const double *q = q0 + (tvQR ? (size_t)(k - 1) * n : 0);
+            gemm(n, 1, n, 1, A, n, 0, pc, n, t1, n);
+            gemm(n, 1, m, 0, APB, n, 0, dk, m, t2, n);
+            for (int i = 0; i < n; ++i) p_[i] = q[i] + t1[i] - t2[i];
+            memcpy(pc, p_, (size_t)n * sizeof(double));
+            if (p_all) memcpy(p + (size_t)(k - 1) * n, pc, (size_t)n * sizeof(double));
+        }
     }
     if (!p_all) memcpy(P, Pc, nn * sizeof(double));
+    if (lin && !p_all) memcpy(p, pc, (size_t)n * sizeof(double));
 
     memcpy(X, x0, (size_t)n * sizeof(double));                 /* :66 */
     for (int k = 1; k <= N - 1; ++k) {                         /* :67-70 */
@@ -169,7 +205,7 @@ int oracle_dp_solve_one_tv(int n, int m, int N, const double *A0, const double *
         for (int i = 0; i < m; ++i) {
             double s = 0.0;
             for (int j = 0; j < n; ++j) s += Kk[IDX(i, j, m)] * xk[j];
-            uk[i] = -s;
+            uk[i] = lin ? -(s + d[(size_t)(k - 1) * m + i]) : -s;   /* u = −Kx (− d) */
         }
         for (int i = 0; i < n; ++i) {
             double s = 0.0, t = 0.0;
@@ -179,7 +215,17 @@ int oracle_dp_solve_one_tv(int n, int m, int N, const double *A0, const double *
         }
     }
     free(Pc); free(P_); free(PA); free(PB); free(APB); free(E); free(T1); free(T2);
+    free(pc); free(p_); free(t1); free(t2);
     return info;
+}
+
+int oracle_dp_solve_one_tv(int n, int m, int N, const double *A0, const double *B0,
+                           const double *Q0, const double *R0, const double *Qf,
+                           const double *x0, double *K, double *P, int p_all, double *X,
+                           double *U, int tvAB, int tvQR)
+{
+    return oracle_dp_solve_one_lin(n, m, N, A0, B0, Q0, R0, Qf, x0, K, P, p_all, X, U, tvAB,
+                                   tvQR, NULL, NULL, NULL, NULL, NULL);
 }
 
 int oracle_dp_solve_one(int n, int m, int N, const double *A, const double *B,
@@ -215,6 +261,37 @@ int64_t oracle_dp_solve_batch_tv(int n, int m, int N, int64_t batch, const doubl
                                         K + b * nm * (size_t)(N - 1), P + b * pstride, p_all,
                                         X + b * (size_t)n * N, U + b * (size_t)m * (N - 1),
                                         tvAB, tvQR);
+        if (info) info[b] = st;
+        bad += (st != 0);
+    }
+    (void)nthreads;
+    return bad;
+}
+
+/* batched driver of oracle_dp_solve_one_lin (q, r follow tvQR's knot layout) */
+int64_t oracle_dp_solve_batch_lin(int n, int m, int N, int64_t batch, const double *A,
+                                  const double *B, const double *Q, const double *R,
+                                  const double *Qf, const double *x0, double *K, double *P,
+                                  int p_all, double *X, double *U, int32_t *info, int nthreads,
+                                  int tvAB, int tvQR, const double *q, const double *r,
+                                  const double *qf, double *d, double *p)
+{
+    size_t nn = (size_t)n * n, nm = (size_t)n * m, mm = (size_t)m * m;
+    size_t kAB = tvAB ? (size_t)(N - 1) : 1, kQR = tvQR ? (size_t)(N - 1) : 1;
+    size_t pstride = p_all ? nn * (size_t)N : nn, vstride = p_all ? (size_t)n * N : (size_t)n;
+    int64_t bad = 0;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 4) num_threads(nthreads) reduction(+ : bad)
+#endif
+    for (int64_t b = 0; b < batch; ++b) {
+        int st = oracle_dp_solve_one_lin(n, m, N, A + b * nn * kAB, B + b * nm * kAB,
+                                         Q + b * nn * kQR, R + b * mm * kQR,
+                                         Qf + b * nn, x0 + b * (size_t)n,
+                                         K + b * nm * (size_t)(N - 1), P + b * pstride, p_all,
+                                         X + b * (size_t)n * N, U + b * (size_t)m * (N - 1),
+                                         tvAB, tvQR, q + b * (size_t)n * kQR,
+                                         r + b * (size_t)m * kQR, qf + b * (size_t)n,
+                                         d + b * (size_t)m * (N - 1), p + b * vstride);
         if (info) info[b] = st;
         bad += (st != 0);
     }

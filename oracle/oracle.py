@@ -43,6 +43,9 @@ def load():
         lib.oracle_dp_solve_batch_tv.restype = i64
         lib.oracle_dp_solve_batch_tv.argtypes = [i32, i32, i32, i64] + [vp] * 8 + [
             i32, vp, vp, vp, i32, i32, i32]
+        lib.oracle_dp_solve_batch_lin.restype = i64
+        lib.oracle_dp_solve_batch_lin.argtypes = [i32, i32, i32, i64] + [vp] * 8 + [
+            i32, vp, vp, vp, i32, i32, i32] + [vp] * 5
         lib.oracle_kkt_solve_one.restype = i32
         lib.oracle_kkt_solve_one.argtypes = [i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, i32, vp,
                                              vp, vp, vp, vp]
@@ -79,6 +82,28 @@ def dp_solve_abi(d: dict, N: int, all_P: bool = False, nthreads: int = 1) -> dic
                                  _p(K), _p(P), 1 if all_P else 0, _p(X), _p(U), _p(info),
                                  nthreads, int(d.get("tv_AB", 0)), int(d.get("tv_QR", 0)))
     return dict(K=K, P=P, X=X, U=U, info=info)
+
+
+def dp_solve_lin_abi(d: dict, N: int, all_P: bool = False, nthreads: int = 1) -> dict:
+    """Oracle DP with linear cost terms (oracle_dp_solve_one_lin): d additionally holds the
+    flat ABI arrays q (n per knot, N−1 knots when tv_QR), r (m, idem) and qf (n).  Returns
+    K, P, X, U, info plus the feedforward d (m per knot) and the linear cost-to-go p."""
+    lib = load()
+    n, m, bt = d["n"], d["m"], d["batch"]
+    f = lambda k: np.ascontiguousarray(np.asarray(d[k], dtype=np.float64))
+    A, B, Q, R, Qf, x0, q, r, qf = (f(k) for k in ("A", "B", "Q", "R", "Qf", "x0", "q", "r", "qf"))
+    K = np.zeros(bt * (N - 1) * m * n)
+    P = np.zeros(bt * n * n * (N if all_P else 1))
+    X = np.zeros(bt * N * n)
+    U = np.zeros(bt * (N - 1) * m)
+    dd = np.zeros(bt * (N - 1) * m)
+    p = np.zeros(bt * n * (N if all_P else 1))
+    info = np.zeros(bt, np.int32)
+    lib.oracle_dp_solve_batch_lin(n, m, N, bt, _p(A), _p(B), _p(Q), _p(R), _p(Qf), _p(x0),
+                                  _p(K), _p(P), 1 if all_P else 0, _p(X), _p(U), _p(info),
+                                  nthreads, int(d.get("tv_AB", 0)), int(d.get("tv_QR", 0)),
+                                  _p(q), _p(r), _p(qf), _p(dd), _p(p))
+    return dict(K=K, P=P, X=X, U=U, info=info, d=dd, p=p)
 
 
 def dp_extended(A, B, Q, R, Qf, N):
@@ -119,18 +144,28 @@ def dp_extended(A, B, Q, R, Qf, N):
     return Ks, Ps
 
 
-def dp_dense_kkt(A, B, Q, R, Qf, x0, N):
+def dp_dense_kkt(A, B, Q, R, Qf, x0, N, q=None, r=None, qf=None, with_lam=False):
     """Dense equality-constrained QP optimum of one LQR problem (logical row-major
-    matrices).  Returns (X (N,n), U (N-1,m))."""
-    n, m = B.shape
+    matrices).  Returns (X (N,n), U (N-1,m)).  Optional linear cost terms q (n or (N-1,n)),
+    r (m or (N-1,m)), qf (n) add gᵀz to the objective; with_lam=True also returns the
+    multipliers λ (N, n): λ[0] of the initial condition x₁ = x0 (the optimal cost's gradient
+    in x0 is −λ[0] = P₁x₁ + p₁) and λ[k] of x_{k+1} = A x_k + B u_k − x_{k+1}, the costate
+    λ[k] = P_{k+1}x_{k+1} + p_{k+1} (0-based knot k)."""
+    n, m = B.shape[-2:]
     nz = N * n + (N - 1) * m
     H = np.zeros((nz, nz))
+    g = np.zeros(nz)
     ix = lambda k: slice(k * (n + m), k * (n + m) + n)
     iu = lambda k: slice(k * (n + m) + n, k * (n + m) + n + m)
     for k in range(N - 1):
         H[ix(k), ix(k)] = Q
         H[iu(k), iu(k)] = R
+        if q is not None:
+            g[ix(k)] = q if np.ndim(q) == 1 else q[k]
+            g[iu(k)] = r if np.ndim(r) == 1 else r[k]
     H[ix(N - 1), ix(N - 1)] = Qf
+    if qf is not None:
+        g[ix(N - 1)] = qf
     D = np.zeros((N * n, nz))
     d = np.zeros(N * n)
     D[0:n, ix(0)] = np.eye(n)
@@ -141,10 +176,12 @@ def dp_dense_kkt(A, B, Q, R, Qf, x0, N):
         D[r, iu(k)] = B
         D[r, ix(k + 1)] = -np.eye(n)
     Kkt = np.block([[H, D.T], [D, np.zeros((N * n, N * n))]])
-    sol = np.linalg.solve(Kkt, np.concatenate([np.zeros(nz), -d]))
+    sol = np.linalg.solve(Kkt, np.concatenate([-g, -d]))
     z = sol[:nz]
     X = np.stack([z[ix(k)] for k in range(N)])
     U = np.stack([z[iu(k)] for k in range(N - 1)])
+    if with_lam:
+        return X, U, sol[nz:].reshape(N, n)
     return X, U
 
 

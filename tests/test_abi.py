@@ -18,7 +18,7 @@ def test_exports_every_header_symbol(lqrx):
 
 
 def test_abi_version(lqrx):
-    assert lqrx.load().lqrx_abi_version() == 2
+    assert lqrx.load().lqrx_abi_version() == 3
 
 
 @pytest.mark.parametrize("field,val,code", [("n", 0, -1), ("m", 0, -1), ("N", 1, -1),
@@ -57,6 +57,28 @@ def test_dp_null_pointer_codes(lqrx):
     assert rc == -2          # A is argument 2
     rc = lqrx.load().lqrx_dp_solve(C.byref(d), p, p, p, p, p, p, p, None, p, p, None, None)
     assert rc == -9          # P is argument 9
+
+
+def test_dp_linear_null_pointer_codes(lqrx):
+    """lqrx_dp_solve_linear: lin (argument 8) and each of its pointers are checked, the
+    outputs K, P, X, U are arguments 9..12."""
+    from lqrx import _lib
+
+    d = _lib.DpDesc(8, 4, 10, 0, 4, 0, 0, 0, 0)
+    buf = np.zeros(16)
+    p = buf.ctypes.data_as(C.c_void_p)
+    lib = lqrx.load()
+    assert lib.lqrx_dp_solve_linear(C.byref(d), p, p, p, p, p, p, None, p, p, p, p, None, None) == -8
+    for k in ("q", "r", "qf", "d", "p"):
+        ln = _lib.DpLinear(p.value, p.value, p.value, p.value, p.value)
+        setattr(ln, k, None)
+        rc = lib.lqrx_dp_solve_linear(C.byref(d), p, p, p, p, p, p, C.byref(ln), p, p, p, p, None, None)
+        assert rc == -8 and k in lib.lqrx_last_error().decode()
+    ln = _lib.DpLinear(p.value, p.value, p.value, p.value, p.value)
+    rc = lib.lqrx_dp_solve_linear(C.byref(d), p, p, p, p, p, p, C.byref(ln), p, None, p, p, None, None)
+    assert rc == -10         # P is argument 10 of the linear entry point
+    d.n = 0
+    assert lib.lqrx_dp_solve_linear(C.byref(d), p, p, p, p, p, p, C.byref(ln), p, p, p, p, None, None) == -1
 
 
 def test_kkt_validation(lqrx):

@@ -163,6 +163,95 @@ def test_dp_oracle_equals_dense_kkt(lqrx):
         assert np.abs(X[t] - Xd).max() <= 1e-10 * max(1.0, np.abs(Xd).max())
 
 
+def _lin_batch(lqrx, n, m, N, bt, seed, tv):
+    """Random batch with linear cost terms, flat ABI arrays (q, r per knot when tv)."""
+    d = lqrx.random_batch(n, m, N, bt, seed=seed)
+    rng = np.random.default_rng(seed + 1)
+    kq = N - 1 if tv else 1
+    d["q"] = rng.standard_normal(bt * kq * n)
+    d["r"] = rng.standard_normal(bt * kq * m)
+    d["qf"] = rng.standard_normal(bt * n)
+    if tv:   # per-knot Q, R (the q, r knot layout follows Q, R: ABI knot_stride_QR)
+        from lqrx.dp import from_abi, to_abi
+        Q = from_abi(d["Q"], (bt, n, n))
+        R = from_abi(d["R"], (bt, m, m))
+        s = 1.0 + 0.5 * rng.random((bt, N - 1, 1, 1))
+        d["Q"] = to_abi((Q[:, None] * s).reshape(bt * (N - 1), n, n)).ravel()
+        d["R"] = to_abi((R[:, None] * s).reshape(bt * (N - 1), m, m)).ravel()
+        d["tv_QR"] = 1
+    return d
+
+
+@pytest.mark.parametrize("tv", [False, True])
+def test_dp_oracle_linear_equals_dense_kkt(lqrx, tv):
+    """Linear cost terms: the rollout with u = −Kx − d equals the
+    optimum of the QP with gᵀz added, and the value function's gradient P_k x_k + p_k equals
+    the QP's costate at every knot (pins K, d, P_k and p_k together)."""
+    from lqrx.dp import abi_to_batch, from_abi
+
+    n, m, N, bt = 5, 2, 21, 4
+    d = _lin_batch(lqrx, n, m, N, bt, 41, tv)
+    out = orc.dp_solve_lin_abi(d, N, all_P=True)
+    assert (out["info"] == 0).all()
+    X = out["X"].reshape(bt, N, n)
+    U = out["U"].reshape(bt, N - 1, m)
+    P = from_abi(out["P"], (bt, N, n, n))
+    p = out["p"].reshape(bt, N, n)
+    A = from_abi(d["A"], (bt, n, n)); B = from_abi(d["B"], (bt, n, m))
+    kq = N - 1 if tv else 1
+    Q = from_abi(d["Q"], (bt, kq, n, n)); R = from_abi(d["R"], (bt, kq, m, m))
+    Qf = from_abi(d["Qf"], (bt, n, n)); x0 = d["x0"].reshape(bt, n)
+    q = d["q"].reshape(bt, kq, n); r = d["r"].reshape(bt, kq, m); qf = d["qf"].reshape(bt, n)
+    for t in range(bt):
+        if tv:   # dense QP with per-knot Q_k, R_k
+            Xd, Ud, lam = _dense_tv(A[t], B[t], Q[t], R[t], Qf[t], x0[t], N, q[t], r[t], qf[t])
+        else:
+            Xd, Ud, lam = orc.dp_dense_kkt(A[t], B[t], Q[t, 0], R[t, 0], Qf[t], x0[t], N,
+                                           q[t, 0], r[t, 0], qf[t], with_lam=True)
+        sc = max(1.0, np.abs(Xd).max(), np.abs(Ud).max())
+        assert np.abs(U[t] - Ud).max() <= 1e-10 * sc
+        assert np.abs(X[t] - Xd).max() <= 1e-10 * sc
+        grad = np.einsum("kij,kj->ki", P[t], X[t]) + p[t]
+        costate = np.concatenate([-lam[:1], lam[1:]])
+        assert np.abs(grad - costate).max() <= 1e-9 * max(1.0, np.abs(costate).max())
+
+
+def _dense_tv(A, B, Q, R, Qf, x0, N, q, r, qf):
+    """Dense QP of a problem with per-knot Q_k, R_k, q_k, r_k (A, B time-invariant)."""
+    n, m = B.shape
+    nz = N * n + (N - 1) * m
+    H = np.zeros((nz, nz)); g = np.zeros(nz)
+    ix = lambda k: slice(k * (n + m), k * (n + m) + n)
+    iu = lambda k: slice(k * (n + m) + n, k * (n + m) + n + m)
+    for k in range(N - 1):
+        H[ix(k), ix(k)] = Q[k]; H[iu(k), iu(k)] = R[k]
+        g[ix(k)] = q[k]; g[iu(k)] = r[k]
+    H[ix(N - 1), ix(N - 1)] = Qf; g[ix(N - 1)] = qf
+    D = np.zeros((N * n, nz)); dd = np.zeros(N * n)
+    D[0:n, ix(0)] = np.eye(n); dd[0:n] = -x0
+    for k in range(N - 1):
+        rr = slice((k + 1) * n, (k + 2) * n)
+        D[rr, ix(k)] = A; D[rr, iu(k)] = B; D[rr, ix(k + 1)] = -np.eye(n)
+    sol = np.linalg.solve(np.block([[H, D.T], [D, np.zeros((N * n, N * n))]]),
+                          np.concatenate([-g, -dd]))
+    z = sol[:nz]
+    return (np.stack([z[ix(k)] for k in range(N)]), np.stack([z[iu(k)] for k in range(N - 1)]),
+            sol[nz:].reshape(N, n))
+
+
+def test_dp_oracle_linear_zero_is_plain(lqrx):
+    """q = r = qf = 0 reproduces the reference recursion bit for bit (d = 0, p = 0)."""
+    n, m, N, bt = 6, 3, 17, 3
+    d = _lin_batch(lqrx, n, m, N, bt, 43, False)
+    for k in ("q", "r", "qf"):
+        d[k] = np.zeros_like(d[k])
+    a = orc.dp_solve_lin_abi(d, N, all_P=True)
+    b = orc.dp_solve_abi(d, N, all_P=True)
+    for k in ("K", "P", "X", "U"):
+        assert np.array_equal(a[k], b[k]), k
+    assert not a["d"].any() and not a["p"].any()
+
+
 def test_dp_oracle_dare_limit(lqrx):
     """Long horizon: K_1 → (R + BᵀP∞B)⁻¹BᵀP∞A and P_1 → P∞ (scipy solve_discrete_are) on
     well-actuated problems (stable A, full-rank B) whose Riccati recursion
