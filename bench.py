@@ -129,7 +129,9 @@ def check_dp_sample(out, sub, idx, n, m, N, bt, tol, threads):
     ti = torch.from_numpy(idx).to(out["K"].device)
     pick = lambda x, w: x.view(bt, w).index_select(0, ti).cpu().numpy().astype(np.float64)
     s = len(idx)
-    ref = orc.dp_solve_abi(dict(sub, n=n, m=m, N=N, batch=s), N, nthreads=threads)
+    lin = "q" in sub
+    ref = (orc.dp_solve_lin_abi if lin else orc.dp_solve_abi)(dict(sub, n=n, m=m, N=N, batch=s), N,
+                                                             nthreads=threads)
 
     def knot_err(a, b):
         a, b = a.reshape(s, a.shape[1], -1), b.reshape(s, b.shape[1], -1)
@@ -146,6 +148,9 @@ def check_dp_sample(out, sub, idx, n, m, N, bt, tol, threads):
              P=knot_err(pick(out["P"], n * n)[:, None], ref["P"].reshape(s, 1, n * n)),
              X=traj_err(pick(out["X"], N * n), ref["X"]),
              U=traj_err(pick(out["U"], (N - 1) * m), ref["U"]))
+    if lin:   # feedforward d and p_1 on their trajectory's scale (they cross zero)
+        e["d"] = traj_err(pick(out["d"], (N - 1) * m), ref["d"])
+        e["p"] = traj_err(pick(out["p"], n), ref["p"])
     return {"trajectories": s, "last_index": int(idx[-1]), "max_rel_err": e, "tol": tol,
             "pass": bool(max(e.values()) <= tol),
             "oracle": "oracle/lqr_oracle.c (restatement of dynamic_programming.jl:54-72)"}
@@ -193,6 +198,8 @@ def main():
     ap.add_argument("--tv", action="store_true",
                     help="dp: time-varying problem (per-knot A_k, B_k, Q_k, R_k; knot_stride 1, "
                          "SURVEY §8(f) rank 1); default batch 16384 (65536 would need 376 GB)")
+    ap.add_argument("--linear", action="store_true",
+                    help="dp: linear cost terms q, r, qf (lqrx_dp_solve_linear, SURVEY §8(f) rank 1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-gather", action="store_true",
                     help="skip the final info + P_1 gather to rank 0 (N > 1)")
@@ -278,13 +285,23 @@ def main():
         t.update(n=n, m=m, batch=bt)
         chk_idx = _sample_index(bt)
         widths = dict(A=n * n, B=n * m, Q=n * n, R=m * m, Qf=n * n, x0=n)
+        if args.linear:   # linear cost terms, same counter-based style: seeded per rank
+            import numpy as np
+            rng = np.random.default_rng(args.seed + 17 * rank)
+            npdt = "float64" if f64 else "float32"
+            host.update(q=rng.standard_normal(bt * n).astype(npdt), r=rng.standard_normal(bt * m).astype(npdt),
+                        qf=rng.standard_normal(bt * n).astype(npdt))
+            widths.update(q=n, r=m, qf=n)
         chk_sub = {k: host[k].reshape(bt, w)[chk_idx].astype("float64").ravel()
                    for k, w in widths.items()}
+        if args.linear:
+            for k in ("q", "r", "qf"):
+                t[k] = torch.from_numpy(host[k]).to(dev)
         del host
         if args.tv:
             # per-knot fields: every knot's block is its own copy in HBM (the kernel streams
             # all N−1 of them), values = the time-invariant draw
-            for k in ("A", "B", "Q", "R"):
+            for k in ("A", "B", "Q", "R") + (("q", "r") if args.linear else ()):
                 v = t[k].view(bt, 1, -1)
                 t[k] = v.expand(bt, N - 1, v.shape[-1]).contiguous().view(-1)
             t.update(tv_AB=1, tv_QR=1)
@@ -339,7 +356,7 @@ def main():
     # output checks, outside the timed region: the whole batch scanned on the device for
     # non-finite values; a strided sample compared with the CPU oracle (rank 0)
     nonfinite = nonfinite_count(out if args.workload != "sqp" else t,
-                                ("K", "P", "X", "U", "dz", "lam", "Z"))
+                                ("K", "P", "X", "U", "d", "p", "dz", "lam", "Z"))
     nonfinite, bad = SH.sum_over_ranks([nonfinite, bad], world, dev)
     sampled = None
     if rank == 0 and args.workload in ("dp", "cartpole", "kkt"):
@@ -483,9 +500,11 @@ def main():
                     traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
                 except Exception:
                     traffic = None
+            if args.linear:
+                traffic = None   # (no PMC pass recorded for the linear-term variant)
             roof = {"bound": "mfma", "achieved": achieved, "peak": peak,
                     "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
-                    "kernel": _dp_kernel_name(n, m, bt, args.tv),
+                    "kernel": _dp_kernel_name(n, m, bt, args.tv or args.linear),
                     "kernel_ms": kern_ms,
                     "flops_per_traj": dp_flops_per_traj(n, m, N),
                     "alg_bytes_per_launch": dp_bytes_per_traj(n, m, N, 8 if f64 else 4, args.tv) * bt}
@@ -521,7 +540,8 @@ def main():
                                           "knot_chain_us": kern_ms * 1e3 / N,
                                           "note": "one serial N-knot chain per wave; the chip holds "
                                                   "the whole batch at <= 1 wave per CU"}}
-            headline = (n, m, N, bt, args.dtype) == (32, 16, 256, 65536, "f64") and not args.tv
+            headline = (n, m, N, bt, args.dtype) == (32, 16, 256, 65536, "f64") and not args.tv \
+                and not args.linear
             if args.workload == "cartpole":
                 metric = f"LQR trajectories/sec (Riccati bwd+fwd), cartpole n=4 m=1 N={N} B={bt}"
                 workload = "cartpole LQR, RK3-linearised (BASELINE.json configs[1])"
@@ -531,7 +551,8 @@ def main():
                             "rollout (BASELINE.json configs[3])")
             else:
                 metric = (f"LQR trajectories/sec (Riccati bwd+fwd), n={n} m={m} N={N} B={bt} {args.dtype}"
-                          + (", time-varying A_k B_k Q_k R_k" if args.tv else ""))
+                          + (", time-varying A_k B_k Q_k R_k" if args.tv else "")
+                          + (", linear cost terms q r qf" if args.linear else ""))
                 cfg5 = (n, m, N, args.dtype) == (64, 32, 512, "f32")
                 workload = (("random dense time-varying LQR (SURVEY §8(f) rank 1)" if args.tv else
                              "random dense time-invariant LQR") + ", Riccati backward pass + forward rollout"

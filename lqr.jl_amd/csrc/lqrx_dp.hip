@@ -356,10 +356,10 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
 //                knot k-1's A, B, R are loaded into the same registers right after knot k's
 //                last product that reads them (the load hides behind the rest of the knot);
 //                Q_k is loaded from global straight into the P_ accumulators.
-//   VAR_LIN    : linear cost terms (lqrx_dp_solve_linear), always with VAR_TV (time-invariant
-//                fields have knot stride 0): d = XᵀG's companion d = Xᵀ(r + Bᵀp) and
-//                p ← q + Aᵀp − Gᵀd (Gᵀ = APB for symmetric P) on the VALU — the vectors
-//                are exchanged through a small LDS image (lin_* helpers below).
+//   VAR_LIN    : linear cost terms (lqrx_dp_solve_linear), alone (time-invariant problem) or
+//                with VAR_TV: K = XᵀG's companion d = Xᵀ(r + Bᵀp) and p ← q + Aᵀp − Gᵀd
+//                (Gᵀ = APB for symmetric P) on the VALU — the vectors are exchanged through
+//                a small LDS image (lin_* helpers below).
 enum : int { VAR_NOSOLVE = 2, VAR_NOROLL = 4, VAR_NOKSTORE = 8, VAR_SWEEPONLY = 16, VAR_TV = 32,
              VAR_LIN = 64 };
 
@@ -400,10 +400,10 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
     using acc = typename Tile<T>::acc;
     constexpr int MP = C::MP, CS = C::CS;
     constexpr bool TV = (VAR & VAR_TV) != 0, LIN = (VAR & VAR_LIN) != 0;
-    static_assert(!LIN || TV, "linear terms use the time-varying variant");
     constexpr int NP = C::NP;
     __shared__ T lds[C::LDS_ELEMS];
-    __shared__ T vimg[LIN ? NP + MP : 1];   // p (NP), then w / d (MP)
+    // p (NP), then w / d (MP); time-invariant q (NP), r (MP) images after them
+    __shared__ T vimg[LIN ? (TV ? NP + MP : 2 * (NP + MP)) : 1];
     // Q (time-invariant, read every knot as the P_ accumulator start) lives in LDS for the
     // horizon: an LDS read per element instead of an L2 round trip per knot
     __shared__ T qimg[TV ? 1 : C::QIMG];
@@ -456,6 +456,10 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
             const T v = i < n ? qf[i] : (T)0;        // p = qf
             vimg[i] = v;
             if (pallv && i < n) pallv[(size_t)(N - 1) * n + i] = v;
+            if constexpr (!TV) vimg[NP + MP + i] = i < n ? qg[i] : (T)0;
+        }
+        if constexpr (!TV) {
+            for (int i = lane; i < MP; i += 64) vimg[2 * NP + MP + i] = i < m ? rg[i] : (T)0;
         }
         __syncthreads();
     }
@@ -473,8 +477,18 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
 
     for (int k = N - 1; k >= 1; --k) { // :61
         acc PB[NT][MT], E[MT][MT], PA[NT][NT], G[MT][NT], Pn[NT][NT];
-        T qv[LIN ? NT : 1], rv[LIN ? MT : 1];      // column layout, issued ahead of the MFMAs
-        if constexpr (LIN) {
+        // column layout; time-varying: issued ahead of the MFMAs, time-invariant: read from
+        // the LDS images where they are used (no registers held across the knot)
+        T qv[LIN ? NT : 1], rv[LIN ? MT : 1];
+        auto lin_qr_lds = [&]() {
+            if constexpr (LIN && !TV) {
+#pragma unroll
+                for (int j = 0; j < NT; ++j) qv[j] = vimg[NP + MP + 16 * j + tcol(lane)];
+#pragma unroll
+                for (int j = 0; j < MT; ++j) rv[j] = vimg[2 * NP + MP + 16 * j + tcol(lane)];
+            }
+        };
+        if constexpr (LIN && TV) {
 #pragma unroll
             for (int j = 0; j < NT; ++j) {
                 const int i = 16 * j + tcol(lane);
@@ -505,20 +519,24 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
         tiles_zero<T, MT, NT>(G);
         mma_tn<T, NT, MT, NT>(G, Bt, PA);                          // :41 K = B'PA
         mma_tn_lower<T, NT, NT>(Pn, At, PA);                       // :51 Q + A'PA (lower)
-        // linear terms, first half (A_k, B_k still in the tiles): w = r + Bᵀp, Aᵀp partials
+        // linear terms, first half (time-varying: before A_k, B_k leave the tiles; time-
+        // invariant: after the solve, where fewer registers are live): w = r + Bᵀp, Aᵀp partials
         T w[LIN ? MT : 1], ap[LIN ? NT : 1];
-        if constexpr (LIN) {
-            T prow[NT][4];
-            lin_rows<T, NT>(prow, vimg, lane);
+        auto lin_first = [&]() {
+            if constexpr (LIN) {
+                T prow[NT][4];
+                lin_rows<T, NT>(prow, vimg, lane);
 #pragma unroll
-            for (int j = 0; j < MT; ++j) w[j] = (T)0;
+                for (int j = 0; j < MT; ++j) w[j] = (T)0;
 #pragma unroll
-            for (int j = 0; j < NT; ++j) ap[j] = (T)0;
-            lin_tn<T, NT, MT>(w, Bt, prow);
-            lin_tn<T, NT, NT>(ap, At, prow);
+                for (int j = 0; j < NT; ++j) ap[j] = (T)0;
+                lin_tn<T, NT, MT>(w, Bt, prow);
+                lin_tn<T, NT, NT>(ap, At, prow);
 #pragma unroll
-            for (int j = 0; j < MT; ++j) w[j] = rv[j] + lin_rowsum(w[j]);
-        }
+                for (int j = 0; j < MT; ++j) w[j] = rv[j] + lin_rowsum(w[j]);
+            }
+        };
+        if constexpr (LIN && TV) lin_first();
         if constexpr (TV) {
             // knot k's A, B, R are consumed: bring in knot k-1's (lands during the solve)
             if (k > 1) {
@@ -586,6 +604,10 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
             if constexpr ((VAR & VAR_NOKSTORE) == 0)
                 tiles_store<T, MT, NT, FULL>(Kt, Kb + (size_t)(k - 1) * nm, m, n, m, lane);
             if constexpr (LIN) {
+                if constexpr (!TV) {
+                    lin_qr_lds();
+                    lin_first();
+                }
                 // second half: d = Xᵀw (the companion of K = XᵀG) ;  p ← q + Aᵀp − Gᵀd
                 T dv[MT], gd[NT];
 #pragma unroll
@@ -659,11 +681,13 @@ static hipError_t launch_dp_tv(const DpArgs &a, hipStream_t s)
     // 2 waves/SIMD where the time-varying kernel fits 256 registers without spills (tile
     // grids up to 2×1, i.e. n ≤ 32, m ≤ 16 — cfg4's shape), else 1
     constexpr int TVW = LQRX_DP_TVWAVES ? LQRX_DP_TVWAVES : ((NT <= 2 && MT <= 1) ? 2 : 1);
-    // linear cost terms: the extra vectors tip cfg4's 2×1 double grid over 256 VGPRs (72–91
-    // spilled at 2 waves/SIMD), so LIN runs 2 waves/SIMD only on the 1×1 (double) and up
-    // to 2×1 (float) grids
+    // linear cost terms.  Time-varying: the extra vectors tip cfg4's 2×1 double grid over 256
+    // VGPRs (72–91 spilled at 2 waves/SIMD), so VAR_TV|VAR_LIN runs 2 waves/SIMD only on the
+    // 1×1 (double) and up to 2×1 (float) grids; time-invariant LIN keeps the plain kernel's
+    // occupancy (its vector work sits after the solve, where fewer tiles are live)
     constexpr int LW = (NT * MT <= (sizeof(T) == 4 ? 2 : 1)) ? 2 : 1;
-    if (a.lin) return launch_dp<T, NT, MT, LW, VAR_TV | VAR_LIN>(a, s);
+    if (a.lin && (a.tv_AB || a.tv_QR)) return launch_dp<T, NT, MT, LW, VAR_TV | VAR_LIN>(a, s);
+    if (a.lin) return launch_dp<T, NT, MT, WAVES, VAR_LIN>(a, s);
     if (a.tv_AB || a.tv_QR) return launch_dp<T, NT, MT, TVW, VAR_TV | LQRX_DP_TVEXTRA>(a, s);
     return launch_dp<T, NT, MT, WAVES, VAR>(a, s);
 }

@@ -47,15 +47,14 @@ __device__ __forceinline__ void lane_load(T (&D)[RP][CP], const T *__restrict__ 
 
 } // namespace
 
-// LIN (linear cost terms, lqrx_dp_solve_linear; instantiated with TV only — a
-// time-invariant field simply has knot stride 0): p = qf, then per knot
+// LIN (linear cost terms, lqrx_dp_solve_linear; q, r follow Q, R: per knot with TV,
+// loaded once otherwise): p = qf, then per knot
 //   d = E⁻¹(r + Bᵀp)  (the same potrf factor, one more potrs column),
 //   p ← q + Aᵀp − APB·d  (APB = AᵀPB = Gᵀ for symmetric P),
 // and the rollout applies u = −(K x + d).  Reference op order: oracle_dp_solve_one_lin.
 template <typename T, int NP, int MP, bool TV, bool SOA, bool LIN = false>
 __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
 {
-    static_assert(!LIN || TV, "linear terms use the time-varying kernel");
     const int64_t b = (int64_t)blockIdx.x * 64 + threadIdx.x;
     if (b >= a.batch) return;   // no barriers / cross-lane ops below
     const int n = a.n, m = a.m, N = a.N;
@@ -113,6 +112,12 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
             for (int i = 0; i < NP; ++i)
                 if (i < n) pall[((int64_t)(N - 1) * n + i) * es] = pv[i];
         }
+        if constexpr (!TV) {   // time-invariant q, r: loaded once
+#pragma unroll
+            for (int i = 0; i < NP; ++i) qv[i] = i < n ? qb[i * es] : (T)0;
+#pragma unroll
+            for (int i = 0; i < MP; ++i) rv[i] = i < m ? rb[i * es] : (T)0;
+        }
     }
     // time-varying: knot k's matrices are prefetched during knot k+1
     constexpr int TN = TV ? NP : 1, TM = TV ? MP : 1;
@@ -156,7 +161,7 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
 #pragma unroll
                 for (int j = 0; j < MP; ++j) R[i][j] = Rn[i][j];
         }
-        if constexpr (LIN) {
+        if constexpr (LIN && TV) {
 #pragma unroll
             for (int i = 0; i < NP; ++i) qv[i] = qn[i];
 #pragma unroll
@@ -409,6 +414,9 @@ __global__ __launch_bounds__(64) void dp_lane_kernel(const DpArgs a)
 // then P_ is re-replicated by four DPP quad broadcasts of the lower-triangle columns (lane r
 // supplies column r).  Rollout: x replicated, lane q computes x_{k+1}[q] = A[q,:]x + B[q,:]u
 // and the quad broadcasts re-assemble x.  Same reference lines as dp_lane_kernel.
+// LIN (linear cost terms): w = r + Bᵀp and d = E⁻¹w replicated (the quad holds the potrf
+// factor anyway), lane q forms p_new[q] = q[q] + A[:,q]ᵀp − G[:,q]ᵀd and the four quad
+// broadcasts re-replicate p; the rollout adds d_k (lane c < m loads d_k[c], broadcast).
 template <int CTRL>
 __device__ __forceinline__ double qbcast(double v)
 {
@@ -426,7 +434,7 @@ __device__ __forceinline__ float qbcast(float v)
 template <int R, typename T>
 __device__ __forceinline__ T qfrom(T v) { return qbcast<R | (R << 2) | (R << 4) | (R << 6)>(v); }
 
-template <typename T, int MP, bool SOA>
+template <typename T, int MP, bool SOA, bool LIN = false>
 __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
 {
     constexpr int NP = 4;
@@ -473,6 +481,20 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
     };
     if (Pall) store_Pcol(Pall + (int64_t)(N - 1) * nn * es);
     int info = 0;
+    // linear terms (time-invariant q, r): p replicated, this lane's q[q], r replicated
+    constexpr int LN = LIN ? NP : 1, LM = LIN ? MP : 1;
+    T pv[LN], rv[LM], qq = (T)0;
+    T *db = LIN ? (T *)a.d + tb((int64_t)(N - 1) * m) : nullptr;
+    T *pall = (LIN && a.p_all) ? (T *)a.p + tb((int64_t)N * n) : nullptr;
+    if constexpr (LIN) {
+        const T *qg = (const T *)a.q + tb(n), *rg = (const T *)a.r + tb(m), *qf = (const T *)a.qf + tb(n);
+#pragma unroll
+        for (int i = 0; i < NP; ++i) pv[i] = i < n ? qf[i * es] : (T)0;
+#pragma unroll
+        for (int i = 0; i < MP; ++i) rv[i] = i < m ? rg[i * es] : (T)0;
+        qq = q < n ? qg[q * es] : (T)0;
+        if (pall && q < n) pall[((int64_t)(N - 1) * n + q) * es] = qf[q * es];
+    }
     for (int k = N - 1; k >= 1; --k) {   // :61
         T PB[NP][MP];
 #pragma unroll
@@ -547,6 +569,44 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
             for (int c = 0; c < MP; ++c)
                 if (c < m) Kk[c * es] = Kq[c];
         }
+        if constexpr (LIN) {
+            // d = E⁻¹(r + Bᵀp) (replicated), p_new[q] = q[q] + A[:,q]ᵀp − G[:,q]ᵀd
+            T yl[MP], dv[MP];
+#pragma unroll
+            for (int i = 0; i < MP; ++i) {
+                T s = (T)0;
+#pragma unroll
+                for (int l = 0; l < NP; ++l) s = fma(B[l][i], pv[l], s);
+                s = rv[i] + s;
+#pragma unroll
+                for (int c = 0; c < i; ++c) s = fma(-L[i][c], yl[c], s);
+                yl[i] = s * Linv[i];
+            }
+#pragma unroll
+            for (int i = MP - 1; i >= 0; --i) {
+                T s = yl[i];
+#pragma unroll
+                for (int c = i + 1; c < MP; ++c) s = fma(-L[c][i], dv[c], s);
+                dv[i] = s * Linv[i];
+            }
+            if (q < m) {   // lane q stores d_k[q]
+                T v = dv[0];
+#pragma unroll
+                for (int c = 1; c < MP; ++c) v = q == c ? dv[c] : v;
+                db[((int64_t)(k - 1) * m + q) * es] = v;
+            }
+            T s = (T)0, t = (T)0;
+#pragma unroll
+            for (int l = 0; l < NP; ++l) s = fma(Acol[l], pv[l], s);
+#pragma unroll
+            for (int c = 0; c < MP; ++c) t = fma(Gq[c], dv[c], t);
+            const T pn = qq + s - t;
+            if (pall && q < n) pall[((int64_t)(k - 1) * n + q) * es] = pn;
+            pv[0] = qfrom<0>(pn);
+            pv[1] = qfrom<1>(pn);
+            pv[2] = qfrom<2>(pn);
+            pv[3] = qfrom<3>(pn);
+        }
         // :51 P_[:,q] = Q[:,q] + AᵀPA[:,q] − Gᵀ Kq = Q[:,q] + Aᵀ(PA[:,q] − PB·Kq)
         // (G = PBᵀA, so GᵀKq = Aᵀ(PB Kq): no full G)
         T wv[NP], Pn[NP];
@@ -576,6 +636,14 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
     }
     if (!a.p_all) store_Pcol((T *)a.P + tb(nn));
     if (a.info && q == 0) a.info[b] = info;
+    if constexpr (LIN) {
+        if (!a.p_all && q < n) {
+            T v = pv[0];
+#pragma unroll
+            for (int i = 1; i < NP; ++i) v = q == i ? pv[i] : v;
+            ((T *)a.p)[tb(n) + q * es] = v;
+        }
+    }
 
     // forward rollout :66-70 — x replicated; lane q forms x_{k+1}[q]
     T *Xb = (T *)a.X + tb((int64_t)N * n), *Ub = (T *)a.U + tb((int64_t)(N - 1) * m);
@@ -585,7 +653,7 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
     for (int i = 0; i < NP; ++i) x[i] = i < n ? x0[i * es] : (T)0;
     if (q < n) Xb[q * es] = q == 0 ? x[0] : (q == 1 ? x[1] : (q == 2 ? x[2] : x[3]));
     constexpr int RD = 8;
-    T ring[RD][MP][NP];
+    T ring[RD][MP][NP], dring[LIN ? RD : 1];
     auto fetch = [&](int k, T (&d)[MP][NP]) {
         if (k > N - 1) return;
         const T *Kk = Kb + (int64_t)(k - 1) * nm * es;
@@ -594,31 +662,48 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
 #pragma unroll
             for (int i = 0; i < MP; ++i) d[i][j] = (i < m && j < n) ? Kk[(i + j * m) * es] : (T)0;
     };
+    auto fetch_d = [&](int k, T &d) {   // lane q < m: d_k[q]
+        if constexpr (LIN) {
+            if (k <= N - 1) d = q < m ? db[((int64_t)(k - 1) * m + q) * es] : (T)0;
+        }
+    };
     // K_k was written by this quad's own lanes above; make those stores visible to the
     // quad's loads (other lanes' stores: complete them and drop any stale L1 line, once)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #pragma unroll
-    for (int d = 0; d < RD; ++d) fetch(1 + d, ring[d]);
+    for (int d = 0; d < RD; ++d) {
+        fetch(1 + d, ring[d]);
+        fetch_d(1 + d, dring[LIN ? d : 0]);
+    }
     for (int k0 = 1; k0 <= N - 1; k0 += RD) {
 #pragma unroll
         for (int d = 0; d < RD; ++d) {
             const int k = k0 + d;
             if (k > N - 1) break;
-            T Kc[MP][NP];
+            T Kc[MP][NP], dq = (T)0;
 #pragma unroll
             for (int j = 0; j < NP; ++j)
 #pragma unroll
                 for (int i = 0; i < MP; ++i) Kc[i][j] = ring[d][i][j];
             fetch(k + RD, ring[d]);
+            if constexpr (LIN) {
+                dq = dring[d];
+                fetch_d(k + RD, dring[d]);
+            }
             T u[MP];
 #pragma unroll
             for (int i = 0; i < MP; ++i) {
                 T s = (T)0;
 #pragma unroll
                 for (int j = 0; j < NP; ++j) s = fma(Kc[i][j], x[j], s);
-                u[i] = -s;
+                if constexpr (LIN) {   // u = −(K x + d), d_k[i] from lane i
+                    const T di = i == 0 ? qfrom<0>(dq) : i == 1 ? qfrom<1>(dq) : i == 2 ? qfrom<2>(dq) : qfrom<3>(dq);
+                    u[i] = -(s + di);
+                } else {
+                    u[i] = -s;
+                }
                 if (q == 0 && i < m) Ub[((int64_t)(k - 1) * m + i) * es] = u[i];
             }
             T s = (T)0;
@@ -641,8 +726,10 @@ static hipError_t launch_lane(const DpArgs &a, hipStream_t s)
 {
     dim3 grid((unsigned)((a.batch + 63) / 64)), block(64);
     const bool tv = a.tv_AB || a.tv_QR, soa = a.layout == 1;
-    if (a.lin && soa) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, true, true, true>), grid, block, 0, s, a);
-    else if (a.lin) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, true, false, true>), grid, block, 0, s, a);
+    if (a.lin && tv && soa) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, true, true, true>), grid, block, 0, s, a);
+    else if (a.lin && tv) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, true, false, true>), grid, block, 0, s, a);
+    else if (a.lin && soa) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, false, true, true>), grid, block, 0, s, a);
+    else if (a.lin) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, false, false, true>), grid, block, 0, s, a);
     else if (tv && soa) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, true, true>), grid, block, 0, s, a);
     else if (tv) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, true, false>), grid, block, 0, s, a);
     else if (soa) hipLaunchKernelGGL((dp_lane_kernel<T, NP, MP, false, true>), grid, block, 0, s, a);
@@ -656,7 +743,7 @@ bool dp_lane_supported(int n, int m) { return n >= 1 && m >= 1 && n <= 4 && m <=
 // lane kernel would leave most CUs idle.  LQRX_DP_SMALL=lane|quad overrides (tests).
 static bool use_quad(const DpArgs &a)
 {
-    if (a.tv_AB || a.tv_QR || a.lin || a.n < 3 || a.n > 4) return false;
+    if (a.tv_AB || a.tv_QR || a.n < 3 || a.n > 4) return false;
     const char *e = std::getenv("LQRX_DP_SMALL");
     if (e && e[0] == 'l') return false;
     if (e && e[0] == 'q') return true;
@@ -667,7 +754,9 @@ template <typename T, int MP>
 static hipError_t launch_quad(const DpArgs &a, hipStream_t s)
 {
     dim3 grid((unsigned)((a.batch * 4 + 63) / 64)), block(64);
-    if (a.layout == 1) hipLaunchKernelGGL((dp_quad_kernel<T, MP, true>), grid, block, 0, s, a);
+    if (a.lin && a.layout == 1) hipLaunchKernelGGL((dp_quad_kernel<T, MP, true, true>), grid, block, 0, s, a);
+    else if (a.lin) hipLaunchKernelGGL((dp_quad_kernel<T, MP, false, true>), grid, block, 0, s, a);
+    else if (a.layout == 1) hipLaunchKernelGGL((dp_quad_kernel<T, MP, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((dp_quad_kernel<T, MP, false>), grid, block, 0, s, a);
     return hipGetLastError();
 }

@@ -172,3 +172,17 @@ def test_dp_linear_device_stream(lqrx, oracle, gpu_ok):
                info=out["info"].cpu().numpy())
     ref = oracle.dp_solve_lin_abi(d, N, all_P=True)
     check(got, ref, n, m, N, bt, True, TOL64)
+
+
+@pytest.mark.parametrize("small", ["lane", "quad"])
+@pytest.mark.parametrize("n,m,N,bt,tvq", [(4, 1, 101, 67, False), (3, 2, 60, 33, False),
+                                          (4, 4, 40, 20, False), (4, 2, 50, 19, True)])
+def test_dp_linear_small_kernels(lqrx, oracle, gpu_ok, monkeypatch, small, n, m, N, bt, tvq):
+    """Both n ≤ 4 kernels with linear terms (LQRX_DP_SMALL forces the choice; time-varying
+    problems always take the lane kernel)."""
+    monkeypatch.setenv("LQRX_DP_SMALL", small)
+    d = lin_problem(lqrx, n, m, N, bt, 900 + n * 5 + m, tv_QR=tvq)
+    for all_P in (True, False):
+        got = lqrx.solve_batch(to_batch(d, N), all_P=all_P)
+        ref = oracle.dp_solve_lin_abi(d, N, all_P=all_P)
+        check(got, ref, n, m, N, bt, all_P, TOL64)

@@ -30,6 +30,8 @@ bench tv --tv --no-cpu-baseline
 bench ls --workload ls --steps 10 --warmup 5 --cpu-seconds 4
 bench sqp --workload sqp --steps 3 --warmup 1 --cpu-seconds 4
 bench sqp_cp --workload sqp --sqp-model cartpole --steps 3 --warmup 1
+bench lin --linear --no-cpu-baseline
+bench lin_cp --workload cartpole --linear --steps 20 --warmup 20 --no-cpu-baseline
 [ -n "$SKIP_PROF" ] && exit 0
 prof() {  # name, args...
   local nm=$1; shift
