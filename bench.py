@@ -496,12 +496,11 @@ def main():
             if os.path.exists(args.traffic_json):
                 try:
                     tj = json.load(open(args.traffic_json))
-                    key = f"n{n}_m{m}_N{N}_B{bt}_{args.dtype}" + ("_tv" if args.tv else "")
+                    key = f"n{n}_m{m}_N{N}_B{bt}_{args.dtype}" + ("_tv" if args.tv else "") \
+                        + ("_lin" if args.linear else "")
                     traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
                 except Exception:
                     traffic = None
-            if args.linear:
-                traffic = None   # (no PMC pass recorded for the linear-term variant)
             roof = {"bound": "mfma", "achieved": achieved, "peak": peak,
                     "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
                     "kernel": _dp_kernel_name(n, m, bt, args.tv or args.linear),

@@ -45,6 +45,8 @@ prof kkt_soa --workload kkt --kkt-layout 1 --steps 20 --warmup 20
 prof cartpole --workload cartpole --steps 20 --warmup 20
 prof tv --tv --steps 3 --warmup 1
 prof ls --workload ls --steps 5 --warmup 2
+prof lin --linear --steps 3 --warmup 1
+prof lin_cp --workload cartpole --linear --steps 20 --warmup 20
 profkt() {  # kernel trace only (whole-step workloads of several kernels)
   local nm=$1; shift
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/${nm}_kt -o kt --output-format csv -- python bench.py "$@" --no-cpu-baseline > $OUT/${nm}_kt.log 2>&1 || { tail -20 $OUT/${nm}_kt.log; exit 7; }
