@@ -106,6 +106,34 @@ def dp_solve_lin_abi(d: dict, N: int, all_P: bool = False, nthreads: int = 1) ->
     return dict(K=K, P=P, X=X, U=U, info=info, d=dd, p=p)
 
 
+def dp_lapack(A, B, Q, R, Qf, x0, N):
+    """dynamic_programming.jl:28-72 for one problem through the same third-party arithmetic
+    the reference calls: LAPACK dpotrf/dpotrs 'U' from OpenBLAS (scipy.linalg.lapack — Julia's
+    LAPACK.potrf!/potrs! are OpenBLAS too) and OpenBLAS dgemm for the products (numpy @).
+    Logical row-major matrices in; returns K (N−1, m, n), P (N, n, n), X (N, n), U (N−1, m)."""
+    from scipy.linalg import lapack
+
+    n, m = B.shape
+    P = np.array(Qf, dtype=np.float64)                    # :58
+    Ks = np.zeros((N - 1, m, n)); Ps = np.zeros((N, n, n)); Ps[N - 1] = P
+    for k in range(N - 1, 0, -1):                        # :61
+        PB = P @ B                                       # :38
+        E = R + B.T @ PB                                 # :39
+        PA = P @ A                                       # :40
+        K = B.T @ PA                                     # :41
+        c, info = lapack.dpotrf(E, lower=0, clean=0)     # :29 potrf!('U', E)
+        K, info2 = lapack.dpotrs(c, K, lower=0)          # :30 potrs!('U', E, K)
+        APB = A.T @ PB                                   # :50
+        P = Q + A.T @ PA - APB @ K                       # :51
+        Ks[k - 1] = K
+        Ps[k - 1] = P
+    X = np.zeros((N, n)); U = np.zeros((N - 1, m)); X[0] = x0
+    for k in range(N - 1):                               # :66-70
+        U[k] = -Ks[k] @ X[k]
+        X[k + 1] = A @ X[k] + B @ U[k]
+    return Ks, Ps, X, U
+
+
 def dp_extended(A, B, Q, R, Qf, N):
     """The backward pass of dynamic_programming.jl:54-64 (compute_gain! :37-43 with
     chol_solve! :28-31, compute_ctg! :48-52, same op order) in x87 80-bit extended precision

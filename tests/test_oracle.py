@@ -252,6 +252,27 @@ def test_dp_oracle_linear_zero_is_plain(lqrx):
     assert not a["d"].any() and not a["p"].any()
 
 
+@pytest.mark.parametrize("n,m,N", [(4, 1, 101), (6, 3, 40), (32, 16, 64)])
+def test_dp_oracle_matches_openblas_lapack(lqrx, n, m, N):
+    """SURVEY §8(c) third-party boundary: the C oracle's hand-written potrf/potrs/gemm agree
+    with OpenBLAS's dpotrf/dpotrs 'U' and dgemm (what Julia's LAPACK.potrf!/potrs! and BLAS
+    call) on the reference op order — per knot K_k, P_k within 1e-12 relative, X, U 1e-12."""
+    from lqrx.dp import abi_to_batch, from_abi
+
+    bt = 3
+    d = lqrx.random_batch(n, m, N, bt, seed=71 + n)
+    out = orc.dp_solve_abi(d, N, all_P=True)
+    b = abi_to_batch(d)
+    K = from_abi(out["K"], (bt, N - 1, m, n)); P = from_abi(out["P"], (bt, N, n, n))
+    X = out["X"].reshape(bt, N, n); U = out["U"].reshape(bt, N - 1, m)
+    for t in range(bt):
+        Kl, Pl, Xl, Ul = orc.dp_lapack(b.A[t], b.B[t], b.Q[t], b.R[t], b.Qf[t], b.x0[t], N)
+        kn = lambda a, r: (np.abs(a - r).reshape(len(r), -1).max(1) / np.abs(r).reshape(len(r), -1).max(1)).max()
+        assert kn(K[t], Kl) <= 1e-12 and kn(P[t], Pl) <= 1e-12
+        assert np.abs(X[t] - Xl).max() <= 1e-12 * max(1.0, np.abs(Xl).max())
+        assert np.abs(U[t] - Ul).max() <= 1e-12 * max(1.0, np.abs(Ul).max())
+
+
 def test_dp_oracle_dare_limit(lqrx):
     """Long horizon: K_1 → (R + BᵀP∞B)⁻¹BᵀP∞A and P_1 → P∞ (scipy solve_discrete_are) on
     well-actuated problems (stable A, full-rank B) whose Riccati recursion
