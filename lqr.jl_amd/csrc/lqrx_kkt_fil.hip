@@ -34,7 +34,8 @@ namespace fil {
 #ifndef LQRX_FIL_ABL
 #define LQRX_FIL_ABL 0   // ablation builds for tools/ only (bits: 1 forward sweep alone, 2 Schur
                          // from one column, 4 no F̃ recompute, 8 primal without Yᵀm, 16 no
-                         // hand-placed VMEM waits, 32 no forward slab stores)
+                         // hand-placed VMEM waits, 32 no forward slab stores, 64 no δz/λ
+                         // stores — timing bounds only, results wrong)
 #endif
 #ifndef LQRX_FIL_N12
 #define LQRX_FIL_N12 1   // 12-byte LDS-DMA pieces for the short chunks (0: dwords only)
@@ -105,6 +106,9 @@ template <int NX_, int M_, int P0_, int PK_, int PN_, bool HDIAG_, bool GINV_, b
         return tri(C::PS) + tri(C::P2) + C::P1 * C::PS + C::PS * C::P2 + C::PS + C::P2;
     }
     static constexpr int SLOT = mx3<slab<F>(), slab<I>(), slab<L>()>();
+    // layout-0 output images (doubles per lane): δz chunk, then [μ; λ] chunk
+    static constexpr int WOUT = mx3<F::W, I::W, L::W>();
+    static constexpr int LOUT = mx3<F::PS + F::P2, I::PS + I::P2, L::PS + L::P2>();
 };
 
 // per-knot offsets (elements) in the packed per-trajectory arrays: knot 0 is class F,
@@ -273,6 +277,30 @@ template <int L> struct SImgS {
     }
 };
 
+// Layout-0 output stores (δz, λ): a wave's 64 chunks of L doubles are first written to an LDS
+// image [t][L] (lane t's chunk at t·L), then stored as L instructions, instruction i moving
+// the image's doubles 64i .. 64i+63 — consecutive lanes write consecutive doubles of one
+// trajectory's chunk (≈ 64/L trajectories per instruction) instead of one double of each of
+// 64 trajectories (64 cache lines per instruction; measured: dropping the layout-0 δz/λ
+// stores altogether cut cfg3 from 0.356 to 0.262 ms).  Same instruction count as the
+// per-lane stores, so the hand-placed vmcnt bounds are unchanged; doubles of dead
+// trajectories get an offset past the buffer range (the store drops them — no exec branch).
+template <int L> struct StPat {
+    uint32_t vo[L];
+    __device__ __forceinline__ void init(int64_t s, int lane, int nlive, const int32_t *sel)
+    {
+#pragma unroll
+        for (int i = 0; i < L; ++i) {
+            const uint32_t p = 64u * (uint32_t)i + (uint32_t)lane;
+            const uint32_t tr = p / (uint32_t)L, e = p - tr * (uint32_t)L;
+            const uint32_t tg = tr < (uint32_t)nlive ? (sel ? (uint32_t)sel[tr] : tr) : 0u;
+            vo[i] = tr < (uint32_t)nlive ? tg * (uint32_t)(s * 8) + 8u * e : 0xFFFFFF00u;
+        }
+    }
+};
+template <int L>
+__device__ __forceinline__ void dense_store(const double (&v)[Z(L)], double *img, const StPat<L> &pat, rsrc_t r,
+                                            uint32_t so, int lane);
 // staging buffer views (lane-linear [t][L] images; SOA: [element][64] images)
 template <class S> struct Buf {
     double *base;
@@ -304,6 +332,34 @@ template <class S> struct Ctx {
     const int32_t *sel = nullptr;                  // layout 0, selected trajectories (a.sel + t0) or null
     uint32_t vsoa = 0, rowb = 0;                   // SOA: lane's row-pair offset, bytes per element row
     uint32_t limY = 0, limy = 0, limH = 0, limg = 0; // SOA: bytes from the wave base to each array's end
+    // layout 0: LDS images of the coalesced δz / λ stores (dense_store), interior patterns
+    double *ozi = nullptr, *oli = nullptr;
+    int64_t sgz = 0, slz = 0;                      // per-trajectory strides of dz, lam
+    StPat<S::I::W> pz;
+    StPat<Z(S::I::PS + S::I::P2)> pl;
+    __device__ __forceinline__ void init_out(const KktArgs &a, double *ost)
+    {
+        ozi = ost;
+        oli = ost + 64 * S::WOUT;
+        sgz = a.sg;
+        slz = a.sl;
+        pz.init(a.sg, lane, nlive, sel);
+        pl.init(a.sl, lane, nlive, sel);
+    }
+    // a chunk of L doubles per trajectory at element offset off: the interior pattern when the
+    // length matches, else a one-off pattern (first / last knot)
+    template <int L, int LI>
+    __device__ __forceinline__ void out_store(const double (&v)[Z(L)], double *img, const StPat<LI> &pi,
+                                              int64_t stride, const double *base, int64_t off) const
+    {
+        if constexpr (L == LI) {
+            dense_store<L>(v, img, pi, make_rsrc(base), (uint32_t)(off * 8), lane);
+        } else {
+            StPat<L> q;
+            q.init(stride, lane, nlive, sel);
+            dense_store<L>(v, img, q, make_rsrc(base), (uint32_t)(off * 8), lane);
+        }
+    }
     // SOA: L element rows from row r0 of one array, as (L+1)/2 row-pair DMAs (lane l → row
     // 2i + l/32, trajectories 2(l mod 32), +1).  Reads past the array's end (dead lanes of the
     // last wave, the odd row of the last pair) are out of the resource's range and return 0.
@@ -387,6 +443,24 @@ __device__ __forceinline__ void bstore(double v, rsrc_t r, uint32_t vo, uint32_t
 {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2_t, v), r, vo, so, 0);
 }
+typedef __attribute__((address_space(3))) double lds_dw;
+template <int L>
+__device__ __forceinline__ void dense_store(const double (&v)[Z(L)], double *img, const StPat<L> &pat, rsrc_t r,
+                                            uint32_t so, int lane)
+{
+    const uint32_t b = (uint32_t)(size_t)(lptr_t)img;
+#pragma unroll
+    for (int j = 0; j < L; ++j) *(lds_dw *)(size_t)(b + (lane * L + j) * 8) = v[j];
+    // one wave: its LDS ops execute in order — only keep the compiler from reordering
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int i = 0; i < L; ++i) bstore(*(lds_dw *)(size_t)(b + (64 * i + lane) * 8), r, pat.vo[i], so);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // reads done before the next writes
+    __builtin_amdgcn_wave_barrier();
+}
+
 // the forward sweep's slab stores (an ablation build can drop them)
 __device__ __forceinline__ void sstore(double v, rsrc_t r, uint32_t vo, uint32_t so)
 {
@@ -966,35 +1040,43 @@ __device__ __forceinline__ void primal_knot(const Ctx<S> &c, int k, const SlabV<
             trsv_n<W>(U, z);
         }
     }
-    if (c.live) {
-        if constexpr (S::SOA) {                                   // coalesced 512-B rows
+    if constexpr ((LQRX_FIL_ABL & 64) != 0) return;
+    if constexpr (S::SOA) {                                       // coalesced 512-B rows
+        if (c.live) {
 #pragma unroll
             for (int j = 0; j < W; ++j) bstore(-z[j], make_rsrc(c.bdz), c.vdz, (uint32_t)(Off<S>::g(k) + j) * c.rowb);
-        } else {
-            const uint32_t so = (uint32_t)(Off<S>::g(k) * 8);
-#pragma unroll
-            for (int j = 0; j < W; ++j) bstore(-z[j], make_rsrc(c.bdz), c.vdz + 8 * j, so);
         }
+    } else {                                                      // dense image, every lane
+        double nz[W];
+#pragma unroll
+        for (int j = 0; j < W; ++j) nz[j] = -z[j];
+        c.template out_store<W, S::I::W>(nz, c.ozi, c.pz, c.sgz, c.bdz, Off<S>::g(k));
     }
 }
 
 template <class S, class C>
 __device__ __forceinline__ void store_lam(const Ctx<S> &c, int k, const SlabV<C> &v)
 {
-    if (!c.live) return;
+    if constexpr ((LQRX_FIL_ABL & 64) != 0) return;
     if constexpr (S::SOA) {
+        if (!c.live) return;
         const uint32_t r0 = (uint32_t)Off<S>::y(k);
 #pragma unroll
         for (int i = 0; i < C::PS; ++i) bstore(v.mu[i], make_rsrc(c.blam), c.vlam, (r0 + i) * c.rowb);
 #pragma unroll
         for (int i = 0; i < C::P2; ++i) bstore(v.la[i], make_rsrc(c.blam), c.vlam, (r0 + C::PS + i) * c.rowb);
         return;
+    } else {                                                      // [μ_k; λ_k], dense image
+        constexpr int LL = C::PS + C::P2;
+        if constexpr (LL > 0) {
+            double lv[LL];
+#pragma unroll
+            for (int i = 0; i < C::PS; ++i) lv[i] = v.mu[i];
+#pragma unroll
+            for (int i = 0; i < C::P2; ++i) lv[C::PS + i] = v.la[i];
+            c.template out_store<LL, Z(S::I::PS + S::I::P2)>(lv, c.oli, c.pl, c.slz, c.blam, Off<S>::y(k));
+        }
     }
-    const uint32_t so = (uint32_t)(Off<S>::y(k) * 8);
-#pragma unroll
-    for (int i = 0; i < C::PS; ++i) bstore(v.mu[i], make_rsrc(c.blam), c.vlam + 8 * i, so);
-#pragma unroll
-    for (int i = 0; i < C::P2; ++i) bstore(v.la[i], make_rsrc(c.blam), c.vlam + 8 * (C::PS + i), so);
 }
 
 // Start of forward step k (class C; Cnn = class of knot k+2): knot k+1 must have landed.
@@ -1019,6 +1101,7 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     using L = typename S::L;
     __shared__ __attribute__((aligned(16))) double stg[3 * S::BUF];
     __shared__ __attribute__((aligned(16))) double sl[3 * SLB<S>];
+    __shared__ __attribute__((aligned(16))) double ost[S::SOA ? 1 : 64 * (S::WOUT + S::LOUT)];
     const int N = a.N;                                          // ≥ 4 (host-checked)
     const int64_t t0 = (int64_t)blockIdx.x * 64;
     Ctx<S> c;
@@ -1066,6 +1149,7 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
         c.py.init(a.sy, c.lane, c.nlive, c.sel);
         c.pH.init(a.sH, c.lane, c.nlive, c.sel);
         c.pg.init(a.sg, c.lane, c.nlive, c.sel);
+        c.init_out(a, ost);
     }
     int info = 0;
 
@@ -1309,6 +1393,7 @@ __global__ __launch_bounds__(64) void kkt_fild_kernel(const KktArgs a, double *_
     using F = typename S::F;
     using I = typename S::I;
     using L = typename S::L;
+    __shared__ __attribute__((aligned(16))) double ost[S::SOA ? 1 : 64 * (S::WOUT + S::LOUT)];
     const int N = a.N;                                          // ≥ 4 (host-checked)
     const int64_t t0 = (int64_t)blockIdx.x * 64;
     Ctx<S> c;
@@ -1328,6 +1413,7 @@ __global__ __launch_bounds__(64) void kkt_fild_kernel(const KktArgs a, double *_
         c.blam = a.lam + t0 * a.sl;
         c.vdz = (uint32_t)(c.lane * a.sg * 8);
         c.vlam = (uint32_t)(c.lane * a.sl * 8);
+        c.init_out(a, ost);
     }
     int info = 0;
 
