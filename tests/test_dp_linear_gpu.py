@@ -186,3 +186,24 @@ def test_dp_linear_small_kernels(lqrx, oracle, gpu_ok, monkeypatch, small, n, m,
         got = lqrx.solve_batch(to_batch(d, N), all_P=all_P)
         ref = oracle.dp_solve_lin_abi(d, N, all_P=all_P)
         check(got, ref, n, m, N, bt, all_P, TOL64)
+
+
+@pytest.mark.parametrize("n,m,N,bt,tvq", [(4, 1, 2, 1, False), (32, 16, 2, 3, True), (6, 2, 3, 65, False),
+                                          (3, 1, 5, 130, True), (64, 32, 2, 1, False)])
+def test_dp_linear_edge_shapes(lqrx, oracle, gpu_ok, n, m, N, bt, tvq):
+    """Shortest horizons (N = 2: one backward knot), single trajectories and ragged waves."""
+    d = lin_problem(lqrx, n, m, N, bt, 4400 + 7 * n + N, tv_QR=tvq)
+    for all_P in (True, False):
+        got = lqrx.solve_batch(to_batch(d, N), all_P=all_P)
+        ref = oracle.dp_solve_lin_abi(d, N, all_P=all_P)
+        check(got, ref, n, m, N, bt, all_P, TOL64)
+
+
+def test_dp_linear_empty_batch(lqrx, gpu_ok):
+    """batch = 0 is a valid no-op, as for lqrx_dp_solve."""
+    import ctypes as C
+    from lqrx import _lib
+
+    d = _lib.DpDesc(8, 4, 10, 0, 0, 0, 0, 0, 0)
+    ln = _lib.DpLinear(None, None, None, None, None)
+    assert lqrx.load().lqrx_dp_solve_linear(C.byref(d), *([None] * 6), C.byref(ln), *([None] * 4), None, None) == 0
