@@ -507,6 +507,13 @@ def main():
                     "kernel_ms": kern_ms,
                     "flops_per_traj": dp_flops_per_traj(n, m, N),
                     "alg_bytes_per_launch": dp_bytes_per_traj(n, m, N, 8 if f64 else 4, args.tv) * bt}
+            if (n, m, args.dtype) == (32, 16, "f64") and not (args.tv or args.linear):
+                # executed work beside the reference-op-count fraction: the fast symmetric form
+                # issues 129 v_mfma_f64_16x16x4 (2048 flop each) per knot (PMC SQ_INSTS_MFMA,
+                # profiles/r02/dp_cfg4_r02_pmc_summary.txt) — the MFMA pipe's real utilisation
+                ex = 129 * 2048.0 * (N - 1)
+                roof["executed_mfma_flops_per_traj"] = ex
+                roof["executed_frac"] = ex * bt / (kern_ms * 1e-3) / 1e12 / peak
             if args.tv:
                 # time-varying: per-knot A_k, B_k, Q_k, R_k make the launch HBM-bound (SURVEY
                 # §8(d) 4-TV row: t_HBM vs t_FLOP near the ridge) — report the HBM roofline on
