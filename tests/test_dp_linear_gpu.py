@@ -207,3 +207,22 @@ def test_dp_linear_empty_batch(lqrx, gpu_ok):
     d = _lib.DpDesc(8, 4, 10, 0, 0, 0, 0, 0, 0)
     ln = _lib.DpLinear(None, None, None, None, None)
     assert lqrx.load().lqrx_dp_solve_linear(C.byref(d), *([None] * 6), C.byref(ln), *([None] * 4), None, None) == 0
+
+
+def test_dp_linear_single_problem_api(lqrx, oracle, gpu_ok):
+    """The reference-shaped surface: LQRProblem(q=, r=, qf=) → solve(sol, DPSolver, prob)
+    fills sol.d (feedforward) and sol.p (linear cost-to-go) beside K, X, U, P."""
+    from lqrx.dp import DPSolver, LQRProblem, LQRSolution, from_abi
+
+    n, m, N = 6, 2, 30
+    d = lin_problem(lqrx, n, m, N, 1, 2024)
+    prob = LQRProblem(Qf=from_abi(d["Qf"], (1, n, n))[0], Q=from_abi(d["Q"], (1, n, n))[0],
+                      R=from_abi(d["R"], (1, m, m))[0], A=from_abi(d["A"], (1, n, n))[0],
+                      B=from_abi(d["B"], (1, n, m))[0], x0=d["x0"].copy(), N=N,
+                      q=d["q"].copy(), r=d["r"].copy(), qf=d["qf"].copy())
+    sol = LQRSolution.of(prob, all_P=True)
+    lqrx.solve(sol, DPSolver.of(prob), prob)
+    ref = oracle.dp_solve_lin_abi(d, N, all_P=True)
+    got = dict(K=sol.K[None], P=sol.P[None], X=sol.X[None], U=sol.U[None], d=sol.d[None], p=sol.p[None],
+               info=np.array([sol.info]))
+    check(got, ref, n, m, N, 1, True, TOL64)
