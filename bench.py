@@ -51,6 +51,8 @@ def _dp_kernel_name(n, m, bt, tv):
         small = os.environ.get("LQRX_DP_SMALL", "")
         quad = n >= 3 and not tv and (small.startswith("q") or (not small.startswith("l") and bt <= 16384))
         return "dp_quad_kernel" if quad else "dp_lane_kernel"
+    if n > 64 or m > 32:
+        return "dp_big_kernel"      # workgroup per trajectory, past the register tiles
     return "dp_riccati_kernel"
 
 

@@ -53,7 +53,7 @@ int main()
     CHECK(lqrx_dp_solve(&b, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, info, nullptr) == -1);
     b = d; b.knot_stride_AB = 5;
     CHECK(lqrx_dp_solve(&b, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, info, nullptr) == -1);
-    b = d; b.n = 65;
+    b = d; b.n = 513;                  // past the workgroup kernel's 512
     CHECK(lqrx_dp_solve(&b, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, info, nullptr) == LQRX_ERR_UNSUPPORTED);
     b = d; b.layout = 9;
     CHECK(lqrx_dp_solve(&b, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, dummy, info, nullptr) < 0);

@@ -721,7 +721,7 @@ hipError_t dp_launch(const DpArgs &a, hipStream_t s)
         if (nt <= 2 && mt <= 2) return launch_dp_tv<float, 2, 2>(a, s);
         if (nt <= 4 && mt <= 2) return launch_dp_tv<float, 4, 2, 1>(a, s);    // cfg5: n=64 m=32
     }
-    return hipErrorNotSupported;
+    return dp_big_launch(a, s);     // past the register tiles: workgroup per trajectory
 }
 
 bool dp_supported(int dtype, int n, int m, bool tv)
@@ -730,7 +730,7 @@ bool dp_supported(int dtype, int n, int m, bool tv)
     (void)tv;
     if (dp_lane_supported(n, m)) return true;
     const int nt = (n + 15) / 16, mt = (m + 15) / 16;
-    return n >= 1 && m >= 1 && nt <= 4 && mt <= 2;
+    return (n >= 1 && m >= 1 && nt <= 4 && mt <= 2) || dp_big_supported(n, m);
 }
 
 } // namespace lqrx

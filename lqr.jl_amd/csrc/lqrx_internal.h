@@ -34,6 +34,10 @@ bool dp_supported(int dtype, int n, int m, bool tv);
 // lane-per-trajectory kernel for n ≤ 4, m ≤ 4 (lqrx_dp_lane.hip)
 hipError_t dp_lane_launch(const DpArgs &a, hipStream_t s);
 bool dp_lane_supported(int n, int m);
+// workgroup-per-trajectory kernel for shapes past the register tiles (lqrx_dp_big.hip):
+// n > 64 or m > 32, up to 512 each
+hipError_t dp_big_launch(const DpArgs &a, hipStream_t s);
+bool dp_big_supported(int n, int m);
 
 struct KktArgs {
     const double *Y, *y, *H, *g; // device, packed per trajectory
