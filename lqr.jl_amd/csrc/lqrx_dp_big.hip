@@ -107,6 +107,11 @@ __global__ __launch_bounds__(BT) void dp_big_kernel(const DpArgs a, T *__restric
     T *db = lin ? (T *)a.d + (size_t)b * (size_t)(N - 1) * m : nullptr;
     T *pall = (lin && a.p_all) ? (T *)a.p + (size_t)b * (size_t)N * n : nullptr;
     __shared__ int s_info;
+    // E (m×m) lives in LDS when it fits (m ≤ 64): the factor's pivot chain and the triangular
+    // solves read it m² times in dependent order — L2 latency per read otherwise
+    constexpr int EL = 64;
+    __shared__ T Es[EL * EL];
+    if (m <= EL) E = Es;
 
     const T *Qf = (const T *)a.Qf + b * nn;
     for (size_t e = tid; e < nn; e += BT) {                     // :58 P .= Qf
