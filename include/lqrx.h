@@ -72,7 +72,9 @@ extern "C" {
  *        dynamic_programming.jl:29; the solve still runs to completion, as there).
  * ------------------------------------------------------------------------------------ */
 typedef struct lqrx_dp_desc {
-    int32_t n, m, N;        /* state dim, control dim, knots (N >= 2)                 */
+    int32_t n, m, N;        /* state dim, control dim, knots (N >= 2); 1 <= n, m <= 512
+                               (n <= 4: lane kernels; n <= 64, m <= 32: register-tiled
+                               MFMA kernel; beyond: workgroup-per-trajectory kernel)      */
     int32_t dtype;          /* LQRX_F64 (reference precision) or LQRX_F32            */
     int64_t batch;          /* number of independent problems                          */
     int32_t layout;         /* 0 = column-major blocks, batch slowest (Julia Array{T,3});
