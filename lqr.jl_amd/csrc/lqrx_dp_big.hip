@@ -13,7 +13,9 @@
 // Time-varying knot strides, all-P output, linear cost terms (d, p) as in the other kernels.
 #include "lqrx_internal.h"
 #include "lqrx_tile.h"
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 namespace lqrx {
 
@@ -85,9 +87,9 @@ __device__ __forceinline__ void wg_mm(T *C, int ldc, int r, int c, const T *Cin,
 }
 
 template <typename T>
-__global__ __launch_bounds__(BT) void dp_big_kernel(const DpArgs a, T *__restrict__ ws, size_t ws_elems)
+__global__ __launch_bounds__(BT) void dp_big_kernel(const DpArgs a, T *__restrict__ ws, size_t ws_elems, int64_t b0)
 {
-    const int64_t b = blockIdx.x;
+    const int64_t b = b0 + blockIdx.x;                          // trajectory; scratch slot blockIdx.x
     if (b >= a.batch) return;
     const int tid = threadIdx.x;
     const int n = a.n, m = a.m, N = a.N;
@@ -99,7 +101,7 @@ __global__ __launch_bounds__(BT) void dp_big_kernel(const DpArgs a, T *__restric
     const bool lin = a.lin != 0;
     const size_t sq = a.tv_QR ? (size_t)n : 0, sr = a.tv_QR ? (size_t)m : 0;
 
-    T *w0 = ws + (size_t)b * ws_elems;
+    T *w0 = ws + (size_t)blockIdx.x * ws_elems;
     T *P = w0, *Pn = P + nn, *PA = Pn + nn, *PB = PA + nn, *APB = PB + nm, *E = APB + nm;
     T *pv = E + mm, *pn = pv + n, *wv = pn + n;
     T *Kb = (T *)a.K + (size_t)b * (size_t)(N - 1) * nm;
@@ -266,15 +268,23 @@ hipError_t dp_big_launch(const DpArgs &a, hipStream_t s)
     const size_t n = a.n, m = a.m;
     const size_t elems = 3 * n * n + 2 * n * m + m * m + 2 * n + m;   // P, P_, PA, PB, APB, E, p, p_, w
     const size_t es = a.dtype == 0 ? 8 : 4;
+    // the batch in chunks whose scratch stays ≤ 4 GiB (n = m = 512: 12.6 MB per trajectory);
+    // the chunks reuse one stream-ordered block, in stream order
+    const int64_t per = (int64_t)(elems * es);
+    int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(a.batch, ((int64_t)4 << 30) / per));
+    if (const char *ev = std::getenv("LQRX_DP_BIG_CHUNK"))   // tests: force the multi-chunk path
+        chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, std::atoll(ev)));
     void *ws = nullptr;
-    hipError_t e = scratch_alloc(&ws, elems * es * (size_t)a.batch, s);
+    hipError_t e = scratch_alloc(&ws, (size_t)per * (size_t)chunk, s);
     if (e != hipSuccess) return e;
-    dim3 grid((unsigned)a.batch), block(BT);
-    if (a.dtype == 0)
-        hipLaunchKernelGGL((dp_big_kernel<double>), grid, block, 0, s, a, (double *)ws, elems);
-    else
-        hipLaunchKernelGGL((dp_big_kernel<float>), grid, block, 0, s, a, (float *)ws, elems);
-    e = hipGetLastError();
+    for (int64_t b0 = 0; b0 < a.batch && e == hipSuccess; b0 += chunk) {
+        dim3 grid((unsigned)std::min<int64_t>(chunk, a.batch - b0)), block(BT);
+        if (a.dtype == 0)
+            hipLaunchKernelGGL((dp_big_kernel<double>), grid, block, 0, s, a, (double *)ws, elems, b0);
+        else
+            hipLaunchKernelGGL((dp_big_kernel<float>), grid, block, 0, s, a, (float *)ws, elems, b0);
+        e = hipGetLastError();
+    }
     hipError_t ef = scratch_free(ws, s);
     return e != hipSuccess ? e : ef;
 }

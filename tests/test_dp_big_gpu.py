@@ -72,3 +72,17 @@ def test_dp_big_unsupported(lqrx, gpu_ok):
 
     d = _lib.DpDesc(513, 4, 5, 0, 2, 0, 0, 0, 0)
     assert lqrx.load().lqrx_dp_solve(C.byref(d), *([None] * 10), None, None) == _lib.ERR_UNSUPPORTED
+
+
+def test_dp_big_chunked_batch(lqrx, oracle, gpu_ok, monkeypatch):
+    """The batch runs in scratch-bounded chunks (≤ 4 GiB each); LQRX_DP_BIG_CHUNK forces
+    chunks of 2 trajectories: results equal the one-chunk solve bit for bit."""
+    from lqrx.dp import abi_to_batch
+
+    n, m, N, bt = 70, 6, 7, 5
+    b = abi_to_batch(lqrx.random_batch(n, m, N, bt, seed=12))
+    one = lqrx.solve_batch(b, all_P=True)
+    monkeypatch.setenv("LQRX_DP_BIG_CHUNK", "2")
+    many = lqrx.solve_batch(b, all_P=True)
+    for k in ("K", "P", "X", "U", "info"):
+        assert np.array_equal(one[k], many[k]), k
