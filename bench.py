@@ -2,11 +2,15 @@
 """bench.py — batched LQR (Riccati backward + forward rollout) throughput on MI355X.
 
 Metric (BASELINE.json): LQR trajectories/sec, n=32 m=16 N=256 B=65536 fp64.
-A "step" = one lqrx_dp_solve launch over the rank's whole batch (inputs resident in HBM,
-outputs K/P/X/U written to HBM).  One process per GPU; for N>1 GPUs the batch is sharded
-(independent problems, no data-path collective): each rank solves its own `--batch`
-trajectories (weak scaling), generated from the same counter-based generator with a
-rank-offset trajectory index.
+A "step" = one lqrx_dp_solve launch over the rank's whole shard (inputs resident in HBM,
+outputs K/P/X/U written to HBM).  One process per GPU: under torch.distributed.run (RANK /
+WORLD_SIZE set by the launcher) or, for a plain `python bench.py --gpus N`, N ranks spawned
+by this script before anything touches a GPU (lqrx.shard.spawn_ranks).  The batch is
+sharded (independent problems, no data-path collective): by default the GLOBAL
+`--batch` is split into contiguous shards (lqrx.shard.shard_range; strong scaling — cfg4
+65536 → 8192 per GPU at 8), with `--scaling weak` every rank solves `--batch` trajectories
+of its own.  Shards come from the same counter-based generator at the shard's first
+trajectory index, so the union of the shards is the one-GPU batch.
 
 Prints ONE JSON line on rank 0 (contract in the task description), with a `roofline`
 object for the Riccati kernel (fp64 compute roofline: algorithmic flops per launch ÷ the
@@ -185,7 +189,35 @@ def nonfinite_count(out, keys):
     return int(sum(int((~torch.isfinite(out[k])).sum().item()) for k in keys if k in out))
 
 
-def main():
+def _rank_main(argv):
+    """Entry of a rank spawned by main() (lqrx.shard.spawn_ranks sets RANK / WORLD_SIZE)."""
+    return main(argv)
+
+
+def dry_run(args):
+    """--dry-run: the launcher, rank set-up, partitioning and MAX-over-ranks of the bench on
+    the CPU (gloo), no GPU and no solve — what tests/test_multirank.py drives at world 2."""
+    from lqrx import shard as SH
+    import torch.distributed as dist
+
+    rank, world, _ = SH.init_ranks("gloo")
+    first, cnt, gb = SH.rank_partition(args.batch, rank, world, args.scaling)
+    wall = SH.timed_steps(lambda: time.sleep(0.001), args.steps, args.warmup, world=world)
+    wall = SH.max_over_ranks(wall, world)
+    spans = [None] * world
+    if world > 1:
+        dist.all_gather_object(spans, (first, cnt))
+    else:
+        spans = [(first, cnt)]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "scaling": args.scaling, "global_batch": gb,
+                          "shards": spans, "steps": args.steps, "wall_s": wall}), flush=True)
+    SH.finish_ranks(world)
+    return 0
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -193,7 +225,12 @@ def main():
     ap.add_argument("--n", type=int, default=32)
     ap.add_argument("--m", type=int, default=16)
     ap.add_argument("--N", type=int, default=256)
-    ap.add_argument("--batch", type=int, default=65536, help="trajectories per GPU")
+    ap.add_argument("--batch", type=int, default=65536,
+                    help="trajectories: the global batch (--scaling strong, default) or per GPU (weak)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong: the global --batch split over the GPUs (SURVEY §8(e)); weak: --batch per GPU")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher + partition + timing scaffolding only, on the CPU (gloo), no solve")
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     ap.add_argument("--seed", type=int, default=20260104)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -220,7 +257,17 @@ def main():
                          "kkt = Dubins block-tridiagonal KKT solve (configs[2], B=16384); "
                          "sqp = Dubins SQP around the KKT solve (SURVEY §8(f) ranks 2-3, B=16384); "
                          "ls = condensed least-squares LQR on cartpole (SURVEY §8(f) rank 4, B=4096)")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher: spawn one rank per GPU now, before this process touches a GPU
+        from lqrx import shard as SH
+        return SH.spawn_ranks(args.gpus, _rank_main, argv)
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}", file=sys.stderr)
+        return 2
+    if args.dry_run:
+        return dry_run(args)
     if args.tv and args.batch == 65536:
         args.batch = 16384
     if args.workload in ("cartpole", "ls"):
@@ -250,7 +297,11 @@ def main():
     if lib.lqrx_device_available() != 1:
         raise RuntimeError("liblqrx.so sees no gfx950 device")
 
-    n, m, N, bt = args.n, args.m, args.N, args.batch
+    # this rank's contiguous shard: [traj0, traj0 + bt) of the global batch
+    traj0, bt, global_batch = SH.rank_partition(args.batch, rank, world, args.scaling)
+    if bt < 1:
+        raise ValueError(f"global batch {args.batch} < {world} ranks")
+    n, m, N = args.n, args.m, args.N
     f64 = args.dtype == "f64"
     dev = torch.device("cuda", local)
     # a created stream, not the null stream: launches on the legacy default stream pay an
@@ -273,7 +324,7 @@ def main():
     elif args.workload in ("dp", "cartpole"):
         tdt = torch.float64 if f64 else torch.float32
         if args.workload == "dp":
-            host = lqrx.random_batch(n, m, N, bt, seed=args.seed, traj0=rank * bt,
+            host = lqrx.random_batch(n, m, N, bt, seed=args.seed, traj0=traj0,
                                      dtype=lqrx.F64 if f64 else lqrx.F32)
         else:
             from lqrx.models import cartpole_batch
@@ -375,18 +426,19 @@ def main():
     # shard to rank 0 over RCCL (grouped send/recv); K stays sharded
     gather = None
     if world > 1 and args.workload in ("dp", "cartpole") and not args.no_gather:
-        try:
-            g = SH.timed_gather({"info": out["info"], "P": out["P"]}, bt * world, world, sync, dev)
-            got = g.pop("got")
-            gather = dict(g, what="info + P_1 of every shard to rank 0 (torch.distributed.gather "
-                                  "= RCCL send/recv); K stays sharded",
-                          root_info_nonzero=int((got["info"] != 0).sum().item()) if got is not None else None)
-            del got
-        except Exception as e:  # the solve measurement stands without the gather
-            gather = {"error": f"{type(e).__name__}: {e}"}
+        # a failure here propagates: the rank exits non-zero (spawn_ranks / the launcher
+        # report it) instead of printing a line with the error folded into a field
+        g = SH.timed_gather({"info": out["info"], "P": out["P"]}, global_batch, world, sync, dev)
+        got = g.pop("got")
+        gather = dict(g, what="info + P_1 of every shard to rank 0 (torch.distributed.gather "
+                              "= RCCL send/recv); K stays sharded",
+                      root_info_nonzero=int((got["info"] != 0).sum().item()) if got is not None else None)
+        if got is not None and got["info"].numel() != global_batch:
+            raise RuntimeError(f"gather delivered {got['info'].numel()} of {global_batch} trajectories")
+        del got
 
     wall = SH.max_over_ranks(wall, world, dev)
-    total = bt * world * args.steps
+    total = global_batch * args.steps
     value = total / wall
     ms_per_step = wall / args.steps * 1e3
 
@@ -578,11 +630,12 @@ def main():
         line = {
             "metric": metric, "value": value, "unit": "trajectories/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
             "dtype": args.dtype, "data": "synthetic (counter-based random problems, "
                                           "SURVEY.md §8(d) generator)",
             "config": {"workload": workload, "n": n, "m": m, "N": N, "batch_per_gpu": bt,
-                       "global_batch": bt * world, "parallelism": f"batch-sharded x{world}"},
+                       "global_batch": global_batch, "parallelism": f"batch-sharded x{world}",
+                       "shard_rank0": [traj0, bt]},
             "roofline": roof,
             "cpu_baseline": cpu,
             "check": {"nonfinite": nonfinite, "info_nonzero": bad, "sampled_parity": sampled},
@@ -592,7 +645,8 @@ def main():
             line["value_solve_plus_gather"] = total / (wall + gather["ms"] * 1e-3)
         print(json.dumps(line), flush=True)
     SH.finish_ranks(world)
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -555,8 +555,10 @@ int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const v
     }
     if (ws) {
         const size_t need = kkt_ws_bytes(d, a);
-        if (ws_bytes < need)
+        if (ws_bytes < need) {
+            if (meta_tmp) (void)lqrx::scratch_free(meta_tmp, s);
             return set_err(-10, "workspace of %zu bytes < %zu (lqrx_kkt_workspace_size)", ws_bytes, need);
+        }
         a.ws = ws;
         a.ws_bytes = ws_bytes;
     }
@@ -570,13 +572,13 @@ int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const v
         }
     } else if (a.force_lane || kkt_force_generic() || !lqrx::kkt_fil_launch(a, d->n1, d->p, d->n2, d->w, s, &e))
         e = lqrx::kkt_launch(a, s);
-    if (meta_tmp) (void)lqrx::scratch_free(meta_tmp, s);   // stream-ordered after the launch
-    if (debug_meta) {
+    if (debug_meta) {   // read the table back before a per-call table is released
         std::vector<int32_t> back(L.meta.size());
         (void)hipStreamSynchronize(s);
         (void)hipMemcpy(back.data(), dmeta, L.meta.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
         if (back != L.meta) std::fprintf(stderr, "LQRX_DEBUG_META: device meta differs from host\n");
     }
+    if (meta_tmp) (void)lqrx::scratch_free(meta_tmp, s);   // stream-ordered after the launch
     if (e == hipErrorNotSupported) return set_err(LQRX_ERR_UNSUPPORTED, "KKT kernel unavailable");
     if (e != hipSuccess) return hip_err(e, "kkt kernel launch");
     if (stream == nullptr && null_sync) {

@@ -22,6 +22,7 @@
 #include "lqrx_internal.h"
 #include "lqrx_tile.h"
 #include <math.h>
+#include <algorithm>
 
 namespace lqrx {
 
@@ -156,16 +157,17 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
                     const double *__restrict__ gR, const double *__restrict__ gQf, const double *__restrict__ gx0,
                     double *__restrict__ gU, double *__restrict__ gX, int32_t *__restrict__ ginfo,
                     double *__restrict__ gAb, double *__restrict__ gbb, int n, int m, int N, int hu_mode,
-                    double *__restrict__ gH, int pb)
+                    double *__restrict__ gH, int pb, int64_t b0)
 {
     extern __shared__ double lds[];
     const LsLayout L = ls_layout(n, m, N, BIG, pb);
     const int K = L.K, Nm = L.Nm, tid = threadIdx.x;
-    const int64_t b = blockIdx.x;
+    const int64_t b = b0 + blockIdx.x;
     double *Sq = lds + L.oSq, *Sf = lds + L.oSf, *Hu = lds + L.oHu, *A = lds + L.oA, *B = lds + L.oB;
     double *Pl = lds + L.oPl, *W = lds + L.oW, *Vq = lds + L.oVq, *Vf = lds + L.oVf, *bb = lds + L.obb;
     double *y = lds + L.oy, *X = lds + L.oX, *dinv = lds + L.odi;
-    double *H = BIG ? gH + b * ((int64_t)Nm * (Nm + 1) / 2) : lds + L.oH;
+    // big path: the scratch holds one chunk of the batch (blocks b0 .. b0 + gridDim.x − 1)
+    double *H = BIG ? gH + (b - b0) * ((int64_t)Nm * (Nm + 1) / 2) : lds + L.oH;
     int *flag = (int *)(lds + L.oFlag);
     const int nn = n * n, nm = n * m, mm = m * m;
 
@@ -345,6 +347,9 @@ ls_condensed_kernel(const double *__restrict__ gA, const double *__restrict__ gB
                 return;
             }
             const double ri = rsqrt_nr(d);
+            // every thread has read the pivot before tid 0 overwrites it with sqrt(d): a lagging
+            // wave (columns u + 64 and up) must not see the scaled value
+            __syncthreads();
             for (int c = u + tid; c < w; c += LS_THREADS) Pn[u * w + c] = c == u ? d * ri : Pn[u * w + c] * ri;
             if (tid == 0) dinv[r0 + u] = ri;
             __syncthreads();
@@ -564,22 +569,30 @@ hipError_t ls_launch(const LsArgs &a, hipStream_t s)
     const void *fn = big ? (const void *)ls_condensed_kernel<true> : (const void *)ls_condensed_kernel<false>;
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    Scratch sc;                          // big path: packed H per trajectory, stream-ordered
-    const int Nm = (a.N - 1) * a.m;
-    if (big) {
-        e = scratch_alloc(&sc.p, (size_t)a.batch * ((size_t)Nm * (Nm + 1) / 2) * sizeof(double), s);
-        if (e != hipSuccess) return e;
-        sc.owned = true;
-    }
     // one workgroup per trajectory; the grid dimension is capped at 2^31−1 by the ABI check
-    if (big)
-        hipLaunchKernelGGL(ls_condensed_kernel<true>, dim3((unsigned)a.batch), dim3(LS_THREADS), lds, s, a.A, a.B,
-                           a.Q, a.R, a.Qf, a.x0, a.U, a.X, a.info, a.Ab, a.bb, a.n, a.m, a.N, a.hu_mode, (double *)sc.p,
-                           ls_panel(a.n, a.m, a.N));
-    else
+    if (!big) {
         hipLaunchKernelGGL(ls_condensed_kernel<false>, dim3((unsigned)a.batch), dim3(LS_THREADS), lds, s, a.A, a.B,
-                           a.Q, a.R, a.Qf, a.x0, a.U, a.X, a.info, a.Ab, a.bb, a.n, a.m, a.N, a.hu_mode, nullptr, LS_PB);
-    e = hipGetLastError();
+                           a.Q, a.R, a.Qf, a.x0, a.U, a.X, a.info, a.Ab, a.bb, a.n, a.m, a.N, a.hu_mode, nullptr, LS_PB,
+                           (int64_t)0);
+        return hipGetLastError();
+    }
+    // big path: packed H per trajectory in one stream-ordered scratch block of at most 4 GiB,
+    // reused by consecutive chunks of the batch in stream order (as dp_big_launch does)
+    const int Nm = (a.N - 1) * a.m;
+    const size_t per = ((size_t)Nm * (Nm + 1) / 2) * sizeof(double);
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(a.batch, (int64_t)((size_t(4) << 30) / per)));
+    Scratch sc;
+    e = scratch_alloc(&sc.p, (size_t)chunk * per, s);
+    if (e != hipSuccess) return e;
+    sc.owned = true;
+    const int pb = ls_panel(a.n, a.m, a.N);
+    for (int64_t b0 = 0; b0 < a.batch && e == hipSuccess; b0 += chunk) {
+        const int64_t nb = std::min<int64_t>(chunk, a.batch - b0);
+        hipLaunchKernelGGL(ls_condensed_kernel<true>, dim3((unsigned)nb), dim3(LS_THREADS), lds, s, a.A, a.B, a.Q,
+                           a.R, a.Qf, a.x0, a.U, a.X, a.info, a.Ab, a.bb, a.n, a.m, a.N, a.hu_mode, (double *)sc.p, pb,
+                           b0);
+        e = hipGetLastError();
+    }
     hipError_t ef = sc.release(s);
     return e != hipSuccess ? e : ef;
 }

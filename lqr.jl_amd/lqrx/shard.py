@@ -14,7 +14,73 @@ import os
 import time
 
 __all__ = ["shard_range", "gather_to_root", "dist_env", "init_ranks", "timed_steps",
-           "max_over_ranks", "sum_over_ranks", "timed_gather", "finish_ranks"]
+           "max_over_ranks", "sum_over_ranks", "timed_gather", "finish_ranks", "spawn_ranks",
+           "rank_partition"]
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_child(rank, world, port, fn, args):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    rc = fn(*args)
+    raise SystemExit(int(rc or 0))
+
+
+def spawn_ranks(nprocs: int, fn, *args, port: int | None = None, timeout: float | None = None) -> int:
+    """One process per GPU without an external launcher: start `nprocs` fresh interpreters
+    (multiprocessing "spawn": fork + exec of python by THIS process, which must not have
+    touched the GPU yet) with RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR=127.0.0.1 /
+    MASTER_PORT set — what torch.distributed.run would set — each running fn(*args).  Waits
+    for all; returns 0 if every rank exited 0, else the first non-zero exit code (a rank
+    killed by a signal gives 128 + signal).  If one rank fails the others are terminated
+    rather than left hanging in a collective."""
+    import multiprocessing as mp
+    import time as _t
+
+    ctx = mp.get_context("spawn")
+    port = port or _free_port()
+    procs = [ctx.Process(target=_rank_child, args=(r, nprocs, port, fn, args)) for r in range(nprocs)]
+    for p in procs:
+        p.start()
+    t0 = _t.monotonic()
+    rc = 0
+    while any(p.is_alive() for p in procs):
+        for p in procs:
+            p.join(0.2)
+            if p.exitcode not in (None, 0) and rc == 0:
+                rc = p.exitcode if p.exitcode > 0 else 128 - p.exitcode
+        if rc or (timeout is not None and _t.monotonic() - t0 > timeout):
+            rc = rc or 124
+            for p in procs:
+                if p.is_alive():
+                    p.terminate()
+            for p in procs:
+                p.join(30)
+            break
+    for p in procs:
+        if p.exitcode not in (None, 0) and rc == 0:
+            rc = p.exitcode if p.exitcode > 0 else 128 - p.exitcode
+    return rc
+
+
+def rank_partition(batch: int, rank: int, world: int, scaling: str = "strong") -> tuple[int, int, int]:
+    """(first trajectory, count, global batch) of this rank's contiguous shard.  "strong": the
+    GLOBAL `batch` is split by shard_range (SURVEY §8(e): cfg4 65536 → 8192 per GPU at 8);
+    "weak": every rank solves `batch` trajectories of its own (first = rank·batch)."""
+    if scaling == "strong":
+        first, cnt = shard_range(batch, rank, world)
+        return first, cnt, batch
+    if scaling == "weak":
+        return rank * batch, batch, batch * world
+    raise ValueError(f"scaling must be 'strong' or 'weak' (got {scaling!r})")
 
 
 def dist_env() -> tuple[int, int, int]:

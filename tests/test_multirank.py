@@ -189,3 +189,58 @@ def test_bench_rank_scaffolding_gloo(lqrx):
     ref = orc.dp_solve_abi(L.random_batch(4, 2, 10, per * world, seed=91), 10)
     assert np.array_equal(res[0][8]["info"], ref["info"])
     assert np.array_equal(res[0][8]["P"], ref["P"])
+
+
+def _run_bench(args, env_extra=None, timeout=240):
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+@pytest.mark.parametrize("scaling,batch", [("strong", 65536), ("strong", 11), ("weak", 5)])
+def test_bench_launcher_spawns_ranks_gloo(scaling, batch):
+    """`python bench.py --gpus 2` without a launcher: bench.py spawns the two ranks itself
+    (lqrx.shard.spawn_ranks, before any GPU call), each joins the process group, and rank 0
+    reports n_gpus == 2; strong scaling splits the GLOBAL batch into shards that tile it,
+    weak scaling gives every rank `batch` of its own (--dry-run: gloo, no solve)."""
+    rc, line, err = _run_bench(["--gpus", "2", "--dry-run", "--batch", str(batch), "--steps", "2",
+                                "--warmup", "1", "--scaling", scaling])
+    assert rc == 0, err[-2000:]
+    assert line["n_gpus"] == 2 and line["scaling"] == scaling
+    spans = [tuple(s) for s in line["shards"]]
+    if scaling == "strong":
+        assert line["global_batch"] == batch
+        assert spans[0][0] == 0 and spans[0][0] + spans[0][1] == spans[1][0]
+        assert spans[1][0] + spans[1][1] == batch and abs(spans[0][1] - spans[1][1]) <= 1
+    else:
+        assert spans == [(0, batch), (batch, batch)] and line["global_batch"] == 2 * batch
+
+
+def test_bench_launcher_world_mismatch_exits_nonzero():
+    """A launcher-set WORLD_SIZE that disagrees with --gpus is an error (exit 2), not a
+    silent one-rank run."""
+    rc, line, _ = _run_bench(["--gpus", "2", "--dry-run"], env_extra={"WORLD_SIZE": "1", "RANK": "0"})
+    assert rc == 2 and line is None
+
+
+def test_spawn_ranks_reports_failure():
+    """A failing rank makes spawn_ranks return non-zero (and stops the other rank)."""
+    from lqrx.shard import spawn_ranks
+    assert spawn_ranks(2, _fail_on_rank1, timeout=120) == 3
+
+
+def _fail_on_rank1():
+    import time
+    if os.environ["RANK"] == "1":
+        return 3
+    time.sleep(30)
+    return 0
