@@ -358,7 +358,8 @@ int kkt_layout(const lqrx_kkt_desc *d, KktLayout &L)
 {
     if (!d) return set_err(-1, "desc is NULL");
     if (d->N < 1) return set_err(-1, "desc.N must be >= 1");
-    if (d->dtype != LQRX_F64) return set_err(LQRX_ERR_UNSUPPORTED, "KKT path is fp64 only");
+    if (d->dtype != LQRX_F64 && d->dtype != LQRX_F32)
+        return set_err(-1, "desc.dtype must be LQRX_F64 or LQRX_F32 (got %d)", d->dtype);
     if (d->batch < 0) return set_err(-1, "desc.batch must be >= 0");
     if (!d->n1 || !d->p || !d->n2 || !d->w) return set_err(-1, "block-size arrays are NULL");
     if (d->h_mode < 0 || d->h_mode > 2) return set_err(-1, "desc.h_mode must be 0, 1 or 2");
@@ -375,8 +376,9 @@ int kkt_layout(const lqrx_kkt_desc *d, KktLayout &L)
             return set_err(-1, "knot %d: n1 (%d) != n2 of knot %d (%d)", k, n1, k - 1, d->n2[k - 1]);
         if (k == d->N - 1 && n2 != 0) return set_err(-1, "last knot must have n2 == 0");
         int rows = n1 + p + n2;
-        if (rows > 64 || w > 64)
-            return set_err(LQRX_ERR_UNSUPPORTED, "knot %d: block %dx%d larger than 64", k, rows, w);
+        if (n1 > 64 || p > 64 || n2 > 64 || w > 128)
+            return set_err(LQRX_ERR_UNSUPPORTED, "knot %d: block (n1 %d, p %d, n2 %d, w %d) past 64 rows per "
+                                                 "part / 128 columns", k, n1, p, n2, w);
         int32_t *m = &L.meta[(size_t)k * 8];
         m[0] = n1; m[1] = p; m[2] = n2; m[3] = w;
         m[4] = (int32_t)L.sY; m[5] = (int32_t)L.sy; m[6] = (int32_t)L.sH; m[7] = (int32_t)L.sg;
@@ -468,6 +470,7 @@ extern "C" int lqrx_kkt_sizes(const lqrx_kkt_desc *d, int64_t *nY, int64_t *ny, 
 }
 
 namespace {
+bool kkt_force_generic();
 // kernel arguments of one KKT call (no device pointers yet)
 lqrx::KktArgs kkt_args(const lqrx_kkt_desc *d, const KktLayout &L)
 {
@@ -479,7 +482,31 @@ lqrx::KktArgs kkt_args(const lqrx_kkt_desc *d, const KktLayout &L)
     static const int force_lane = [] { const char *v = std::getenv("LQRX_KKT_FORCE_LANE"); return v && *v == '1'; }();
     a.force_lane = force_lane;
     a.layout = d->layout;
+    a.dtype = d->dtype == LQRX_F32 ? 1 : 0;
     return a;
+}
+// Kernel family for a call.  fp32: the large-block MFMA kernels only.  fp64: the
+// compile-time shapes (FIL) first, then the LDS-staged / small lane generic kernels, then the
+// large-block kernels (which also replace the scratch-spilling lane<8,8,8,12,16> kernel);
+// LQRX_KKT_BIG=1 forces the large-block kernels wherever they apply, =0 never uses them.
+enum { KK_NONE = 0, KK_FIL, KK_GENERIC, KK_BIG };
+int kkt_big_env()
+{
+    static const int v = [] { const char *e = std::getenv("LQRX_KKT_BIG"); return e && *e ? std::atoi(e) : -1; }();
+    return v;
+}
+int kkt_route(const lqrx_kkt_desc *d, const lqrx::KktArgs &a)
+{
+    const bool big = kkt_big_env() != 0 && lqrx::kkt_big_supported(a, d->n1, d->p, d->n2, d->w);
+    if (d->dtype == LQRX_F32) return big ? KK_BIG : KK_NONE;
+    if (kkt_big_env() == 1 && big) return KK_BIG;
+    size_t b = 0;
+    const bool fil = !a.force_lane && !kkt_force_generic() && lqrx::kkt_fil_scratch_bytes(a, d->n1, d->p, d->n2, d->w, &b);
+    if (d->layout == 1) return fil ? KK_FIL : KK_NONE;
+    if (fil) return KK_FIL;
+    const int gc = lqrx::kkt_generic_class(a);
+    if (gc == 1 || gc == 2 || (gc == 3 && (!big || a.force_lane))) return KK_GENERIC;
+    return big ? KK_BIG : KK_NONE;
 }
 // LQRX_KKT_GENERIC=1 forces the generic (runtime-shaped) kernel, for A/B checks
 bool kkt_force_generic()
@@ -490,9 +517,12 @@ bool kkt_force_generic()
 size_t kkt_ws_bytes(const lqrx_kkt_desc *d, const lqrx::KktArgs &a)
 {
     size_t b = 0;
-    if (!a.force_lane && !kkt_force_generic() && lqrx::kkt_fil_scratch_bytes(a, d->n1, d->p, d->n2, d->w, &b))
-        return b;
-    return lqrx::kkt_scratch_bytes(a);
+    switch (kkt_route(d, a)) {
+    case KK_FIL: (void)lqrx::kkt_fil_scratch_bytes(a, d->n1, d->p, d->n2, d->w, &b); return b;
+    case KK_BIG: return lqrx::kkt_big_scratch_bytes(a, d->n1, d->p, d->n2, d->w);
+    case KK_GENERIC: return lqrx::kkt_scratch_bytes(a);
+    default: return 0;
+    }
 }
 int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const void *H, const void *g,
                    void *dz, void *lam, int32_t *info, void *ws, size_t ws_bytes, void *stream,
@@ -563,14 +593,19 @@ int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const v
         a.ws_bytes = ws_bytes;
     }
     static const int debug_meta = [] { const char *v = std::getenv("LQRX_DEBUG_META"); return v && *v == '1'; }();
-    if (d->layout == 1) {
-        // batch-fastest inputs are served by the compile-time-shaped kernel only
-        if (!lqrx::kkt_fil_launch(a, d->n1, d->p, d->n2, d->w, s, &e)) {
-            if (meta_tmp) (void)lqrx::scratch_free(meta_tmp, s);
+    const int route = kkt_route(d, a);
+    if (route == KK_NONE) {
+        if (meta_tmp) (void)lqrx::scratch_free(meta_tmp, s);
+        if (d->layout == 1)
             return set_err(LQRX_ERR_UNSUPPORTED, "layout 1 needs a compile-time KKT shape (Dubins; cartpole, "
                                                  "DoubleIntegrator(2|3) with diagonal H) and N >= 4");
-        }
-    } else if (a.force_lane || kkt_force_generic() || !lqrx::kkt_fil_launch(a, d->n1, d->p, d->n2, d->w, s, &e))
+        return set_err(LQRX_ERR_UNSUPPORTED, "no KKT kernel for this structure / options (%s; large blocks need "
+                                             "n1, p, n2 <= 64, padded rows <= 128, w <= 128, layout 0 and a "
+                                             "diagonal H or ginv = 0)",
+                       d->dtype == LQRX_F32 ? "fp32" : "fp64");
+    }
+    if (route == KK_BIG) e = lqrx::kkt_big_launch(a, d->n1, d->p, d->n2, d->w, s);
+    else if (route == KK_GENERIC || !lqrx::kkt_fil_launch(a, d->n1, d->p, d->n2, d->w, s, &e))
         e = lqrx::kkt_launch(a, s);
     if (debug_meta) {   // read the table back before a per-call table is released
         std::vector<int32_t> back(L.meta.size());
@@ -604,26 +639,26 @@ extern "C" int lqrx_kkt_solve_host(const lqrx_kkt_desc *d, const void *Y, const 
     int st = kkt_layout(d, L);
     if (st) return st;
     if (d->batch == 0) return 0;
-    const size_t bt = (size_t)d->batch;
+    const size_t bt = (size_t)d->batch, es = d->dtype == LQRX_F32 ? 4 : 8;
     const size_t szin[4] = {(size_t)L.sY, (size_t)L.sy, (size_t)L.sH, (size_t)L.sg};
     const void *hin[4] = {Y, y, H, g};
     DevBuf din[4], ddz, dlam, dinfo;
     for (int i = 0; i < 4; ++i) {
         if (!hin[i]) return set_err(-(i + 2), "input pointer %d is NULL", i + 2);
-        if ((st = dev_alloc(din[i], szin[i] * 8 * bt, "hipMalloc input"))) return st;
-        hipError_t e = hipMemcpy(din[i].p, hin[i], szin[i] * 8 * bt, hipMemcpyHostToDevice);
+        if ((st = dev_alloc(din[i], szin[i] * es * bt, "hipMalloc input"))) return st;
+        hipError_t e = hipMemcpy(din[i].p, hin[i], szin[i] * es * bt, hipMemcpyHostToDevice);
         if (e != hipSuccess) return hip_err(e, "H2D");
     }
     if (!dz) return set_err(-6, "dz is NULL");
     if (!lam) return set_err(-7, "lam is NULL");
-    if ((st = dev_alloc(ddz, (size_t)L.sg * 8 * bt, "hipMalloc dz"))) return st;
-    if ((st = dev_alloc(dlam, (size_t)L.sy * 8 * bt, "hipMalloc lam"))) return st;
+    if ((st = dev_alloc(ddz, (size_t)L.sg * es * bt, "hipMalloc dz"))) return st;
+    if ((st = dev_alloc(dlam, (size_t)L.sy * es * bt, "hipMalloc lam"))) return st;
     if ((st = dev_alloc(dinfo, 4 * bt, "hipMalloc info"))) return st;
     st = lqrx_kkt_solve(d, din[0].p, din[1].p, din[2].p, din[3].p, ddz.p, dlam.p,
                         (int32_t *)dinfo.p, nullptr);
     if (st < 0) return st;
-    hipError_t e = hipMemcpy(dz, ddz.p, (size_t)L.sg * 8 * bt, hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemcpy(lam, dlam.p, (size_t)L.sy * 8 * bt, hipMemcpyDeviceToHost);
+    hipError_t e = hipMemcpy(dz, ddz.p, (size_t)L.sg * es * bt, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(lam, dlam.p, (size_t)L.sy * es * bt, hipMemcpyDeviceToHost);
     if (e == hipSuccess && info) e = hipMemcpy(info, dinfo.p, 4 * bt, hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_err(e, "D2H");
     return st;

@@ -51,6 +51,7 @@ struct KktArgs {
     int maxw, maxrows, max_p1, max_ps, max_p2;
     int force_lane; // debug: LQRX_KKT_FORCE_LANE=1 selects the register-only kernel
     int layout;     // 0 per-trajectory packed; 1 batch fastest (compile-time shapes only)
+    int dtype;      // 0 f64; 1 f32 (the big-block kernels only: Y..lam then point at floats)
     // internal (SQP): solve only the trajectories sel[0 .. *nsel) (device arrays; layout-0
     // LDS-staged kernel only — the other kernels solve the whole batch, which is also correct)
     const int32_t *sel, *nsel;
@@ -59,6 +60,9 @@ struct KktArgs {
 };
 
 hipError_t kkt_launch(const KktArgs &a, hipStream_t s);
+// which generic (runtime-shaped, fp64) kernel kkt_launch would pick: 0 none, 1 LDS-staged
+// ≤ (3,3,3,5,6), 2 lane ≤ (4,4,4,8,8), 3 lane ≤ (8,8,8,12,16) (runtime-indexed arrays in scratch)
+int kkt_generic_class(const KktArgs &a);
 
 // Stream-ordered scratch from a library-owned memory pool (one per device) whose release
 // threshold keeps freed blocks mapped: a per-call hipMallocAsync/hipFreeAsync pair then
@@ -92,6 +96,14 @@ bool kkt_fil_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const
 // slab bytes of the FIL kernel for this structure; false when no FIL shape serves it
 bool kkt_fil_scratch_bytes(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
                            const int32_t *w, size_t *bytes);
+
+// large-block MFMA kernels (lqrx_kkt_big.hip): any structure with n1, p, n2 ≤ 64, padded
+// rows ≤ 128, w ≤ 128, diagonal H or the SOC variant, layout 0, fp64 or fp32
+bool kkt_big_supported(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2, const int32_t *w);
+size_t kkt_big_scratch_bytes(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
+                             const int32_t *w);
+hipError_t kkt_big_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
+                          const int32_t *w, hipStream_t s);
 
 // ---- batched trajectory SQP (lqrx_sqp.hip) ----
 enum { SQP_DUBINS = 0, SQP_CARTPOLE = 1, SQP_DI1 = 2, SQP_DI2 = 3, SQP_DI3 = 4 };   // = LQRX_MODEL_*

@@ -1008,6 +1008,15 @@ size_t kkt_scratch_bytes(const KktArgs &a)
     return 0;
 }
 
+int kkt_generic_class(const KktArgs &a)
+{
+    const int P1 = a.max_p1, PS = a.max_ps, P2 = a.max_p2, W = a.maxw, R = a.maxrows;
+    if (!a.force_lane && P1 <= 3 && PS <= 3 && P2 <= 3 && W <= 5 && R <= 6) return 1;
+    if (P1 <= 4 && PS <= 4 && P2 <= 4 && W <= 8 && R <= 8) return 2;
+    if (P1 <= 8 && PS <= 8 && P2 <= 8 && W <= 12 && R <= 16) return 3;
+    return 0;
+}
+
 hipError_t kkt_launch(const KktArgs &a, hipStream_t s)
 {
     // block-size maxima from the structure (host copy in a.hmeta)

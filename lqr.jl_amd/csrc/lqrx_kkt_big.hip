@@ -1,0 +1,950 @@
+// lqrx_kkt_big.hip — block-tridiagonal KKT solve for large blocks (any structure with every
+// block dimension ≤ 64, padded Y rows ≤ 128, w ≤ 128), fp64 and fp32, on MFMA tiles.
+//
+// Reference: CholeskySolver._solve! (/root/reference/src/cholesky_solver.jl:166-182) =
+//   calculate_shur_factors!  jacobian_blocks.jl:220-286   (shur! :231-242, copy_shur! :249-286)
+//   cholesky!(chol, shur)    cholesky_solve.jl:47-67       (block upper Cholesky, LAPACK potrf/trsm)
+//   forward_substitution!    cholesky_solve.jl:93-117
+//   backward_substitution!   cholesky_solve.jl:119-143
+//   calculate_primals!       cholesky_solver.jl:185-236
+// with the diagonal BlockCholesky mode (block_cholesky.jl:82-91) and the SOC variant
+// (Ginv = false, :254-273).  The reference handles any block size through LAPACK; the
+// compile-time-shaped lane kernels (lqrx_kkt_fil.hip) stop at a few rows.
+//
+// Two kernels, one 256-thread workgroup (4 waves) per trajectory:
+//
+// kkt_big_fwd_kernel — the forward sweep.  At step k the workgroup
+//   (1) forms the Schur pieces of knot k+1, YYt = Y H⁻¹ Yᵀ (upper 16×16 tiles only, on
+//       v_mfma_{f32,f64}_16x16x4 with operands from a 16-column LDS slab of Y_{k+1} that the
+//       256 threads stream in coalesced, one slab prefetched in registers ahead) and
+//       r = Y H⁻¹ g; the A ≡ previous-C alias of copy_shur! (:166) is an add into C_k, the
+//       `d .+= r_[1]` of :251 an add into d_k;
+//   (2) factors knot k with explicit inverses of the diagonal factors, so every triangular
+//       solve of the reference becomes an MFMA product:
+//          D̃ = Ã⁻ᵀD, F̃ = Ã⁻ᵀF              (Ã⁻¹ = W_{k−1}, kept in LDS)       :49, :57
+//          B̃ = chol(B − D̃ᵀD̃), Binv = B̃⁻¹                                     :50-53
+//          Ẽ = B̃⁻ᵀ(E − D̃ᵀF̃)                                                  :59-60
+//          C̃ = chol(C − F̃ᵀF̃ − ẼᵀẼ), W_k = C̃⁻¹                                 :61-62
+//       chol+inverse is blocked by 16: a 16×16 leaf (potrf + triangular inverse in one
+//       wave's registers, the pivot test → info), panel and trailing updates on MFMA, the
+//       off-diagonal inverse blocks assembled on MFMA;
+//   (3) runs the forward substitution (:93-117) with the inverses, and stores Binv, Ẽ, W_k
+//       (packed upper triangles) and the forward μ, λ in a per-trajectory slab;
+//   (4) writes knot k+1's Schur tiles (held in registers across (2)-(3)) into LDS.
+//
+// kkt_big_bwd_kernel — backward substitution (:119-143) fused with primal recovery
+//   (cholesky_solver.jl:185-236), k = N−1 … 0, Y_k staged in LDS (coalesced), GEMVs only:
+//   the reference's D̃_{k+1}μ_{k+1} + F̃_{k+1}λ_{k+1} = W_kᵀ·(D2 H⁻¹ t), t = [C; D1]ᵀ[μ; λ]
+//   of knot k+1 — the same t that knot k+1's residual needs (no F̃ in the slab, no matrix
+//   recompute);  λ_k = W_k(λ_k + ·), μ_k = Binv(μ_k − Ẽλ_k), negated;
+//   δz = −H⁻¹(D1ᵀλ_k + Cᵀμ_k + D2ᵀλ_{k−1} + g).
+//
+// Everything is padded to 16 per block (zero rows, identity on padded pivots) so tiles never
+// straddle block boundaries; the arithmetic on padding adds exact zeros.
+#include "lqrx_internal.h"
+#include "lqrx_tile.h"
+#include <algorithm>
+#include <cstdlib>
+
+namespace lqrx {
+namespace {
+
+constexpr int KB_THREADS = 256;
+constexpr int KB_PMAX = 64;    // n1, p, n2 per knot
+constexpr int KB_RMAX = 128;   // padded rows P1 + Ps + P2
+constexpr int KB_WMAX = 128;   // width
+constexpr int KB_MAXT = 9;     // Schur tiles per wave: 36 upper tiles of an 8×8 grid / 4 waves
+constexpr int KB_F1T = 8;      // factor-phase tiles per wave (D̃ + F̃: 2·16 tiles / 4 waves)
+constexpr int KB_LDY = 144;    // Y-slab column stride: ≥ 128 rows, ≡ 16 (mod 64) floats / (mod 32) doubles
+
+__host__ __device__ __forceinline__ int r16(int x) { return (x + 15) & ~15; }
+
+template <typename T> using acc_t = typename Tile<T>::acc;
+
+__device__ __forceinline__ double rcp_full(double a) { return rcp_nr2(a); }
+__device__ __forceinline__ float rcp_full(float a) { return rcp_nr(a); }
+
+// per-knot block sizes (actual and padded) and packed-input offsets (meta table, lqrx_api.cpp)
+struct Kn {
+    int p1, ps, p2, w, rows;
+    int P1, Ps, P2, R, nsl;
+    int oY, oy, oH, og;
+};
+__device__ __forceinline__ Kn kn_load(const int32_t *__restrict__ meta, int k)
+{
+    const int32_t *m = meta + 8 * k;
+    Kn q;
+    q.p1 = m[0]; q.ps = m[1]; q.p2 = m[2]; q.w = m[3];
+    q.oY = m[4]; q.oy = m[5]; q.oH = m[6]; q.og = m[7];
+    q.rows = q.p1 + q.ps + q.p2;
+    q.P1 = r16(q.p1); q.Ps = r16(q.ps); q.P2 = r16(q.p2);
+    q.R = q.P1 + q.Ps + q.P2;
+    q.nsl = (q.w + 15) >> 4;
+    return q;
+}
+
+// slab of one knot: [W packed P2(P2+1)/2][Binv packed Ps(Ps+1)/2][Ẽ Ps×P2][μ Ps][λ P2]
+__host__ __device__ __forceinline__ int64_t slab_size(int Ps, int P2)
+{
+    return (int64_t)P2 * (P2 + 1) / 2 + (int64_t)Ps * (Ps + 1) / 2 + (int64_t)Ps * P2 + Ps + P2;
+}
+
+// LDS offsets of knot k's Schur blocks (leading dimension LD): C, F, E, B, D in that order,
+// present blocks only (host: kb_lds_layout takes the max over knots)
+struct Bo {
+    int C, F, E, B, D, end;
+};
+__host__ __device__ __forceinline__ Bo blk_off(int P1, int Ps, int P2, int LD)
+{
+    Bo o;
+    int x = 0;
+    o.C = x; x += P2 ? LD * P2 : 0;
+    o.F = x; x += (P1 && P2) ? LD * P2 : 0;
+    o.E = x; x += (Ps && P2) ? LD * P2 : 0;
+    o.B = x; x += Ps ? LD * Ps : 0;
+    o.D = x; x += (P1 && Ps) ? LD * Ps : 0;
+    o.end = x;
+    return o;
+}
+
+// ---------------------------------------------------------------- tile primitives (LDS)
+// c (+/−)= op(A)·op(B) for one 16×16 output tile over K (multiple of 16) contraction indices.
+// op(A)[i][k] = TA ? A[k + i·lda] : A[i + k·lda];  op(B)[k][j] = TB ? B[j + k·ldb] : B[k + j·ldb]
+template <typename T, bool TA, bool TB, bool NEG>
+__device__ __forceinline__ acc_t<T> tmm(acc_t<T> c, const T *A, int lda, const T *B, int ldb, int K, int lane)
+{
+    const int i = lane & 15, g = lane >> 4;
+    const T *pa = TA ? A + g + i * lda : A + i + g * lda;
+    const T *pb = TB ? B + i + g * ldb : B + g + i * ldb;
+    const int sa = TA ? 4 : 4 * lda, sb = TB ? 4 * ldb : 4;
+    for (int k0 = 0; k0 < K; k0 += 16) {
+        T a[4], b[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            a[s] = pa[s * sa];
+            b[s] = pb[s * sb];
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) c = NEG ? Tile<T>::mma_nega(a[s], b[s], c) : Tile<T>::mma(a[s], b[s], c);
+        pa += 4 * sa;
+        pb += 4 * sb;
+    }
+    return c;
+}
+
+template <typename T>
+__device__ __forceinline__ acc_t<T> tload(const T *X, int ld, int lane)
+{
+    acc_t<T> c;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) c[r] = X[Tile<T>::row(lane, r) + (lane & 15) * ld];
+    return c;
+}
+template <typename T>
+__device__ __forceinline__ void tstore(T *X, int ld, acc_t<T> c, int lane)
+{
+#pragma unroll
+    for (int r = 0; r < 4; ++r) X[Tile<T>::row(lane, r) + (lane & 15) * ld] = c[r];
+}
+template <typename T>
+__device__ __forceinline__ void tadd(T *X, int ld, acc_t<T> c, int lane)
+{
+#pragma unroll
+    for (int r = 0; r < 4; ++r) X[Tile<T>::row(lane, r) + (lane & 15) * ld] += c[r];
+}
+template <typename T> __device__ __forceinline__ acc_t<T> tzero() { return acc_t<T>{0, 0, 0, 0}; }
+
+// c (+/−)= A·M with M a C-layout register tile used as the B operand (register r = k-slice
+// r, k = Tile<T>::row(lane, r)) and A[i][k] read from LDS (column-major, ld).
+template <typename T, bool NEG>
+__device__ __forceinline__ acc_t<T> tmm_reg(acc_t<T> c, const T *A, int ld, acc_t<T> M, int lane)
+{
+    const int i = lane & 15;
+    T a[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a[r] = A[i + Tile<T>::row(lane, r) * ld];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) c = NEG ? Tile<T>::mma_nega(a[r], M[r], c) : Tile<T>::mma(a[r], M[r], c);
+    return c;
+}
+
+// ---------------------------------------------------------------- 16×16 leaf (one wave)
+// In place: X (upper triangle of an SPD 16×16 block, column-major, ld) → T = U⁻¹ with
+// UᵀU = X (upper, strictly-lower part zeroed).  Lane c (< 16) holds column c in registers;
+// pivot i broadcasts row i of U by v_readlane (uniform lane and register indices).  q = the
+// block's real pivots; pivots ≥ q are identity padding.  Returns 1 + the first pivot that is
+// not positive (potrf's info), else 0.  Mirrors dpotf2 'U' (dynamic_programming.jl:29,
+// cholesky_solve.jl:2) up to the rsqrt-multiply instead of sqrt-divide.
+template <typename T>
+__device__ int leaf_chol_inv(T *X, int ld, int q, int lane)
+{
+    const int c = lane & 15;
+    T col[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) col[r] = X[r + c * ld];
+    int bad = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const T d = readlane(col[i], i);
+        if (!(d > (T)0) && i < q && !bad) bad = i + 1;
+        const T s = rsqrt_nr(d);
+        col[i] = c >= i ? col[i] * s : (T)0;
+#pragma unroll
+        for (int r = i + 1; r < 16; ++r) col[r] = fma(-readlane(col[i], r), col[i], col[r]);
+    }
+    // T = U⁻¹, column c: for k = 15 … 0, T[k][c] = (δ_kc − Σ_{j>k} U[k][j] T[j][c]) / U[k][k]
+    T t[16];
+#pragma unroll
+    for (int k = 15; k >= 0; --k) {
+        T acc = c == k ? (T)1 : (T)0;
+#pragma unroll
+        for (int j = k + 1; j < 16; ++j) acc = fma(-readlane(col[k], j), t[j], acc);
+        t[k] = acc * rcp_full(readlane(col[k], k));
+    }
+    if (lane < 16) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) X[r + c * ld] = t[r];
+    }
+    return bad;
+}
+
+// ---------------------------------------------------------------- blocked chol + inverse
+// In place on the LDS image X (leading dimension LD, upper 16×16 tiles of a P×P SPD matrix
+// whose real size is p; P = 16·nb, nb ≤ 4): X ← U⁻¹ with UᵀU = X (upper tiles; diagonal tiles
+// have a zero strictly-lower part).  Right-looking by 16: leaf (wave 0) → panel
+// U_{jb,J} = T_jjᵀ X_{jb,J} → trailing X_IJ −= U_{jb,I}ᵀ U_{jb,J} (MFMA, waves round-robin);
+// then W_IJ = −T_I Σ_{L=I+1..J} U_IL W_LJ, column J by wave J−1, every U read before any
+// write.  Returns 0, or 1 + the first non-positive pivot (all threads).
+template <typename T>
+__device__ int chol_inv(T *X, int LD, int p, int P, int *flag, int tid)
+{
+    const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), nb = P >> 4;
+    for (int i = p + tid; i < P; i += KB_THREADS) X[i + i * LD] = (T)1;   // identity padding
+    if (tid == 0) *flag = 0;
+    __syncthreads();
+    for (int jb = 0; jb < nb; ++jb) {
+        T *Xjj = X + 16 * jb * (1 + LD);
+        if (wave == 0) {
+            const int bad = leaf_chol_inv<T>(Xjj, LD, min(16, p - 16 * jb), lane);
+            if (lane == 0 && bad && !*flag) *flag = 16 * jb + bad;
+        }
+        __syncthreads();
+        if (jb + 1 < nb) {
+            for (int J = jb + 1 + wave; J < nb; J += 4) {
+                T *Xj = X + 16 * jb + 16 * J * LD;
+                const acc_t<T> c = tmm<T, true, false, false>(tzero<T>(), Xjj, LD, Xj, LD, 16, lane);
+                tstore(Xj, LD, c, lane);
+            }
+            __syncthreads();
+            const int m = nb - jb - 1;
+            for (int qq = wave; qq < m * (m + 1) / 2; qq += 4) {
+                int I = 0, rem = qq;
+                while (rem >= m - I) {
+                    rem -= m - I;
+                    ++I;
+                }
+                const int gI = jb + 1 + I, gJ = gI + rem;
+                T *Xij = X + 16 * gI + 16 * gJ * LD;
+                acc_t<T> c = tload(Xij, LD, lane);
+                c = tmm<T, true, false, true>(c, X + 16 * jb + 16 * gI * LD, LD, X + 16 * jb + 16 * gJ * LD, LD, 16,
+                                              lane);
+                tstore(Xij, LD, c, lane);
+            }
+            __syncthreads();
+        }
+    }
+    if (nb > 1) {
+        const int J = wave + 1;
+        acc_t<T> w0 = tzero<T>(), w1 = tzero<T>(), w2 = tzero<T>();
+        if (J < nb) {
+            const T *TJ = X + 16 * J * (1 + LD);
+#pragma unroll
+            for (int I = 2; I >= 0; --I) {
+                if (I < J) {
+                    acc_t<T> s = tmm<T, false, false, false>(tzero<T>(), X + 16 * I + 16 * J * LD, LD, TJ, LD, 16, lane);
+                    if (I + 1 <= 1 && 1 < J) s = tmm_reg<T, false>(s, X + 16 * I + 16 * 1 * LD, LD, w1, lane);
+                    if (I + 1 <= 2 && 2 < J) s = tmm_reg<T, false>(s, X + 16 * I + 16 * 2 * LD, LD, w2, lane);
+                    const acc_t<T> r = tmm_reg<T, true>(tzero<T>(), X + 16 * I * (1 + LD), LD, s, lane);
+                    if (I == 0) w0 = r;
+                    else if (I == 1) w1 = r;
+                    else w2 = r;
+                }
+            }
+        }
+        __syncthreads();
+        if (J < nb) {
+            tstore(X + 16 * J * LD, LD, w0, lane);
+            if (J > 1) tstore(X + 16 + 16 * J * LD, LD, w1, lane);
+            if (J > 2) tstore(X + 32 + 16 * J * LD, LD, w2, lane);
+        }
+    }
+    __syncthreads();
+    return *flag;
+}
+
+// out[i] = init[i] (±) Σ_{k<K(i)} M[k + i·ld]·x[k] for i < n (column dots), 4 threads per
+// output; TRI: K(i) = min(K, i + 1) (upper-triangular M, i.e. Mᵀx); n ≤ 64.
+template <typename T, bool TRI, bool NEG>
+__device__ __forceinline__ void coldot(T *out, const T *init, const T *M, int ld, const T *x, int K, int n, int tid)
+{
+    const int i = tid >> 2, part = tid & 3;
+    T s = (T)0;
+    if (i < n) {
+        const int Ki = TRI ? min(K, i + 1) : K;
+        for (int k = part; k < Ki; k += 4) s = fma(M[k + i * ld], x[k], s);
+    }
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    if (i < n && part == 0) out[i] = init ? (NEG ? init[i] - s : init[i] + s) : (NEG ? -s : s);
+}
+
+template <typename T>
+struct KbArgs {
+    const T *Y, *y, *H, *g;
+    T *dz, *lam, *slab;
+    int32_t *info;
+    const int32_t *meta;
+    int N, ginv;
+    int64_t b0;                    // first trajectory of this chunk
+    int64_t sY, sy, sH, sg, sS;    // per-trajectory strides (elements); sS: slab
+    int LD, LDY, LDB;              // LDS leading dims: blocks, Y slab (fwd), staged Y (bwd)
+    int oWp, oBlk, oSl, oV;        // fwd LDS offsets (elements of T)
+    int oYl, oWl, oV2;             // bwd LDS offsets
+};
+
+// padded row → row of Y (−1 for a padding row)
+__device__ __forceinline__ int rowmap(const Kn &q, int pr)
+{
+    if (pr < q.P1) return pr < q.p1 ? pr : -1;
+    pr -= q.P1;
+    if (pr < q.Ps) return pr < q.ps ? q.p1 + pr : -1;
+    pr -= q.Ps;
+    return pr < q.p2 ? q.p1 + q.ps + pr : -1;
+}
+__device__ __forceinline__ int part_of(const Kn &q, int I)
+{
+    const int r = 16 * I;
+    return r < q.P1 ? 0 : (r < q.P1 + q.Ps ? 1 : 2);
+}
+
+// ---------------------------------------------------------------- forward sweep
+template <typename T>
+__global__ void __launch_bounds__(KB_THREADS, sizeof(T) == 4 ? 2 : 1) kkt_big_fwd_kernel(KbArgs<T> a)
+{
+    extern __shared__ __align__(16) unsigned char kb_lds_raw[];
+    T *lds = (T *)kb_lds_raw;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g4 = lane >> 4,
+              i16 = lane & 15;
+    const int64_t t = a.b0 + blockIdx.x;
+    const int LD = a.LD;
+    constexpr int LDY = KB_LDY;
+    T *Wp = lds + a.oWp, *blk = lds + a.oBlk, *sl = lds + a.oSl, *hs = sl + 16 * LDY, *gs = hs + 16;
+    T *vc = lds + a.oV, *vd = vc + 64, *vlp = vd + 64, *vmu = vlp + 64, *vla = vmu + 64, *vt1 = vla + 64,
+      *vt2 = vt1 + 64, *rn = vt2 + 64;
+    int *flag = (int *)(rn + KB_RMAX);
+    const T *Yt = a.Y + t * a.sY, *yt = a.y + t * a.sy, *Ht = a.H + t * a.sH, *gt = a.g + t * a.sg;
+    T *St = a.slab + (int64_t)blockIdx.x * a.sS;
+    const int N = a.N;
+    int info = 0;
+    int64_t oS = 0;
+
+    // ---- Y slab pipeline: 16 columns × R padded rows, prefetched into registers.  Thread
+    // (c = tid/16, i = tid%16) moves column c, rows i + 16v: each 16-row block lies in one
+    // partition (the padding is per block), so its source row base is uniform.
+    T pre[KB_RMAX / 16];
+    T preh = (T)0, preg = (T)0;
+    const int scol = tid >> 4;
+    auto fetch = [&](const Kn &q, int s) {
+        const int c = 16 * s + scol;
+        const T *src = Yt + q.oY + (int64_t)c * q.rows + i16;
+        const bool cok = c < q.w;
+#pragma unroll
+        for (int v = 0; v < KB_RMAX / 16; ++v) {
+            T x = (T)0;
+            if (16 * v < q.R) {
+                const int r0 = 16 * v;
+                int rb, lim;
+                if (r0 < q.P1) {
+                    rb = r0; lim = q.p1 - r0;
+                } else if (r0 < q.P1 + q.Ps) {
+                    rb = q.p1 + r0 - q.P1; lim = q.ps - (r0 - q.P1);
+                } else {
+                    rb = q.p1 + q.ps + r0 - q.P1 - q.Ps; lim = q.p2 - (r0 - q.P1 - q.Ps);
+                }
+                if (cok && i16 < lim) x = src[rb];
+            }
+            pre[v] = x;
+        }
+        if (tid < 16) {
+            const int cc = 16 * s + tid;
+            preh = cc < q.w ? (a.ginv ? (T)1 / Ht[q.oH + cc] : (T)1) : (T)0;
+            preg = (cc < q.w && a.ginv) ? gt[q.og + cc] : (T)0;
+        }
+    };
+    auto commit = [&](const Kn &q) {
+#pragma unroll
+        for (int v = 0; v < KB_RMAX / 16; ++v)
+            if (16 * v < q.R) sl[16 * v + i16 + scol * LDY] = pre[v];
+        if (tid < 16) {
+            hs[tid] = preh;
+            gs[tid] = preg;
+        }
+    };
+
+    // ---- Schur pieces of knot q (shur!, jacobian_blocks.jl:231-242): upper tiles of
+    // Y H⁻¹ Yᵀ into acc (tile qq = wave + 4·slot of the padded grid), r = Y H⁻¹ g into rn
+    acc_t<T> acc[KB_MAXT];
+    int tI[KB_MAXT], tJ[KB_MAXT];
+    auto schur = [&](const Kn &q, bool has_next, const Kn &qn) {
+        const int nbt = q.R >> 4, ntile = nbt * (nbt + 1) / 2;
+#pragma unroll
+        for (int s = 0; s < KB_MAXT; ++s) {
+            int qq = wave + 4 * s, I = 0;
+            if (qq < ntile)
+                while (qq >= nbt - I) {
+                    qq -= nbt - I;
+                    ++I;
+                }
+            tI[s] = I;
+            tJ[s] = I + qq;
+            acc[s] = tzero<T>();
+        }
+        if (tid < q.R) rn[tid] = (T)0;
+        for (int s = 0; s < q.nsl; ++s) {
+            __syncthreads();
+            commit(q);
+            __syncthreads();
+            if (s + 1 < q.nsl) fetch(q, s + 1);
+            else if (has_next) fetch(qn, 0);
+            if (tid < q.R) {
+                T v = rn[tid];
+#pragma unroll
+                for (int c = 0; c < 16; ++c) v = fma(sl[tid + c * LDY] * hs[c], gs[c], v);
+                rn[tid] = v;
+            }
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const int kc = 4 * kk + g4;
+                const T h = hs[kc];
+                const T *col = sl + kc * LDY + i16;
+#pragma unroll
+                for (int s2 = 0; s2 < KB_MAXT; ++s2) {
+                    if (wave + 4 * s2 < ntile) {
+                        const T av = col[16 * tI[s2]];
+                        const T bv = col[16 * tJ[s2]] * h;
+                        acc[s2] = Tile<T>::mma(av, bv, acc[s2]);
+                    }
+                }
+            }
+        }
+    };
+    // knot q's non-alias Schur tiles (copy_shur!, :271-286) → LDS blocks; c, d = r − y
+    auto store_schur = [&](const Kn &q) {
+        const Bo b = blk_off(q.P1, q.Ps, q.P2, LD);
+        const int nbt = q.R >> 4, ntile = nbt * (nbt + 1) / 2;
+#pragma unroll
+        for (int s = 0; s < KB_MAXT; ++s) {
+            if (wave + 4 * s >= ntile) continue;
+            const int pi = part_of(q, tI[s]), pj = part_of(q, tJ[s]);
+            if (pi == 0 && pj == 0) continue;                               // A: added into C_{k−1}
+            const int li = 16 * tI[s] - (pi == 0 ? 0 : pi == 1 ? q.P1 : q.P1 + q.Ps);
+            const int lj = 16 * tJ[s] - (pj == 0 ? 0 : pj == 1 ? q.P1 : q.P1 + q.Ps);
+            const int o = pi == 0 ? (pj == 1 ? b.D : b.F) : pi == 1 ? (pj == 1 ? b.B : b.E) : b.C;
+            tstore(blk + o + li + lj * LD, LD, acc[s], lane);
+        }
+        if (tid < 64) {
+            vc[tid] = tid < q.ps ? rn[q.P1 + tid] - yt[q.oy + tid] : (T)0;
+            vd[tid] = tid < q.p2 ? rn[q.P1 + q.Ps + tid] - yt[q.oy + q.ps + tid] : (T)0;
+        }
+    };
+
+    Kn q0 = kn_load(a.meta, 0);
+    const Kn q1first = N > 1 ? kn_load(a.meta, 1) : q0;
+    if (tid < 64) vlp[tid] = (T)0;
+    fetch(q0, 0);
+    schur(q0, N > 1, q1first);
+    __syncthreads();
+    store_schur(q0);
+
+    for (int k = 0; k < N; ++k) {
+        const Bo b0 = blk_off(q0.P1, q0.Ps, q0.P2, LD);
+        const bool nxt = k + 1 < N;
+        Kn q1 = nxt ? kn_load(a.meta, k + 1) : q0;
+        if (nxt) {
+            const bool nn = k + 2 < N;
+            const Kn q2 = nn ? kn_load(a.meta, k + 2) : q1;
+            schur(q1, nn, q2);
+            // A ≡ C_k alias (:166): knot k+1's D2 H⁻¹ D2ᵀ adds into C_k; d_k .+= r_[1] (:251)
+#pragma unroll
+            for (int s = 0; s < KB_MAXT; ++s) {
+                if (wave + 4 * s < (q1.R >> 4) * ((q1.R >> 4) + 1) / 2 && 16 * tJ[s] < q1.P1)
+                    tadd(blk + b0.C + 16 * tI[s] + 16 * tJ[s] * LD, LD, acc[s], lane);
+            }
+            if (tid < q1.p1) vd[tid] += rn[tid];
+        }
+        __syncthreads();
+
+        // ---- cholesky!(U, F) for knot k (cholesky_solve.jl:47-67)
+        const int n1t = q0.P1 >> 4, nst = q0.Ps >> 4, n2t = q0.P2 >> 4;
+        if (q0.P1) {
+            // D̃ = Ã⁻ᵀD (:49), F̃ = Ã⁻ᵀF (:57) with Ã⁻¹ = W_{k−1} (upper): in place over D, F
+            const int nD = n1t * nst, nF = n1t * n2t;
+            acc_t<T> f1[KB_F1T];
+#pragma unroll
+            for (int s = 0; s < KB_F1T; ++s) {
+                const int qq = wave + 4 * s;
+                if (qq < nD + nF) {
+                    const bool isD = qq < nD;
+                    const int r = isD ? qq : qq - nD, nc = isD ? nst : n2t, I = r / nc, J = r - I * nc;
+                    f1[s] = tmm<T, true, false, false>(tzero<T>(), Wp + 16 * I * LD, LD,
+                                                       blk + (isD ? b0.D : b0.F) + 16 * J * LD, LD, 16 * (I + 1), lane);
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int s = 0; s < KB_F1T; ++s) {
+                const int qq = wave + 4 * s;
+                if (qq < nD + nF) {
+                    const bool isD = qq < nD;
+                    const int r = isD ? qq : qq - nD, nc = isD ? nst : n2t, I = r / nc, J = r - I * nc;
+                    tstore(blk + (isD ? b0.D : b0.F) + 16 * I + 16 * J * LD, LD, f1[s], lane);
+                }
+            }
+            __syncthreads();
+            // B −= D̃ᵀD̃ (:50-52), E −= D̃ᵀF̃ (:59), C −= F̃ᵀF̃ (:61): upper tiles of B and C
+            const int nB = nst * (nst + 1) / 2, nE = nst * n2t, nC = n2t * (n2t + 1) / 2;
+            for (int qq = wave; qq < nB + nE + nC; qq += 4) {
+                int I, J, o;
+                const T *Aop, *Bop;
+                if (qq < nB || qq >= nB + nE) {
+                    const bool isB = qq < nB;
+                    const int m = isB ? nst : n2t;
+                    int rem = isB ? qq : qq - nB - nE;
+                    I = 0;
+                    while (rem >= m - I) {
+                        rem -= m - I;
+                        ++I;
+                    }
+                    J = I + rem;
+                    o = isB ? b0.B : b0.C;
+                    Aop = blk + (isB ? b0.D : b0.F);
+                    Bop = Aop;
+                } else {
+                    const int r = qq - nB;
+                    I = r / n2t;
+                    J = r - I * n2t;
+                    o = b0.E;
+                    Aop = blk + b0.D;
+                    Bop = blk + b0.F;
+                }
+                T *X = blk + o + 16 * I + 16 * J * LD;
+                acc_t<T> c = tload(X, LD, lane);
+                c = tmm<T, true, false, true>(c, Aop + 16 * I * LD, LD, Bop + 16 * J * LD, LD, q0.P1, lane);
+                tstore(X, LD, c, lane);
+            }
+            __syncthreads();
+        }
+        if (q0.ps) {
+            // B̃ = chol(B) (:53) → Binv = B̃⁻¹ in place
+            const int bad = chol_inv<T>(blk + b0.B, LD, q0.ps, q0.Ps, flag, tid);
+            if (bad && !info) info = k + 1;
+            if (q0.P2) {
+                // Ẽ = B̃⁻ᵀE (:60), in place
+                acc_t<T> f1[4];
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const int qq = wave + 4 * s;
+                    if (qq < nst * n2t) {
+                        const int I = qq / n2t, J = qq - I * n2t;
+                        f1[s] = tmm<T, true, false, false>(tzero<T>(), blk + b0.B + 16 * I * LD, LD,
+                                                           blk + b0.E + 16 * J * LD, LD, 16 * (I + 1), lane);
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const int qq = wave + 4 * s;
+                    if (qq < nst * n2t) {
+                        const int I = qq / n2t, J = qq - I * n2t;
+                        tstore(blk + b0.E + 16 * I + 16 * J * LD, LD, f1[s], lane);
+                    }
+                }
+                __syncthreads();
+                // C −= ẼᵀẼ (:61)
+                for (int qq = wave; qq < n2t * (n2t + 1) / 2; qq += 4) {
+                    int I = 0, rem = qq;
+                    while (rem >= n2t - I) {
+                        rem -= n2t - I;
+                        ++I;
+                    }
+                    const int J = I + rem;
+                    T *X = blk + b0.C + 16 * I + 16 * J * LD;
+                    acc_t<T> c = tload(X, LD, lane);
+                    c = tmm<T, true, false, true>(c, blk + b0.E + 16 * I * LD, LD, blk + b0.E + 16 * J * LD, LD, q0.Ps,
+                                                  lane);
+                    tstore(X, LD, c, lane);
+                }
+                __syncthreads();
+            }
+        }
+        if (q0.p2) {
+            // C̃ = chol(C) (:62) → W_k = C̃⁻¹ in place
+            const int bad = chol_inv<T>(blk + b0.C, LD, q0.p2, q0.P2, flag, tid);
+            if (bad && !info) info = k + 1;
+        }
+        // ---- forward_substitution! (:93-117): μ = B̃⁻ᵀ(c − D̃ᵀλ_{k−1}), λ = C̃⁻ᵀ(d − F̃ᵀλ_{k−1} − Ẽᵀμ)
+        if (q0.ps) {
+            if (q0.P1) {
+                coldot<T, false, true>(vt1, vc, blk + b0.D, LD, vlp, q0.P1, q0.Ps, tid);
+                __syncthreads();
+            } else if (tid < 64) {
+                vt1[tid] = vc[tid];
+            }
+            __syncthreads();
+            coldot<T, true, false>(vmu, nullptr, blk + b0.B, LD, vt1, q0.Ps, q0.Ps, tid);
+            __syncthreads();
+        }
+        if (q0.p2) {
+            if (q0.P1) {
+                coldot<T, false, true>(vt2, vd, blk + b0.F, LD, vlp, q0.P1, q0.P2, tid);
+                __syncthreads();
+            } else if (tid < 64) {
+                vt2[tid] = vd[tid];
+            }
+            __syncthreads();
+            if (q0.ps) {
+                coldot<T, false, true>(vt2, vt2, blk + b0.E, LD, vmu, q0.Ps, q0.P2, tid);
+                __syncthreads();
+            }
+            coldot<T, true, false>(vla, nullptr, blk + b0.C, LD, vt2, q0.P2, q0.P2, tid);
+            __syncthreads();
+        }
+        // ---- slab: W_k, Binv (packed upper), Ẽ, μ, λ of the forward sweep
+        {
+            T *Sk = St + oS;
+            const int oB = q0.P2 * (q0.P2 + 1) / 2, oE = oB + q0.Ps * (q0.Ps + 1) / 2, oM = oE + q0.Ps * q0.P2;
+            for (int j = wave; j < q0.P2; j += 4)
+                if (lane <= j) Sk[j * (j + 1) / 2 + lane] = blk[b0.C + lane + j * LD];
+            for (int j = wave; j < q0.Ps; j += 4)
+                if (lane <= j) Sk[oB + j * (j + 1) / 2 + lane] = blk[b0.B + lane + j * LD];
+            if (q0.Ps && q0.P2)
+                for (int j = wave; j < q0.P2; j += 4)
+                    if (lane < q0.Ps) Sk[oE + lane + j * q0.Ps] = blk[b0.E + lane + j * LD];
+            if (tid < q0.Ps) Sk[oM + tid] = vmu[tid];
+            if (tid < q0.P2) Sk[oM + q0.Ps + tid] = vla[tid];
+            oS += slab_size(q0.Ps, q0.P2);
+            // W_k becomes Ã⁻¹ of knot k+1 (U[k+1].A ≡ U[k].C, :166); λ_k its λ_{k−1}
+            for (int e = tid; e < q0.P2 * q0.P2; e += KB_THREADS) {
+                const int j = e / q0.P2, i = e - j * q0.P2;
+                Wp[i + j * LD] = blk[b0.C + i + j * LD];
+            }
+            if (tid < 64) vlp[tid] = tid < q0.P2 ? vla[tid] : (T)0;
+        }
+        __syncthreads();
+        if (nxt) {
+            store_schur(q1);
+            __syncthreads();
+        }
+        q0 = q1;
+    }
+    if (tid == 0 && a.info) a.info[t] = info;
+}
+
+// ---------------------------------------------------------------- backward sweep + primals
+template <typename T>
+__global__ void __launch_bounds__(KB_THREADS) kkt_big_bwd_kernel(KbArgs<T> a)
+{
+    extern __shared__ __align__(16) unsigned char kb_lds_raw[];
+    T *lds = (T *)kb_lds_raw;
+    const int tid = threadIdx.x;
+    const int64_t t = a.b0 + blockIdx.x;
+    const int LDB = a.LDB, N = a.N;
+    T *Yl = lds + a.oYl, *Wl = lds + a.oWl;
+    const T *Bl = nullptr, *El = nullptr;   // Binv, Ẽ: read from the slab (end knots only)
+    T *xm = lds + a.oV2, *xl = xm + 64, *tv = xl + 64, *hv = tv + KB_WMAX, *gv = hv + KB_WMAX, *vv = gv + KB_WMAX,
+      *zv = vv + 64, *nl = zv + 64, *ev = nl + 64, *nm = ev + 64, *fm = nm + 64, *fl = fm + 64;
+    const T *Yt = a.Y + t * a.sY, *Ht = a.H + t * a.sH, *gt = a.g + t * a.sg;
+    T *dzt = a.dz + t * a.sg, *lat = a.lam + t * a.sy;
+    const T *St = a.slab + (int64_t)blockIdx.x * a.sS;
+
+    int64_t oS = 0;
+    for (int k = 0; k < N; ++k) {
+        const int32_t *m = a.meta + 8 * k;
+        oS += slab_size(r16(m[1]), r16(m[2]));
+    }
+    // stage knot k's slab (W packed, Binv packed, Ẽ, μ, λ of the forward sweep) into LDS
+    auto stage_slab = [&](const Kn &q, int64_t o) {
+        const T *Sk = St + o;
+        const int nW = q.P2 * (q.P2 + 1) / 2, nBv = q.Ps * (q.Ps + 1) / 2, nE = q.Ps * q.P2;
+        for (int e = tid; e < nW; e += KB_THREADS) Wl[e] = Sk[e];
+        Bl = Sk + nW;
+        El = Sk + nW + nBv;
+        if (tid < 64) {
+            fm[tid] = tid < q.Ps ? Sk[nW + nBv + nE + tid] : (T)0;
+            fl[tid] = tid < q.P2 ? Sk[nW + nBv + nE + q.Ps + tid] : (T)0;
+        }
+    };
+    // x ← B̃⁻¹ x for packed upper Binv (row dots): out[i] = Σ_{c ≥ i} U⁻¹[i][c] x[c]
+    auto rowdot_packed = [&](T *out, const T *P, const T *x, int n) {
+        const int i = tid >> 2, part = tid & 3;
+        T s = (T)0;
+        if (i < n)
+            for (int c = i + part; c < n; c += 4) s = fma(P[c * (c + 1) / 2 + i], x[c], s);
+        s += __shfl_xor(s, 1);
+        s += __shfl_xor(s, 2);
+        if (i < n && part == 0) out[i] = s;
+    };
+
+    // terminal knot (backward_substitution! :139-143): μ_N = −B̃⁻¹μ, λ_N as the forward gave it
+    Kn qj = kn_load(a.meta, N - 1);
+    oS -= slab_size(qj.Ps, qj.P2);
+    stage_slab(qj, oS);
+    __syncthreads();
+    if (qj.ps) rowdot_packed(nm, Bl, fm, qj.ps);
+    __syncthreads();
+    if (tid < 64) {
+        xm[tid] = tid < qj.ps ? -nm[tid] : (T)0;
+        xl[tid] = tid < qj.p2 ? fl[tid] : (T)0;
+    }
+    __syncthreads();
+    if (tid < qj.ps) lat[qj.oy + tid] = xm[tid];
+    if (tid < qj.p2) lat[qj.oy + qj.ps + tid] = xl[tid];
+
+    for (int j = N - 1; j >= 0; --j) {
+        // stage Y_j (rows × w, column stride LDB), 1/h and g
+        {
+            const int tot = qj.rows * qj.w, sr = KB_THREADS % qj.rows, sc = KB_THREADS / qj.rows;
+            int r = tid % qj.rows, c = tid / qj.rows;
+            for (int e = tid; e < tot; e += KB_THREADS) {
+                Yl[r + c * LDB] = Yt[qj.oY + e];
+                r += sr;
+                c += sc;
+                if (r >= qj.rows) {
+                    r -= qj.rows;
+                    ++c;
+                }
+            }
+            if (tid < qj.w) {
+                hv[tid] = a.ginv ? (T)1 / Ht[qj.oH + tid] : (T)1;
+                gv[tid] = a.ginv ? gt[qj.og + tid] : (T)0;
+            }
+        }
+        Kn qp = qj;
+        if (j > 0) {
+            qp = kn_load(a.meta, j - 1);
+            oS -= slab_size(qp.Ps, qp.P2);
+            stage_slab(qp, oS);
+        }
+        __syncthreads();
+        // t = [C; D1]ᵀ[μ_j; λ_j]  (calc_residual!'s Cᵀμ + D1ᵀλ, :219-231)
+        {
+            const int c = tid >> 1, h = tid & 1;
+            T s = (T)0;
+            if (c < qj.w) {
+                for (int r = qj.p1 + h; r < qj.rows; r += 2) {
+                    const int rr = r - qj.p1;
+                    s = fma(Yl[r + c * LDB], rr < qj.ps ? xm[rr] : xl[rr - qj.ps], s);
+                }
+            }
+            s += __shfl_xor(s, 1);
+            if (c < qj.w && h == 0) tv[c] = s;
+        }
+        __syncthreads();
+        if (j > 0) {
+            // v = D2 H⁻¹ t = D_{k+1}μ_{k+1} + F_{k+1}λ_{k+1} (the Schur blocks of knot j)
+            {
+                const int i = tid >> 2, part = tid & 3;
+                T s = (T)0;
+                if (i < qj.p1)
+                    for (int c = part; c < qj.w; c += 4) s = fma(Yl[i + c * LDB], tv[c] * hv[c], s);
+                s += __shfl_xor(s, 1);
+                s += __shfl_xor(s, 2);
+                if (part == 0 && i < 64) vv[i] = i < qj.p1 ? s : (T)0;
+            }
+            __syncthreads();
+            // λ_{j−1} = C̃⁻¹(λ + C̃⁻ᵀ v) = W(λ + Wᵀv)  (:128-135)
+            {
+                const int i = tid >> 2, part = tid & 3;
+                T s = (T)0;
+                if (i < qp.p2)
+                    for (int kk = part; kk <= i; kk += 4) s = fma(Wl[i * (i + 1) / 2 + kk], vv[kk], s);
+                s += __shfl_xor(s, 1);
+                s += __shfl_xor(s, 2);
+                if (part == 0 && i < 64) zv[i] = i < qp.p2 ? fl[i] + s : (T)0;
+            }
+            __syncthreads();
+            rowdot_packed(nl, Wl, zv, qp.p2);
+            __syncthreads();
+            if (qp.ps) {
+                // μ_{j−1} = B̃⁻¹(μ − Ẽλ)  (:136-137)
+                {
+                    const int i = tid >> 2, part = tid & 3;
+                    T s = (T)0;
+                    if (i < qp.ps)
+                        for (int c = part; c < qp.p2; c += 4) s = fma(El[i + c * qp.Ps], nl[c], s);
+                    s += __shfl_xor(s, 1);
+                    s += __shfl_xor(s, 2);
+                    if (part == 0 && i < qp.ps) ev[i] = fm[i] - s;
+                }
+                __syncthreads();
+                rowdot_packed(nm, Bl, ev, qp.ps);
+                __syncthreads();
+            }
+            // negate (:138) and hand over: x = [μ_{j−1}; λ_{j−1}] for knot j−1
+            if (tid < 64) {
+                xl[tid] = tid < qp.p2 ? -nl[tid] : (T)0;
+                xm[tid] = tid < qp.ps ? -nm[tid] : (T)0;
+            }
+            __syncthreads();
+            if (tid < qp.ps) lat[qp.oy + tid] = xm[tid];
+            if (tid < qp.p2) lat[qp.oy + qp.ps + tid] = xl[tid];
+        }
+        // δz_j = −H⁻¹(t + D2ᵀλ_{j−1} + g)  (calc_residual! + calc_primals!, :195-236)
+        {
+            const int c = tid >> 1, h = tid & 1;
+            T s = (T)0;
+            if (c < qj.w && j > 0)
+                for (int r = h; r < qj.p1; r += 2) s = fma(Yl[r + c * LDB], xl[r], s);
+            s += __shfl_xor(s, 1);
+            if (c < qj.w && h == 0) {
+                const T res = tv[c] + s + gv[c];
+                dzt[qj.og + c] = -(res * hv[c]);
+            }
+        }
+        __syncthreads();
+        qj = qp;
+    }
+}
+
+// ---------------------------------------------------------------- host: plan and launch
+struct KbPlan {
+    int PM, LD, LDY, LDB, maxrows, maxw, blk;
+    int64_t S;                      // slab elements per trajectory
+    int oWp, oBlk, oSl, oV, nf;     // fwd LDS (elements)
+    int oYl, oWl, oV2, nb;          // bwd LDS (elements)
+};
+
+// the big kernels' block limits and LDS plan for this structure; false = not served
+bool kb_plan(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2, const int32_t *w, int tsize,
+             KbPlan &P)
+{
+    if (a.layout != 0 || (a.ginv && a.h_mode != 2) || a.N < 1) return false;
+    int PM = 16, RM = 16, maxrows = 1, maxw = 1, PMW = 0;
+    int64_t S = 0;
+    for (int k = 0; k < a.N; ++k) {
+        if (n1[k] > KB_PMAX || p[k] > KB_PMAX || n2[k] > KB_PMAX || w[k] > KB_WMAX) return false;
+        const int P1 = r16(n1[k]), Ps = r16(p[k]), P2 = r16(n2[k]), R = P1 + Ps + P2;
+        if (R > KB_RMAX) return false;
+        PM = std::max(PM, std::max(P1, std::max(Ps, P2)));
+        RM = std::max(RM, R);
+        maxrows = std::max(maxrows, n1[k] + p[k] + n2[k]);
+        maxw = std::max(maxw, w[k]);
+        PMW = std::max(PMW, P2);
+        S += slab_size(Ps, P2);
+    }
+    // bank-conflict pads (MI355X LDS: 64 banks × 4 B): tile operands read as (lane·ld + group)
+    P.PM = PM;
+    P.LD = PM + 4;
+    P.LDY = KB_LDY;
+    P.LDB = maxrows | 1;
+    P.maxrows = maxrows;
+    P.maxw = maxw;
+    int blk = 0;
+    for (int k = 0; k < a.N; ++k) blk = std::max(blk, blk_off(r16(n1[k]), r16(p[k]), r16(n2[k]), P.LD).end);
+    P.blk = blk;
+    P.S = S;
+    int o = 0;
+    P.oWp = o; o += P.LD * PM;
+    P.oBlk = o; o += blk;
+    P.oSl = o; o += P.LDY * 16 + 32;
+    o = (o + 3) & ~3;
+    P.oV = o; o += 7 * 64 + KB_RMAX + 4;   // vectors + the int flag
+    P.nf = o;
+    o = 0;
+    P.oYl = o; o += P.LDB * maxw;
+    o = (o + 3) & ~3;
+    P.oWl = o; o += std::max(1, PMW * (PMW + 1) / 2);
+    o = (o + 3) & ~3;
+    P.oV2 = o; o += 2 * 64 + 3 * KB_WMAX + 7 * 64;
+    P.nb = o;
+    constexpr size_t LDS_CAP = 160 * 1024;
+    return (size_t)P.nf * tsize <= LDS_CAP && (size_t)P.nb * tsize <= LDS_CAP;
+}
+
+size_t kb_slab_cap()    // LQRX_KKT_BIG_SLAB_MB bounds the stream-ordered slab (default 24 GiB)
+{
+    static const size_t v = [] {
+        const char *e = std::getenv("LQRX_KKT_BIG_SLAB_MB");
+        return e ? (size_t)std::strtoull(e, nullptr, 10) << 20 : (size_t)24 << 30;
+    }();
+    return v;
+}
+
+int64_t kb_chunk(const KktArgs &a, const KbPlan &P, int tsize, size_t avail)
+{
+    const size_t per = (size_t)P.S * tsize;
+    return std::max<int64_t>(1, std::min<int64_t>(a.batch, (int64_t)(avail / std::max<size_t>(per, 1))));
+}
+
+template <typename T>
+hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
+{
+    const size_t per = (size_t)P.S * sizeof(T);
+    const int64_t chunk = kb_chunk(a, P, sizeof(T), a.ws ? a.ws_bytes : kb_slab_cap());
+    Scratch sc;
+    hipError_t e = sc.get(a, (size_t)chunk * per, s);
+    if (e != hipSuccess) return e;
+    const size_t lf = (size_t)P.nf * sizeof(T), lb = (size_t)P.nb * sizeof(T);
+    if ((e = hipFuncSetAttribute((const void *)kkt_big_fwd_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)lf)) != hipSuccess ||
+        (e = hipFuncSetAttribute((const void *)kkt_big_bwd_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)lb)) != hipSuccess) {
+        (void)sc.release(s);
+        return e;
+    }
+    KbArgs<T> k{};
+    k.Y = (const T *)a.Y; k.y = (const T *)a.y; k.H = (const T *)a.H; k.g = (const T *)a.g;
+    k.dz = (T *)a.dz; k.lam = (T *)a.lam; k.slab = (T *)sc.p; k.info = a.info; k.meta = a.meta;
+    k.N = a.N; k.ginv = a.ginv;
+    k.sY = a.sY; k.sy = a.sy; k.sH = a.sH; k.sg = a.sg; k.sS = P.S;
+    k.LD = P.LD; k.LDY = P.LDY; k.LDB = P.LDB;
+    k.oWp = P.oWp; k.oBlk = P.oBlk; k.oSl = P.oSl; k.oV = P.oV;
+    k.oYl = P.oYl; k.oWl = P.oWl; k.oV2 = P.oV2;
+    for (int64_t b0 = 0; b0 < a.batch && e == hipSuccess; b0 += chunk) {
+        const int64_t nb = std::min<int64_t>(chunk, a.batch - b0);
+        k.b0 = b0;
+        hipLaunchKernelGGL(kkt_big_fwd_kernel<T>, dim3((unsigned)nb), dim3(KB_THREADS), lf, s, k);
+        hipLaunchKernelGGL(kkt_big_bwd_kernel<T>, dim3((unsigned)nb), dim3(KB_THREADS), lb, s, k);
+        e = hipGetLastError();
+    }
+    const hipError_t ef = sc.release(s);
+    return e != hipSuccess ? e : ef;
+}
+
+} // namespace
+
+bool kkt_big_supported(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2, const int32_t *w)
+{
+    KbPlan P;
+    return kb_plan(a, n1, p, n2, w, a.dtype == 1 ? 4 : 8, P);
+}
+
+size_t kkt_big_scratch_bytes(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
+                             const int32_t *w)
+{
+    KbPlan P;
+    const int ts = a.dtype == 1 ? 4 : 8;
+    if (!kb_plan(a, n1, p, n2, w, ts, P)) return 0;
+    return (size_t)kb_chunk(a, P, ts, kb_slab_cap()) * (size_t)P.S * ts;
+}
+
+hipError_t kkt_big_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
+                          const int32_t *w, hipStream_t s)
+{
+    KbPlan P;
+    const int ts = a.dtype == 1 ? 4 : 8;
+    if (!kb_plan(a, n1, p, n2, w, ts, P)) return hipErrorNotSupported;
+    return a.dtype == 1 ? kb_launch_t<float>(a, P, s) : kb_launch_t<double>(a, P, s);
+}
+
+} // namespace lqrx

@@ -50,10 +50,11 @@ class KktStructure:
         sg = int(np.sum(self.w))
         return sY, sy, sH, sg
 
-    def desc(self, batch, h_mode, ginv, layout=0):
+    def desc(self, batch, h_mode, ginv, layout=0, dtype=None):
         arrs = [np.ascontiguousarray(a, dtype=np.int32) for a in (self.n1, self.p, self.n2, self.w)]
         ptr = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32))
-        d = _lib.KktDesc(self.N, _lib.F64, batch, *[ptr(a) for a in arrs], h_mode, ginv, layout, 0)
+        dtype = _lib.F64 if dtype is None else dtype
+        d = _lib.KktDesc(self.N, dtype, batch, *[ptr(a) for a in arrs], h_mode, ginv, layout, 0)
         d._keep = arrs  # keep the arrays alive with the descriptor
         return d
 
@@ -100,10 +101,13 @@ class KktProblem:
     g: np.ndarray
 
 
-def random_kkt(st: KktStructure, batch: int, seed: int, h_mode: int = H_DIAG) -> KktProblem:
+def random_kkt(st: KktStructure, batch: int, seed: int, h_mode: int = H_DIAG, dyn: str = "small") -> KktProblem:
     """Synthetic KKT data with the reference's Jacobian structure: D1_k = [A_k B_k],
     D2_{k+1} = [−I 0] (dynamics x_{k+1} = f(x_k, u_k)), stage rows C random (the initial
-    condition / goal rows are [I 0]); H_k SPD (diagonal, block-diagonal or dense)."""
+    condition / goal rows are [I 0]); H_k SPD (diagonal, block-diagonal or dense).
+    dyn "small": A = I + 0.1·G, B = 0.1·G (the small shapes); "dense": the SURVEY §8(d)
+    random-dense scaling A = I + (0.1/√n)·G, B = G/√n, which keeps large n (cfg5's 64)
+    well conditioned."""
     rng = np.random.default_rng(seed)
     n, m, N = st.n, st.m, st.N
     sY, sy, sH, sg = st.sizes(h_mode)
@@ -126,8 +130,12 @@ def random_kkt(st: KktStructure, batch: int, seed: int, h_mode: int = H_DIAG) ->
             else:
                 blk[:, n1:n1 + p, :] = rng.standard_normal((batch, p, w))
         if n2:
-            A = np.eye(n) + 0.1 * rng.standard_normal((batch, n, n))
-            B = 0.1 * rng.standard_normal((batch, n, m))
+            if dyn == "dense":
+                A = np.eye(n) + (0.1 / np.sqrt(n)) * rng.standard_normal((batch, n, n))
+                B = rng.standard_normal((batch, n, m)) / np.sqrt(n)
+            else:
+                A = np.eye(n) + 0.1 * rng.standard_normal((batch, n, n))
+                B = 0.1 * rng.standard_normal((batch, n, m))
             blk[:, n1 + p:, :n] = A
             blk[:, n1 + p:, n:n + m] = B
         Y[:, oY:oY + rows * w] = np.swapaxes(blk, 1, 2).reshape(batch, -1)
@@ -152,19 +160,22 @@ def _ptr(a):
     return a.ctypes.data_as(C.c_void_p)
 
 
-def kkt_solve(pb: KktProblem, ginv: int = 1, layout: int = 0):
+def kkt_solve(pb: KktProblem, ginv: int = 1, layout: int = 0, dtype: int | None = None):
     """Batched _solve! via lqrx_kkt_solve_host.  Returns dict dz (batch, NN), lam
     (batch, P), info (batch,), rc.  layout=1 hands the library batch-fastest (SoA) copies
-    ([element][batch]) and transposes the outputs back — same results."""
+    ([element][batch]) and transposes the outputs back — same results.  dtype=F32 rounds the
+    inputs to float32 and runs the fp32 (large-block) kernels; outputs come back as float32."""
     lib = _lib.load()
     st, bt = pb.st, pb.batch
     sY, sy, sH, sg = st.sizes(pb.h_mode)
-    d = st.desc(bt, pb.h_mode, ginv, layout)
-    f = (lambda a: np.ascontiguousarray(np.asarray(a, dtype=np.float64).T)) if layout == 1 else \
-        (lambda a: np.ascontiguousarray(a, dtype=np.float64))
+    dtype = _lib.F64 if dtype is None else dtype
+    npdt = np.float32 if dtype == _lib.F32 else np.float64
+    d = st.desc(bt, pb.h_mode, ginv, layout, dtype)
+    f = (lambda a: np.ascontiguousarray(np.asarray(a, dtype=npdt).T)) if layout == 1 else \
+        (lambda a: np.ascontiguousarray(a, dtype=npdt))
     Y, y, H, g = f(pb.Y), f(pb.y), f(pb.H), f(pb.g)
-    dz = np.zeros((sg, bt) if layout == 1 else (bt, sg))
-    lam = np.zeros((sy, bt) if layout == 1 else (bt, sy))
+    dz = np.zeros((sg, bt) if layout == 1 else (bt, sg), npdt)
+    lam = np.zeros((sy, bt) if layout == 1 else (bt, sy), npdt)
     info = np.zeros(bt, np.int32)
     rc = _lib.check(lib.lqrx_kkt_solve_host(C.byref(d), _ptr(Y), _ptr(y), _ptr(H), _ptr(g),
                                             _ptr(dz), _ptr(lam), _ptr(info)))
@@ -178,11 +189,12 @@ def second_order_correction(pb: KktProblem):
     return kkt_solve(pb, ginv=0)
 
 
-def workspace_size(st: KktStructure, batch: int, h_mode: int, ginv: int = 1, layout: int = 0) -> int:
+def workspace_size(st: KktStructure, batch: int, h_mode: int, ginv: int = 1, layout: int = 0,
+                   dtype: int | None = None) -> int:
     """Bytes of device workspace lqrx_kkt_solve_ws needs (lqrx_kkt_workspace_size)."""
     lib = _lib.load()
     n = C.c_size_t(0)
-    _lib.check(lib.lqrx_kkt_workspace_size(C.byref(st.desc(batch, h_mode, ginv, layout)), C.byref(n)))
+    _lib.check(lib.lqrx_kkt_workspace_size(C.byref(st.desc(batch, h_mode, ginv, layout, dtype)), C.byref(n)))
     return n.value
 
 
@@ -190,19 +202,23 @@ def kkt_solve_device(st: KktStructure, t: dict, h_mode: int, ginv: int = 1,
                      stream: int | None = None, out: dict | None = None, workspace=None,
                      layout: int = 0) -> dict:
     """Device-pointer entry on torch tensors (flat, ABI layout `layout`): t has Y, y, H, g,
-    batch.  `workspace` (a device uint8 tensor of >= workspace_size() bytes) selects
-    lqrx_kkt_solve_ws: no allocation inside the call."""
+    batch; float32 tensors select dtype F32.  `workspace` (a device uint8 tensor of >=
+    workspace_size() bytes) selects lqrx_kkt_solve_ws: no allocation inside the call."""
     import torch
 
     lib = _lib.load()
     bt = t["batch"]
     sY, sy, sH, sg = st.sizes(h_mode)
     dev = t["Y"].device
+    tdt = t["Y"].dtype
+    if any(t[k].dtype != tdt for k in ("y", "H", "g")):
+        raise ValueError("Y, y, H, g must share one dtype")
+    dtype = _lib.F32 if tdt == torch.float32 else _lib.F64
     if out is None:
-        out = dict(dz=torch.empty(bt * sg, dtype=torch.float64, device=dev),
-                   lam=torch.empty(bt * sy, dtype=torch.float64, device=dev),
+        out = dict(dz=torch.empty(bt * sg, dtype=tdt, device=dev),
+                   lam=torch.empty(bt * sy, dtype=tdt, device=dev),
                    info=torch.empty(bt, dtype=torch.int32, device=dev))
-    d = st.desc(bt, h_mode, ginv, layout)
+    d = st.desc(bt, h_mode, ginv, layout, dtype)
     p = lambda x: C.c_void_p(x.data_ptr())
     args = [C.byref(d), p(t["Y"]), p(t["y"]), p(t["H"]), p(t["g"]), p(out["dz"]), p(out["lam"]),
             p(out["info"])]
