@@ -87,11 +87,64 @@ def cpu_baseline(n, m, N, target_s=12.0, threads=None):
                        f"{threads} threads, {dt:.1f} s")
 
 
-def kkt_structure(name, N):
-    """The KKT block structure of the kkt workload: the Dubins car of BASELINE configs[2], or
-    the reference's own known-answer structure DoubleIntegrator(3, N) (test/problems.jl:14-56)."""
+def kkt_structure(name, N, n=None, m=None):
+    """The KKT block structure of the kkt workload: the Dubins car of BASELINE configs[2], the
+    reference's own known-answer structure DoubleIntegrator(3, N) (test/problems.jl:14-56), or
+    "dense": the trajectory structure (conblocks.jl:403-425) at any n, m with dense random
+    dynamics blocks — BASELINE configs[4]'s banded KKT at n=64 m=32 N=512."""
     import lqrx.kkt as K
+    if name == "dense":
+        return K.trajectory_structure(n, m, N)
     return K.dubins_structure(N) if name == "dubins" else K.double_integrator_structure(3, N)
+
+
+def kkt_big_flops(st):
+    """Flops of one large-block KKT solve, per trajectory, in two counts.
+    reference: the op count of the reference's calls (cholesky_solver.jl _solve!): shur! as
+      ldiv + r = YJ·g + the full YYt = Y·JYt gemm (jacobian_blocks.jl:231-242), cholesky! with
+      potrf/trsm/gemm per block (cholesky_solve.jl:47-67), forward/backward substitution
+      (:93-143) and the primal recovery (cholesky_solver.jl:201-236);
+    minimal: the same with every symmetric product counted once (YYt's upper triangle, the
+      syrk updates) — what an implementation that exploits symmetry must execute; the roofline
+      `achieved` uses this one so the fraction cannot exceed what the hardware can do."""
+    import numpy as np
+    ref = mini = 0.0
+    for k in range(st.N):
+        p1, ps, p2, w = int(st.n1[k]), int(st.p[k]), int(st.n2[k]), int(st.w[k])
+        r = p1 + ps + p2
+        sub = (w * r + 2.0 * r * w                                  # ldiv, r = YJ·g
+               + p1 * p1 * ps + ps ** 3 / 3.0 + p1 * p1 * p2        # trsm D, potrf B, trsm F
+               + 2.0 * p1 * ps * p2 + ps * ps * p2 + p2 ** 3 / 3.0  # E − DᵀF, trsm E, potrf C
+               + 4.0 * (p1 * ps + ps * ps / 2 + p1 * p2 + ps * p2 + p2 * p2 / 2)   # fwd + bwd subst
+               + 2.0 * r * w + w)                                    # residual + ldiv
+        ref += sub + 2.0 * r * r * w + 2.0 * p1 * ps * ps + 2.0 * p1 * p2 * p2 + 2.0 * ps * p2 * p2
+        mini += sub + r * (r + 1.0) * w + p1 * ps * (ps + 1.0) + p1 * p2 * (p2 + 1.0) + ps * p2 * (p2 + 1.0)
+    return ref, mini
+
+
+def cpu_baseline_kkt_dense(st, target_s=12.0, threads=None):
+    """CPU oracle (C restatement of _solve!, fp64, OpenMP) on a bounded sample of the
+    large-block workload (host-generated trajectories of the same structure)."""
+    import lqrx.kkt as K
+    from oracle import oracle as orc
+
+    threads = threads or max(1, min(16, os.cpu_count() or 1))
+    os_ = orc.KktStructure(st.n, st.m, st.N, st.p)
+    pb = K.random_kkt(st, threads, seed=1, h_mode=K.H_DIAG, dyn="dense")
+    t0 = time.perf_counter()
+    orc.kkt_solve_batch(os_, threads, pb.Y, pb.y, pb.H, pb.g, h_mode=2, nthreads=threads)
+    dt = time.perf_counter() - t0                    # one round: `threads` solves in parallel
+    rounds = int(max(1, min(4, target_s / max(dt, 1e-9))))
+    sample = threads * rounds
+    if rounds > 1:
+        pb = K.random_kkt(st, sample, seed=2, h_mode=K.H_DIAG, dyn="dense")
+        t0 = time.perf_counter()
+        orc.kkt_solve_batch(os_, sample, pb.Y, pb.y, pb.H, pb.g, h_mode=2, nthreads=threads)
+        dt = time.perf_counter() - t0
+    return dict(value=sample / dt, unit="trajectories/s", cores=threads, kind="port",
+                sample=f"{sample} KKT solves n={st.n} m={st.m} N={st.N} (trajectory structure, dense "
+                       f"dynamics), fp64, oracle/lqr_oracle.c (C restatement of _solve!), OpenMP "
+                       f"{threads} threads, {dt:.1f} s")
 
 
 def cpu_baseline_kkt(N, target_s=12.0, threads=None, structure="dubins"):
@@ -119,6 +172,7 @@ def cpu_baseline_kkt(N, target_s=12.0, threads=None, structure="dubins"):
 
 
 def _sample_index(batch, k=64):
+    k = min(k, batch)
     import numpy as np
     return np.unique(np.linspace(0, batch - 1, k).round().astype(np.int64))
 
@@ -183,6 +237,32 @@ def check_kkt_sample(out, pb, st, idx, bt, threads):
             "oracle": "oracle/lqr_oracle.c (restatement of cholesky_solver.jl _solve!)"}
 
 
+def check_kkt_dense_sample(out, t, st, idx, bt, threads, f64):
+    """Checker for the large-block workload: the sampled trajectories' inputs copied back from
+    HBM (as the kernel saw them, fp32 or fp64) and solved by the fp64 C oracle; fp64 1e-10,
+    fp32 1e-4 relative per trajectory (tests/test_kkt_big_gpu.py)."""
+    import numpy as np
+    import torch
+    from oracle import oracle as orc
+
+    ti = torch.from_numpy(idx).to(out["dz"].device)
+    s = len(idx)
+    pick = lambda x: x.view(bt, -1).index_select(0, ti).double().cpu().numpy()
+    Y, y, H, g = (pick(t[k]) for k in ("Y", "y", "H", "g"))
+    ref = orc.kkt_solve_batch(orc.KktStructure(st.n, st.m, st.N, st.p), s, Y, y, H, g, h_mode=2,
+                              nthreads=threads)
+    dz, lam = pick(out["dz"]), pick(out["lam"])
+
+    def rel(a, b):
+        b = b.reshape(a.shape)
+        return float((np.abs(a - b).max(axis=1) / np.maximum(1e-300, np.abs(b).max(axis=1))).max())
+    e = dict(dz=rel(dz, ref["dz"]), lam=rel(lam, ref["lam"]))
+    tol = 1e-10 if f64 else 1e-4
+    return {"trajectories": s, "last_index": int(idx[-1]), "max_rel_err": e, "tol": tol,
+            "pass": bool(max(e.values()) <= tol and (ref["info"] == 0).all()),
+            "oracle": "oracle/lqr_oracle.c (restatement of cholesky_solver.jl _solve!), fp64 on the same inputs"}
+
+
 def nonfinite_count(out, keys):
     """Whole-batch scan of the timed launch's outputs on the device."""
     import torch
@@ -243,8 +323,10 @@ def main(argv=None):
     ap.add_argument("--no-gather", action="store_true",
                     help="skip the final info + P_1 gather to rank 0 (N > 1)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
-    ap.add_argument("--kkt-structure", choices=["dubins", "di"], default="dubins",
-                    help="kkt workload: Dubins (configs[2]) or DoubleIntegrator(3,N) (test/problems.jl)")
+    ap.add_argument("--kkt-structure", choices=["dubins", "di", "dense"], default="dubins",
+                    help="kkt workload: Dubins (configs[2]), DoubleIntegrator(3,N) (test/problems.jl), or "
+                         "dense: the trajectory structure at --n/--m with dense dynamics, generated in HBM "
+                         "(configs[4]: --n 64 --m 32 --N 512 --batch 8192 --dtype f32)")
     ap.add_argument("--kkt-layout", type=int, choices=[0, 1], default=0,
                     help="kkt workload: ABI layout 0 (per trajectory, the reference's blocks) or 1 "
                          "(batch fastest, SoA)")
@@ -274,7 +356,7 @@ def main(argv=None):
         args.n, args.m, args.N = 4, 1, 101
         if args.batch == 65536:
             args.batch = 4096
-    if args.workload in ("kkt", "sqp"):
+    if args.workload in ("kkt", "sqp") and not (args.workload == "kkt" and args.kkt_structure == "dense"):
         args.n, args.m = 3, 2                       # Dubins car (test/dubins.jl)
         if args.workload == "sqp" and args.sqp_model == "cartpole":
             args.n, args.m = 4, 1
@@ -381,6 +463,19 @@ def main(argv=None):
         def step():
             t["Z"].copy_(z0)                                  # same problem every step
             Q.sqp_solve_device(sqp_prob, t, stream=sh)
+    elif args.kkt_structure == "dense":
+        # large-block KKT (configs[4]): inputs generated in HBM, fp64 or fp32
+        import lqrx.kkt as K
+        st = kkt_structure("dense", N, n, m)
+        tdt = torch.float64 if f64 else torch.float32
+        t = K.random_kkt_device(st, bt, args.seed + 1000 * rank, dev, tdt)
+        ws = torch.empty(K.workspace_size(st, bt, K.H_DIAG, 1, 0, lqrx.F64 if f64 else lqrx.F32),
+                         dtype=torch.uint8, device=dev)
+        out = K.kkt_solve_device(st, t, K.H_DIAG, 1, stream=sh, workspace=ws)
+        pb = None
+
+        def step():
+            K.kkt_solve_device(st, t, K.H_DIAG, 1, stream=sh, out=out, workspace=ws)
     else:
         import lqrx.kkt as K
         st = kkt_structure(args.kkt_structure, N)
@@ -414,7 +509,9 @@ def main(argv=None):
     sampled = None
     if rank == 0 and args.workload in ("dp", "cartpole", "kkt"):
         thr = max(1, min(16, os.cpu_count() or 1))
-        if args.workload == "kkt":
+        if args.workload == "kkt" and args.kkt_structure == "dense":
+            sampled = check_kkt_dense_sample(out, t, st, _sample_index(bt, 4), bt, thr, f64)
+        elif args.workload == "kkt":
             o = out if not args.kkt_layout else \
                 {k: out[k].view(-1, bt).t().contiguous().view(-1) for k in ("dz", "lam")}
             sampled = check_kkt_sample(o, pb, st, _sample_index(bt), bt, thr)
@@ -514,6 +611,37 @@ def main(argv=None):
                 cpu = {"value": nb / el, "unit": "trajectories/s", "cores": 1, "kind": "port",
                        "sample": f"{nb} cartpole trajectories, oracle/ls_oracle.py (numpy restatement of "
                                  f"least_squares.jl solve!, OpenBLAS), {el:.1f} s"}
+        elif args.workload == "kkt" and args.kkt_structure == "dense":
+            import lqrx.kkt as K
+            sY, sy, sH, sg = st.sizes(K.H_DIAG)
+            es = 8 if f64 else 4
+            alg_bytes = (sY + sy + sH + sg + sg + sy) * es * bt      # inputs + dz + λ
+            fl_ref, fl_min = kkt_big_flops(st)
+            peak = PEAK_FP64_TFLOPS if f64 else PEAK_FP32_TFLOPS
+            achieved = fl_min * bt / (kern_ms * 1e-3) / 1e12
+            t_hbm = alg_bytes / (PEAK_HBM_GBS * 1e9)
+            t_fl = fl_min * bt / (peak * 1e12)
+            traffic = None
+            key = f"kkt_dense_n{n}_m{m}_N{N}_B{bt}_{args.dtype}"
+            if os.path.exists(args.traffic_json):
+                try:
+                    traffic = json.load(open(args.traffic_json)).get(key, {}).get("hbm_bytes_per_launch")
+                except Exception:
+                    traffic = None
+            roof = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                    "frac": achieved / peak, "traffic": traffic, "traffic_key": key,
+                    "kernel": "kkt_big_fwd_kernel + kkt_big_bwd_kernel", "kernel_ms": kern_ms,
+                    "flops_per_traj_minimal": fl_min, "flops_per_traj_reference": fl_ref,
+                    "reference_count_tflops": fl_ref * bt / (kern_ms * 1e-3) / 1e12,
+                    "alg_bytes_per_launch": alg_bytes, "hbm_gbs_alg": alg_bytes / (kern_ms * 1e-3) / 1e9,
+                    "t_hbm_ms": t_hbm * 1e3, "t_flop_ms": t_fl * 1e3,
+                    "frac_of_binding": max(t_hbm, t_fl) / (kern_ms * 1e-3)}
+            metric = (f"KKT solves/sec (banded block-tridiagonal _solve!, trajectory structure n={n} m={m} "
+                      f"N={N}, {args.dtype})")
+            workload = ("large-block banded KKT solve, cholesky_solver.jl _solve! (BASELINE.json configs[4]"
+                        + (")" if (n, m, N, args.dtype) == (64, 32, 512, "f32") else " shape family)"))
+            cpu = cpu_baseline_kkt_dense(st, target_s=args.cpu_seconds) \
+                if not args.no_cpu_baseline and world == 1 else None
         elif args.workload == "kkt":
             import lqrx.kkt as K
             sY, sy, sH, sg = st.sizes(K.H_DIAG)

@@ -35,20 +35,41 @@ dtypecode(::Type{Float32}) = Int32(1)
 
 """
     LQRSolution(n, m, N, batch=1; T=Float64, all_P=false)
+    LQRSolution(prob::LQRProblem)
 
-K[:,:,k,b] = gain of knot k (m×n); X[:,k,b]; U[:,k,b]; P = P₁ (or all P_k); info[b].
+The output container src/LQR.jl:19 exports but never defines, with the fields
+src/dynamic_programming.jl touches: `sol.K[k]` (the m×n gain of knot k, :62, :68),
+`sol.X[k]` (:66-69), `sol.U[k]` (:68-69) — for one problem these are Vectors of views (a
+batch gives Matrices of views, `sol.K[k, b]`) into the column-major batch arrays Kdata
+(m, n, N-1, batch), Xdata (n, N, batch), Udata (m, N-1, batch) that the C ABI writes in place
+(layout 0, no copies); P = P₁ (or all P_k) and info (first non-SPD knot, 0 = ok).
 """
-struct LQRSolution{T}
-    K::Array{T,4}
+struct LQRSolution{T,VK,VX,VU}
+    K::VK
+    X::VX
+    U::VU
+    Kdata::Array{T,4}
     P::Array{T}
-    X::Array{T,3}
-    U::Array{T,3}
+    Xdata::Array{T,3}
+    Udata::Array{T,3}
     info::Vector{Int32}
 end
-LQRSolution(n, m, N, batch=1; T=Float64, all_P=false) =
-    LQRSolution{T}(zeros(T, m, n, N - 1, batch),
-                   all_P ? zeros(T, n, n, N, batch) : zeros(T, n, n, batch),
-                   zeros(T, n, N, batch), zeros(T, m, N - 1, batch), zeros(Int32, batch))
+function LQRSolution(n, m, N, batch=1; T=Float64, all_P=false)
+    Kd = zeros(T, m, n, N - 1, batch)
+    Xd = zeros(T, n, N, batch)
+    Ud = zeros(T, m, N - 1, batch)
+    P = all_P ? zeros(T, n, n, N, batch) : zeros(T, n, n, batch)
+    if batch == 1
+        K = [view(Kd, :, :, k, 1) for k in 1:N-1]
+        X = [view(Xd, :, k, 1) for k in 1:N]
+        U = [view(Ud, :, k, 1) for k in 1:N-1]
+    else
+        K = [view(Kd, :, :, k, b) for k in 1:N-1, b in 1:batch]
+        X = [view(Xd, :, k, b) for k in 1:N, b in 1:batch]
+        U = [view(Ud, :, k, b) for k in 1:N-1, b in 1:batch]
+    end
+    LQRSolution{T,typeof(K),typeof(X),typeof(U)}(K, X, U, Kd, P, Xd, Ud, zeros(Int32, batch))
+end
 
 """
     LQRBatch(A, B, Q, R, Qf, x0, N)   A: n×n×batch, B: n×m×batch, …, x0: n×batch
@@ -65,7 +86,7 @@ end
 DPSolver(b::LQRBatch{T}) where T = DPSolver{T}(size(b.B, 1), size(b.B, 2), b.N)
 
 """
-    solve!(sol, solver, prob)
+    solve!(sol, solver, prob::LQRBatch)
 
 Batched Riccati backward pass + forward rollout on the GPU (host arrays in, host arrays
 out; lqrx_dp_solve_host).  Same outputs as src/dynamic_programming.jl:54-72 for every
@@ -81,21 +102,51 @@ function solve!(sol::LQRSolution{T}, solver::DPSolver{T}, prob::LQRBatch{T}) whe
                    (Ref{DpDesc}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T},
                     Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{Int32}),
                    d, prob.A, prob.B, prob.Q, prob.R, prob.Qf, prob.x0,
-                   sol.K, sol.P, sol.X, sol.U, sol.info)
+                   sol.Kdata, sol.P, sol.Xdata, sol.Udata, sol.info)
     end
     return check(rc)
 end
 
-# Single-problem form with the reference's LQRProblem fields (lqr_problem.jl:1-11)
-struct LQRProblem{n,m,T}
-    Qf::Matrix{T}; Q::Matrix{T}; R::Matrix{T}; A::Matrix{T}; B::Matrix{T}
-    x0::Vector{T}; u0::Vector{T}; tf::T; N::Int
+# ---- the reference's own single-problem surface (src/lqr_problem.jl:1-11) -------------
+# LQRProblem{n,m,T,TQ,TR} with the reference's field order; Q/Qf/R may be Diagonal (TQ, TR)
+# and A/B SizedMatrix — anything AbstractMatrix: solve! densifies them into the ABI buffers.
+# With it the reference's three lines (test/dp.jl:14-20) run unchanged through the C ABI:
+#     sol = LQRSolution(prob); solver = DPSolver(prob); solve!(sol, solver, prob)
+struct LQRProblem{n,m,T,TQ,TR}
+    Qf::TQ
+    Q::TQ
+    R::TR
+    A::AbstractMatrix{T}
+    B::AbstractMatrix{T}
+    x0::AbstractVector{T}
+    u0::AbstractVector{T}
+    tf::T
+    N::Int
 end
-function solve!(sol::LQRSolution{T}, prob::LQRProblem{n,m,T}) where {n,m,T}
-    b = LQRBatch{T}(reshape(prob.A, n, n, 1), reshape(prob.B, n, m, 1), reshape(prob.Q, n, n, 1),
-                    reshape(prob.R, m, m, 1), reshape(prob.Qf, n, n, 1), reshape(prob.x0, n, 1), prob.N)
-    solve!(sol, DPSolver(b), b)
+LQRProblem(Qf::TQ, Q::TQ, R::TR, A::AbstractMatrix{T}, B::AbstractMatrix{T}, x0::AbstractVector,
+           u0::AbstractVector, tf::Real, N::Integer) where {T,TQ,TR} =
+    LQRProblem{size(B, 1),size(B, 2),T,TQ,TR}(Qf, Q, R, A, B, x0, u0, T(tf), Int(N))
+Base.size(prob::LQRProblem{n,m}) where {n,m} = n, m, prob.N                    # lqr_problem.jl:21
+num_vars(prob::LQRProblem{n,m}) where {n,m} = prob.N * n + (prob.N - 1) * m     # :22-25
+
+LQRSolution(prob::LQRProblem{n,m,T}) where {n,m,T} = LQRSolution(n, m, prob.N, 1; T=T)
+DPSolver(prob::LQRProblem{n,m,T}) where {n,m,T} = DPSolver{T}(n, m, prob.N)
+
+"""
+    solve!(sol, solver::DPSolver, prob::LQRProblem)
+
+The reference's solve! (src/dynamic_programming.jl:54-72) for one problem: the
+LQRProblem fields (Diagonal / Sized / dense) densified column-major into a batch of one,
+lqrx_dp_solve_host, results written through sol.K[k], sol.X[k], sol.U[k] (views of
+sol.Kdata …) and sol.P = solver.P₁.
+"""
+function solve!(sol::LQRSolution{T}, solver::DPSolver{T}, prob::LQRProblem{n,m,T}) where {n,m,T}
+    dense3(M, r, c) = reshape(Matrix{T}(M), r, c, 1)      # Diagonal(q) → n×n, SizedMatrix → Matrix
+    b = LQRBatch{T}(dense3(prob.A, n, n), dense3(prob.B, n, m), dense3(prob.Q, n, n),
+                    dense3(prob.R, m, m), dense3(prob.Qf, n, n), reshape(Vector{T}(prob.x0), n, 1), prob.N)
+    return solve!(sol, solver, b)
 end
+solve!(sol::LQRSolution{T}, prob::LQRProblem{n,m,T}) where {n,m,T} = solve!(sol, DPSolver(prob), prob)
 
 # ---- linear cost terms (lqrx_dp_linear; SURVEY §8(f) rank 1, no upstream counterpart) ----
 struct DpLinear
@@ -123,7 +174,7 @@ function solve_linear!(sol::LQRSolution{T}, d::Array{T,3}, p::Array{T}, solver::
                    (Ref{DpDesc}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ref{DpLinear},
                     Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{Int32}),
                    desc, prob.A, prob.B, prob.Q, prob.R, prob.Qf, prob.x0, lin,
-                   sol.K, sol.P, sol.X, sol.U, sol.info)
+                   sol.Kdata, sol.P, sol.Xdata, sol.Udata, sol.info)
     end
     return check(rc)
 end
@@ -144,17 +195,18 @@ the per-knot ConstraintBlock.Y / .y, cost Hessian and gradient, packed (column-m
 blocks, concatenated over knots) with the batch as the last dimension.  ginv=0 is the
 second_order_correction! variant (:254-273).
 """
-function kkt_solve!(dz::Matrix{Float64}, lam::Matrix{Float64}, info::Vector{Int32},
+function kkt_solve!(dz::Matrix{T}, lam::Matrix{T}, info::Vector{Int32},
                     n1::Vector{Int32}, p::Vector{Int32}, n2::Vector{Int32}, w::Vector{Int32},
-                    Y::Matrix{Float64}, y::Matrix{Float64}, H::Matrix{Float64}, g::Matrix{Float64};
-                    h_mode::Integer=2, ginv::Integer=1)
+                    Y::Matrix{T}, y::Matrix{T}, H::Matrix{T}, g::Matrix{T};
+                    h_mode::Integer=2, ginv::Integer=1) where {T<:Union{Float64,Float32}}
+    # Float32 runs the large-block MFMA kernels (blocks up to 64 rows, w up to 128; diagonal
+    # H or ginv = 0) — BASELINE configs[4]'s banded KKT
     batch = size(Y, 2)
     GC.@preserve n1 p n2 w Y y H g dz lam info begin
-        d = Ref(KktDesc(length(n1), 0, batch, pointer(n1), pointer(p), pointer(n2), pointer(w),
+        d = Ref(KktDesc(length(n1), dtypecode(T), batch, pointer(n1), pointer(p), pointer(n2), pointer(w),
                         h_mode, ginv, 0, 0))
         rc = ccall((:lqrx_kkt_solve_host, liblqrx), Cint,
-                   (Ref{KktDesc}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
-                    Ptr{Float64}, Ptr{Float64}, Ptr{Int32}),
+                   (Ref{KktDesc}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{Int32}),
                    d, Y, y, H, g, dz, lam, info)
     end
     return check(rc)
@@ -229,6 +281,7 @@ function sqp_solve!(Z::Matrix{Float64}, lam::Matrix{Float64}, iters::Vector{Int3
     return check(rc)
 end
 
-export LQRProblem, LQRSolution, LQRBatch, DPSolver, solve!, kkt_solve!, ls_solve!, sqp_solve!
+export LQRProblem, LQRSolution, LQRBatch, DPSolver, solve!, solve_linear!, kkt_solve!, ls_solve!,
+       sqp_solve!, num_vars
 
 end # module

@@ -154,7 +154,12 @@ class LQRBatch:
 
     @classmethod
     def of(cls, probs: list[LQRProblem]):
-        st = lambda f: np.stack([np.asarray(getattr(p, f), dtype=np.float64) for p in probs])
+        """Stack problems; a 1-D Q, Qf or R is a diagonal (the reference's LQRProblem allows
+        TQ, TR = Diagonal, lqr_problem.jl:1-4) and is densified."""
+        def field_(p, f):
+            a = np.asarray(getattr(p, f), dtype=np.float64)
+            return np.diag(a) if f in ("Q", "Qf", "R") and a.ndim == 1 else a
+        st = lambda f: np.stack([field_(p, f) for p in probs])
         lin = probs[0].q is not None
         return cls(st("A"), st("B"), st("Q"), st("R"), st("Qf"), st("x0"), probs[0].N,
                    q=st("q") if lin else None, r=st("r") if lin else None,

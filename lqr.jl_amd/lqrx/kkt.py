@@ -156,6 +156,48 @@ def random_kkt(st: KktStructure, batch: int, seed: int, h_mode: int = H_DIAG, dy
     return KktProblem(st, batch, h_mode, Y, y, H, g)
 
 
+def random_kkt_device(st: KktStructure, batch: int, seed: int, device, dtype=None):
+    """random_kkt(…, h_mode=H_DIAG, dyn="dense") generated directly in HBM (torch, per knot),
+    for batches whose Y does not fit host memory (BASELINE configs[4]: n=64 m=32 N=512
+    B=8192 fp32 is 206 GB of Y).  Same block structure and distributions; a different
+    random stream than the host generator.  Returns dict Y, y, H, g (flat), batch."""
+    import torch
+
+    dtype = dtype or torch.float64
+    gen = torch.Generator(device=device)
+    gen.manual_seed(int(seed))
+    n, m, N = st.n, st.m, st.N
+    sY, sy, sH, sg = st.sizes(H_DIAG)
+    Y = torch.zeros(batch, sY, dtype=dtype, device=device)
+    eye = torch.eye(n, dtype=dtype, device=device)
+    oY = 0
+    for k in range(N):
+        n1, p, n2, w = int(st.n1[k]), int(st.p[k]), int(st.n2[k]), int(st.w[k])
+        rows = n1 + p + n2
+        blk = Y[:, oY:oY + rows * w].view(batch, w, rows)        # [b][column][row]: column-major block
+        if n1:
+            blk[:, :n, :n1] = -eye[:, :n1]
+        if p:
+            if k == 0 or k == N - 1:
+                if p <= n:
+                    blk[:, :n, n1:n1 + p] = eye[:, :p]
+                else:
+                    blk[:, :, n1:n1 + p] = torch.randn(batch, w, p, generator=gen, dtype=dtype, device=device)
+            else:
+                blk[:, :, n1:n1 + p] = torch.randn(batch, w, p, generator=gen, dtype=dtype, device=device)
+        if n2:
+            A = torch.randn(batch, n, n2, generator=gen, dtype=dtype, device=device) * (0.1 / np.sqrt(n))
+            A += eye[:, :n2]
+            blk[:, :n, n1 + p:] = A                               # column j of A_kᵀ… rows of D1 = [A B]
+            blk[:, n:n + m, n1 + p:] = torch.randn(batch, m, n2, generator=gen, dtype=dtype,
+                                                   device=device) / np.sqrt(n)
+        oY += rows * w
+    y = 0.1 * torch.randn(batch, sy, generator=gen, dtype=dtype, device=device)
+    H = 0.1 + torch.rand(batch, sH, generator=gen, dtype=dtype, device=device)
+    g = torch.randn(batch, sg, generator=gen, dtype=dtype, device=device)
+    return dict(Y=Y.view(-1), y=y.view(-1), H=H.view(-1), g=g.view(-1), batch=batch)
+
+
 def _ptr(a):
     return a.ctypes.data_as(C.c_void_p)
 

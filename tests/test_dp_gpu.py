@@ -98,3 +98,34 @@ def test_dp_deterministic(lqrx, gpu_ok):
     a1 = lqrx.solve_batch(b)
     a2 = lqrx.solve_batch(b)
     assert np.array_equal(a1["K"], a2["K"]) and np.array_equal(a1["X"], a2["X"])
+
+
+def test_reference_call_shape_diagonal_costs(lqrx, oracle, gpu_ok):
+    """The reference's own call sequence (test/dp.jl:14-20) through the C ABI:
+    sol = LQRSolution(prob); solver = DPSolver(prob); solve!(sol, solver, prob) — here
+    LQRSolution.of / DPSolver.of / lqrx.solve — with LQRProblem's Q, Qf, R given as
+    Diagonal (lqr_problem.jl:1-4 allows TQ, TR = Diagonal; test/problems.jl builds them that
+    way), densified on the way into the ABI.  sol.K[k] is knot k's m×n gain."""
+    from lqrx.dp import from_abi, to_abi
+
+    n, m, N, dt = 4, 2, 51, 0.1                    # DoubleIntegrator(2) (test/problems.jl:14-56)
+    I2 = np.eye(2)
+    A = np.block([[I2, dt * I2], [0 * I2, I2]])
+    B = np.vstack([0.5 * dt * dt * I2, dt * I2])
+    q = np.array([10.0, 10.0, 1.0, 1.0])
+    prob = lqrx.LQRProblem(Qf=10 * q, Q=q, R=np.full(m, 0.1), A=A, B=B, x0=np.array([1.0, -1, 0, 0.5]),
+                           u0=np.zeros(m), tf=5.0, N=N)
+    sol = lqrx.LQRSolution.of(prob)
+    solver = lqrx.DPSolver.of(prob)
+    lqrx.solve(sol, solver, prob)
+    d = dict(A=to_abi(A[None]).ravel(), B=to_abi(B[None]).ravel(), Q=to_abi(np.diag(q)[None]).ravel(),
+             R=to_abi(np.diag(np.full(m, 0.1))[None]).ravel(), Qf=to_abi(np.diag(10 * q)[None]).ravel(),
+             x0=prob.x0.copy(), n=n, m=m, N=N, batch=1)
+    ref = oracle.dp_solve_abi(d, N)
+    K = from_abi(ref["K"], (1, N - 1, m, n))[0]
+    assert sol.info == 0
+    for k in (0, N // 2, N - 2):
+        assert sol.K[k].shape == (m, n)
+        assert np.abs(sol.K[k] - K[k]).max() <= TOL64 * np.abs(K[k]).max()
+    assert np.abs(sol.X - ref["X"].reshape(N, n)).max() <= TOL64 * np.abs(ref["X"]).max()
+    assert np.abs(sol.P - from_abi(ref["P"], (1, n, n))[0]).max() <= TOL64 * np.abs(ref["P"]).max()
