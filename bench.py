@@ -171,6 +171,29 @@ def cpu_baseline_kkt(N, target_s=12.0, threads=None, structure="dubins"):
                        f"of _solve!), OpenMP {threads} threads, {dt:.1f} s")
 
 
+TRAFFIC_FILES = ("traffic_r03.json", "traffic_r02.json")
+
+
+def traffic_lookup(key, path=None):
+    """roofline.traffic: PMC HBM bytes per launch of this exact workload from the committed
+    profiles/traffic_*.json (FETCH_SIZE×2 + WRITE_SIZE passes, tools/traffic_json.py), newest
+    round first, with where it came from — the file, the key, the commit it was measured at and
+    the PMC run — so a stale figure is visible in the line itself."""
+    paths = [path] if path else [os.path.join(ROOT, "profiles", f) for f in TRAFFIC_FILES]
+    for p in paths:
+        if not os.path.exists(p):
+            continue
+        try:
+            e = json.load(open(p)).get(key)
+        except Exception:
+            e = None
+        if e and e.get("hbm_bytes_per_launch"):
+            return e["hbm_bytes_per_launch"], {"file": os.path.relpath(p, ROOT), "key": key,
+                                               "measured_at_head": e.get("measured_at_head"),
+                                               "pmc_source": e.get("source")}
+    return None, {"file": None, "key": key, "note": "no PMC FETCH/WRITE pass recorded for this workload"}
+
+
 def _sample_index(batch, k=64):
     k = min(k, batch)
     import numpy as np
@@ -322,7 +345,8 @@ def main(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-gather", action="store_true",
                     help="skip the final info + P_1 gather to rank 0 (N > 1)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC traffic table (default: profiles/traffic_r03.json, then traffic_r02.json)")
     ap.add_argument("--kkt-structure", choices=["dubins", "di", "dense"], default="dubins",
                     help="kkt workload: Dubins (configs[2]), DoubleIntegrator(3,N) (test/problems.jl), or "
                          "dense: the trajectory structure at --n/--m with dense dynamics, generated in HBM "
@@ -540,6 +564,7 @@ def main(argv=None):
     ms_per_step = wall / args.steps * 1e3
 
     if rank == 0:
+        tsrc = None
         if args.workload == "sqp":
             import lqrx.kkt as K
             import lqrx.sqp as Q
@@ -586,14 +611,8 @@ def main(argv=None):
             # reference op count (least_squares.jl:171-182): ĀᵀĀ as a dense gemm, Āᵀb̄, potrf, potrs
             fl = 2.0 * Nn * Nm * Nm + 2.0 * Nn * Nm + Nm ** 3 / 3.0 + 2.0 * Nm * Nm
             achieved = fl * bt / (kern_ms * 1e-3) / 1e12
-            traffic = None
-            if os.path.exists(args.traffic_json):
-                try:
-                    traffic = json.load(open(args.traffic_json)).get(f"ls_cartpole_N{N}_B{bt}_f64", {}) \
-                        .get("hbm_bytes_per_launch")
-                except Exception:
-                    traffic = None
-            roof = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+            traffic, tsrc = traffic_lookup(f"ls_cartpole_N{N}_B{bt}_f64", args.traffic_json)
+            roof = {"traffic_source": tsrc, "bound": "mfma", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                     "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic,
                     "kernel": "ls_condensed_kernel (fp64 VALU, LDS-resident H)", "kernel_ms": kern_ms,
                     "flops_per_traj": fl}
@@ -621,15 +640,9 @@ def main(argv=None):
             achieved = fl_min * bt / (kern_ms * 1e-3) / 1e12
             t_hbm = alg_bytes / (PEAK_HBM_GBS * 1e9)
             t_fl = fl_min * bt / (peak * 1e12)
-            traffic = None
-            key = f"kkt_dense_n{n}_m{m}_N{N}_B{bt}_{args.dtype}"
-            if os.path.exists(args.traffic_json):
-                try:
-                    traffic = json.load(open(args.traffic_json)).get(key, {}).get("hbm_bytes_per_launch")
-                except Exception:
-                    traffic = None
+            traffic, tsrc = traffic_lookup(f"kkt_dense_n{n}_m{m}_N{N}_B{bt}_{args.dtype}", args.traffic_json)
             roof = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                    "frac": achieved / peak, "traffic": traffic, "traffic_key": key,
+                    "frac": achieved / peak, "traffic": traffic, "traffic_source": tsrc,
                     "kernel": "kkt_big_fwd_kernel + kkt_big_bwd_kernel", "kernel_ms": kern_ms,
                     "flops_per_traj_minimal": fl_min, "flops_per_traj_reference": fl_ref,
                     "reference_count_tflops": fl_ref * bt / (kern_ms * 1e-3) / 1e12,
@@ -647,17 +660,12 @@ def main(argv=None):
             sY, sy, sH, sg = st.sizes(K.H_DIAG)
             alg_bytes = (sY + sy + sH + sg + sg + sy) * 8 * bt     # inputs + dz + λ
             achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-            traffic = None
-            key = f"kkt_{args.kkt_structure}_N{N}_B{bt}_f64" + ("_soa" if args.kkt_layout else "")
-            if os.path.exists(args.traffic_json):
-                try:
-                    traffic = json.load(open(args.traffic_json)).get(key, {}).get("hbm_bytes_per_launch")
-                except Exception:
-                    traffic = None
+            traffic, tsrc = traffic_lookup(f"kkt_{args.kkt_structure}_N{N}_B{bt}_f64"
+                                           + ("_soa" if args.kkt_layout else ""), args.traffic_json)
             kname = ("kkt_fil_kernel" if args.kkt_structure == "dubins" else "kkt_fild_kernel") if N >= 4 \
                 else "kkt_staged_kernel"
             roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                    "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": tsrc,
                     "kernel": kname,
                     "kernel_ms": kern_ms,
                     "alg_bytes_per_traj": alg_bytes / bt}
@@ -674,15 +682,8 @@ def main(argv=None):
             flops = dp_flops_per_traj(n, m, N) * bt
             achieved = flops / (kern_ms * 1e-3) / 1e12
             peak = PEAK_FP64_TFLOPS if f64 else PEAK_FP32_TFLOPS
-            traffic = None
-            if os.path.exists(args.traffic_json):
-                try:
-                    tj = json.load(open(args.traffic_json))
-                    key = f"n{n}_m{m}_N{N}_B{bt}_{args.dtype}" + ("_tv" if args.tv else "") \
-                        + ("_lin" if args.linear else "")
-                    traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
-                except Exception:
-                    traffic = None
+            traffic, tsrc = traffic_lookup(f"n{n}_m{m}_N{N}_B{bt}_{args.dtype}" + ("_tv" if args.tv else "")
+                                           + ("_lin" if args.linear else ""), args.traffic_json)
             roof = {"bound": "mfma", "achieved": achieved, "peak": peak,
                     "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
                     "kernel": _dp_kernel_name(n, m, bt, args.tv or args.linear),
@@ -747,6 +748,8 @@ def main(argv=None):
                             + (" (BASELINE.json configs[4], per GPU)" if cfg5 else " (non-baseline shape)"))
             cpu = cpu_baseline(n, m, N, target_s=args.cpu_seconds) \
                 if not args.no_cpu_baseline and world == 1 else None
+        if tsrc is not None:
+            roof.setdefault("traffic_source", tsrc)
         if roof.get("bound") == "hbm":
             # beside the 8 TB/s spec: the measured achievable streaming rate
             # (MI355X_MICROARCH.md: float4 copy, 6.29 TB/s); peak and frac stay on the spec

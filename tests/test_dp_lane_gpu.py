@@ -212,3 +212,45 @@ def test_time_varying_info_middle_knot(lqrx, oracle, gpu_ok, n, m, N, k0):
     ok = [0, 2, 3, 4]
     assert relerr_per_knot(got["K"][ok], refK[ok]) <= TOL64
     assert relerr_per_knot(got["K"][1:2, k0:], refK[1:2, k0:]) <= TOL64   # knots k0+1 … N−1
+
+
+@pytest.mark.parametrize("n,m,N,mode", [(32, 16, 40, "all"), (32, 16, 40, "one"), (8, 4, 30, "all"),
+                                        (6, 3, 60, "one"), (20, 5, 33, "slow"), (64, 32, 24, "one")])
+def test_time_varying_info_gradual_indefiniteness(lqrx, oracle, gpu_ok, n, m, N, mode):
+    """E = R_k + BᵀPB loses definiteness GRADUALLY along the horizon: R_k ramps linearly
+    through zero (R_k = (2k/N − 1)·I, or only its last eigenvalue — "one" — or a slow ramp
+    with an offset) with B_k scaled by 1e-2, so E's smallest eigenvalue crosses zero over
+    several knots instead of flipping at one.  The MFMA kernel (n ≥ 5) inverts E by a
+    warm-started Newton–Schulz iteration after the first knot; it must not converge onto the
+    inverse of an indefinite E: info must equal the oracle's first failing knot (potrf's
+    info, dynamic_programming.jl:29), and every knot solved before it must still match."""
+    from lqrx.dp import to_abi, from_abi
+
+    bt = 3
+    b = _tv_batch(lqrx, n, m, N, bt, seed=91 + n, tv_ab=True, tv_qr=True)
+    b.R = np.array(b.R)
+    b.B = np.array(b.B) * 1e-2
+    k = np.arange(1, N)                                   # knot k at index k − 1
+    if mode == "slow":
+        ramp = 0.3 * (k / N - 0.45)
+    else:
+        ramp = 2.0 * k / N - 1.0
+    for t in (1, 2):                                      # trajectory 0 stays SPD
+        for j, r in enumerate(ramp):
+            if mode == "one":
+                b.R[t, j] = np.eye(m)
+                b.R[t, j, m - 1, m - 1] = r
+            else:
+                b.R[t, j] = r * np.eye(m)
+    got = lqrx.solve_batch(b, all_P=True)
+    d = {f: to_abi(getattr(b, f)).ravel() for f in ("A", "B", "Q", "R", "Qf")}
+    d.update(x0=b.x0.ravel(), n=n, m=m, batch=bt, tv_AB=1, tv_QR=1)
+    ref = oracle.dp_solve_abi(d, N, all_P=True)
+    assert ref["info"][0] == 0 and ref["info"][1] > 0 and ref["info"][2] > 0
+    assert list(got["info"]) == list(ref["info"]), (got["info"], ref["info"])
+    assert got["rc"] == 1
+    refK = from_abi(ref["K"], (bt, N - 1, m, n))
+    assert relerr_per_knot(got["K"][:1], refK[:1]) <= TOL64
+    for t in (1, 2):
+        k0 = int(ref["info"][t])                          # knots k0+1 … N−1 solved before the break
+        assert relerr_per_knot(got["K"][t:t + 1, k0:], refK[t:t + 1, k0:]) <= TOL64

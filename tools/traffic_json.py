@@ -9,7 +9,7 @@ coalesced reads → ×2; WRITE_SIZE is exact for 16-B/lane streaming stores; bot
 import csv, glob, json, os, sys
 
 key, ks, fdir, wdir = sys.argv[1:5]
-out = sys.argv[5] if len(sys.argv) > 5 else os.path.join(os.path.dirname(__file__), "..", "profiles", "traffic_r01.json")
+out = sys.argv[5] if len(sys.argv) > 5 else os.path.join(os.path.dirname(__file__), "..", "profiles", "traffic_r03.json")
 
 
 def per_dispatch(d, counter):
@@ -33,6 +33,7 @@ tj[key] = {
               f"({ks} rows only); FETCH_SIZE x2 (gfx950 wide-read undercount, "
               "MI355X_MICROARCH.md HBM section), KiB->bytes x1024",
     "source": f"{fdir}, {wdir}",
+    "measured_at_head": os.environ.get("GIT_HEAD"),
 }
 json.dump(tj, open(out, "w"), indent=1)
 print(key, tj[key]["hbm_bytes_per_launch"] / 1e9, "GB/launch")
