@@ -210,12 +210,30 @@ __device__ int leaf_chol_inv(T *X, int ld, int q, int lane)
 
 // ---------------------------------------------------------------- blocked chol + inverse
 // In place on the LDS image X (leading dimension LD, upper 16×16 tiles of a P×P SPD matrix
-// whose real size is p; P = 16·nb, nb ≤ 4): X ← U⁻¹ with UᵀU = X (upper tiles; diagonal tiles
+// whose real size is p; P = 16·nb, nb ≤ NBM ≤ 8): X ← U⁻¹ with UᵀU = X (upper tiles; diagonal tiles
 // have a zero strictly-lower part).  Right-looking by 16: leaf (wave 0) → panel
 // U_{jb,J} = T_jjᵀ X_{jb,J} → trailing X_IJ −= U_{jb,I}ᵀ U_{jb,J} (MFMA, waves round-robin);
-// then W_IJ = −T_I Σ_{L=I+1..J} U_IL W_LJ, column J by wave J−1, every U read before any
-// write.  Returns 0, or 1 + the first non-positive pivot (all threads).
-template <typename T>
+// then W_IJ = −T_I Σ_{L=I+1..J} U_IL W_LJ (inv_column), column J by wave (J−1) mod 4, every U
+// read before any write.  Returns 0, or 1 + the first non-positive pivot (all threads).
+// W_IJ = −T_I Σ_{L=I+1..J} U_IL W_LJ for one block column J, bottom-up; W_LJ (L < J) stay in
+// registers (w[L]) and feed the next products as C-layout B operands; W_JJ = T_J is in LDS.
+template <typename T, int NBM>
+__device__ __forceinline__ void inv_column(const T *X, int LD, int J, int lane, acc_t<T> (&w)[NBM])
+{
+    const T *TJ = X + 16 * J * (1 + LD);
+#pragma unroll
+    for (int I = NBM - 2; I >= 0; --I) {
+        if (I < J) {
+            acc_t<T> s = tmm<T, false, false, false>(tzero<T>(), X + 16 * I + 16 * J * LD, LD, TJ, LD, 16, lane);
+#pragma unroll
+            for (int L = I + 1; L < NBM - 1; ++L)
+                if (L < J) s = tmm_reg<T, false>(s, X + 16 * I + 16 * L * LD, LD, w[L], lane);
+            w[I] = tmm_reg<T, true>(tzero<T>(), X + 16 * I * (1 + LD), LD, s, lane);
+        }
+    }
+}
+
+template <typename T, int NBM = 4>
 __device__ int chol_inv(T *X, int LD, int p, int P, int *flag, int tid)
 {
     const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), nb = P >> 4;
@@ -254,28 +272,17 @@ __device__ int chol_inv(T *X, int LD, int p, int P, int *flag, int tid)
         }
     }
     if (nb > 1) {
-        const int J = wave + 1;
-        acc_t<T> w0 = tzero<T>(), w1 = tzero<T>(), w2 = tzero<T>();
-        if (J < nb) {
-            const T *TJ = X + 16 * J * (1 + LD);
-#pragma unroll
-            for (int I = 2; I >= 0; --I) {
-                if (I < J) {
-                    acc_t<T> s = tmm<T, false, false, false>(tzero<T>(), X + 16 * I + 16 * J * LD, LD, TJ, LD, 16, lane);
-                    if (I + 1 <= 1 && 1 < J) s = tmm_reg<T, false>(s, X + 16 * I + 16 * 1 * LD, LD, w1, lane);
-                    if (I + 1 <= 2 && 2 < J) s = tmm_reg<T, false>(s, X + 16 * I + 16 * 2 * LD, LD, w2, lane);
-                    const acc_t<T> r = tmm_reg<T, true>(tzero<T>(), X + 16 * I * (1 + LD), LD, s, lane);
-                    if (I == 0) w0 = r;
-                    else if (I == 1) w1 = r;
-                    else w2 = r;
-                }
-            }
-        }
+        // column J by wave (J − 1) mod 4; a wave holds its columns' W tiles in registers until
+        // every wave has read the U tiles it needs (the barrier), then writes them over U
+        acc_t<T> wa[NBM], wb[NBM];
+        const int Ja = wave + 1, Jb = wave + 5;
+        if (Ja < nb) inv_column<T, NBM>(X, LD, Ja, lane, wa);
+        if (NBM > 5 && Jb < nb) inv_column<T, NBM>(X, LD, Jb, lane, wb);
         __syncthreads();
-        if (J < nb) {
-            tstore(X + 16 * J * LD, LD, w0, lane);
-            if (J > 1) tstore(X + 16 + 16 * J * LD, LD, w1, lane);
-            if (J > 2) tstore(X + 32 + 16 * J * LD, LD, w2, lane);
+#pragma unroll
+        for (int I = 0; I < NBM - 1; ++I) {
+            if (I < Ja && Ja < nb) tstore(X + 16 * I + 16 * Ja * LD, LD, wa[I], lane);
+            if (NBM > 5 && I < Jb && Jb < nb) tstore(X + 16 * I + 16 * Jb * LD, LD, wb[I], lane);
         }
     }
     __syncthreads();
@@ -310,6 +317,13 @@ struct KbArgs {
     int LD, LDY, LDB;              // LDS leading dims: blocks, Y slab (fwd), staged Y (bwd)
     int oWp, oBlk, oSl, oV;        // fwd LDS offsets (elements of T)
     int oYl, oWl, oV2;             // bwd LDS offsets
+    // dense / block-diagonal H (kkt_big_hfac_kernel ran first): Y, g point at its Z = Y U⁻¹,
+    // gz = U⁻ᵀg (chunk-relative, yrel = 1), the sweeps use H = I, the backward sweep applies
+    // −U⁻¹ (packed per knot in Ui, per-trajectory stride sU) to the residual, and info already
+    // holds −(k+1) for a non-SPD H_k
+    int hfac, yrel;
+    const T *Ui;
+    int64_t sU;
 };
 
 // padded row → row of Y (−1 for a padding row)
@@ -342,7 +356,8 @@ __global__ void __launch_bounds__(KB_THREADS, sizeof(T) == 4 ? 2 : 1) kkt_big_fw
     T *vc = lds + a.oV, *vd = vc + 64, *vlp = vd + 64, *vmu = vlp + 64, *vla = vmu + 64, *vt1 = vla + 64,
       *vt2 = vt1 + 64, *rn = vt2 + 64;
     int *flag = (int *)(rn + KB_RMAX);
-    const T *Yt = a.Y + t * a.sY, *yt = a.y + t * a.sy, *Ht = a.H + t * a.sH, *gt = a.g + t * a.sg;
+    const int64_t ty = a.yrel ? (int64_t)blockIdx.x : t;          // Y / g: the caller's or Z, gz
+    const T *Yt = a.Y + ty * a.sY, *yt = a.y + t * a.sy, *Ht = a.H + t * a.sH, *gt = a.g + ty * a.sg;
     T *St = a.slab + (int64_t)blockIdx.x * a.sS;
     const int N = a.N;
     int info = 0;
@@ -377,7 +392,7 @@ __global__ void __launch_bounds__(KB_THREADS, sizeof(T) == 4 ? 2 : 1) kkt_big_fw
         }
         if (tid < 16) {
             const int cc = 16 * s + tid;
-            preh = cc < q.w ? (a.ginv ? (T)1 / Ht[q.oH + cc] : (T)1) : (T)0;
+            preh = cc < q.w ? ((a.ginv && !a.hfac) ? (T)1 / Ht[q.oH + cc] : (T)1) : (T)0;
             preg = (cc < q.w && a.ginv) ? gt[q.og + cc] : (T)0;
         }
     };
@@ -647,7 +662,13 @@ __global__ void __launch_bounds__(KB_THREADS, sizeof(T) == 4 ? 2 : 1) kkt_big_fw
         }
         q0 = q1;
     }
-    if (tid == 0 && a.info) a.info[t] = info;
+    if (tid == 0 && a.info) {
+        if (a.hfac) {
+            if (a.info[t] == 0) a.info[t] = info;   // a non-SPD H_k (−(k+1)) takes precedence
+        } else {
+            a.info[t] = info;
+        }
+    }
 }
 
 // ---------------------------------------------------------------- backward sweep + primals
@@ -662,9 +683,17 @@ __global__ void __launch_bounds__(KB_THREADS) kkt_big_bwd_kernel(KbArgs<T> a)
     T *Yl = lds + a.oYl, *Wl = lds + a.oWl;
     const T *Bl = nullptr, *El = nullptr;   // Binv, Ẽ: read from the slab (end knots only)
     T *xm = lds + a.oV2, *xl = xm + 64, *tv = xl + 64, *hv = tv + KB_WMAX, *gv = hv + KB_WMAX, *vv = gv + KB_WMAX,
-      *zv = vv + 64, *nl = zv + 64, *ev = nl + 64, *nm = ev + 64, *fm = nm + 64, *fl = fm + 64;
-    const T *Yt = a.Y + t * a.sY, *Ht = a.H + t * a.sH, *gt = a.g + t * a.sg;
+      *zv = vv + KB_WMAX, *nl = zv + 64, *ev = nl + 64, *nm = ev + 64, *fm = nm + 64, *fl = fm + 64;
+    const int64_t ty = a.yrel ? (int64_t)blockIdx.x : t;
+    const T *Yt = a.Y + ty * a.sY, *Ht = a.H + t * a.sH, *gt = a.g + ty * a.sg;
     T *dzt = a.dz + t * a.sg, *lat = a.lam + t * a.sy;
+    const T *Ut = a.hfac ? a.Ui + (int64_t)blockIdx.x * a.sU : nullptr;
+    int64_t oU = 0;
+    if (a.hfac)
+        for (int k = 0; k < N; ++k) {
+            const int w = a.meta[8 * k + 3];
+            oU += (int64_t)w * (w + 1) / 2;
+        }
     const T *St = a.slab + (int64_t)blockIdx.x * a.sS;
 
     int64_t oS = 0;
@@ -725,7 +754,7 @@ __global__ void __launch_bounds__(KB_THREADS) kkt_big_bwd_kernel(KbArgs<T> a)
                 }
             }
             if (tid < qj.w) {
-                hv[tid] = a.ginv ? (T)1 / Ht[qj.oH + tid] : (T)1;
+                hv[tid] = (a.ginv && !a.hfac) ? (T)1 / Ht[qj.oH + tid] : (T)1;
                 gv[tid] = a.ginv ? gt[qj.og + tid] : (T)0;
             }
         }
@@ -808,18 +837,112 @@ __global__ void __launch_bounds__(KB_THREADS) kkt_big_bwd_kernel(KbArgs<T> a)
             s += __shfl_xor(s, 1);
             if (c < qj.w && h == 0) {
                 const T res = tv[c] + s + gv[c];
-                dzt[qj.og + c] = -(res * hv[c]);
+                if (a.hfac) vv[c] = res;                 // δz = −U⁻¹(Zᵀλ + U⁻ᵀg) below
+                else dzt[qj.og + c] = -(res * hv[c]);
             }
         }
         __syncthreads();
+        if (a.hfac) {
+            // δz = −H⁻¹ res = −U⁻¹ (U⁻ᵀ res'), res' already U⁻ᵀ-applied: row dots on packed U⁻¹
+            oU -= (int64_t)qj.w * (qj.w + 1) / 2;
+            const T *Uk = Ut + oU;
+            const int i = tid >> 1, h = tid & 1;
+            T s = (T)0;
+            if (i < qj.w)
+                for (int c = i + h; c < qj.w; c += 2) s = fma(Uk[c * (c + 1) / 2 + i], vv[c], s);
+            s += __shfl_xor(s, 1);
+            if (i < qj.w && h == 0) dzt[qj.og + i] = -s;
+            __syncthreads();
+        }
         qj = qp;
     }
+}
+
+// ---------------------------------------------------------------- dense / block-diagonal H
+// kkt_big_hfac_kernel (BlockCholesky dense and block-diagonal modes, block_cholesky.jl:55-77,
+// 145-153): per trajectory and knot, H_k = UᵀU (potrf 'U'; a non-positive pivot → info =
+// −(k+1), as the oracle reports it) → U⁻¹ (chol_inv, up to 8 diagonal blocks), then
+//   Z_k = Y_k U⁻¹   so that Z Zᵀ = Y H⁻¹ Yᵀ (shur!'s YYt, jacobian_blocks.jl:234-240),
+//   gz_k = U⁻ᵀ g_k  so that Z gz = Y H⁻¹ g (:236) and the residual Zᵀλ + gz = U⁻ᵀ(Yᵀλ + g),
+// with U⁻¹ kept (packed) for the backward sweep's δz = −U⁻¹(Zᵀλ + gz) (calc_primals!,
+// cholesky_solver.jl:195-199).  The sweeps then run with H = I on (Z, gz).
+template <typename T>
+struct KhArgs {
+    const T *Y, *H, *g;
+    T *Z, *gz, *Ui;
+    int32_t *info;
+    const int32_t *meta;
+    int N, LDH;
+    int64_t b0, sY, sH, sg, sU;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(KB_THREADS, 1) kkt_big_hfac_kernel(KhArgs<T> a)
+{
+    extern __shared__ __align__(16) unsigned char kb_lds_raw[];
+    T *X = (T *)kb_lds_raw;
+    int *flag = (int *)(X + a.LDH * KB_WMAX);
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6),
+              i16 = lane & 15, g4 = lane >> 4;
+    const int64_t t = a.b0 + blockIdx.x, c = blockIdx.x;
+    const int LDH = a.LDH;
+    const T *Yt = a.Y + t * a.sY, *Ht = a.H + t * a.sH, *gt = a.g + t * a.sg;
+    T *Zt = a.Z + c * a.sY, *gzt = a.gz + c * a.sg, *Ut = a.Ui + c * a.sU;
+    int hfail = 0;
+    int64_t oU = 0;
+    for (int k = 0; k < a.N; ++k) {
+        const Kn q = kn_load(a.meta, k);
+        const int w = q.w, W16 = r16(w), rows = q.rows;
+        for (int e = tid; e < W16 * W16; e += KB_THREADS) {
+            const int j = e / W16, i = e - j * W16;
+            X[i + j * LDH] = (i < w && j < w) ? Ht[q.oH + i + j * w] : (T)0;
+        }
+        __syncthreads();
+        const int bad = chol_inv<T, 8>(X, LDH, w, W16, flag, tid);
+        if (bad && !hfail) hfail = k + 1;
+        {   // gz = U⁻ᵀ g
+            const int i = tid >> 1, h = tid & 1;
+            T s = (T)0;
+            if (i < w)
+                for (int kk = h; kk <= i; kk += 2) s = fma(X[kk + i * LDH], gt[q.og + kk], s);
+            s += __shfl_xor(s, 1);
+            if (i < w && h == 0) gzt[q.og + i] = s;
+        }
+        for (int j = wave; j < w; j += 4)
+            for (int i = lane; i <= j; i += 64) Ut[oU + j * (j + 1) / 2 + i] = X[i + j * LDH];
+        // Z = Y U⁻¹ (rows × w): A = Y from global (column-major, ld rows), B = U⁻¹ from LDS
+        const int RT = (rows + 15) >> 4, WT = W16 >> 4;
+        for (int qq = wave; qq < RT * WT; qq += 4) {
+            const int I = qq / WT, J = qq - I * WT, row = 16 * I + i16;
+            acc_t<T> cc = tzero<T>();
+            for (int kt = 0; kt <= J; ++kt) {
+#pragma unroll
+                for (int s2 = 0; s2 < 4; ++s2) {
+                    const int kk = 16 * kt + 4 * s2 + g4;
+                    const T av = (row < rows && kk < w) ? Yt[q.oY + row + kk * rows] : (T)0;
+                    const T bv = X[kk + (16 * J + i16) * LDH];
+                    cc = Tile<T>::mma(av, bv, cc);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int rr = 16 * I + Tile<T>::row(lane, r), col = 16 * J + i16;
+                if (rr < rows && col < w) Zt[q.oY + rr + col * rows] = cc[r];
+            }
+        }
+        oU += (int64_t)w * (w + 1) / 2;
+        __syncthreads();
+    }
+    if (tid == 0 && a.info) a.info[t] = hfail ? -hfail : 0;
 }
 
 // ---------------------------------------------------------------- host: plan and launch
 struct KbPlan {
     int PM, LD, LDY, LDB, maxrows, maxw, blk;
     int64_t S;                      // slab elements per trajectory
+    bool hfac;                      // dense / block-diagonal H with ginv: the hfac pre-pass
+    int LDH, nh;                    // its LDS leading dimension and size (elements)
+    int64_t sU;                     // packed U⁻¹ elements per trajectory
     int oWp, oBlk, oSl, oV, nf;     // fwd LDS (elements)
     int oYl, oWl, oV2, nb;          // bwd LDS (elements)
 };
@@ -828,9 +951,10 @@ struct KbPlan {
 bool kb_plan(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2, const int32_t *w, int tsize,
              KbPlan &P)
 {
-    if (a.layout != 0 || (a.ginv && a.h_mode != 2) || a.N < 1) return false;
+    if (a.layout != 0 || a.N < 1) return false;
+    P.hfac = a.ginv && a.h_mode != 2;
     int PM = 16, RM = 16, maxrows = 1, maxw = 1, PMW = 0;
-    int64_t S = 0;
+    int64_t S = 0, sU = 0;
     for (int k = 0; k < a.N; ++k) {
         if (n1[k] > KB_PMAX || p[k] > KB_PMAX || n2[k] > KB_PMAX || w[k] > KB_WMAX) return false;
         const int P1 = r16(n1[k]), Ps = r16(p[k]), P2 = r16(n2[k]), R = P1 + Ps + P2;
@@ -841,6 +965,7 @@ bool kb_plan(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_
         maxw = std::max(maxw, w[k]);
         PMW = std::max(PMW, P2);
         S += slab_size(Ps, P2);
+        sU += (int64_t)w[k] * (w[k] + 1) / 2;
     }
     // bank-conflict pads (MI355X LDS: 64 banks × 4 B): tile operands read as (lane·ld + group)
     P.PM = PM;
@@ -865,10 +990,13 @@ bool kb_plan(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_
     o = (o + 3) & ~3;
     P.oWl = o; o += std::max(1, PMW * (PMW + 1) / 2);
     o = (o + 3) & ~3;
-    P.oV2 = o; o += 2 * 64 + 3 * KB_WMAX + 7 * 64;
+    P.oV2 = o; o += 2 * 64 + 4 * KB_WMAX + 6 * 64;
     P.nb = o;
+    P.sU = P.hfac ? sU : 0;
+    P.LDH = r16(maxw) + 4;
+    P.nh = P.hfac ? P.LDH * KB_WMAX + 4 : 0;
     constexpr size_t LDS_CAP = 160 * 1024;
-    return (size_t)P.nf * tsize <= LDS_CAP && (size_t)P.nb * tsize <= LDS_CAP;
+    return (size_t)P.nf * tsize <= LDS_CAP && (size_t)P.nb * tsize <= LDS_CAP && (size_t)P.nh * tsize <= LDS_CAP;
 }
 
 size_t kb_slab_cap()    // LQRX_KKT_BIG_SLAB_MB bounds the stream-ordered slab (default 24 GiB)
@@ -880,27 +1008,44 @@ size_t kb_slab_cap()    // LQRX_KKT_BIG_SLAB_MB bounds the stream-ordered slab (
     return v;
 }
 
+// scratch elements per trajectory: the slab, plus Z, gz and packed U⁻¹ for a dense H
+int64_t kb_per_traj(const KktArgs &a, const KbPlan &P)
+{
+    return P.S + (P.hfac ? a.sY + a.sg + P.sU : 0);
+}
+
 int64_t kb_chunk(const KktArgs &a, const KbPlan &P, int tsize, size_t avail)
 {
-    const size_t per = (size_t)P.S * tsize;
+    const size_t per = (size_t)kb_per_traj(a, P) * tsize;
     return std::max<int64_t>(1, std::min<int64_t>(a.batch, (int64_t)(avail / std::max<size_t>(per, 1))));
 }
 
 template <typename T>
 hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
 {
-    const size_t per = (size_t)P.S * sizeof(T);
+    const size_t per = (size_t)kb_per_traj(a, P) * sizeof(T);
     const int64_t chunk = kb_chunk(a, P, sizeof(T), a.ws ? a.ws_bytes : kb_slab_cap());
     Scratch sc;
     hipError_t e = sc.get(a, (size_t)chunk * per, s);
     if (e != hipSuccess) return e;
     const size_t lf = (size_t)P.nf * sizeof(T), lb = (size_t)P.nb * sizeof(T);
+    const size_t lh = (size_t)P.nh * sizeof(T);
     if ((e = hipFuncSetAttribute((const void *)kkt_big_fwd_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)lf)) != hipSuccess ||
         (e = hipFuncSetAttribute((const void *)kkt_big_bwd_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)lb)) != hipSuccess) {
+                                 (int)lb)) != hipSuccess ||
+        (P.hfac && (e = hipFuncSetAttribute((const void *)kkt_big_hfac_kernel<T>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lh)) != hipSuccess)) {
         (void)sc.release(s);
         return e;
+    }
+    // scratch: [slab chunk·S][Z chunk·sY][gz chunk·sg][U⁻¹ chunk·sU]
+    T *slab = (T *)sc.p, *Z = slab + chunk * P.S, *gz = Z + chunk * a.sY, *Ui = gz + chunk * a.sg;
+    KhArgs<T> h{};
+    if (P.hfac) {
+        h.Y = (const T *)a.Y; h.H = (const T *)a.H; h.g = (const T *)a.g;
+        h.Z = Z; h.gz = gz; h.Ui = Ui; h.info = a.info; h.meta = a.meta; h.N = a.N; h.LDH = P.LDH;
+        h.sY = a.sY; h.sH = a.sH; h.sg = a.sg; h.sU = P.sU;
     }
     KbArgs<T> k{};
     k.Y = (const T *)a.Y; k.y = (const T *)a.y; k.H = (const T *)a.H; k.g = (const T *)a.g;
@@ -910,9 +1055,17 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
     k.LD = P.LD; k.LDY = P.LDY; k.LDB = P.LDB;
     k.oWp = P.oWp; k.oBlk = P.oBlk; k.oSl = P.oSl; k.oV = P.oV;
     k.oYl = P.oYl; k.oWl = P.oWl; k.oV2 = P.oV2;
+    k.slab = slab;
+    if (P.hfac) {
+        k.hfac = 1; k.yrel = 1; k.Y = Z; k.g = gz; k.Ui = Ui; k.sU = P.sU;
+    }
     for (int64_t b0 = 0; b0 < a.batch && e == hipSuccess; b0 += chunk) {
         const int64_t nb = std::min<int64_t>(chunk, a.batch - b0);
         k.b0 = b0;
+        if (P.hfac) {
+            h.b0 = b0;
+            hipLaunchKernelGGL(kkt_big_hfac_kernel<T>, dim3((unsigned)nb), dim3(KB_THREADS), lh, s, h);
+        }
         hipLaunchKernelGGL(kkt_big_fwd_kernel<T>, dim3((unsigned)nb), dim3(KB_THREADS), lf, s, k);
         hipLaunchKernelGGL(kkt_big_bwd_kernel<T>, dim3((unsigned)nb), dim3(KB_THREADS), lb, s, k);
         e = hipGetLastError();
@@ -935,7 +1088,7 @@ size_t kkt_big_scratch_bytes(const KktArgs &a, const int32_t *n1, const int32_t 
     KbPlan P;
     const int ts = a.dtype == 1 ? 4 : 8;
     if (!kb_plan(a, n1, p, n2, w, ts, P)) return 0;
-    return (size_t)kb_chunk(a, P, ts, kb_slab_cap()) * (size_t)P.S * ts;
+    return (size_t)kb_chunk(a, P, ts, kb_slab_cap()) * (size_t)kb_per_traj(a, P) * ts;
 }
 
 hipError_t kkt_big_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,

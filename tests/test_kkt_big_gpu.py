@@ -219,3 +219,52 @@ def test_big_kkt_slab_chunks(lqrx, gpu_ok, tmp_path):
     env = dict(os.environ, LQRX_KKT_BIG_SLAB_MB="0")     # 0 MB → one trajectory per chunk
     p = subprocess.run([sys.executable, str(f), root], env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
+
+
+@pytest.mark.parametrize("n,m,N,h_mode", [(5, 2, 101, 0), (7, 3, 41, 1), (6, 3, 33, 0), (16, 8, 21, 0),
+                                          (32, 16, 13, 1), (64, 32, 9, 0)])
+def test_big_kkt_dense_h(lqrx, gpu_ok, n, m, N, h_mode):
+    """Dense (h_mode 0) and block-diagonal (1) cost Hessians (BlockCholesky, block_cholesky.jl:
+    55-77) on the large-block path: the hfac pre-pass factors each H_k (w up to 96 here, eight
+    16-blocks), the sweeps run on Z = Y U⁻¹ and gz = U⁻ᵀg, and δz = −U⁻¹(Zᵀλ + gz).  Covers the
+    structures the scratch-spilling lane<8,8,8,12,16> kernel used to serve with a dense H."""
+    import lqrx.kkt as K
+
+    st = K.trajectory_structure(n, m, N)
+    pb = K.random_kkt(st, 4, seed=n + N + h_mode, h_mode=h_mode, dyn="dense" if n >= 8 else "small")
+    got = K.kkt_solve(pb)
+    ref = _ref(st, pb)
+    assert got["rc"] == 0 and (got["info"] == 0).all()
+    assert traj_rel(got["dz"], ref["dz"]) <= TOL
+    assert traj_rel(got["lam"], ref["lam"]) <= TOL
+
+
+def test_big_kkt_dense_h_f32(lqrx, gpu_ok):
+    """fp32 with a dense H (n=32, m=16: w = 48)."""
+    import lqrx.kkt as K
+
+    st = K.trajectory_structure(32, 16, 33)
+    pb = _round32(K.random_kkt(st, 3, seed=5, h_mode=K.H_DENSE, dyn="dense"))
+    got = K.kkt_solve(pb, dtype=lqrx.F32)
+    ref = _ref(st, pb)
+    assert got["rc"] == 0 and (got["info"] == 0).all()
+    e = max(traj_rel(got["dz"], ref["dz"]), traj_rel(got["lam"], ref["lam"]))
+    print(f"fp32 dense H: max rel err {e:.3e}")
+    assert e <= F32_TOL
+
+
+def test_big_kkt_dense_h_info(lqrx, gpu_ok):
+    """A non-SPD H_k reports info = −(k+1) for its first knot (the oracle's convention; the
+    reference's potrf! at block_cholesky.jl:63 discards it), ahead of any Schur failure."""
+    import lqrx.kkt as K
+
+    st = K.trajectory_structure(16, 8, 15)
+    pb = K.random_kkt(st, 3, seed=9, h_mode=K.H_DENSE, dyn="dense")
+    w = st.w.astype(int)
+    o = int(np.sum(w[:6] * w[:6]))
+    pb.H[2, o:o + w[6] * w[6]] *= -1.0                   # H at knot 6 (0-based) of trajectory 2
+    got = K.kkt_solve(pb)
+    ref = _ref(st, pb)
+    assert ref["info"][2] == -7
+    assert list(got["info"]) == list(ref["info"])
+    assert traj_rel(got["dz"][:2], ref["dz"][:2]) <= TOL
