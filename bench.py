@@ -60,30 +60,50 @@ def _dp_kernel_name(n, m, bt, tv):
     return "dp_riccati_kernel"
 
 
-def cpu_baseline(n, m, N, target_s=12.0, threads=None):
+def cpu_baseline(n, m, N, target_s=12.0, threads=None, tv=False, linear=False):
     """Time the CPU oracle (C restatement of dynamic_programming.jl, OpenMP over the batch)
-    on a bounded sample of the same workload; returns traj/s and the sample description."""
+    on a bounded sample of the same workload; returns traj/s and the sample description.
+    tv: per-knot A_k, B_k, Q_k, R_k streamed by the oracle (oracle_dp_solve_batch_tv with
+    tv_AB = tv_QR = 1); linear: the q, r, qf terms (oracle_dp_solve_one_lin) — the same
+    problem class the GPU line solves."""
     import numpy as np
     import lqrx
     from oracle import oracle as orc
 
     threads = threads or max(1, min(16, os.cpu_count() or 1))
     orc.load()
+
+    def problem(bt):
+        d = lqrx.random_batch(n, m, N, bt, seed=20260104)
+        if linear:
+            rng = np.random.default_rng(7)
+            d.update(q=rng.standard_normal(bt * n), r=rng.standard_normal(bt * m),
+                     qf=rng.standard_normal(bt * n))
+        if tv:
+            for k in ("A", "B", "Q", "R") + (("q", "r") if linear else ()):
+                v = np.asarray(d[k]).reshape(bt, 1, -1)
+                d[k] = np.ascontiguousarray(np.broadcast_to(v, (bt, N - 1, v.shape[-1]))).ravel()
+            d.update(tv_AB=1, tv_QR=1)
+        return d
+
+    solve = orc.dp_solve_lin_abi if linear else orc.dp_solve_abi
     probe = threads * 2
-    d = lqrx.random_batch(n, m, N, probe, seed=20260104)
+    d = problem(probe)
     t0 = time.perf_counter()
-    orc.dp_solve_abi(d, N, nthreads=threads)
+    solve(d, N, nthreads=threads)
     dt = time.perf_counter() - t0
     per = dt / probe
-    sample = int(max(probe, min(65536, target_s / max(per, 1e-9))))
+    sample = int(max(probe, min(65536 if not tv else 8192, target_s / max(per, 1e-9))))
     sample = (sample // threads) * threads or threads
-    d = lqrx.random_batch(n, m, N, sample, seed=20260104)
+    d = problem(sample)
     t0 = time.perf_counter()
-    orc.dp_solve_abi(d, N, nthreads=threads)
+    solve(d, N, nthreads=threads)
     dt = time.perf_counter() - t0
+    what = ", ".join(w for w, on in (("time-varying per-knot A_k B_k Q_k R_k", tv),
+                                     ("linear cost terms q r qf", linear)) if on)
     return dict(value=sample / dt, unit="trajectories/s", cores=threads, kind="port",
-                sample=f"{sample} trajectories of n={n} m={m} N={N} fp64, oracle/lqr_oracle.c "
-                       f"(op-for-op C restatement of dynamic_programming.jl), OpenMP "
+                sample=f"{sample} trajectories of n={n} m={m} N={N} fp64{' (' + what + ')' if what else ''}, "
+                       f"oracle/lqr_oracle.c (op-for-op C restatement of dynamic_programming.jl), OpenMP "
                        f"{threads} threads, {dt:.1f} s")
 
 
@@ -746,7 +766,7 @@ def main(argv=None):
                 workload = (("random dense time-varying LQR (SURVEY §8(f) rank 1)" if args.tv else
                              "random dense time-invariant LQR") + ", Riccati backward pass + forward rollout"
                             + (" (BASELINE.json configs[4], per GPU)" if cfg5 else " (non-baseline shape)"))
-            cpu = cpu_baseline(n, m, N, target_s=args.cpu_seconds) \
+            cpu = cpu_baseline(n, m, N, target_s=args.cpu_seconds, tv=args.tv, linear=args.linear) \
                 if not args.no_cpu_baseline and world == 1 else None
         if tsrc is not None:
             roof.setdefault("traffic_source", tsrc)

@@ -103,8 +103,11 @@ int main()
     CHECK(lqrx_kkt_workspace_size(&k, nullptr) == -2);
     lqrx_kkt_desc kb = k; kb.h_mode = 3;
     CHECK(lqrx_kkt_sizes(&kb, &nY, nullptr, nullptr, nullptr, nullptr) == -1);
-    kb = k; kb.dtype = LQRX_F32;
-    CHECK(lqrx_kkt_sizes(&kb, &nY, nullptr, nullptr, nullptr, nullptr) == LQRX_ERR_UNSUPPORTED);
+    kb = k; kb.dtype = LQRX_F32;                               // fp32: the large-block kernels
+    CHECK(lqrx_kkt_sizes(&kb, &nY, nullptr, nullptr, nullptr, nullptr) == 0);
+    CHECK(lqrx_kkt_workspace_size(&kb, &ws) == 0 && ws > 0);
+    kb = k; kb.dtype = 7;
+    CHECK(lqrx_kkt_sizes(&kb, &nY, nullptr, nullptr, nullptr, nullptr) == -1);
     std::vector<int32_t> bad = n1;
     bad[7] = 2;                                                 // n1[k] != n2[k-1]
     kb = k; kb.n1 = bad.data();

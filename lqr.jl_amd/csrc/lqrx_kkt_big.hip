@@ -44,10 +44,50 @@
 #include "lqrx_internal.h"
 #include "lqrx_tile.h"
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
+#include <utility>
 
 namespace lqrx {
 namespace {
+
+// timing ablations (tools/tv_ablate.sh builds; results are wrong by design): bit 1 the 16×16
+// leaf returns at once, 2 no Schur MFMAs, 4 no forward substitution, 8 no slab stores,
+// 16 no chol_inv at all
+#ifndef KB_ABL
+#define KB_ABL 0
+#endif
+
+// KB_PROF builds (timing only): per-phase shader-clock cycles of the forward sweep summed
+// into KbArgs::prof[wave][phase] (0 prefactor, 1 factor wave, 2 Schur waves, 3 step barrier,
+// 4 hand-over)
+#ifdef KB_PROF
+#define KB_T0() int64_t kb_t0 = clock64()
+#define KB_T(i)                                                                                             \
+    do {                                                                                                    \
+        const int64_t kb_t1 = clock64();                                                                    \
+        kb_acc[i] += kb_t1 - kb_t0;                                                                         \
+        kb_t0 = kb_t1;                                                                                      \
+    } while (0)
+#define KB_F0() int64_t kb_f0 = clock64()
+#define KB_F(i)                                                                                             \
+    do {                                                                                                    \
+        const int64_t kb_f1 = clock64();                                                                    \
+        kb_acc[i] += kb_f1 - kb_f0;                                                                         \
+        kb_f0 = kb_f1;                                                                                      \
+    } while (0)
+#define KB_FLUSH()                                                                                          \
+    do {                                                                                                    \
+        if (lane == 0 && a.prof)                                                                            \
+            for (int i_ = 0; i_ < 10; ++i_) atomicAdd((unsigned long long *)&a.prof[wave * 16 + i_], (unsigned long long)kb_acc[i_]); \
+    } while (0)
+#else
+#define KB_T0()
+#define KB_T(i)
+#define KB_F0()
+#define KB_F(i)
+#define KB_FLUSH()
+#endif
 
 constexpr int KB_THREADS = 256;
 constexpr int KB_PMAX = 64;    // n1, p, n2 per knot
@@ -55,7 +95,9 @@ constexpr int KB_RMAX = 128;   // padded rows P1 + Ps + P2
 constexpr int KB_WMAX = 128;   // width
 constexpr int KB_MAXT = 9;     // Schur tiles per wave: 36 upper tiles of an 8×8 grid / 4 waves
 constexpr int KB_F1T = 8;      // factor-phase tiles per wave (D̃ + F̃: 2·16 tiles / 4 waves)
-constexpr int KB_LDY = 144;    // Y-slab column stride: ≥ 128 rows, ≡ 16 (mod 64) floats / (mod 32) doubles
+constexpr int KB_LDY = 144;
+constexpr int KB_BPRE = KB_RMAX * KB_WMAX / 256;   // backward: Y_k elements per thread (≤ 64)
+constexpr int KB_WPRE = 9;                         // backward: packed W elements per thread (≤ 2080/256)    // Y-slab column stride: ≥ 128 rows, ≡ 16 (mod 64) floats / (mod 32) doubles
 
 __host__ __device__ __forceinline__ int r16(int x) { return (x + 15) & ~15; }
 
@@ -132,6 +174,37 @@ __device__ __forceinline__ acc_t<T> tmm(acc_t<T> c, const T *A, int lda, const T
     return c;
 }
 
+// the same with a compile-time contraction length KT·16: every operand load is issued before
+// the MFMAs (the compiler can also interleave independent calls)
+template <typename T, bool TA, bool TB, bool NEG, int KT>
+__device__ __forceinline__ acc_t<T> tmmk(acc_t<T> c, const T *A, int lda, const T *B, int ldb, int lane)
+{
+    const int i = lane & 15, g = lane >> 4;
+    const T *pa = TA ? A + g + i * lda : A + i + g * lda;
+    const T *pb = TB ? B + i + g * ldb : B + g + i * ldb;
+    const int sa = TA ? 4 : 4 * lda, sb = TB ? 4 * ldb : 4;
+    T a[4 * KT], b[4 * KT];
+#pragma unroll
+    for (int s = 0; s < 4 * KT; ++s) {
+        a[s] = pa[s * sa];
+        b[s] = pb[s * sb];
+    }
+#pragma unroll
+    for (int s = 0; s < 4 * KT; ++s) c = NEG ? Tile<T>::mma_nega(a[s], b[s], c) : Tile<T>::mma(a[s], b[s], c);
+    return c;
+}
+// runtime KT (1..4) → compile-time instance
+template <typename T, bool TA, bool TB, bool NEG>
+__device__ __forceinline__ acc_t<T> tmm4(acc_t<T> c, const T *A, int lda, const T *B, int ldb, int kt, int lane)
+{
+    switch (kt) {
+    case 1: return tmmk<T, TA, TB, NEG, 1>(c, A, lda, B, ldb, lane);
+    case 2: return tmmk<T, TA, TB, NEG, 2>(c, A, lda, B, ldb, lane);
+    case 3: return tmmk<T, TA, TB, NEG, 3>(c, A, lda, B, ldb, lane);
+    default: return tmmk<T, TA, TB, NEG, 4>(c, A, lda, B, ldb, lane);
+    }
+}
+
 template <typename T>
 __device__ __forceinline__ acc_t<T> tload(const T *X, int ld, int lane)
 {
@@ -176,9 +249,10 @@ __device__ __forceinline__ acc_t<T> tmm_reg(acc_t<T> c, const T *A, int ld, acc_
 // not positive (potrf's info), else 0.  Mirrors dpotf2 'U' (dynamic_programming.jl:29,
 // cholesky_solve.jl:2) up to the rsqrt-multiply instead of sqrt-divide.
 template <typename T>
-__device__ int leaf_chol_inv(T *X, int ld, int q, int lane)
+__device__ __forceinline__ int leaf_chol_inv(T *X, int ld, int q, int lane)
 {
     const int c = lane & 15;
+    if (KB_ABL & 1) return 0;
     T col[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) col[r] = X[r + c * ld];
@@ -237,6 +311,7 @@ template <typename T, int NBM = 4>
 __device__ int chol_inv(T *X, int LD, int p, int P, int *flag, int tid)
 {
     const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), nb = P >> 4;
+    if (KB_ABL & 16) return 0;
     for (int i = p + tid; i < P; i += KB_THREADS) X[i + i * LD] = (T)1;   // identity padding
     if (tid == 0) *flag = 0;
     __syncthreads();
@@ -324,6 +399,7 @@ struct KbArgs {
     int hfac, yrel;
     const T *Ui;
     int64_t sU;
+    int64_t *prof;                 // KB_PROF builds: [4 waves][8] cycle sums
 };
 
 // padded row → row of Y (−1 for a padding row)
@@ -341,328 +417,490 @@ __device__ __forceinline__ int part_of(const Kn &q, int I)
     return r < q.P1 ? 0 : (r < q.P1 + q.Ps ? 1 : 2);
 }
 
+// ---------------------------------------------------------------- single-wave factor tools
+// chol_inv on ONE wave (the factor wave of the forward sweep): the same blocked algorithm,
+// wave-level ordering only (no workgroup barriers).  The inverse is assembled from the last
+// block column down: column J reads U_IL (L ≤ J) of rows I < J and writes W_IJ, which the
+// columns after it (smaller J) never read.  Returns 0 or 1 + the first non-positive pivot.
+template <typename T>
+__device__ int chol_inv_w(T *X, int LD, int p, int P, int lane)
+{
+    const int nb = P >> 4;
+    for (int i = p + lane; i < P; i += 64) X[i + i * LD] = (T)1;
+    int bad = 0;
+    for (int jb = 0; jb < nb; ++jb) {
+        T *Xjj = X + 16 * jb * (1 + LD);
+        const int b = leaf_chol_inv<T>(Xjj, LD, min(16, p - 16 * jb), lane);
+        if (b && !bad) bad = 16 * jb + b;
+        for (int J = jb + 1; J < nb; ++J) {
+            T *Xj = X + 16 * jb + 16 * J * LD;
+            tstore(Xj, LD, tmm<T, true, false, false>(tzero<T>(), Xjj, LD, Xj, LD, 16, lane), lane);
+        }
+        for (int I = jb + 1; I < nb; ++I)
+            for (int J = I; J < nb; ++J) {
+                T *Xij = X + 16 * I + 16 * J * LD;
+                tstore(Xij, LD,
+                       tmm<T, true, false, true>(tload(Xij, LD, lane), X + 16 * jb + 16 * I * LD, LD,
+                                                 X + 16 * jb + 16 * J * LD, LD, 16, lane),
+                       lane);
+            }
+    }
+    for (int J = nb - 1; J >= 1; --J) {
+        acc_t<T> w[4];
+        inv_column<T, 4>(X, LD, J, lane, w);
+#pragma unroll
+        for (int I = 0; I < 3; ++I)
+            if (I < J) tstore(X + 16 * I + 16 * J * LD, LD, w[I], lane);
+    }
+    return bad;
+}
+
+// out[i] = init[i] ± Σ_{k<K(i)} M[k + i·ld]·x[k] for i < n ≤ 64, one lane per output
+// (TRI: K(i) = min(K, i + 1): Mᵀx for upper-triangular M); in place (out == init) is fine
+template <typename T, bool TRI, bool NEG>
+__device__ __forceinline__ void coldot_w(T *out, const T *init, const T *M, int ld, const T *x, int K, int n, int lane)
+{
+    if (lane < n) {
+        const int Ki = TRI ? min(K, lane + 1) : K;
+        const T *mc = M + lane * ld;
+        T s0 = (T)0, s1 = (T)0, s2 = (T)0, s3 = (T)0;
+        int k = 0;
+        for (; k + 3 < Ki; k += 4) {
+            s0 = fma(mc[k], x[k], s0);
+            s1 = fma(mc[k + 1], x[k + 1], s1);
+            s2 = fma(mc[k + 2], x[k + 2], s2);
+            s3 = fma(mc[k + 3], x[k + 3], s3);
+        }
+        for (; k < Ki; ++k) s0 = fma(mc[k], x[k], s0);
+        const T sum = (s0 + s1) + (s2 + s3);
+        out[lane] = init ? (NEG ? init[lane] - sum : init[lane] + sum) : (NEG ? -sum : sum);
+    }
+}
+
+// ---------------------------------------------------------------- Schur pieces (3 waves)
+// Upper 16×16 tiles of Y H⁻¹ Yᵀ over a knot's padded row blocks (NBT of them), tile q (row-
+// major over I ≤ J) owned by Schur wave q mod 3; compile-time per (NBT, wave), so the row-block
+// fragments a wave needs are registers with static indices.
+__host__ __device__ constexpr int tm_I(int nbt, int q)
+{
+    int I = 0;
+    while (q >= nbt - I) {
+        q -= nbt - I;
+        ++I;
+    }
+    return I;
+}
+__host__ __device__ constexpr int tm_J(int nbt, int q)
+{
+    int I = 0;
+    while (q >= nbt - I) {
+        q -= nbt - I;
+        ++I;
+    }
+    return I + q;
+}
+constexpr int KB_ST = 12;      // Schur tiles per Schur wave: 36 / 3
+__host__ __device__ constexpr bool tm_need(int nbt, int si, int v)
+{
+    if (v % 3 == si) return true;                       // r = Y H⁻¹ g rows of block v
+    for (int q = si; q < nbt * (nbt + 1) / 2; q += 3)
+        if (tm_I(nbt, q) == v || tm_J(nbt, q) == v) return true;
+    return false;
+}
+
+// compile-time loop: f(std::integral_constant<int, i>) for i = 0 … N−1 (indices stay constant
+// expressions, so register arrays indexed by them never go to scratch)
+template <typename F, int... Is>
+__device__ __forceinline__ void sfor_(F &&f, std::integer_sequence<int, Is...>)
+{
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void sfor(F &&f)
+{
+    sfor_(f, std::make_integer_sequence<int, N>{});
+}
+
+// shur! (jacobian_blocks.jl:231-242) for knot q by Schur wave SI: this wave's tiles of
+// YYt = Y·(H⁻¹Yᵀ) into acc and its rows of r = Y H⁻¹ g into rn (padded row order), Y read
+// column by column straight from HBM (each k-step: one 4-column slice, lane = (row i, column
+// g) as the MFMA operand maps want), one slice prefetched ahead.
+template <typename T, int NBT, int SI>
+__device__ __forceinline__ void schur_part(const Kn &q, const T *Yt, const T *Ht, const T *gt, bool hinv, bool useg,
+                                           acc_t<T> (&acc)[KB_ST], T *rn, int lane)
+{
+    const int i16 = lane & 15, g4 = lane >> 4;
+    int rb[NBT], lim[NBT];
+#pragma unroll
+    for (int v = 0; v < NBT; ++v) {
+        const int r0 = 16 * v;
+        if (r0 < q.P1) {
+            rb[v] = r0;
+            lim[v] = q.p1 - r0;
+        } else if (r0 < q.P1 + q.Ps) {
+            rb[v] = q.p1 + r0 - q.P1;
+            lim[v] = q.ps - (r0 - q.P1);
+        } else {
+            rb[v] = q.p1 + q.ps + r0 - q.P1 - q.Ps;
+            lim[v] = q.p2 - (r0 - q.P1 - q.Ps);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < KB_ST; ++t) acc[t] = tzero<T>();
+    T rp[NBT];
+#pragma unroll
+    for (int v = 0; v < NBT; ++v) rp[v] = (T)0;
+    const int nks = (q.w + 3) >> 2;
+    const T *base = Yt + q.oY + i16;
+    auto load = [&](int s, T (&f)[NBT], T &h, T &gg) __attribute__((always_inline)) {
+        const int c = 4 * s + g4;
+        const bool ok = c < q.w;
+        const T *src = base + (int64_t)(ok ? c : 0) * q.rows;
+        sfor<NBT>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            if constexpr (tm_need(NBT, SI, v)) f[v] = (ok && i16 < lim[v]) ? src[rb[v]] : (T)0;
+        });
+        h = ok ? (hinv ? (T)1 / Ht[q.oH + c] : (T)1) : (T)0;
+        gg = (ok && useg) ? gt[q.og + c] : (T)0;
+    };
+    auto step = [&](const T (&f)[NBT], T h, T gg) __attribute__((always_inline)) {
+        sfor<KB_ST>([&](auto tc) {
+            constexpr int t = decltype(tc)::value, qq = SI + 3 * t;
+            if constexpr (qq < NBT * (NBT + 1) / 2) {
+                constexpr int I = tm_I(NBT, qq), J = tm_J(NBT, qq);
+                const T av = f[I];
+                const T bv = f[J] * h;
+                if (KB_ABL & 2) acc[t][0] += av * bv;
+                else acc[t] = Tile<T>::mma(av, bv, acc[t]);
+            }
+        });
+        sfor<NBT>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            if constexpr (v % 3 == SI) rp[v] = fma(f[v] * h, gg, rp[v]);
+        });
+    };
+    T fa[NBT], fb[NBT], ha = (T)0, hb = (T)0, ga = (T)0, gb = (T)0;
+#pragma unroll
+    for (int v = 0; v < NBT; ++v) fa[v] = fb[v] = (T)0;
+    load(0, fa, ha, ga);
+    for (int s = 0; s < nks; s += 2) {
+        if (s + 1 < nks) load(s + 1, fb, hb, gb);
+        step(fa, ha, ga);
+        if (s + 1 < nks) {
+            if (s + 2 < nks) load(s + 2, fa, ha, ga);
+            step(fb, hb, gb);
+        }
+    }
+    sfor<NBT>([&](auto vc) {
+        constexpr int v = decltype(vc)::value;
+        if constexpr (v % 3 == SI) {
+            T x = rp[v];
+            x += __shfl_xor(x, 16);
+            x += __shfl_xor(x, 32);
+            if (lane < 16) rn[16 * v + lane] = x;
+        }
+    });
+}
+
+// copy_shur! (:271-286): this wave's non-alias tiles of knot q into its LDS blocks
+template <typename T, int NBT, int SI>
+__device__ __forceinline__ void schur_store(const Kn &q, T *blk, int LD, const acc_t<T> (&acc)[KB_ST], int lane)
+{
+    const Bo b = blk_off(q.P1, q.Ps, q.P2, LD);
+    sfor<KB_ST>([&](auto tc) {
+        constexpr int t = decltype(tc)::value, qq = SI + 3 * t;
+        if constexpr (qq < NBT * (NBT + 1) / 2) {
+            constexpr int I = tm_I(NBT, qq), J = tm_J(NBT, qq);
+            const int pi = part_of(q, I), pj = part_of(q, J);
+            if (!(pi == 0 && pj == 0)) {                             // A: added into C_{k−1}
+                const int li = 16 * I - (pi == 0 ? 0 : pi == 1 ? q.P1 : q.P1 + q.Ps);
+                const int lj = 16 * J - (pj == 0 ? 0 : pj == 1 ? q.P1 : q.P1 + q.Ps);
+                const int o = pi == 0 ? (pj == 1 ? b.D : b.F) : pi == 1 ? (pj == 1 ? b.B : b.E) : b.C;
+                tstore(blk + o + li + lj * LD, LD, acc[t], lane);
+            }
+        }
+    });
+}
+
+// the A ≡ previous-C alias (:166, copy_shur! `A .+= YYt[p1, p1]`): knot q's D2 H⁻¹ D2ᵀ tiles
+// add into C of the knot before it (at LDS offset oC)
+template <typename T, int NBT, int SI>
+__device__ __forceinline__ void schur_addA(const Kn &q, T *Cprev, int LD, const acc_t<T> (&acc)[KB_ST], int lane)
+{
+    sfor<KB_ST>([&](auto tc) {
+        constexpr int t = decltype(tc)::value, qq = SI + 3 * t;
+        if constexpr (qq < NBT * (NBT + 1) / 2) {
+            constexpr int I = tm_I(NBT, qq), J = tm_J(NBT, qq);
+            if (16 * J < q.P1) tadd(Cprev + 16 * I + 16 * J * LD, LD, acc[t], lane);
+        }
+    });
+}
+
+// runtime NBT (1..8) and Schur-wave index (0..2) → the compile-time instances
+#define KB_NBT_SWITCH(nbt, CALL)                                                                            \
+    switch (nbt) {                                                                                          \
+    case 1: CALL(1); break;                                                                                 \
+    case 2: CALL(2); break;                                                                                 \
+    case 3: CALL(3); break;                                                                                 \
+    case 4: CALL(4); break;                                                                                 \
+    case 5: CALL(5); break;                                                                                 \
+    case 6: CALL(6); break;                                                                                 \
+    case 7: CALL(7); break;                                                                                 \
+    default: CALL(8); break;                                                                                \
+    }
+template <typename T, int SI>
+__device__ __forceinline__ void schur_part_d(const Kn &q, const T *Yt, const T *Ht, const T *gt, bool hinv, bool useg,
+                             acc_t<T> (&acc)[KB_ST], T *rn, int lane)
+{
+#define KB_C(NB) schur_part<T, NB, SI>(q, Yt, Ht, gt, hinv, useg, acc, rn, lane)
+    KB_NBT_SWITCH(q.R >> 4, KB_C)
+#undef KB_C
+}
+template <typename T, int SI>
+__device__ __forceinline__ void schur_store_d(const Kn &q, T *blk, int LD, const acc_t<T> (&acc)[KB_ST], int lane)
+{
+#define KB_C(NB) schur_store<T, NB, SI>(q, blk, LD, acc, lane)
+    KB_NBT_SWITCH(q.R >> 4, KB_C)
+#undef KB_C
+}
+template <typename T, int SI>
+__device__ __forceinline__ void schur_addA_d(const Kn &q, T *Cprev, int LD, const acc_t<T> (&acc)[KB_ST], int lane)
+{
+#define KB_C(NB) schur_addA<T, NB, SI>(q, Cprev, LD, acc, lane)
+    KB_NBT_SWITCH(q.R >> 4, KB_C)
+#undef KB_C
+}
+
 // ---------------------------------------------------------------- forward sweep
+// Per trajectory one workgroup of 4 waves.  At step k the "factor wave" (wave k mod 4, rotated
+// so the serial work spreads over the SIMDs) factors knot k alone — potrf/inverse chain,
+// forward substitution, slab stores — while the other three ("Schur waves") form the Schur
+// pieces of knot k+2 from HBM.  Between steps (three barriers): the Schur tiles of knot k+1
+// (computed one step earlier and held in registers, `pend`) go into the LDS blocks, knot k+2's
+// A-tiles add into C_{k+1}, and all four waves run the products D̃ = Ã⁻ᵀD, F̃ = Ã⁻ᵀF and the
+// updates B −= D̃ᵀD̃, E −= D̃ᵀF̃, C −= F̃ᵀF̃ of knot k+1.
 template <typename T>
 __global__ void __launch_bounds__(KB_THREADS, sizeof(T) == 4 ? 2 : 1) kkt_big_fwd_kernel(KbArgs<T> a)
 {
     extern __shared__ __align__(16) unsigned char kb_lds_raw[];
     T *lds = (T *)kb_lds_raw;
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g4 = lane >> 4,
-              i16 = lane & 15;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t t = a.b0 + blockIdx.x;
     const int LD = a.LD;
-    constexpr int LDY = KB_LDY;
-    T *Wp = lds + a.oWp, *blk = lds + a.oBlk, *sl = lds + a.oSl, *hs = sl + 16 * LDY, *gs = hs + 16;
+    T *Wp = lds + a.oWp, *blk = lds + a.oBlk;
     T *vc = lds + a.oV, *vd = vc + 64, *vlp = vd + 64, *vmu = vlp + 64, *vla = vmu + 64, *vt1 = vla + 64,
-      *vt2 = vt1 + 64, *rn = vt2 + 64;
-    int *flag = (int *)(rn + KB_RMAX);
-    const int64_t ty = a.yrel ? (int64_t)blockIdx.x : t;          // Y / g: the caller's or Z, gz
+      *vt2 = vt1 + 64, *rnb = vt2 + 64;                      // rnb: r of two knots, [2][KB_RMAX]
+    int *infol = (int *)(rnb + 2 * KB_RMAX);
+    const int64_t ty = a.yrel ? (int64_t)blockIdx.x : t;
     const T *Yt = a.Y + ty * a.sY, *yt = a.y + t * a.sy, *Ht = a.H + t * a.sH, *gt = a.g + ty * a.sg;
     T *St = a.slab + (int64_t)blockIdx.x * a.sS;
     const int N = a.N;
-    int info = 0;
+    const bool hinv = a.ginv && !a.hfac, useg = a.ginv;
     int64_t oS = 0;
 
-    // ---- Y slab pipeline: 16 columns × R padded rows, prefetched into registers.  Thread
-    // (c = tid/16, i = tid%16) moves column c, rows i + 16v: each 16-row block lies in one
-    // partition (the padding is per block), so its source row base is uniform.
-    T pre[KB_RMAX / 16];
-    T preh = (T)0, preg = (T)0;
-    const int scol = tid >> 4;
-    auto fetch = [&](const Kn &q, int s) {
-        const int c = 16 * s + scol;
-        const T *src = Yt + q.oY + (int64_t)c * q.rows + i16;
-        const bool cok = c < q.w;
-#pragma unroll
-        for (int v = 0; v < KB_RMAX / 16; ++v) {
-            T x = (T)0;
-            if (16 * v < q.R) {
-                const int r0 = 16 * v;
-                int rb, lim;
-                if (r0 < q.P1) {
-                    rb = r0; lim = q.p1 - r0;
-                } else if (r0 < q.P1 + q.Ps) {
-                    rb = q.p1 + r0 - q.P1; lim = q.ps - (r0 - q.P1);
-                } else {
-                    rb = q.p1 + q.ps + r0 - q.P1 - q.Ps; lim = q.p2 - (r0 - q.P1 - q.Ps);
-                }
-                if (cok && i16 < lim) x = src[rb];
-            }
-            pre[v] = x;
-        }
-        if (tid < 16) {
-            const int cc = 16 * s + tid;
-            preh = cc < q.w ? ((a.ginv && !a.hfac) ? (T)1 / Ht[q.oH + cc] : (T)1) : (T)0;
-            preg = (cc < q.w && a.ginv) ? gt[q.og + cc] : (T)0;
-        }
+    acc_t<T> acc[KB_ST], pend[KB_ST];
+    int sip = -1;
+#ifdef KB_PROF
+    int64_t kb_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif                                           // Schur-wave index `pend` was made with
+    auto schur = [&](const Kn &q, int si, T *rn) __attribute__((always_inline)) {
+        if (si == 0) schur_part_d<T, 0>(q, Yt, Ht, gt, hinv, useg, acc, rn, lane);
+        else if (si == 1) schur_part_d<T, 1>(q, Yt, Ht, gt, hinv, useg, acc, rn, lane);
+        else if (si == 2) schur_part_d<T, 2>(q, Yt, Ht, gt, hinv, useg, acc, rn, lane);
     };
-    auto commit = [&](const Kn &q) {
-#pragma unroll
-        for (int v = 0; v < KB_RMAX / 16; ++v)
-            if (16 * v < q.R) sl[16 * v + i16 + scol * LDY] = pre[v];
-        if (tid < 16) {
-            hs[tid] = preh;
-            gs[tid] = preg;
-        }
-    };
-
-    // ---- Schur pieces of knot q (shur!, jacobian_blocks.jl:231-242): upper tiles of
-    // Y H⁻¹ Yᵀ into acc (tile qq = wave + 4·slot of the padded grid), r = Y H⁻¹ g into rn
-    acc_t<T> acc[KB_MAXT];
-    int tI[KB_MAXT], tJ[KB_MAXT];
-    auto schur = [&](const Kn &q, bool has_next, const Kn &qn) {
-        const int nbt = q.R >> 4, ntile = nbt * (nbt + 1) / 2;
-#pragma unroll
-        for (int s = 0; s < KB_MAXT; ++s) {
-            int qq = wave + 4 * s, I = 0;
-            if (qq < ntile)
-                while (qq >= nbt - I) {
-                    qq -= nbt - I;
-                    ++I;
-                }
-            tI[s] = I;
-            tJ[s] = I + qq;
-            acc[s] = tzero<T>();
-        }
-        if (tid < q.R) rn[tid] = (T)0;
-        for (int s = 0; s < q.nsl; ++s) {
-            __syncthreads();
-            commit(q);
-            __syncthreads();
-            if (s + 1 < q.nsl) fetch(q, s + 1);
-            else if (has_next) fetch(qn, 0);
-            if (tid < q.R) {
-                T v = rn[tid];
-#pragma unroll
-                for (int c = 0; c < 16; ++c) v = fma(sl[tid + c * LDY] * hs[c], gs[c], v);
-                rn[tid] = v;
-            }
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-                const int kc = 4 * kk + g4;
-                const T h = hs[kc];
-                const T *col = sl + kc * LDY + i16;
-#pragma unroll
-                for (int s2 = 0; s2 < KB_MAXT; ++s2) {
-                    if (wave + 4 * s2 < ntile) {
-                        const T av = col[16 * tI[s2]];
-                        const T bv = col[16 * tJ[s2]] * h;
-                        acc[s2] = Tile<T>::mma(av, bv, acc[s2]);
-                    }
-                }
-            }
-        }
-    };
-    // knot q's non-alias Schur tiles (copy_shur!, :271-286) → LDS blocks; c, d = r − y
-    auto store_schur = [&](const Kn &q) {
-        const Bo b = blk_off(q.P1, q.Ps, q.P2, LD);
-        const int nbt = q.R >> 4, ntile = nbt * (nbt + 1) / 2;
-#pragma unroll
-        for (int s = 0; s < KB_MAXT; ++s) {
-            if (wave + 4 * s >= ntile) continue;
-            const int pi = part_of(q, tI[s]), pj = part_of(q, tJ[s]);
-            if (pi == 0 && pj == 0) continue;                               // A: added into C_{k−1}
-            const int li = 16 * tI[s] - (pi == 0 ? 0 : pi == 1 ? q.P1 : q.P1 + q.Ps);
-            const int lj = 16 * tJ[s] - (pj == 0 ? 0 : pj == 1 ? q.P1 : q.P1 + q.Ps);
-            const int o = pi == 0 ? (pj == 1 ? b.D : b.F) : pi == 1 ? (pj == 1 ? b.B : b.E) : b.C;
-            tstore(blk + o + li + lj * LD, LD, acc[s], lane);
-        }
+    // knot q (= k+1): its pending tiles → LDS blocks, c, d = r − y
+    auto store_pending = [&](const Kn &q, const T *rn) __attribute__((always_inline)) {
+        if (sip == 0) schur_store_d<T, 0>(q, blk, LD, pend, lane);
+        else if (sip == 1) schur_store_d<T, 1>(q, blk, LD, pend, lane);
+        else if (sip == 2) schur_store_d<T, 2>(q, blk, LD, pend, lane);
         if (tid < 64) {
             vc[tid] = tid < q.ps ? rn[q.P1 + tid] - yt[q.oy + tid] : (T)0;
             vd[tid] = tid < q.p2 ? rn[q.P1 + q.Ps + tid] - yt[q.oy + q.ps + tid] : (T)0;
         }
     };
-
-    Kn q0 = kn_load(a.meta, 0);
-    const Kn q1first = N > 1 ? kn_load(a.meta, 1) : q0;
-    if (tid < 64) vlp[tid] = (T)0;
-    fetch(q0, 0);
-    schur(q0, N > 1, q1first);
-    __syncthreads();
-    store_schur(q0);
-
-    for (int k = 0; k < N; ++k) {
-        const Bo b0 = blk_off(q0.P1, q0.Ps, q0.P2, LD);
-        const bool nxt = k + 1 < N;
-        Kn q1 = nxt ? kn_load(a.meta, k + 1) : q0;
-        if (nxt) {
-            const bool nn = k + 2 < N;
-            const Kn q2 = nn ? kn_load(a.meta, k + 2) : q1;
-            schur(q1, nn, q2);
-            // A ≡ C_k alias (:166): knot k+1's D2 H⁻¹ D2ᵀ adds into C_k; d_k .+= r_[1] (:251)
+    // knot q2 (= k+2): A-tiles into C of q (= k+1), d_{k+1} .+= r_[1] (:251); pend ← acc
+    auto add_next = [&](const Kn &q, const Kn &q2, int si, const T *rn2) __attribute__((always_inline)) {
+        const Bo b = blk_off(q.P1, q.Ps, q.P2, LD);
+        if (si == 0) schur_addA_d<T, 0>(q2, blk + b.C, LD, acc, lane);
+        else if (si == 1) schur_addA_d<T, 1>(q2, blk + b.C, LD, acc, lane);
+        else if (si == 2) schur_addA_d<T, 2>(q2, blk + b.C, LD, acc, lane);
+        if (tid < q2.p1) vd[tid] += rn2[tid];
+    };
+    auto keep = [&](int si) __attribute__((always_inline)) {
 #pragma unroll
-            for (int s = 0; s < KB_MAXT; ++s) {
-                if (wave + 4 * s < (q1.R >> 4) * ((q1.R >> 4) + 1) / 2 && 16 * tJ[s] < q1.P1)
-                    tadd(blk + b0.C + 16 * tI[s] + 16 * tJ[s] * LD, LD, acc[s], lane);
+        for (int u = 0; u < KB_ST; ++u) pend[u] = acc[u];
+        sip = si;
+    };
+    // products of knot q needing every wave: D̃ = Ã⁻ᵀD (:49), F̃ = Ã⁻ᵀF (:57) with Ã⁻¹ = W_{k−1}
+    // in Wp (in place: all results in registers before the barrier), then B −= D̃ᵀD̃ (:50-52),
+    // E −= D̃ᵀF̃ (:59), C −= F̃ᵀF̃ (:61) on the upper tiles
+    auto prefactor = [&](const Kn &q0) __attribute__((always_inline)) {
+        if (!q0.P1) return;
+        const Bo b0 = blk_off(q0.P1, q0.Ps, q0.P2, LD);
+        const int n1t = q0.P1 >> 4, nst = q0.Ps >> 4, n2t = q0.P2 >> 4, nD = n1t * nst, nF = n1t * n2t;
+        acc_t<T> f1[KB_F1T];
+#pragma unroll
+        for (int s2 = 0; s2 < KB_F1T; ++s2) {
+            const int qq = wave + 4 * s2;
+            if (qq < nD + nF) {
+                const bool isD = qq < nD;
+                const int r = isD ? qq : qq - nD, nc = isD ? nst : n2t, I = r / nc, J = r - I * nc;
+                f1[s2] = tmm<T, true, false, false>(tzero<T>(), Wp + 16 * I * LD, LD,
+                                                    blk + (isD ? b0.D : b0.F) + 16 * J * LD, LD, 16 * (I + 1), lane);
             }
-            if (tid < q1.p1) vd[tid] += rn[tid];
         }
         __syncthreads();
-
-        // ---- cholesky!(U, F) for knot k (cholesky_solve.jl:47-67)
-        const int n1t = q0.P1 >> 4, nst = q0.Ps >> 4, n2t = q0.P2 >> 4;
-        if (q0.P1) {
-            // D̃ = Ã⁻ᵀD (:49), F̃ = Ã⁻ᵀF (:57) with Ã⁻¹ = W_{k−1} (upper): in place over D, F
-            const int nD = n1t * nst, nF = n1t * n2t;
-            acc_t<T> f1[KB_F1T];
 #pragma unroll
-            for (int s = 0; s < KB_F1T; ++s) {
-                const int qq = wave + 4 * s;
-                if (qq < nD + nF) {
-                    const bool isD = qq < nD;
-                    const int r = isD ? qq : qq - nD, nc = isD ? nst : n2t, I = r / nc, J = r - I * nc;
-                    f1[s] = tmm<T, true, false, false>(tzero<T>(), Wp + 16 * I * LD, LD,
-                                                       blk + (isD ? b0.D : b0.F) + 16 * J * LD, LD, 16 * (I + 1), lane);
-                }
+        for (int s2 = 0; s2 < KB_F1T; ++s2) {
+            const int qq = wave + 4 * s2;
+            if (qq < nD + nF) {
+                const bool isD = qq < nD;
+                const int r = isD ? qq : qq - nD, nc = isD ? nst : n2t, I = r / nc, J = r - I * nc;
+                tstore(blk + (isD ? b0.D : b0.F) + 16 * I + 16 * J * LD, LD, f1[s2], lane);
             }
-            __syncthreads();
-#pragma unroll
-            for (int s = 0; s < KB_F1T; ++s) {
-                const int qq = wave + 4 * s;
-                if (qq < nD + nF) {
-                    const bool isD = qq < nD;
-                    const int r = isD ? qq : qq - nD, nc = isD ? nst : n2t, I = r / nc, J = r - I * nc;
-                    tstore(blk + (isD ? b0.D : b0.F) + 16 * I + 16 * J * LD, LD, f1[s], lane);
+        }
+        __syncthreads();
+        const int nB = nst * (nst + 1) / 2, nE = nst * n2t, nC = n2t * (n2t + 1) / 2;
+        for (int qq = wave; qq < nB + nE + nC; qq += 4) {
+            int I, J, o;
+            const T *Aop, *Bop;
+            if (qq < nB || qq >= nB + nE) {
+                const bool isB = qq < nB;
+                const int m = isB ? nst : n2t;
+                int rem = isB ? qq : qq - nB - nE;
+                I = 0;
+                while (rem >= m - I) {
+                    rem -= m - I;
+                    ++I;
                 }
+                J = I + rem;
+                o = isB ? b0.B : b0.C;
+                Aop = blk + (isB ? b0.D : b0.F);
+                Bop = Aop;
+            } else {
+                const int r = qq - nB;
+                I = r / n2t;
+                J = r - I * n2t;
+                o = b0.E;
+                Aop = blk + b0.D;
+                Bop = blk + b0.F;
             }
-            __syncthreads();
-            // B −= D̃ᵀD̃ (:50-52), E −= D̃ᵀF̃ (:59), C −= F̃ᵀF̃ (:61): upper tiles of B and C
-            const int nB = nst * (nst + 1) / 2, nE = nst * n2t, nC = n2t * (n2t + 1) / 2;
-            for (int qq = wave; qq < nB + nE + nC; qq += 4) {
-                int I, J, o;
-                const T *Aop, *Bop;
-                if (qq < nB || qq >= nB + nE) {
-                    const bool isB = qq < nB;
-                    const int m = isB ? nst : n2t;
-                    int rem = isB ? qq : qq - nB - nE;
-                    I = 0;
-                    while (rem >= m - I) {
-                        rem -= m - I;
-                        ++I;
+            T *X = blk + o + 16 * I + 16 * J * LD;
+            acc_t<T> c = tload(X, LD, lane);
+            c = tmm<T, true, false, true>(c, Aop + 16 * I * LD, LD, Bop + 16 * J * LD, LD, q0.P1, lane);
+            tstore(X, LD, c, lane);
+        }
+    };
+    // the factor wave's part of knot q0 (cholesky_solve.jl:47-67 after the products above,
+    // forward_substitution! :93-117, the slab): single wave, no barriers
+    auto factor = [&](const Kn &q0, int k) __attribute__((always_inline)) {
+        const Bo b0 = blk_off(q0.P1, q0.Ps, q0.P2, LD);
+        const int nst = q0.Ps >> 4, n2t = q0.P2 >> 4;
+        int bad = 0;
+        KB_F0();
+        for (int pass = 0; pass < 2; ++pass) {         // B̃ (:53) → Binv, then C̃ (:62) → W_k
+            const bool isB = pass == 0;
+            const int pp = isB ? q0.ps : q0.p2;
+            if (!pp || (KB_ABL & 16)) continue;
+            bad |= chol_inv_w<T>(blk + (isB ? b0.B : b0.C), LD, pp, isB ? q0.Ps : q0.P2, lane);
+            if (isB && q0.P2) {
+                for (int J = 0; J < n2t; ++J)                                  // Ẽ = B̃⁻ᵀE (:60)
+                    for (int I = nst - 1; I >= 0; --I) {
+                        T *X = blk + b0.E + 16 * I + 16 * J * LD;
+                        tstore(X, LD,
+                               tmm<T, true, false, false>(tzero<T>(), blk + b0.B + 16 * I * LD, LD,
+                                                          blk + b0.E + 16 * J * LD, LD, 16 * (I + 1), lane),
+                               lane);
                     }
-                    J = I + rem;
-                    o = isB ? b0.B : b0.C;
-                    Aop = blk + (isB ? b0.D : b0.F);
-                    Bop = Aop;
-                } else {
-                    const int r = qq - nB;
-                    I = r / n2t;
-                    J = r - I * n2t;
-                    o = b0.E;
-                    Aop = blk + b0.D;
-                    Bop = blk + b0.F;
-                }
-                T *X = blk + o + 16 * I + 16 * J * LD;
-                acc_t<T> c = tload(X, LD, lane);
-                c = tmm<T, true, false, true>(c, Aop + 16 * I * LD, LD, Bop + 16 * J * LD, LD, q0.P1, lane);
-                tstore(X, LD, c, lane);
-            }
-            __syncthreads();
-        }
-        if (q0.ps) {
-            // B̃ = chol(B) (:53) → Binv = B̃⁻¹ in place
-            const int bad = chol_inv<T>(blk + b0.B, LD, q0.ps, q0.Ps, flag, tid);
-            if (bad && !info) info = k + 1;
-            if (q0.P2) {
-                // Ẽ = B̃⁻ᵀE (:60), in place
-                acc_t<T> f1[4];
-#pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    const int qq = wave + 4 * s;
-                    if (qq < nst * n2t) {
-                        const int I = qq / n2t, J = qq - I * n2t;
-                        f1[s] = tmm<T, true, false, false>(tzero<T>(), blk + b0.B + 16 * I * LD, LD,
-                                                           blk + b0.E + 16 * J * LD, LD, 16 * (I + 1), lane);
+                for (int I = 0; I < n2t; ++I)                                  // C −= ẼᵀẼ (:61)
+                    for (int J = I; J < n2t; ++J) {
+                        T *X = blk + b0.C + 16 * I + 16 * J * LD;
+                        tstore(X, LD,
+                               tmm<T, true, false, true>(tload(X, LD, lane), blk + b0.E + 16 * I * LD, LD,
+                                                         blk + b0.E + 16 * J * LD, LD, q0.Ps, lane),
+                               lane);
                     }
-                }
-                __syncthreads();
-#pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    const int qq = wave + 4 * s;
-                    if (qq < nst * n2t) {
-                        const int I = qq / n2t, J = qq - I * n2t;
-                        tstore(blk + b0.E + 16 * I + 16 * J * LD, LD, f1[s], lane);
-                    }
-                }
-                __syncthreads();
-                // C −= ẼᵀẼ (:61)
-                for (int qq = wave; qq < n2t * (n2t + 1) / 2; qq += 4) {
-                    int I = 0, rem = qq;
-                    while (rem >= n2t - I) {
-                        rem -= n2t - I;
-                        ++I;
-                    }
-                    const int J = I + rem;
-                    T *X = blk + b0.C + 16 * I + 16 * J * LD;
-                    acc_t<T> c = tload(X, LD, lane);
-                    c = tmm<T, true, false, true>(c, blk + b0.E + 16 * I * LD, LD, blk + b0.E + 16 * J * LD, LD, q0.Ps,
-                                                  lane);
-                    tstore(X, LD, c, lane);
-                }
-                __syncthreads();
+            }
+            if (isB) KB_F(5);
+        }
+        if (bad && lane == 0 && *infol == 0) *infol = k + 1;
+        KB_F(6);
+        if (!(KB_ABL & 4)) {
+            if (q0.ps) {       // μ = B̃⁻ᵀ(c − D̃ᵀλ_{k−1})
+                if (q0.P1) coldot_w<T, false, true>(vt1, vc, blk + b0.D, LD, vlp, q0.P1, q0.Ps, lane);
+                else vt1[lane] = vc[lane];
+                coldot_w<T, true, false>(vmu, nullptr, blk + b0.B, LD, vt1, q0.Ps, q0.Ps, lane);
+            }
+            if (q0.p2) {       // λ = C̃⁻ᵀ(d − F̃ᵀλ_{k−1} − Ẽᵀμ)
+                if (q0.P1) coldot_w<T, false, true>(vt2, vd, blk + b0.F, LD, vlp, q0.P1, q0.P2, lane);
+                else vt2[lane] = vd[lane];
+                if (q0.ps) coldot_w<T, false, true>(vt2, vt2, blk + b0.E, LD, vmu, q0.Ps, q0.P2, lane);
+                coldot_w<T, true, false>(vla, nullptr, blk + b0.C, LD, vt2, q0.P2, q0.P2, lane);
             }
         }
-        if (q0.p2) {
-            // C̃ = chol(C) (:62) → W_k = C̃⁻¹ in place
-            const int bad = chol_inv<T>(blk + b0.C, LD, q0.p2, q0.P2, flag, tid);
-            if (bad && !info) info = k + 1;
-        }
-        // ---- forward_substitution! (:93-117): μ = B̃⁻ᵀ(c − D̃ᵀλ_{k−1}), λ = C̃⁻ᵀ(d − F̃ᵀλ_{k−1} − Ẽᵀμ)
-        if (q0.ps) {
-            if (q0.P1) {
-                coldot<T, false, true>(vt1, vc, blk + b0.D, LD, vlp, q0.P1, q0.Ps, tid);
-                __syncthreads();
-            } else if (tid < 64) {
-                vt1[tid] = vc[tid];
-            }
-            __syncthreads();
-            coldot<T, true, false>(vmu, nullptr, blk + b0.B, LD, vt1, q0.Ps, q0.Ps, tid);
-            __syncthreads();
-        }
-        if (q0.p2) {
-            if (q0.P1) {
-                coldot<T, false, true>(vt2, vd, blk + b0.F, LD, vlp, q0.P1, q0.P2, tid);
-                __syncthreads();
-            } else if (tid < 64) {
-                vt2[tid] = vd[tid];
-            }
-            __syncthreads();
-            if (q0.ps) {
-                coldot<T, false, true>(vt2, vt2, blk + b0.E, LD, vmu, q0.Ps, q0.P2, tid);
-                __syncthreads();
-            }
-            coldot<T, true, false>(vla, nullptr, blk + b0.C, LD, vt2, q0.P2, q0.P2, tid);
-            __syncthreads();
-        }
-        // ---- slab: W_k, Binv (packed upper), Ẽ, μ, λ of the forward sweep
-        {
+        KB_F(7);
+        if (!(KB_ABL & 8)) {  // slab: W_k, Binv (packed upper), Ẽ, μ, λ
             T *Sk = St + oS;
             const int oB = q0.P2 * (q0.P2 + 1) / 2, oE = oB + q0.Ps * (q0.Ps + 1) / 2, oM = oE + q0.Ps * q0.P2;
-            for (int j = wave; j < q0.P2; j += 4)
+            for (int j = 0; j < q0.P2; ++j)
                 if (lane <= j) Sk[j * (j + 1) / 2 + lane] = blk[b0.C + lane + j * LD];
-            for (int j = wave; j < q0.Ps; j += 4)
+            for (int j = 0; j < q0.Ps; ++j)
                 if (lane <= j) Sk[oB + j * (j + 1) / 2 + lane] = blk[b0.B + lane + j * LD];
-            if (q0.Ps && q0.P2)
-                for (int j = wave; j < q0.P2; j += 4)
+            if (q0.Ps)
+                for (int j = 0; j < q0.P2; ++j)
                     if (lane < q0.Ps) Sk[oE + lane + j * q0.Ps] = blk[b0.E + lane + j * LD];
-            if (tid < q0.Ps) Sk[oM + tid] = vmu[tid];
-            if (tid < q0.P2) Sk[oM + q0.Ps + tid] = vla[tid];
-            oS += slab_size(q0.Ps, q0.P2);
-            // W_k becomes Ã⁻¹ of knot k+1 (U[k+1].A ≡ U[k].C, :166); λ_k its λ_{k−1}
-            for (int e = tid; e < q0.P2 * q0.P2; e += KB_THREADS) {
-                const int j = e / q0.P2, i = e - j * q0.P2;
-                Wp[i + j * LD] = blk[b0.C + i + j * LD];
-            }
-            if (tid < 64) vlp[tid] = tid < q0.P2 ? vla[tid] : (T)0;
+            if (lane < q0.Ps) Sk[oM + lane] = vmu[lane];
+            if (lane < q0.P2) Sk[oM + q0.Ps + lane] = vla[lane];
         }
-        __syncthreads();
-        if (nxt) {
-            store_schur(q1);
+        KB_F(8);
+        // W_k becomes Ã⁻¹ of knot k+1 (U[k+1].A ≡ U[k].C, :166); λ_k its λ_{k−1}
+        for (int j = 0; j < q0.P2; ++j)
+            if (lane < q0.P2) Wp[lane + j * LD] = blk[b0.C + lane + j * LD];
+        vlp[lane] = lane < q0.P2 ? vla[lane] : (T)0;
+        KB_F(9);
+    };
+
+    // steps k = −2, −1 form the Schur pieces of knots 0 and 1 (no factor work yet); every
+    // helper has a single call site (each inlines its compile-time instances once)
+    Kn qa = kn_load(a.meta, 0), qb = qa, qc = qa;          // knots k, k+1, k+2 of step k
+    if (tid == 0) *infol = 0;
+    if (tid < 64) vlp[tid] = (T)0;
+    for (int k = -2; k < N; ++k) {
+        KB_T0();
+        const int fw = (k + 4) & 3, sic = wave == fw ? -1 : ((wave - fw - 1) & 3);
+        const bool n1 = k + 1 < N, n2 = k + 2 < N;
+        if (k >= 0) {
+            prefactor(qa);
             __syncthreads();
         }
-        q0 = q1;
+        KB_T(0);
+        if (wave == fw) {
+            if (k >= 0) factor(qa, k);
+            KB_T(1);
+        } else if (n2) {
+            schur(qc, sic, rnb + ((k + 2) & 1) * KB_RMAX);
+            KB_T(2);
+        }
+        if (k >= 0) oS += slab_size(qa.Ps, qa.P2);
+        __syncthreads();
+        KB_T(3);
+        if (n1 && k >= -1) {
+            store_pending(qb, rnb + ((k + 1) & 1) * KB_RMAX);
+            __syncthreads();
+        }
+        if (n2) {
+            if (k >= -1) add_next(qb, qc, sic, rnb + ((k + 2) & 1) * KB_RMAX);
+            keep(sic);
+        }
+        __syncthreads();
+        KB_T(4);
+        qa = qb;                                              // advance
+        qb = qc;
+        if (k + 3 < N) qc = kn_load(a.meta, k + 3);
     }
+    KB_FLUSH();
     if (tid == 0 && a.info) {
+        const int info = *infol;
         if (a.hfac) {
             if (a.info[t] == 0) a.info[t] = info;   // a non-SPD H_k (−(k+1)) takes precedence
         } else {
@@ -701,16 +939,65 @@ __global__ void __launch_bounds__(KB_THREADS) kkt_big_bwd_kernel(KbArgs<T> a)
         const int32_t *m = a.meta + 8 * k;
         oS += slab_size(r16(m[1]), r16(m[2]));
     }
-    // stage knot k's slab (W packed, Binv packed, Ẽ, μ, λ of the forward sweep) into LDS
-    auto stage_slab = [&](const Kn &q, int64_t o) {
+    // knot k's slab (W packed, Binv packed, Ẽ, μ, λ of the forward sweep): W and the two
+    // vectors go through registers into LDS (prefetched one knot ahead); Binv, Ẽ (end knots
+    // only) are read from the slab in place
+    T wpre[KB_WPRE], fpre = (T)0;
+    auto slab_fetch = [&](const Kn &q, int64_t o) {
         const T *Sk = St + o;
         const int nW = q.P2 * (q.P2 + 1) / 2, nBv = q.Ps * (q.Ps + 1) / 2, nE = q.Ps * q.P2;
-        for (int e = tid; e < nW; e += KB_THREADS) Wl[e] = Sk[e];
-        Bl = Sk + nW;
-        El = Sk + nW + nBv;
-        if (tid < 64) {
-            fm[tid] = tid < q.Ps ? Sk[nW + nBv + nE + tid] : (T)0;
-            fl[tid] = tid < q.P2 ? Sk[nW + nBv + nE + q.Ps + tid] : (T)0;
+#pragma unroll
+        for (int u = 0; u < KB_WPRE; ++u) {
+            const int e = tid + KB_THREADS * u;
+            wpre[u] = e < nW ? Sk[e] : (T)0;
+        }
+        if (tid < 128) {
+            const int i = tid & 63;
+            fpre = tid < 64 ? (i < q.Ps ? Sk[nW + nBv + nE + i] : (T)0) : (i < q.P2 ? Sk[nW + nBv + nE + q.Ps + i] : (T)0);
+        }
+    };
+    auto slab_commit = [&](const Kn &q, int64_t o) {
+        const int nW = q.P2 * (q.P2 + 1) / 2, nBv = q.Ps * (q.Ps + 1) / 2;
+#pragma unroll
+        for (int u = 0; u < KB_WPRE; ++u) {
+            const int e = tid + KB_THREADS * u;
+            if (e < nW) Wl[e] = wpre[u];
+        }
+        if (tid < 128) (tid < 64 ? fm : fl)[tid & 63] = fpre;
+        Bl = St + o + nW;
+        El = St + o + nW + nBv;
+    };
+    // Y_k (rows × w, contiguous in the packed input): every load of a thread in flight at once
+    T ypre[KB_BPRE], hpre = (T)0, gpre = (T)0;
+    auto y_fetch = [&](const Kn &q) {
+        const int tot = q.rows * q.w;
+        const T *src = Yt + q.oY;
+#pragma unroll
+        for (int u = 0; u < KB_BPRE; ++u) {
+            const int e = tid + KB_THREADS * u;
+            ypre[u] = e < tot ? src[e] : (T)0;
+        }
+        if (tid < q.w) {
+            hpre = (a.ginv && !a.hfac) ? (T)1 / Ht[q.oH + tid] : (T)1;
+            gpre = a.ginv ? gt[q.og + tid] : (T)0;
+        }
+    };
+    auto y_commit = [&](const Kn &q) {
+        const int tot = q.rows * q.w, sr = KB_THREADS % q.rows, sc = KB_THREADS / q.rows;
+        int r = tid % q.rows, c = tid / q.rows;
+#pragma unroll
+        for (int u = 0; u < KB_BPRE; ++u) {
+            if (tid + KB_THREADS * u < tot) Yl[r + c * LDB] = ypre[u];
+            r += sr;
+            c += sc;
+            if (r >= q.rows) {
+                r -= q.rows;
+                ++c;
+            }
+        }
+        if (tid < q.w) {
+            hv[tid] = hpre;
+            gv[tid] = gpre;
         }
     };
     // x ← B̃⁻¹ x for packed upper Binv (row dots): out[i] = Σ_{c ≥ i} U⁻¹[i][c] x[c]
@@ -726,8 +1013,10 @@ __global__ void __launch_bounds__(KB_THREADS) kkt_big_bwd_kernel(KbArgs<T> a)
 
     // terminal knot (backward_substitution! :139-143): μ_N = −B̃⁻¹μ, λ_N as the forward gave it
     Kn qj = kn_load(a.meta, N - 1);
+    y_fetch(qj);
     oS -= slab_size(qj.Ps, qj.P2);
-    stage_slab(qj, oS);
+    slab_fetch(qj, oS);
+    slab_commit(qj, oS);
     __syncthreads();
     if (qj.ps) rowdot_packed(nm, Bl, fm, qj.ps);
     __syncthreads();
@@ -738,33 +1027,28 @@ __global__ void __launch_bounds__(KB_THREADS) kkt_big_bwd_kernel(KbArgs<T> a)
     __syncthreads();
     if (tid < qj.ps) lat[qj.oy + tid] = xm[tid];
     if (tid < qj.p2) lat[qj.oy + qj.ps + tid] = xl[tid];
+    int64_t oSp = oS;
+    if (N > 1) {                                   // knot N−2's slab, for step j = N−1
+        const Kn q = kn_load(a.meta, N - 2);
+        oSp -= slab_size(q.Ps, q.P2);
+        slab_fetch(q, oSp);
+    }
 
     for (int j = N - 1; j >= 0; --j) {
-        // stage Y_j (rows × w, column stride LDB), 1/h and g
-        {
-            const int tot = qj.rows * qj.w, sr = KB_THREADS % qj.rows, sc = KB_THREADS / qj.rows;
-            int r = tid % qj.rows, c = tid / qj.rows;
-            for (int e = tid; e < tot; e += KB_THREADS) {
-                Yl[r + c * LDB] = Yt[qj.oY + e];
-                r += sr;
-                c += sc;
-                if (r >= qj.rows) {
-                    r -= qj.rows;
-                    ++c;
-                }
-            }
-            if (tid < qj.w) {
-                hv[tid] = (a.ginv && !a.hfac) ? (T)1 / Ht[qj.oH + tid] : (T)1;
-                gv[tid] = a.ginv ? gt[qj.og + tid] : (T)0;
-            }
-        }
+        y_commit(qj);
         Kn qp = qj;
         if (j > 0) {
             qp = kn_load(a.meta, j - 1);
-            oS -= slab_size(qp.Ps, qp.P2);
-            stage_slab(qp, oS);
+            slab_commit(qp, oSp);
         }
         __syncthreads();
+        // prefetch for step j−1: Y_{j−1} and knot j−2's slab
+        if (j > 0) y_fetch(qp);
+        if (j > 1) {
+            const Kn q2 = kn_load(a.meta, j - 2);
+            oSp -= slab_size(q2.Ps, q2.P2);
+            slab_fetch(q2, oSp);
+        }
         // t = [C; D1]ᵀ[μ_j; λ_j]  (calc_residual!'s Cᵀμ + D1ᵀλ, :219-231)
         {
             const int c = tid >> 1, h = tid & 1;
@@ -981,9 +1265,9 @@ bool kb_plan(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_
     int o = 0;
     P.oWp = o; o += P.LD * PM;
     P.oBlk = o; o += blk;
-    P.oSl = o; o += P.LDY * 16 + 32;
+    P.oSl = o;                              // (the forward sweep reads Y straight from HBM)
     o = (o + 3) & ~3;
-    P.oV = o; o += 7 * 64 + KB_RMAX + 4;   // vectors + the int flag
+    P.oV = o; o += 7 * 64 + 2 * KB_RMAX + 4;   // vectors, r of two knots, the info int
     P.nf = o;
     o = 0;
     P.oYl = o; o += P.LDB * maxw;
@@ -1059,6 +1343,12 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
     if (P.hfac) {
         k.hfac = 1; k.yrel = 1; k.Y = Z; k.g = gz; k.Ui = Ui; k.sU = P.sU;
     }
+#ifdef KB_PROF
+    static int64_t *prof = nullptr;
+    if (!prof) (void)hipMalloc((void **)&prof, 64 * sizeof(int64_t));
+    (void)hipMemsetAsync(prof, 0, 64 * sizeof(int64_t), s);
+    k.prof = prof;
+#endif
     for (int64_t b0 = 0; b0 < a.batch && e == hipSuccess; b0 += chunk) {
         const int64_t nb = std::min<int64_t>(chunk, a.batch - b0);
         k.b0 = b0;
@@ -1070,6 +1360,21 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
         hipLaunchKernelGGL(kkt_big_bwd_kernel<T>, dim3((unsigned)nb), dim3(KB_THREADS), lb, s, k);
         e = hipGetLastError();
     }
+#ifdef KB_PROF
+    {
+        int64_t h[64];
+        (void)hipStreamSynchronize(s);
+        (void)hipMemcpy(h, prof, sizeof h, hipMemcpyDeviceToHost);
+        const double steps = (double)a.batch * (a.N + 2);
+        std::fprintf(stderr, "KB_PROF cycles per step and wave [prefactor factor schur barrier handover | "
+                             "F: cholB+E cholC fwdsubst slab Wcopy]:\n");
+        for (int w = 0; w < 4; ++w) {
+            std::fprintf(stderr, "  wave %d:", w);
+            for (int i = 0; i < 10; ++i) std::fprintf(stderr, " %8.0f", h[16 * w + i] / steps);
+            std::fprintf(stderr, "\n");
+        }
+    }
+#endif
     const hipError_t ef = sc.release(s);
     return e != hipSuccess ? e : ef;
 }

@@ -10,7 +10,8 @@
 #   TAG=r03a PMC="SQ_WAVES SQ_INSTS_VALU;SQ_INSTS_LDS" tools/gpu_measure.sh pmc [bench args]
 #                                                       one rocprofv3 --pmc pass per ';' group
 #
-# $OUT = gpurun_out/$TAG.  Every GPU step runs under its own timeout and the script stops at
+# $OUT = gpurun_out/$TAG.  KREGEX (default "lqrx") restricts the PMC passes to the library's
+# kernels; only the stats / counter CSVs are kept (gpurun copies back ≤ 64 MiB).  Every GPU step runs under its own timeout and the script stops at
 # the first failure (no retries).  On the CPU side afterwards: tools/traffic_json.py turns the
 # FETCH/WRITE CSVs into profiles/traffic_*.json (gfx950 FETCH×2 correction), tools/
 # pmc_summary.py summarises SQ passes; copy what is judged into profiles/<round>/.
@@ -20,6 +21,8 @@ export TMPDIR=/tmp
 MODE=${1:?mode: tests|bench|prof|pmc}
 shift
 OUT=gpurun_out/${TAG:-run}
+KREGEX=${KREGEX:-lqrx}
+trim() { find "$OUT" -type f \( -name "*.csv" -o -name "*.json" -o -name "*.db" \) ! -name "*stats.csv" ! -name "*counter_collection.csv" ! -name "bench.json" -delete 2>/dev/null; true; }
 mkdir -p "$OUT"
 nproc > "$OUT/host.txt"
 lscpu | head -20 >> "$OUT/host.txt"
@@ -38,19 +41,22 @@ prof)
     cat "$OUT/bench.json"
     timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- \
         python bench.py "$@" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/kt.log" 2>&1 || { tail -20 "$OUT/kt.log"; exit 3; }
-    timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv -- \
+    trim
+    timeout -k 10 400 rocprofv3 --kernel-include-regex "$KREGEX" --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv -- \
         python bench.py "$@" --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/fetch.log" 2>&1 || { tail -20 "$OUT/fetch.log"; exit 4; }
-    timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv -- \
+    timeout -k 10 400 rocprofv3 --kernel-include-regex "$KREGEX" --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv -- \
         python bench.py "$@" --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/write.log" 2>&1 || { tail -20 "$OUT/write.log"; exit 5; }
+    trim
     find "$OUT" -name "*stats.csv" ;;
 pmc)
     i=0
     IFS=';' read -ra GROUPS_ <<< "${PMC:?PMC=\"COUNTERS;COUNTERS\"}"
     for grp in "${GROUPS_[@]}"; do
         i=$((i + 1))
-        timeout -s KILL 300 rocprofv3 --pmc $grp -d "$OUT/pmc$i" -o pmc$i --output-format csv -- \
+        timeout -s KILL 300 rocprofv3 --kernel-include-regex "$KREGEX" --pmc $grp -d "$OUT/pmc$i" -o pmc$i --output-format csv -- \
             python bench.py "$@" --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/pmc$i.log" 2>&1 || { tail -20 "$OUT/pmc$i.log"; exit 6; }
-    done ;;
+    done
+    trim ;;
 *)
     echo "unknown mode $MODE" >&2; exit 1 ;;
 esac

@@ -1,6 +1,7 @@
 #!/bin/bash
-# Build (here, on the CPU) liblqrx variants for A/B runs (tools/gpu_tvabl.sh runs the bench on
-# each with LQRX_LIB).  One source (SRC, default lqrx_dp.hip) is rebuilt with extra defines; the
+# Build (here, on the CPU) liblqrx variants for A/B runs (the bench runs on each with
+# LQRX_LIB=tools/abl/liblqrx_<name>.so).  Large-block KKT ablations:
+#   SRC=lqrx_kkt_big.hip tools/tv_ablate.sh noleaf:-DKB_ABL=1 noschur:-DKB_ABL=2 ...  One source (SRC, default lqrx_dp.hip) is rebuilt with extra defines; the
 # others are linked from the in-tree build.  Arguments: name:defines ...  Defaults (SRC =
 # lqrx_dp.hip): the time-varying DP ablation of profiles/r02/dp_tv_ablation_r02.txt —
 #   TVABL bit 1: Q_k re-read from knot 1 (cache-resident); bit 2: A_k/B_k/R_k likewise
@@ -9,7 +10,7 @@ set -e
 cd "$(dirname "$0")/../lqr.jl_amd/csrc"
 SRC=${SRC:-lqrx_dp.hip}
 OBJS=""
-for f in lqrx_dp.hip lqrx_dp_lane.hip lqrx_layout.hip lqrx_kkt.hip lqrx_kkt_fil.hip lqrx_sqp.hip lqrx_ls.hip lqrx_api.cpp; do
+for f in $(sed -n 's/^SRCS *= *//p' Makefile); do
   [ $f = $SRC ] || OBJS="$OBJS build/$f.o"
 done
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -I../../include -munsafe-fp-atomics"
