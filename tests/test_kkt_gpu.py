@@ -107,8 +107,11 @@ def test_kkt_fil_shapes(lqrx, gpu_ok, model, N, batch, h_mode, ginv):
     N = 5 the system is square and a few of the random problems lose 1e-5 to rounding in the
     oracle and the generic kernel alike — measured, tools/kkt_shape_diag.py).
     DoubleIntegrator(3) (the structure of test/cholesky_solve.jl) runs the direct variant
-    kkt_fild_kernel for diagonal H / SOC."""
+    kkt_fild_kernel for diagonal H / SOC, the large-block kernel for dense H; at N = 4 its
+    S reaches cond ~7e6 and the oracle itself is 4.6e-11 from the exact solution, so the
+    trajectories past 1e-10 are held to the refined truth instead (tests/kkt_truth.py)."""
     import lqrx.kkt as K
+    from kkt_truth import check
 
     if model == "dubins":
         st = K.dubins_structure(N)
@@ -120,8 +123,7 @@ def test_kkt_fil_shapes(lqrx, gpu_ok, model, N, batch, h_mode, ginv):
     got = K.kkt_solve(pb, ginv=ginv)
     ref = _ref(st, pb, ginv)
     assert got["rc"] == 0 and (got["info"] == 0).all()
-    assert rel(got["dz"], ref["dz"].reshape(batch, -1)) <= TOL
-    assert rel(got["lam"], ref["lam"].reshape(batch, -1)) <= TOL
+    check(st, pb, ginv, got, ref, TOL)
 
 
 def test_kkt_workspace_entry(lqrx, gpu_ok):
