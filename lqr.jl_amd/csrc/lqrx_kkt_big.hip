@@ -1220,6 +1220,792 @@ __global__ void __launch_bounds__(KB_THREADS, 1) kkt_big_hfac_kernel(KhArgs<T> a
     if (tid == 0 && a.info) a.info[t] = hfail ? -hfail : 0;
 }
 
+// ================================================================ split forward sweep
+// The fused forward kernel above keeps one trajectory per workgroup: its Schur waves wait on
+// HBM behind a one-slice prefetch, its factor wave on a serial LDS chain, and two
+// trajectories fit a CU (KB_PROF, configs[4]: ~107 k cycles per step for ~10 k cycles of
+// MFMA work).  The split path runs the two halves as separate kernels:
+//   kb_schur_kernel  — shur! (jacobian_blocks.jl:231-242) for every knot, in parallel over
+//                      (trajectory, run of KS_L knots): Y H⁻¹ Yᵀ (upper tiles) and Y H⁻¹ g on
+//                      MFMA, Y streamed from HBM through a KS_PF-deep register ring; writes a
+//                      per-knot image of the Schur blocks with copy_shur!'s A ≡ previous-C
+//                      alias (:166) and `d .+= r_[1]` (:251) already applied;
+//   kb_factor_kernel — cholesky! + forward_substitution! (cholesky_solve.jl:47-117), one wave
+//                      per trajectory, every block a register-tile array and every product
+//                      in the TN form of lqrx_tile.h (D += MᵀY without data movement); LDS only
+//                      for the 16×16 leaves and tile transposes.  Several trajectories per
+//                      SIMD hide each other's chains.
+// Served when every knot has at most two of (n1, p, n2) nonzero: the trajectory structure
+// of conblocks.jl:403-425 (first (0,n,n), interior (n,0,n), last (n,n,0)) and any structure
+// without stage constraints at interior knots.  The backward kernel is shared (same slab).
+
+constexpr int KS_L = 16;       // knots per Schur unit (one extra A-only pass per unit)
+constexpr int KS_PF = 4;       // k-slices in flight per Schur wave
+constexpr int KF_W = 4;        // trajectories (waves) per factor workgroup
+constexpr int KF_LU = 68;      // factor LDS image leading dimension
+
+// image of one knot (elements of T from the knot's base): tiles D, F, B, E, C (256 elements
+// each, lane-major C layout: element 4·lane + r = register r of lane `lane`), then
+// v = [c (Ps) | d (P2)]; block tile offsets in tiles, v and end in elements
+struct Im {
+    int D, F, B, E, C, v, end;
+};
+__host__ __device__ __forceinline__ Im img_off(int P1, int Ps, int P2)
+{
+    const int a = P1 >> 4, s = Ps >> 4, b = P2 >> 4;
+    Im o;
+    int x = 0;
+    o.D = x; x += a * s;
+    o.F = x; x += a * b;
+    o.B = x; x += s * (s + 1) / 2;
+    o.E = x; x += s * b;
+    o.C = x; x += b * (b + 1) / 2;
+    o.v = 256 * x;
+    o.end = o.v + Ps + P2;
+    return o;
+}
+// elements of knot k's image slot (64-aligned, so every tile starts 256-B aligned)
+__host__ __device__ __forceinline__ int64_t img_len(const int32_t *meta, int k)
+{
+    const int32_t *m = meta + 8 * k;
+    return (img_off(r16(m[0]), r16(m[1]), r16(m[2])).end + 63) & ~(int64_t)63;
+}
+// index of the upper tile (i ≤ j) of an n×n tile grid, row-major over the upper triangle
+__host__ __device__ constexpr int upn(int i, int j, int n) { return i * n - i * (i - 1) / 2 + (j - i); }
+__host__ __device__ constexpr int up4(int i, int j) { return upn(i, j, 4); }
+__device__ __forceinline__ void tri_ij(int nbt, int q, int &I, int &J)
+{
+    I = 0;
+    while (q >= nbt - I) {
+        q -= nbt - I;
+        ++I;
+    }
+    J = I + q;
+}
+
+template <typename T>
+__device__ __forceinline__ void gstore_tile(T *p, const acc_t<T> &c, int lane) { *(acc_t<T> *)(p + 4 * lane) = c; }
+template <typename T>
+__device__ __forceinline__ acc_t<T> gload_tile(const T *p, int lane) { return *(const acc_t<T> *)(p + 4 * lane); }
+// the transpose of the column-major 16×16 block at X as a C-layout tile
+template <typename T>
+__device__ __forceinline__ acc_t<T> tload_t(const T *X, int ld, int lane)
+{
+    acc_t<T> c;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) c[r] = X[(lane & 15) + Tile<T>::row(lane, r) * ld];
+    return c;
+}
+// D (+/−)= Mᵀ·Y for single C-layout tiles
+template <typename T, bool NEG = false>
+__device__ __forceinline__ acc_t<T> mtn(const acc_t<T> &M, const acc_t<T> &Y, acc_t<T> D)
+{
+#pragma unroll
+    for (int r = 0; r < 4; ++r) D = NEG ? Tile<T>::mma_nega(M[r], Y[r], D) : Tile<T>::mma(M[r], Y[r], D);
+    return D;
+}
+// wave-level ordering of LDS traffic between lanes (in-order LDS per wave; compiler fence)
+__device__ __forceinline__ void wsync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---------------------------------------------------------------- Schur kernel
+template <typename T>
+struct KsArgs {
+    const T *Y, *y, *H, *g;
+    T *img;
+    const int32_t *meta;
+    int N, nruns, hinv, useg, yrel;
+    int64_t b0, sY, sy, sH, sg, IMGT;   // IMGT: image elements per trajectory
+};
+
+__host__ __device__ constexpr bool ks_need(int nbt, int si, int nw, int v)
+{
+    if (v % nw == si) return true;     // r = Y H⁻¹ g rows of block v
+    for (int q = si; q < nbt * (nbt + 1) / 2; q += nw)
+        if (tm_I(nbt, q) == v || tm_J(nbt, q) == v) return true;
+    return false;
+}
+
+// this wave's upper tiles (q = SI + NW·t) of Y H⁻¹ Yᵀ over the knot's padded row blocks and
+// its rows (v ≡ SI mod NW) of r = Y H⁻¹ g into rn; k-slices of 4 columns, KS_PF in flight
+template <typename T, int NBT, int SI, int NW>
+__device__ __forceinline__ void schur_tiles(const Kn &q, const T *Yt, const T *Ht, const T *gt, bool hinv, bool useg,
+                                            acc_t<T> (&acc)[(36 + NW - 1) / NW], T *rn, int lane)
+{
+    constexpr int ST = (36 + NW - 1) / NW, NTT = NBT * (NBT + 1) / 2;
+    const int i16 = lane & 15, g4 = lane >> 4;
+    int rb[NBT], lim[NBT];
+#pragma unroll
+    for (int v = 0; v < NBT; ++v) {
+        const int r0 = 16 * v;
+        if (r0 < q.P1) {
+            rb[v] = r0;
+            lim[v] = q.p1 - r0;
+        } else if (r0 < q.P1 + q.Ps) {
+            rb[v] = q.p1 + r0 - q.P1;
+            lim[v] = q.ps - (r0 - q.P1);
+        } else {
+            rb[v] = q.p1 + q.ps + r0 - q.P1 - q.Ps;
+            lim[v] = q.p2 - (r0 - q.P1 - q.Ps);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < ST; ++t) acc[t] = tzero<T>();
+    T rp[NBT];
+#pragma unroll
+    for (int v = 0; v < NBT; ++v) rp[v] = (T)0;
+    const int nks = (q.w + 3) >> 2;
+    // uniform bases + 32-bit lane offsets (global_load … saddr: no 64-bit address per load)
+    const T *base = Yt + q.oY, *hb = Ht + q.oH, *gb = gt + q.og;
+    T f[KS_PF][NBT], hh[KS_PF], gg[KS_PF];
+    auto load = [&](int s, T (&fr)[NBT], T &h, T &g_) __attribute__((always_inline)) {
+        const int c = 4 * s + g4;
+        const bool ok = c < q.w;
+        const uint32_t off = (uint32_t)((ok ? c : 0) * q.rows + i16);
+        sfor<NBT>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            if constexpr (ks_need(NBT, SI, NW, v)) fr[v] = (ok && i16 < lim[v]) ? base[off + (uint32_t)rb[v]] : (T)0;
+        });
+        h = ok ? (hinv ? (T)1 / hb[(uint32_t)c] : (T)1) : (T)0;
+        g_ = (ok && useg) ? gb[(uint32_t)c] : (T)0;
+    };
+    auto step = [&](const T (&fr)[NBT], T h, T g_) __attribute__((always_inline)) {
+        T fh[NBT];
+        sfor<NBT>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            if constexpr (ks_need(NBT, SI, NW, v)) fh[v] = fr[v] * h;
+        });
+        sfor<ST>([&](auto tc) {
+            constexpr int t = decltype(tc)::value, qq = SI + NW * t;
+            if constexpr (qq < NTT) {
+                constexpr int I = tm_I(NBT, qq), J = tm_J(NBT, qq);
+                acc[t] = Tile<T>::mma(fr[I], fh[J], acc[t]);
+            }
+        });
+        sfor<NBT>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            if constexpr (v % NW == SI) rp[v] = fma(fh[v], g_, rp[v]);
+        });
+    };
+    sfor<KS_PF>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        load(u, f[u], hh[u], gg[u]);
+    });
+    for (int s0 = 0; s0 < nks; s0 += KS_PF) {
+        sfor<KS_PF>([&](auto uc) {
+            constexpr int u = decltype(uc)::value;
+            if (s0 + u < nks) {
+                step(f[u], hh[u], gg[u]);
+                load(s0 + u + KS_PF, f[u], hh[u], gg[u]);
+            }
+        });
+    }
+    sfor<NBT>([&](auto vc) {
+        constexpr int v = decltype(vc)::value;
+        if constexpr (v % NW == SI) {
+            T x = rp[v];
+            x += __shfl_xor(x, 16);
+            x += __shfl_xor(x, 32);
+            if (lane < 16) rn[16 * v + lane] = x;
+        }
+    });
+}
+
+template <typename T, int NW, int NBT>
+__device__ __forceinline__ void schur_tiles_d(const Kn &q, int si, const T *Yt, const T *Ht, const T *gt, bool hinv,
+                                              bool useg, acc_t<T> (&acc)[(36 + NW - 1) / NW], T *rn, int lane)
+{
+    if (si == 0) schur_tiles<T, NBT, 0, NW>(q, Yt, Ht, gt, hinv, useg, acc, rn, lane);
+    else if (si == 1) schur_tiles<T, NBT, 1 % NW, NW>(q, Yt, Ht, gt, hinv, useg, acc, rn, lane);
+    else if (NW > 2 && si == 2) schur_tiles<T, NBT, 2 % NW, NW>(q, Yt, Ht, gt, hinv, useg, acc, rn, lane);
+    else if (NW > 3) schur_tiles<T, NBT, 3 % NW, NW>(q, Yt, Ht, gt, hinv, useg, acc, rn, lane);
+}
+
+// image tile of the global upper tile (I, J) of knot q (−1: an A tile, which belongs to the
+// knot before)
+__device__ __forceinline__ int img_tile(const Kn &q, const Im &o, int I, int J)
+{
+    const int a = q.P1 >> 4, s = q.Ps >> 4, b = q.P2 >> 4;
+    const int pi = I < a ? 0 : (I < a + s ? 1 : 2), pj = J < a ? 0 : (J < a + s ? 1 : 2);
+    const int li = I - (pi == 0 ? 0 : pi == 1 ? a : a + s), lj = J - (pj == 0 ? 0 : pj == 1 ? a : a + s);
+    if (pi == 0) return pj == 0 ? -1 : (pj == 1 ? o.D + li * s + lj : o.F + li * b + lj);
+    if (pi == 1) return pj == 1 ? o.B + upn(li, lj, s) : o.E + li * b + lj;
+    return o.C + upn(li, lj, b);
+}
+
+// One workgroup of NW waves per (trajectory, run of KS_L knots).  Knot k's tiles are split
+// over the waves and go to knot k's image as they are (C without the alias); once knot k+1's
+// tiles exist, the waves owning its A tiles add them into knot k's C tiles in the image
+// (read-modify-write, ordered by the workgroup barrier) and knot k's v = [c | d + r1_{k+1}] is
+// written from the two knots' r (LDS).  The run's last pass forms only the A tiles (and r1)
+// of the first knot of the next run.
+template <typename T, int NW, int NBT>
+__global__ void __launch_bounds__(64 * NW) kb_schur_kernel(KsArgs<T> a)
+{
+    constexpr int ST = (36 + NW - 1) / NW;
+    __shared__ T rbuf[2][KB_RMAX];                 // r of two knots (padded row order)
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t u = blockIdx.x, tl = u / a.nruns;
+    const int run = (int)(u - tl * a.nruns);
+    const int64_t t = a.b0 + tl, ty = a.yrel ? tl : t;
+    const T *Yt = a.Y + ty * a.sY, *yt = a.y + t * a.sy, *Ht = a.H + t * a.sH, *gt = a.g + ty * a.sg;
+    T *img = a.img + tl * a.IMGT;
+    const int k0 = run * KS_L, k1 = min(k0 + KS_L, a.N);
+    int64_t oI = 0, oIp = 0;                       // image offsets of knot k and knot k−1
+    for (int j = 0; j < k0; ++j) oI += img_len(a.meta, j);
+    acc_t<T> acc[ST];
+    Kn qp = kn_load(a.meta, k0);                   // knot k−1
+    // v of knot kk (= qp): [c | d + r1 of knot kk+1 (if nx)]
+    auto write_v = [&](int kk, bool nx, int p1n) __attribute__((always_inline)) {
+        const Im o = img_off(qp.P1, qp.Ps, qp.P2);
+        T *ik = img + oIp;
+        const T *rk = rbuf[kk & 1], *rx = rbuf[(kk + 1) & 1];
+        for (int e = tid; e < qp.Ps + qp.P2; e += 64 * NW) {
+            T v;
+            if (e < qp.Ps) {
+                v = e < qp.ps ? rk[qp.P1 + e] - yt[qp.oy + e] : (T)0;
+            } else {
+                const int j = e - qp.Ps;
+                v = j < qp.p2 ? rk[qp.P1 + qp.Ps + j] - yt[qp.oy + qp.ps + j] : (T)0;
+                if (nx && j < p1n) v += rx[j];
+            }
+            ik[o.v + e] = v;
+        }
+    };
+    for (int k = k0; k <= k1 && k < a.N; ++k) {
+        const Kn q = kn_load(a.meta, k);
+        const bool aonly = k == k1;
+        Kn qs = q;
+        if (aonly) {
+            qs.ps = qs.p2 = 0;
+            qs.Ps = qs.P2 = 0;
+            qs.R = qs.P1;
+        }
+        // tiles over the launch's NBT×NBT block grid (the largest knot); rows past this
+        // knot's R are zero fragments and their tiles are not stored
+        if (qs.R) schur_tiles_d<T, NW, NBT>(qs, wave, Yt, Ht, gt, a.hinv != 0, a.useg != 0, acc, rbuf[k & 1], lane);
+        const int nbt = qs.R >> 4, n1t = qs.P1 >> 4;
+        if (!aonly) {
+            const Im o = img_off(q.P1, q.Ps, q.P2);
+            T *ik = img + oI;
+#pragma unroll
+            for (int s = 0; s < ST; ++s) {
+                const int qq = wave + NW * s;
+                if (qq < NBT * (NBT + 1) / 2) {
+                    int I, J;
+                    tri_ij(NBT, qq, I, J);
+                    const int it = J < nbt ? img_tile(q, o, I, J) : -1;
+                    if (it >= 0) gstore_tile(ik + 256 * it, acc[s], lane);
+                }
+            }
+        }
+        __syncthreads();                           // knot k−1's C tiles stored; rbuf[k & 1] complete
+        if (k > k0) {
+            // copy_shur! alias: knot k's A tiles into knot k−1's C tiles
+            const Im o = img_off(qp.P1, qp.Ps, qp.P2);
+            T *ip = img + oIp;
+            const int b = qp.P2 >> 4;
+#pragma unroll
+            for (int s = 0; s < ST; ++s) {
+                const int qq = wave + NW * s;
+                if (qq < NBT * (NBT + 1) / 2) {
+                    int I, J;
+                    tri_ij(NBT, qq, I, J);
+                    if (J < n1t) {
+                        T *pc = ip + 256 * (o.C + upn(I, J, b));
+                        gstore_tile(pc, gload_tile(pc, lane) + acc[s], lane);
+                    }
+                }
+            }
+            write_v(k - 1, true, q.p1);
+        }
+        if (!aonly) {
+            qp = q;
+            oIp = oI;
+            oI += img_len(a.meta, k);
+        }
+        __syncthreads();                           // rbuf reuse
+    }
+    if (k1 == a.N) write_v(a.N - 1, false, 0);     // the last knot: nothing to alias
+}
+
+// ---------------------------------------------------------------- factor kernel
+template <typename T>
+struct KfArgs {
+    const T *img;
+    T *slab;
+    int32_t *info;
+    const int32_t *meta;
+    int N, hfac;
+    int64_t b0, nb, IMGT, sS;
+};
+
+// In place on the upper tiles X (packed up4) of a P×P SPD matrix (nb ≤ 4 block rows, p real
+// pivots): X ← U⁻¹ with UᵀU = X.  Right-looking by 16 as chol_inv: leaf (LDS, one wave) →
+// panel U_{jb,J} = T_jjᵀ X_{jb,J} → trailing X_IJ −= U_{jb,I}ᵀ U_{jb,J}, all in registers;
+// then W_IJ = −T_I Σ_{L=I+1..J} U_IL W_LJ with U_ILᵀ and T_Iᵀ read transposed from the LDS
+// image U (leading dimension KF_LU) the factor phase left there.  Returns 0 or 1 + the
+// first non-positive pivot.
+template <typename T>
+__device__ int chol_inv_reg(acc_t<T> (&X)[10], int nb, int p, T *U, int lane)
+{
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb)
+        if (jb < nb) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * jb + Tile<T>::row(lane, r), c = 16 * jb + (lane & 15);
+                if (i == c && i >= p) X[up4(jb, jb)][r] = (T)1;     // identity padding
+            }
+        }
+    int bad = 0;
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) {
+        if (jb < nb) {
+            T *Dg = U + 16 * jb * (1 + KF_LU);
+            tstore(Dg, KF_LU, X[up4(jb, jb)], lane);
+            wsync();
+            const int b = leaf_chol_inv<T>(Dg, KF_LU, min(16, p - 16 * jb), lane);
+            if (b && !bad) bad = 16 * jb + b;
+            wsync();
+            X[up4(jb, jb)] = tload(Dg, KF_LU, lane);
+#pragma unroll
+            for (int J = jb + 1; J < 4; ++J)
+                if (J < nb) {
+                    X[up4(jb, J)] = mtn<T>(X[up4(jb, jb)], X[up4(jb, J)], tzero<T>());
+                    tstore(U + 16 * jb + 16 * J * KF_LU, KF_LU, X[up4(jb, J)], lane);
+                }
+#pragma unroll
+            for (int I = jb + 1; I < 4; ++I)
+#pragma unroll
+                for (int J = I; J < 4; ++J)
+                    if (J < nb) X[up4(I, J)] = mtn<T, true>(X[up4(jb, I)], X[up4(jb, J)], X[up4(I, J)]);
+        }
+    }
+    wsync();
+#pragma unroll
+    for (int J = 1; J < 4; ++J)
+        if (J < nb) {
+#pragma unroll
+            for (int I = J - 1; I >= 0; --I) {
+                acc_t<T> s = tzero<T>();
+#pragma unroll
+                for (int L = I + 1; L <= J; ++L)
+                    s = mtn<T>(tload_t(U + 16 * I + 16 * L * KF_LU, KF_LU, lane), X[up4(L, J)], s);
+                X[up4(I, J)] = mtn<T, true>(tload_t(U + 16 * I * (1 + KF_LU), KF_LU, lane), s, tzero<T>());
+            }
+        }
+    return bad;
+}
+
+// y (column layout: lane holds y[16j + (lane & 15)]) = Mᵀx for x in row layout
+// (x[i][r] = x[16i + row(lane, r)]); UP: M is upper (packed up4), else full [i·4 + j]
+template <typename T, bool UP, int NM>
+__device__ __forceinline__ void mtv(T (&y)[4], const acc_t<T> (&M)[NM], const T (&x)[4][4], int ni, int nj)
+{
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        T s = (T)0;
+        if (j < nj) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (i < ni && (!UP || i <= j)) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) s = fma(M[UP ? up4(i, j) : i * 4 + j][r], x[i][r], s);
+                }
+        }
+        s += __shfl_xor(s, 16);
+        s += __shfl_xor(s, 32);
+        y[j] = s;
+    }
+}
+// column layout → row layout through the wave's LDS vector buffer
+template <typename T>
+__device__ __forceinline__ void col2row(T (&x)[4][4], const T (&y)[4], T *vb, int lane)
+{
+    if (lane < 16) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) vb[16 * j + lane] = y[j];
+    }
+    wsync();
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[i][r] = vb[16 * i + Tile<T>::row(lane, r)];
+    wsync();
+}
+
+// One wave per trajectory.  Registers: X (10 upper tiles) holds W_{k−1} = Ã⁻¹ at the start of
+// knot k, then B → B̃⁻¹, then C → W_k; G (a 4×4 tile grid) holds D̃ or F̃ (knots with an n1
+// block) or E → Ẽ (the first knot's shape, n1 = 0).  With at most two blocks per knot those
+// lifetimes never overlap.
+template <typename T>
+__global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_kernel(KfArgs<T> a)
+{
+    extern __shared__ __align__(16) unsigned char kb_lds_raw[];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t tl = (int64_t)blockIdx.x * KF_W + wave;
+    if (tl >= a.nb) return;                          // whole wave; no workgroup barriers below
+    T *U = (T *)kb_lds_raw + wave * (64 * KF_LU + 64), *vb = U + 64 * KF_LU;
+    const int64_t t = a.b0 + tl;
+    const T *imt = a.img + tl * a.IMGT;
+    T *St = a.slab + tl * a.sS;
+    int64_t oI = 0, oS = 0;
+    acc_t<T> X[10], G[16];
+    T lam[4][4];                                     // λ_{k−1}, row layout
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lam[i][r] = (T)0;
+    int info = 0;
+    for (int k = 0; k < a.N; ++k) {
+        const Kn q = kn_load(a.meta, k);
+        const Im o = img_off(q.P1, q.Ps, q.P2);
+        const T *ik = imt + oI;
+        T *Sk = St + oS;
+        oI += img_len(a.meta, k);
+        oS += slab_size(q.Ps, q.P2);
+        const int n1t = q.P1 >> 4, nst = q.Ps >> 4, n2t = q.P2 >> 4;
+        const int oB = q.P2 * (q.P2 + 1) / 2, oE = oB + q.Ps * (q.Ps + 1) / 2, oM = oE + q.Ps * q.P2;
+        T yv[4] = {(T)0, (T)0, (T)0, (T)0};
+        int bad = 0;
+        if (n1t) {
+            // D̃ = Ã⁻ᵀD or F̃ = Ã⁻ᵀF with Ã⁻¹ = W_{k−1} (:49, :57), one column of tiles at a time
+            const int gc = nst ? nst : n2t;
+            const T *Yb = ik + 256 * (nst ? o.D : o.F);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (j < gc) {
+                    acc_t<T> Yc[4];
+#pragma unroll
+                    for (int L = 0; L < 4; ++L)
+                        if (L < n1t) Yc[L] = gload_tile(Yb + 256 * (L * gc + j), lane);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (i < n1t) {
+                            acc_t<T> g = tzero<T>();
+#pragma unroll
+                            for (int L = 0; L <= i; ++L) g = mtn<T>(X[up4(L, i)], Yc[L], g);
+                            G[i * 4 + j] = g;
+                        }
+                }
+            mtv<T, false>(yv, G, lam, n1t, gc);      // D̃ᵀλ_{k−1} or F̃ᵀλ_{k−1}
+        }
+        T mur[4][4];                                 // μ, row layout (for Ẽᵀμ)
+        if (nst) {
+            // B̃ = chol(B − D̃ᵀD̃) (:50-53) → X = B̃⁻¹
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = i; j < 4; ++j)
+                    if (j < nst) {
+                        acc_t<T> c = gload_tile(ik + 256 * (o.B + upn(i, j, nst)), lane);
+                        if (n1t) {
+#pragma unroll
+                            for (int L = 0; L < 4; ++L)
+                                if (L < n1t) c = mtn<T, true>(G[L * 4 + i], G[L * 4 + j], c);
+                        }
+                        X[up4(i, j)] = c;
+                    }
+            bad |= chol_inv_reg<T>(X, nst, q.ps, U, lane);
+            // μ = B̃⁻ᵀ(c − D̃ᵀλ_{k−1})  (:101-107)
+            T x[4], xr[4][4], mu[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[j] = (j < nst ? ik[o.v + 16 * j + (lane & 15)] : (T)0) - yv[j];
+            col2row<T>(xr, x, vb, lane);
+            mtv<T, true>(mu, X, xr, nst, nst);
+            col2row<T>(mur, mu, vb, lane);
+            // slab: B̃⁻¹ packed upper, μ
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = i; j < 4; ++j)
+                    if (j < nst) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int row = 16 * i + Tile<T>::row(lane, r), col = 16 * j + (lane & 15);
+                            if (row <= col) Sk[oB + col * (col + 1) / 2 + row] = X[up4(i, j)][r];
+                        }
+                    }
+            if (lane < 16) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (j < nst) Sk[oM + 16 * j + lane] = mu[j];
+            }
+            if (n2t) {
+                // (n1 = 0 here) Ẽ = B̃⁻ᵀE (:59-60) into G, column by column
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (j < n2t) {
+                        acc_t<T> Ec[4];
+#pragma unroll
+                        for (int L = 0; L < 4; ++L)
+                            if (L < nst) Ec[L] = gload_tile(ik + 256 * (o.E + L * n2t + j), lane);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            if (i < nst) {
+                                acc_t<T> e = tzero<T>();
+#pragma unroll
+                                for (int L = 0; L <= i; ++L) e = mtn<T>(X[up4(L, i)], Ec[L], e);
+                                G[i * 4 + j] = e;
+#pragma unroll
+                                for (int r = 0; r < 4; ++r)
+                                    Sk[oE + 16 * i + Tile<T>::row(lane, r) + (16 * j + (lane & 15)) * q.Ps] = e[r];
+                            }
+                    }
+            }
+        }
+        if (n2t) {
+            // C̃ = chol(C − F̃ᵀF̃ − ẼᵀẼ) (:61-62) → X = W_k
+            const int gr = n1t ? n1t : nst;          // G = F̃ (n1 rows) or Ẽ (p rows)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = i; j < 4; ++j)
+                    if (j < n2t) {
+                        acc_t<T> c = gload_tile(ik + 256 * (o.C + upn(i, j, n2t)), lane);
+#pragma unroll
+                        for (int L = 0; L < 4; ++L)
+                            if (L < gr) c = mtn<T, true>(G[L * 4 + i], G[L * 4 + j], c);
+                        X[up4(i, j)] = c;
+                    }
+            bad |= chol_inv_reg<T>(X, n2t, q.p2, U, lane);
+            // λ = C̃⁻ᵀ(d − F̃ᵀλ_{k−1} − Ẽᵀμ)  (:108-116)
+            T x[4], xr[4][4], lc[4];
+            if (nst) mtv<T, false>(yv, G, mur, nst, n2t);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[j] = (j < n2t ? ik[o.v + q.Ps + 16 * j + (lane & 15)] : (T)0) - yv[j];
+            col2row<T>(xr, x, vb, lane);
+            mtv<T, true>(lc, X, xr, n2t, n2t);
+            col2row<T>(lam, lc, vb, lane);
+            // slab: W_k packed upper, λ
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = i; j < 4; ++j)
+                    if (j < n2t) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int row = 16 * i + Tile<T>::row(lane, r), col = 16 * j + (lane & 15);
+                            if (row <= col) Sk[col * (col + 1) / 2 + row] = X[up4(i, j)][r];
+                        }
+                    }
+            if (lane < 16) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (j < n2t) Sk[oM + q.Ps + 16 * j + lane] = lc[j];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) lam[i][r] = (T)0;
+        }
+        if (bad && !info) info = k + 1;
+    }
+    if (lane == 0 && a.info) {
+        if (a.hfac) {
+            if (a.info[t] == 0) a.info[t] = info;   // a non-SPD H_k (−(k+1)) takes precedence
+        } else {
+            a.info[t] = info;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- backward sweep (split path)
+// backward_substitution! (cholesky_solve.jl:119-143) fused with calculate_primals!
+// (cholesky_solver.jl:185-236), one wave per trajectory — the same operations as
+// kkt_big_bwd_kernel without its workgroup barriers and LDS staging of Y: every GEMV over Y_j
+// reads HBM/L2 directly, lane = column for Yᵀ-products (t, D2ᵀλ: each lane a contiguous run
+// of its column) and lane = row for Y-products (v: coalesced columns); the multipliers pass
+// between lanes through a small per-wave LDS vector area.  Bound by the bytes of Y (read
+// once per knot; the D2 rows a second time, from L2).
+constexpr int KBW_V = 8 * 64;     // per-wave LDS vector elements
+template <typename T>
+__global__ void __launch_bounds__(64 * KF_W) kb_bwd_kernel(KbArgs<T> a, int64_t nb)
+{
+    extern __shared__ __align__(16) unsigned char kb_lds_raw[];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t tl = (int64_t)blockIdx.x * KF_W + wave;
+    if (tl >= nb) return;
+    T *xb = (T *)kb_lds_raw + wave * KBW_V;          // x = [μ_j; λ_j] in Y's row order past D2
+    T *tb = xb + 128, *vb = tb + 128, *zb = vb + 64, *lb = zb + 64, *eb = lb + 64;
+    const int64_t t = a.b0 + tl, ty = a.yrel ? tl : t;
+    const T *Yt = a.Y + ty * a.sY, *Ht = a.H + t * a.sH, *gt = a.g + ty * a.sg;
+    T *dzt = a.dz + t * a.sg, *lat = a.lam + t * a.sy;
+    const T *Ut = a.hfac ? a.Ui + tl * a.sU : nullptr;
+    const T *St = a.slab + tl * a.sS;
+    const int N = a.N;
+    int64_t oS = 0, oU = 0;
+    for (int k = 0; k < N; ++k) {
+        const int32_t *m = a.meta + 8 * k;
+        oS += slab_size(r16(m[1]), r16(m[2]));
+        if (a.hfac) oU += (int64_t)m[3] * (m[3] + 1) / 2;
+    }
+    // x ← B̃⁻¹ x for packed upper B̃⁻¹ (row dots), lane = row
+    auto rowdot = [&](const T *P, const T *x, int n) __attribute__((always_inline)) {
+        T s0 = (T)0, s1 = (T)0;
+        if (lane < n) {
+            int c = lane;
+            for (; c + 1 < n; c += 2) {
+                s0 = fma(P[c * (c + 1) / 2 + lane], x[c], s0);
+                s1 = fma(P[(c + 1) * (c + 2) / 2 + lane], x[c + 1], s1);
+            }
+            if (c < n) s0 = fma(P[c * (c + 1) / 2 + lane], x[c], s0);
+        }
+        return s0 + s1;
+    };
+    // terminal knot (:139-143): μ_N = −B̃⁻¹μ, λ_N as the forward sweep left it
+    Kn qj = kn_load(a.meta, N - 1);
+    oS -= slab_size(qj.Ps, qj.P2);
+    {
+        const T *Sk = St + oS;
+        const int nW = qj.P2 * (qj.P2 + 1) / 2, nBv = qj.Ps * (qj.Ps + 1) / 2, nE = qj.Ps * qj.P2;
+        const T *fm = Sk + nW + nBv + nE, *fl = fm + qj.Ps;
+        const T nm = rowdot(Sk + nW, fm, qj.ps);
+        const T xm = -nm, xl = lane < qj.p2 ? fl[lane] : (T)0;
+        if (lane < qj.ps) {
+            xb[lane] = xm;
+            lat[qj.oy + lane] = xm;
+        }
+        if (lane < qj.p2) {
+            xb[qj.ps + lane] = xl;
+            lat[qj.oy + qj.ps + lane] = xl;
+        }
+    }
+    wsync();
+    for (int j = N - 1; j >= 0; --j) {
+        const T *Yk = Yt + qj.oY;
+        const int nr = qj.rows - qj.p1;
+        // t = [C; D1]ᵀ[μ_j; λ_j] (calc_residual!'s Cᵀμ + D1ᵀλ, :219-231), lane = column
+        T tc[2], hc[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int c = lane + 64 * u;
+            T s0 = (T)0, s1 = (T)0, s2 = (T)0, s3 = (T)0, h = (T)0;
+            if (c < qj.w) {
+                const T *col = Yk + (int64_t)c * qj.rows + qj.p1;
+                int r = 0;
+                for (; r + 3 < nr; r += 4) {
+                    s0 = fma(col[r], xb[r], s0);
+                    s1 = fma(col[r + 1], xb[r + 1], s1);
+                    s2 = fma(col[r + 2], xb[r + 2], s2);
+                    s3 = fma(col[r + 3], xb[r + 3], s3);
+                }
+                for (; r < nr; ++r) s0 = fma(col[r], xb[r], s0);
+                h = (a.ginv && !a.hfac) ? (T)1 / Ht[qj.oH + c] : (T)1;
+                tb[c] = ((s0 + s1) + (s2 + s3)) * h;
+            }
+            tc[u] = (s0 + s1) + (s2 + s3);
+            hc[u] = h;
+        }
+        wsync();
+        Kn qp = qj;
+        if (j > 0) {
+            qp = kn_load(a.meta, j - 1);
+            oS -= slab_size(qp.Ps, qp.P2);
+            const T *Sk = St + oS;
+            const int nW = qp.P2 * (qp.P2 + 1) / 2, nBv = qp.Ps * (qp.Ps + 1) / 2, nE = qp.Ps * qp.P2;
+            const T *Bl = Sk + nW, *El = Bl + nBv, *fm = El + nE, *fl = fm + qp.Ps;
+            // v = D2 H⁻¹ t = D_{k+1}μ_{k+1} + F_{k+1}λ_{k+1}, lane = row (coalesced columns)
+            {
+                T s0 = (T)0, s1 = (T)0;
+                if (lane < qj.p1) {
+                    int c = 0;
+                    for (; c + 1 < qj.w; c += 2) {
+                        s0 = fma(Yk[lane + (int64_t)c * qj.rows], tb[c], s0);
+                        s1 = fma(Yk[lane + (int64_t)(c + 1) * qj.rows], tb[c + 1], s1);
+                    }
+                    if (c < qj.w) s0 = fma(Yk[lane + (int64_t)c * qj.rows], tb[c], s0);
+                }
+                vb[lane] = s0 + s1;
+            }
+            wsync();
+            // λ_{j−1} = C̃⁻¹(λ + C̃⁻ᵀv) = W(λ + Wᵀv)  (:128-135): z = fl + Wᵀv (lane = column)
+            {
+                T s0 = (T)0, s1 = (T)0;
+                if (lane < qp.P2) {
+                    const T *wc = Sk + lane * (lane + 1) / 2;
+                    int i = 0;
+                    for (; i + 1 <= lane; i += 2) {
+                        s0 = fma(wc[i], vb[i], s0);
+                        s1 = fma(wc[i + 1], vb[i + 1], s1);
+                    }
+                    if (i <= lane) s0 = fma(wc[i], vb[i], s0);
+                    zb[lane] = fl[lane] + (s0 + s1);
+                }
+            }
+            wsync();
+            const T nl = rowdot(Sk, zb, qp.P2);
+            lb[lane] = nl;
+            T nm = (T)0;
+            if (qp.ps) {
+                // μ_{j−1} = B̃⁻¹(μ − Ẽλ)  (:136-137)
+                wsync();
+                T s = (T)0;
+                if (lane < qp.Ps)
+                    for (int c = 0; c < qp.P2; ++c) s = fma(El[lane + c * qp.Ps], lb[c], s);
+                eb[lane] = lane < qp.Ps ? fm[lane] - s : (T)0;
+                wsync();
+                nm = rowdot(Bl, eb, qp.Ps);
+            }
+            wsync();
+            // negate (:138) and hand over: x = [μ_{j−1}; λ_{j−1}] for knot j−1
+            if (lane < qp.ps) {
+                xb[lane] = -nm;
+                lat[qp.oy + lane] = -nm;
+            }
+            if (lane < qp.p2) {
+                xb[qp.ps + lane] = -nl;
+                lat[qp.oy + qp.ps + lane] = -nl;
+            }
+            lb[lane] = -nl;
+            wsync();
+        }
+        // δz_j = −H⁻¹(t + D2ᵀλ_{j−1} + g)  (calc_residual! + calc_primals!, :195-236), lane = column
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int c = lane + 64 * u;
+            if (c < qj.w) {
+                T s0 = (T)0, s1 = (T)0;
+                if (j > 0) {
+                    const T *col = Yk + (int64_t)c * qj.rows;
+                    int r = 0;
+                    for (; r + 1 < qj.p1; r += 2) {
+                        s0 = fma(col[r], lb[r], s0);
+                        s1 = fma(col[r + 1], lb[r + 1], s1);
+                    }
+                    if (r < qj.p1) s0 = fma(col[r], lb[r], s0);
+                }
+                const T res = tc[u] + (s0 + s1) + (a.ginv ? gt[qj.og + c] : (T)0);
+                if (a.hfac) tb[c] = res;
+                else dzt[qj.og + c] = -(res * hc[u]);
+            }
+        }
+        if (a.hfac) {
+            // δz = −U⁻¹ res (res already U⁻ᵀ-applied), row dots on the packed U⁻¹
+            wsync();
+            oU -= (int64_t)qj.w * (qj.w + 1) / 2;
+            const T *Uk = Ut + oU;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int i = lane + 64 * u;
+                if (i < qj.w) {
+                    T s = (T)0;
+                    for (int c = i; c < qj.w; ++c) s = fma(Uk[c * (c + 1) / 2 + i], tb[c], s);
+                    dzt[qj.og + i] = -s;
+                }
+            }
+        }
+        wsync();
+        qj = qp;
+    }
+}
+
 // ---------------------------------------------------------------- host: plan and launch
 struct KbPlan {
     int PM, LD, LDY, LDB, maxrows, maxw, blk;
@@ -1229,7 +2015,18 @@ struct KbPlan {
     int64_t sU;                     // packed U⁻¹ elements per trajectory
     int oWp, oBlk, oSl, oV, nf;     // fwd LDS (elements)
     int oYl, oWl, oV2, nb;          // bwd LDS (elements)
+    bool split;                     // the split forward sweep (Schur kernel + factor kernel)
+    int64_t IMGT;                   // split: image elements per trajectory
+    int nruns;                      // split: Schur units per trajectory
+    int nbt;                        // split: the Schur kernel's block grid (max R / 16)
 };
+
+// LQRX_KKT_SPLIT=1 enables the split path (default off until validated on hardware)
+int kb_split_env()
+{
+    static const int v = [] { const char *e = std::getenv("LQRX_KKT_SPLIT"); return e && *e ? std::atoi(e) : 0; }();
+    return v;
+}
 
 // the big kernels' block limits and LDS plan for this structure; false = not served
 bool kb_plan(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2, const int32_t *w, int tsize,
@@ -1279,29 +2076,46 @@ bool kb_plan(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_
     P.sU = P.hfac ? sU : 0;
     P.LDH = r16(maxw) + 4;
     P.nh = P.hfac ? P.LDH * KB_WMAX + 4 : 0;
+    // split path: at most two of (n1, p, n2) nonzero at every knot (register tile budget of
+    // the factor kernel: one 4×4 grid of Ã⁻ᵀ[D|F] or Ẽ, plus B and C)
+    P.split = kb_split_env() != 0;
+    int64_t IMGT = 0;
+    for (int k = 0; k < a.N; ++k) {
+        if ((n1[k] > 0) + (p[k] > 0) + (n2[k] > 0) > 2) P.split = false;
+        if (k + 1 < a.N && n2[k] != n1[k + 1]) P.split = false;
+        IMGT += (img_off(r16(n1[k]), r16(p[k]), r16(n2[k])).end + 63) & ~(int64_t)63;
+    }
+    P.IMGT = IMGT;
+    P.nruns = (a.N + KS_L - 1) / KS_L;
+    P.nbt = RM >> 4;
     constexpr size_t LDS_CAP = 160 * 1024;
     return (size_t)P.nf * tsize <= LDS_CAP && (size_t)P.nb * tsize <= LDS_CAP && (size_t)P.nh * tsize <= LDS_CAP;
 }
 
-size_t kb_slab_cap()    // LQRX_KKT_BIG_SLAB_MB bounds the stream-ordered slab (default 24 GiB)
+size_t kb_slab_cap()    // LQRX_KKT_BIG_SLAB_MB bounds the stream-ordered scratch (default 40 GiB)
 {
     static const size_t v = [] {
         const char *e = std::getenv("LQRX_KKT_BIG_SLAB_MB");
-        return e ? (size_t)std::strtoull(e, nullptr, 10) << 20 : (size_t)24 << 30;
+        return e ? (size_t)std::strtoull(e, nullptr, 10) << 20 : (size_t)40 << 30;
     }();
     return v;
 }
 
-// scratch elements per trajectory: the slab, plus Z, gz and packed U⁻¹ for a dense H
+// scratch elements per trajectory: the slab, plus Z, gz and packed U⁻¹ for a dense H, plus
+// the Schur images of the split path
 int64_t kb_per_traj(const KktArgs &a, const KbPlan &P)
 {
-    return P.S + (P.hfac ? a.sY + a.sg + P.sU : 0);
+    return P.S + (P.hfac ? a.sY + a.sg + P.sU : 0) + (P.split ? P.IMGT : 0);
 }
 
+// trajectories per chunk: as many as `avail` holds, then evened out over the chunks (a
+// short last chunk would leave most of the GPU idle in the factor kernel)
 int64_t kb_chunk(const KktArgs &a, const KbPlan &P, int tsize, size_t avail)
 {
     const size_t per = (size_t)kb_per_traj(a, P) * tsize;
-    return std::max<int64_t>(1, std::min<int64_t>(a.batch, (int64_t)(avail / std::max<size_t>(per, 1))));
+    const int64_t most = std::max<int64_t>(1, std::min<int64_t>(a.batch, (int64_t)(avail / std::max<size_t>(per, 1))));
+    const int64_t nch = (a.batch + most - 1) / most;
+    return std::max<int64_t>(1, (a.batch + nch - 1) / nch);
 }
 
 template <typename T>
@@ -1323,8 +2137,27 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
         (void)sc.release(s);
         return e;
     }
-    // scratch: [slab chunk·S][Z chunk·sY][gz chunk·sg][U⁻¹ chunk·sU]
+    // scratch: [slab chunk·S][Z chunk·sY][gz chunk·sg][U⁻¹ chunk·sU] (dense H) [images chunk·IMGT] (split)
     T *slab = (T *)sc.p, *Z = slab + chunk * P.S, *gz = Z + chunk * a.sY, *Ui = gz + chunk * a.sg;
+    T *img = P.hfac ? Ui + chunk * P.sU : Z;
+    constexpr int KS_NW = sizeof(T) == 4 ? 2 : 4;
+    const size_t lfac = (size_t)KF_W * (64 * KF_LU + 64) * sizeof(T);
+    if (P.split && (e = hipFuncSetAttribute((const void *)kb_factor_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)lfac)) != hipSuccess) {
+        (void)sc.release(s);
+        return e;
+    }
+    KsArgs<T> ks{};
+    KfArgs<T> kf{};
+    if (P.split) {
+        ks.Y = P.hfac ? Z : (const T *)a.Y; ks.y = (const T *)a.y; ks.H = (const T *)a.H;
+        ks.g = P.hfac ? gz : (const T *)a.g;
+        ks.img = img; ks.meta = a.meta; ks.N = a.N; ks.nruns = P.nruns;
+        ks.hinv = a.ginv && !P.hfac; ks.useg = a.ginv; ks.yrel = P.hfac;
+        ks.sY = a.sY; ks.sy = a.sy; ks.sH = a.sH; ks.sg = a.sg; ks.IMGT = P.IMGT;
+        kf.img = img; kf.slab = slab; kf.info = a.info; kf.meta = a.meta; kf.N = a.N; kf.hfac = P.hfac;
+        kf.IMGT = P.IMGT; kf.sS = P.S;
+    }
     KhArgs<T> h{};
     if (P.hfac) {
         h.Y = (const T *)a.Y; h.H = (const T *)a.H; h.g = (const T *)a.g;
@@ -1356,8 +2189,25 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
             h.b0 = b0;
             hipLaunchKernelGGL(kkt_big_hfac_kernel<T>, dim3((unsigned)nb), dim3(KB_THREADS), lh, s, h);
         }
-        hipLaunchKernelGGL(kkt_big_fwd_kernel<T>, dim3((unsigned)nb), dim3(KB_THREADS), lf, s, k);
-        hipLaunchKernelGGL(kkt_big_bwd_kernel<T>, dim3((unsigned)nb), dim3(KB_THREADS), lb, s, k);
+        if (P.split) {
+            ks.b0 = b0;
+            kf.b0 = b0;
+            kf.nb = nb;
+            const dim3 gs((unsigned)(nb * P.nruns)), bs(64 * KS_NW);
+            switch (P.nbt) {
+#define KS_L_(NB) case NB: hipLaunchKernelGGL((kb_schur_kernel<T, KS_NW, NB>), gs, bs, 0, s, ks); break;
+            KS_L_(1) KS_L_(2) KS_L_(3) KS_L_(4) KS_L_(5) KS_L_(6) KS_L_(7)
+            default: hipLaunchKernelGGL((kb_schur_kernel<T, KS_NW, 8>), gs, bs, 0, s, ks); break;
+#undef KS_L_
+            }
+            hipLaunchKernelGGL(kb_factor_kernel<T>, dim3((unsigned)((nb + KF_W - 1) / KF_W)), dim3(64 * KF_W), lfac, s, kf);
+        } else
+            hipLaunchKernelGGL(kkt_big_fwd_kernel<T>, dim3((unsigned)nb), dim3(KB_THREADS), lf, s, k);
+        if (P.split)
+            hipLaunchKernelGGL(kb_bwd_kernel<T>, dim3((unsigned)((nb + KF_W - 1) / KF_W)), dim3(64 * KF_W),
+                               (size_t)KF_W * KBW_V * sizeof(T), s, k, nb);
+        else
+            hipLaunchKernelGGL(kkt_big_bwd_kernel<T>, dim3((unsigned)nb), dim3(KB_THREADS), lb, s, k);
         e = hipGetLastError();
     }
 #ifdef KB_PROF
