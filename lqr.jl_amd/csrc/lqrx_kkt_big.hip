@@ -1330,6 +1330,17 @@ __host__ __device__ constexpr bool ks_need(int nbt, int si, int nw, int v)
     return false;
 }
 
+// raw buffer load of one element (voffset + soffset bytes; 0 past the descriptor's size)
+template <typename T> __device__ __forceinline__ T bload(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so);
+template <> __device__ __forceinline__ float bload<float>(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo, (int)so, 0));
+}
+template <> __device__ __forceinline__ double bload<double>(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so)
+{
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)vo, (int)so, 0));
+}
+
 // this wave's upper tiles (q = SI + NW·t) of Y H⁻¹ Yᵀ over the knot's padded row blocks and
 // its rows (v ≡ SI mod NW) of r = Y H⁻¹ g into rn; k-slices of 4 columns, KS_PF in flight
 template <typename T, int NBT, int SI, int NW>
@@ -1359,21 +1370,31 @@ __device__ __forceinline__ void schur_tiles(const Kn &q, const T *Yt, const T *H
 #pragma unroll
     for (int v = 0; v < NBT; ++v) rp[v] = (T)0;
     const int nks = (q.w + 3) >> 2;
-    // uniform bases + 32-bit lane offsets (global_load … saddr: no 64-bit address per load)
-    const T *base = Yt + q.oY, *hb = Ht + q.oH, *gb = gt + q.og;
+    // raw buffer loads: the knot's Y block, H and g rows as descriptors whose size bounds the
+    // reads (out-of-range returns 0: columns past w); per lane one byte offset per row block
+    // (rows past the block's real rows get an out-of-range offset), the slice in soffset —
+    // no address arithmetic and no exec-mask branch per load
+    constexpr uint32_t TS = sizeof(T), OOB = 0x80000000u;
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)(Yt + q.oY), (short)0, q.rows * q.w * (int)TS, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void *)(Ht + q.oH), (short)0, q.w * (int)TS, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void *)(gt + q.og), (short)0, q.w * (int)TS, 0x00020000);
+    uint32_t vo[NBT];
+#pragma unroll
+    for (int v = 0; v < NBT; ++v) vo[v] = i16 < lim[v] ? (uint32_t)((g4 * q.rows + rb[v] + i16) * (int)TS) : OOB;
+    const uint32_t so_col = (uint32_t)(4 * q.rows * (int)TS);
     T f[KS_PF][NBT], hh[KS_PF], gg[KS_PF];
     auto load = [&](int s, T (&fr)[NBT], T &h, T &g_) __attribute__((always_inline)) {
-        const int c = 4 * s + g4;
-        const bool ok = c < q.w;
-        const uint32_t off = (uint32_t)((ok ? c : 0) * q.rows + i16);
+        const uint32_t so = (uint32_t)s * so_col;
         sfor<NBT>([&](auto vc) {
             constexpr int v = decltype(vc)::value;
-            if constexpr (ks_need(NBT, SI, NW, v)) fr[v] = (ok && i16 < lim[v]) ? base[off + (uint32_t)rb[v]] : (T)0;
+            if constexpr (ks_need(NBT, SI, NW, v)) fr[v] = bload<T>(ry, vo[v], so);
         });
-        h = ok ? (hinv ? (T)1 / hb[(uint32_t)c] : (T)1) : (T)0;
-        g_ = (ok && useg) ? gb[(uint32_t)c] : (T)0;
+        // raw H and g: the reciprocal is taken in step(), so nothing here waits for a load
+        h = bload<T>(rh, (uint32_t)(g4 * (int)TS), (uint32_t)(4 * s) * TS);
+        g_ = bload<T>(rg, (uint32_t)(g4 * (int)TS), (uint32_t)(4 * s) * TS);
     };
-    auto step = [&](const T (&fr)[NBT], T h, T g_) __attribute__((always_inline)) {
+    auto step = [&](const T (&fr)[NBT], T hx, T gx, int s) __attribute__((always_inline)) {
+        const T h = 4 * s + g4 < q.w ? (hinv ? (T)1 / hx : (T)1) : (T)0, g_ = useg ? gx : (T)0;
         T fh[NBT];
         sfor<NBT>([&](auto vc) {
             constexpr int v = decltype(vc)::value;
@@ -1395,13 +1416,15 @@ __device__ __forceinline__ void schur_tiles(const Kn &q, const T *Yt, const T *H
         constexpr int u = decltype(uc)::value;
         load(u, f[u], hh[u], gg[u]);
     });
+    // branch-free body (slices past w read 0 through the descriptors' bounds and get h = 0),
+    // so the wait-count pass sees the same loads in flight on every path: each step waits
+    // only for its own slice, issued KS_PF steps earlier
     for (int s0 = 0; s0 < nks; s0 += KS_PF) {
         sfor<KS_PF>([&](auto uc) {
             constexpr int u = decltype(uc)::value;
-            if (s0 + u < nks) {
-                step(f[u], hh[u], gg[u]);
-                load(s0 + u + KS_PF, f[u], hh[u], gg[u]);
-            }
+            step(f[u], hh[u], gg[u], s0 + u);
+            load(s0 + u + KS_PF, f[u], hh[u], gg[u]);
+            __builtin_amdgcn_sched_barrier(0);       // keep the ring order (no load sinking)
         });
     }
     sfor<NBT>([&](auto vc) {
@@ -1662,10 +1685,24 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_k
 #pragma unroll
         for (int r = 0; r < 4; ++r) lam[i][r] = (T)0;
     int info = 0;
+    // the D or F tiles of knot kn (n1 > 0) into G, every load in flight at once
+    auto prefetch_g = [&](int kn, int64_t oIn) __attribute__((always_inline)) {
+        const Kn qn = kn_load(a.meta, kn);
+        if (!(qn.P1 >> 4)) return;
+        const Im on = img_off(qn.P1, qn.Ps, qn.P2);
+        const int n1n = qn.P1 >> 4, gc = qn.Ps ? qn.Ps >> 4 : qn.P2 >> 4;
+        const T *Yb = imt + oIn + 256 * (qn.Ps ? on.D : on.F);
+#pragma unroll
+        for (int L = 0; L < 4; ++L)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (L < n1n && j < gc) G[L * 4 + j] = gload_tile(Yb + 256 * (L * gc + j), lane);
+    };
     for (int k = 0; k < a.N; ++k) {
         const Kn q = kn_load(a.meta, k);
         const Im o = img_off(q.P1, q.Ps, q.P2);
         const T *ik = imt + oI;
+        prefetch_g(k, oI);
         T *Sk = St + oS;
         oI += img_len(a.meta, k);
         oS += slab_size(q.Ps, q.P2);
@@ -1674,16 +1711,15 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_k
         T yv[4] = {(T)0, (T)0, (T)0, (T)0};
         int bad = 0;
         if (n1t) {
-            // D̃ = Ã⁻ᵀD or F̃ = Ã⁻ᵀF with Ã⁻¹ = W_{k−1} (:49, :57), one column of tiles at a time
+            // D̃ = Ã⁻ᵀD or F̃ = Ã⁻ᵀF with Ã⁻¹ = W_{k−1} (:49, :57), in place on the loaded
+            // tiles, one column of tiles at a time
             const int gc = nst ? nst : n2t;
-            const T *Yb = ik + 256 * (nst ? o.D : o.F);
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 if (j < gc) {
                     acc_t<T> Yc[4];
 #pragma unroll
-                    for (int L = 0; L < 4; ++L)
-                        if (L < n1t) Yc[L] = gload_tile(Yb + 256 * (L * gc + j), lane);
+                    for (int L = 0; L < 4; ++L) Yc[L] = G[L * 4 + j];
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
                         if (i < n1t) {
@@ -1773,12 +1809,14 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_k
                             if (L < gr) c = mtn<T, true>(G[L * 4 + i], G[L * 4 + j], c);
                         X[up4(i, j)] = c;
                     }
+            // Ẽᵀμ for λ while G still holds Ẽ
+            T ey[4];
+            if (nst) mtv<T, false>(ey, G, mur, nst, n2t);
             bad |= chol_inv_reg<T>(X, n2t, q.p2, U, lane);
             // λ = C̃⁻ᵀ(d − F̃ᵀλ_{k−1} − Ẽᵀμ)  (:108-116)
             T x[4], xr[4][4], lc[4];
-            if (nst) mtv<T, false>(yv, G, mur, nst, n2t);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) x[j] = (j < n2t ? ik[o.v + q.Ps + 16 * j + (lane & 15)] : (T)0) - yv[j];
+            for (int j = 0; j < 4; ++j) x[j] = (j < n2t ? ik[o.v + q.Ps + 16 * j + (lane & 15)] : (T)0) - (nst ? ey[j] : yv[j]);
             col2row<T>(xr, x, vb, lane);
             mtv<T, true>(lc, X, xr, n2t, n2t);
             col2row<T>(lam, lc, vb, lane);
@@ -1825,6 +1863,45 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_k
 // between lanes through a small per-wave LDS vector area.  Bound by the bytes of Y (read
 // once per knot; the D2 rows a second time, from L2).
 constexpr int KBW_V = 8 * 64;     // per-wave LDS vector elements
+constexpr int KBW_W = 2080 + 64;  // per-wave LDS image of the packed W (≤ 64×65/2)
+
+// Σ_{r<n} p[r]·x[r] for a contiguous run p (global) and x (LDS, broadcast reads), n ≤ 128:
+// every load of a 32-element chunk issued before its FMAs (16-B vector loads when `vec`)
+template <typename T>
+__device__ __forceinline__ T dot_run(const T *p, const T *x, int n, bool vec)
+{
+    constexpr int V = 16 / sizeof(T);
+    typedef T tv __attribute__((ext_vector_type(V)));
+    T s0 = (T)0, s1 = (T)0;
+    for (int r0 = 0; r0 < n; r0 += 32) {
+        T y[32];
+        if (vec && r0 + 32 <= n) {
+#pragma unroll
+            for (int j = 0; j < 32 / V; ++j) {
+                const tv w = *(const tv *)(p + r0 + V * j);
+#pragma unroll
+                for (int e = 0; e < V; ++e) y[V * j + e] = w[e];
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 32; ++j) y[j] = r0 + j < n ? p[r0 + j] : (T)0;
+        }
+        // x past n is not data (stale LDS, possibly NaN): never multiply it, even by 0
+        if (r0 + 32 <= n) {
+#pragma unroll
+            for (int j = 0; j < 32; j += 2) {
+                s0 = fma(y[j], x[r0 + j], s0);
+                s1 = fma(y[j + 1], x[r0 + j + 1], s1);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 32; ++j)
+                if (r0 + j < n) s0 = fma(y[j], x[r0 + j], s0);
+        }
+    }
+    return s0 + s1;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(64 * KF_W) kb_bwd_kernel(KbArgs<T> a, int64_t nb)
 {
@@ -1832,8 +1909,9 @@ __global__ void __launch_bounds__(64 * KF_W) kb_bwd_kernel(KbArgs<T> a, int64_t 
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t tl = (int64_t)blockIdx.x * KF_W + wave;
     if (tl >= nb) return;
-    T *xb = (T *)kb_lds_raw + wave * KBW_V;          // x = [μ_j; λ_j] in Y's row order past D2
-    T *tb = xb + 128, *vb = tb + 128, *zb = vb + 64, *lb = zb + 64, *eb = lb + 64;
+    constexpr int V = 16 / sizeof(T);
+    T *xb = (T *)kb_lds_raw + wave * (KBW_V + KBW_W);  // x = [μ_j; λ_j] in Y's row order past D2
+    T *tb = xb + 128, *vb = tb + 128, *zb = vb + 64, *lb = zb + 64, *eb = lb + 64, *wl = xb + KBW_V;
     const int64_t t = a.b0 + tl, ty = a.yrel ? tl : t;
     const T *Yt = a.Y + ty * a.sY, *Ht = a.H + t * a.sH, *gt = a.g + ty * a.sg;
     T *dzt = a.dz + t * a.sg, *lat = a.lam + t * a.sy;
@@ -1846,7 +1924,7 @@ __global__ void __launch_bounds__(64 * KF_W) kb_bwd_kernel(KbArgs<T> a, int64_t 
         oS += slab_size(r16(m[1]), r16(m[2]));
         if (a.hfac) oU += (int64_t)m[3] * (m[3] + 1) / 2;
     }
-    // x ← B̃⁻¹ x for packed upper B̃⁻¹ (row dots), lane = row
+    // out_i = Σ_{c ≥ i} P[c(c+1)/2 + i]·x[c] for packed upper P (row dots), lane = row
     auto rowdot = [&](const T *P, const T *x, int n) __attribute__((always_inline)) {
         T s0 = (T)0, s1 = (T)0;
         if (lane < n) {
@@ -1878,29 +1956,32 @@ __global__ void __launch_bounds__(64 * KF_W) kb_bwd_kernel(KbArgs<T> a, int64_t 
         }
     }
     wsync();
+    const bool ybase16 = ((uintptr_t)Yt % 16) == 0;
     for (int j = N - 1; j >= 0; --j) {
         const T *Yk = Yt + qj.oY;
         const int nr = qj.rows - qj.p1;
+        // 16-B loads of column runs need every column start 16-B aligned
+        const bool vt = ybase16 && (qj.oY % V) == 0 && (qj.rows % V) == 0 && (qj.p1 % V) == 0;
+        const bool vs = ybase16 && (qj.oY % V) == 0 && (qj.rows % V) == 0;
+        T hraw[2], graw[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int c = lane + 64 * u;
+            hraw[u] = (c < qj.w && a.ginv && !a.hfac) ? Ht[qj.oH + c] : (T)1;
+            graw[u] = (c < qj.w && a.ginv) ? gt[qj.og + c] : (T)0;
+        }
         // t = [C; D1]ᵀ[μ_j; λ_j] (calc_residual!'s Cᵀμ + D1ᵀλ, :219-231), lane = column
         T tc[2], hc[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int c = lane + 64 * u;
-            T s0 = (T)0, s1 = (T)0, s2 = (T)0, s3 = (T)0, h = (T)0;
+            T tt = (T)0, h = (T)0;
             if (c < qj.w) {
-                const T *col = Yk + (int64_t)c * qj.rows + qj.p1;
-                int r = 0;
-                for (; r + 3 < nr; r += 4) {
-                    s0 = fma(col[r], xb[r], s0);
-                    s1 = fma(col[r + 1], xb[r + 1], s1);
-                    s2 = fma(col[r + 2], xb[r + 2], s2);
-                    s3 = fma(col[r + 3], xb[r + 3], s3);
-                }
-                for (; r < nr; ++r) s0 = fma(col[r], xb[r], s0);
-                h = (a.ginv && !a.hfac) ? (T)1 / Ht[qj.oH + c] : (T)1;
-                tb[c] = ((s0 + s1) + (s2 + s3)) * h;
+                tt = dot_run<T>(Yk + (int64_t)c * qj.rows + qj.p1, xb, nr, vt);
+                h = (a.ginv && !a.hfac) ? (T)1 / hraw[u] : (T)1;
+                tb[c] = tt * h;
             }
-            tc[u] = (s0 + s1) + (s2 + s3);
+            tc[u] = tt;
             hc[u] = h;
         }
         wsync();
@@ -1911,25 +1992,58 @@ __global__ void __launch_bounds__(64 * KF_W) kb_bwd_kernel(KbArgs<T> a, int64_t 
             const T *Sk = St + oS;
             const int nW = qp.P2 * (qp.P2 + 1) / 2, nBv = qp.Ps * (qp.Ps + 1) / 2, nE = qp.Ps * qp.P2;
             const T *Bl = Sk + nW, *El = Bl + nBv, *fm = El + nE, *fl = fm + qp.Ps;
-            // v = D2 H⁻¹ t = D_{k+1}μ_{k+1} + F_{k+1}λ_{k+1}, lane = row (coalesced columns)
+            // W_{j−1} (packed) → LDS, all loads in flight at once
+            {
+                const int nv = nW / V;
+                const bool wv = ((uintptr_t)Sk % 16) == 0;
+                if (wv) {
+                    typedef T tv __attribute__((ext_vector_type(V)));
+                    for (int e0 = 0; e0 < nv; e0 += 64 * 8) {
+                        tv w8[8];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) {
+                            const int e = e0 + lane + 64 * u;
+                            if (e < nv) w8[u] = *(const tv *)(Sk + V * e);
+                        }
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) {
+                            const int e = e0 + lane + 64 * u;
+                            if (e < nv) *(tv *)(wl + V * e) = w8[u];
+                        }
+                    }
+                    for (int e = V * nv + lane; e < nW; e += 64) wl[e] = Sk[e];
+                } else {
+                    for (int e = lane; e < nW; e += 64) wl[e] = Sk[e];
+                }
+            }
+            // v = D2 H⁻¹ t = D_{k+1}μ_{k+1} + F_{k+1}λ_{k+1}, lane = row (coalesced columns, 16 in flight)
             {
                 T s0 = (T)0, s1 = (T)0;
-                if (lane < qj.p1) {
-                    int c = 0;
-                    for (; c + 1 < qj.w; c += 2) {
-                        s0 = fma(Yk[lane + (int64_t)c * qj.rows], tb[c], s0);
-                        s1 = fma(Yk[lane + (int64_t)(c + 1) * qj.rows], tb[c + 1], s1);
+                const int rl = lane < qj.p1 ? lane : 0;
+                for (int c0 = 0; c0 < qj.w; c0 += 16) {
+                    T y[16];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) y[u] = c0 + u < qj.w ? Yk[rl + (int64_t)(c0 + u) * qj.rows] : (T)0;
+                    if (c0 + 16 <= qj.w) {
+#pragma unroll
+                        for (int u = 0; u < 16; u += 2) {
+                            s0 = fma(y[u], tb[c0 + u], s0);
+                            s1 = fma(y[u + 1], tb[c0 + u + 1], s1);
+                        }
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < 16; ++u)
+                            if (c0 + u < qj.w) s0 = fma(y[u], tb[c0 + u], s0);
                     }
-                    if (c < qj.w) s0 = fma(Yk[lane + (int64_t)c * qj.rows], tb[c], s0);
                 }
-                vb[lane] = s0 + s1;
+                vb[lane] = lane < qj.p1 ? s0 + s1 : (T)0;
             }
             wsync();
             // λ_{j−1} = C̃⁻¹(λ + C̃⁻ᵀv) = W(λ + Wᵀv)  (:128-135): z = fl + Wᵀv (lane = column)
             {
                 T s0 = (T)0, s1 = (T)0;
                 if (lane < qp.P2) {
-                    const T *wc = Sk + lane * (lane + 1) / 2;
+                    const T *wc = wl + lane * (lane + 1) / 2;
                     int i = 0;
                     for (; i + 1 <= lane; i += 2) {
                         s0 = fma(wc[i], vb[i], s0);
@@ -1940,7 +2054,7 @@ __global__ void __launch_bounds__(64 * KF_W) kb_bwd_kernel(KbArgs<T> a, int64_t 
                 }
             }
             wsync();
-            const T nl = rowdot(Sk, zb, qp.P2);
+            const T nl = rowdot(wl, zb, qp.P2);
             lb[lane] = nl;
             T nm = (T)0;
             if (qp.ps) {
@@ -1971,17 +2085,8 @@ __global__ void __launch_bounds__(64 * KF_W) kb_bwd_kernel(KbArgs<T> a, int64_t 
         for (int u = 0; u < 2; ++u) {
             const int c = lane + 64 * u;
             if (c < qj.w) {
-                T s0 = (T)0, s1 = (T)0;
-                if (j > 0) {
-                    const T *col = Yk + (int64_t)c * qj.rows;
-                    int r = 0;
-                    for (; r + 1 < qj.p1; r += 2) {
-                        s0 = fma(col[r], lb[r], s0);
-                        s1 = fma(col[r + 1], lb[r + 1], s1);
-                    }
-                    if (r < qj.p1) s0 = fma(col[r], lb[r], s0);
-                }
-                const T res = tc[u] + (s0 + s1) + (a.ginv ? gt[qj.og + c] : (T)0);
+                const T sd = j > 0 ? dot_run<T>(Yk + (int64_t)c * qj.rows, lb, qj.p1, vs) : (T)0;
+                const T res = tc[u] + sd + graw[u];
                 if (a.hfac) tb[c] = res;
                 else dzt[qj.og + c] = -(res * hc[u]);
             }
@@ -2140,7 +2245,7 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
     // scratch: [slab chunk·S][Z chunk·sY][gz chunk·sg][U⁻¹ chunk·sU] (dense H) [images chunk·IMGT] (split)
     T *slab = (T *)sc.p, *Z = slab + chunk * P.S, *gz = Z + chunk * a.sY, *Ui = gz + chunk * a.sg;
     T *img = P.hfac ? Ui + chunk * P.sU : Z;
-    constexpr int KS_NW = sizeof(T) == 4 ? 2 : 4;
+    constexpr int KS_NW = 4;
     const size_t lfac = (size_t)KF_W * (64 * KF_LU + 64) * sizeof(T);
     if (P.split && (e = hipFuncSetAttribute((const void *)kb_factor_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                             (int)lfac)) != hipSuccess) {
@@ -2205,7 +2310,7 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
             hipLaunchKernelGGL(kkt_big_fwd_kernel<T>, dim3((unsigned)nb), dim3(KB_THREADS), lf, s, k);
         if (P.split)
             hipLaunchKernelGGL(kb_bwd_kernel<T>, dim3((unsigned)((nb + KF_W - 1) / KF_W)), dim3(64 * KF_W),
-                               (size_t)KF_W * KBW_V * sizeof(T), s, k, nb);
+                               (size_t)KF_W * (KBW_V + KBW_W) * sizeof(T), s, k, nb);
         else
             hipLaunchKernelGGL(kkt_big_bwd_kernel<T>, dim3((unsigned)nb), dim3(KB_THREADS), lb, s, k);
         e = hipGetLastError();
