@@ -2126,10 +2126,10 @@ struct KbPlan {
     int nbt;                        // split: the Schur kernel's block grid (max R / 16)
 };
 
-// LQRX_KKT_SPLIT=1 enables the split path (default off until validated on hardware)
+// LQRX_KKT_SPLIT=0 keeps every structure on the fused forward kernel (A/B checks)
 int kb_split_env()
 {
-    static const int v = [] { const char *e = std::getenv("LQRX_KKT_SPLIT"); return e && *e ? std::atoi(e) : 0; }();
+    static const int v = [] { const char *e = std::getenv("LQRX_KKT_SPLIT"); return e && *e ? std::atoi(e) : 1; }();
     return v;
 }
 

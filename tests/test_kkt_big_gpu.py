@@ -268,3 +268,46 @@ def test_big_kkt_dense_h_info(lqrx, gpu_ok):
     assert ref["info"][2] == -7
     assert list(got["info"]) == list(ref["info"])
     assert traj_rel(got["dz"][:2], ref["dz"][:2]) <= TOL
+
+
+_FUSED_SCRIPT = r"""
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1] + "/lqr.jl_amd", sys.argv[1]]
+import lqrx, lqrx.kkt as K
+from oracle import oracle as orc
+worst = 0.0
+for n, m, N, dt in ((16, 8, 21, lqrx.F64), (64, 32, 9, lqrx.F64), (32, 16, 13, lqrx.F32)):
+    st = K.trajectory_structure(n, m, N)
+    pb = K.random_kkt(st, 3, seed=n + N, h_mode=K.H_DIAG, dyn="dense")
+    if dt == lqrx.F32:
+        import dataclasses
+        f = lambda a: np.asarray(a, np.float32).astype(np.float64)
+        pb = dataclasses.replace(pb, Y=f(pb.Y), y=f(pb.y), H=f(pb.H), g=f(pb.g))
+    got = K.kkt_solve(pb, dtype=dt)
+    ref = orc.kkt_solve_batch(orc.KktStructure(n, m, N, st.p), 3, pb.Y, pb.y, pb.H, pb.g, h_mode=2, nthreads=4)
+    r = ref["dz"].reshape(3, -1)
+    e = (np.abs(np.asarray(got["dz"], np.float64) - r).max(axis=1) / np.abs(r).max(axis=1)).max()
+    tol = 1e-10 if dt == lqrx.F64 else 1e-4
+    print(n, m, N, dt, "rel err", e)
+    if not (e <= tol and (got["info"] == 0).all()):
+        sys.exit(1)
+"""
+
+
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_big_kkt_fused_and_split_forward(lqrx, gpu_ok, tmp_path, split):
+    """Both forward sweeps of the large-block path on the trajectory structure: the split
+    Schur-kernel + factor-kernel path (default) and the fused one-workgroup-per-trajectory
+    kernel (LQRX_KKT_SPLIT=0, which every structure with stage constraints at interior knots
+    takes), fp64 and fp32, against the oracle (one child process each: the switch is read
+    once per process)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    f = tmp_path / "fused.py"
+    f.write_text(_FUSED_SCRIPT)
+    env = dict(os.environ, LQRX_KKT_SPLIT=split)
+    p = subprocess.run([sys.executable, str(f), root], env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
