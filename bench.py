@@ -663,7 +663,7 @@ def main(argv=None):
             traffic, tsrc = traffic_lookup(f"kkt_dense_n{n}_m{m}_N{N}_B{bt}_{args.dtype}", args.traffic_json)
             roof = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                     "frac": achieved / peak, "traffic": traffic, "traffic_source": tsrc,
-                    "kernel": "kkt_big_fwd_kernel + kkt_big_bwd_kernel", "kernel_ms": kern_ms,
+                    "kernel": "kb_schur_kernel + kb_factor_kernel + kb_bwd_kernel (split path, lqrx_kkt_big.hip)", "kernel_ms": kern_ms,
                     "flops_per_traj_minimal": fl_min, "flops_per_traj_reference": fl_ref,
                     "reference_count_tflops": fl_ref * bt / (kern_ms * 1e-3) / 1e12,
                     "alg_bytes_per_launch": alg_bytes, "hbm_gbs_alg": alg_bytes / (kern_ms * 1e-3) / 1e9,
