@@ -1239,8 +1239,18 @@ __global__ void __launch_bounds__(KB_THREADS, 1) kkt_big_hfac_kernel(KhArgs<T> a
 // of conblocks.jl:403-425 (first (0,n,n), interior (n,0,n), last (n,n,0)) and any structure
 // without stage constraints at interior knots.  The backward kernel is shared (same slab).
 
-constexpr int KS_L = 16;       // knots per Schur unit (one extra A-only pass per unit)
-constexpr int KS_PF = 4;       // k-slices in flight per Schur wave
+// tunables (tools/tv_ablate.sh A/B builds override them)
+#ifndef KS_L_KNOTS
+#define KS_L_KNOTS 64
+#endif
+#ifndef KS_PF_SLICES
+#define KS_PF_SLICES 2
+#endif
+#ifndef KS_MIN_BLOCKS
+#define KS_MIN_BLOCKS 4
+#endif
+constexpr int KS_L = KS_L_KNOTS;     // knots per Schur unit (one extra A-only pass per unit)
+constexpr int KS_PF = KS_PF_SLICES;  // k-slices in flight per Schur wave
 constexpr int KF_W = 4;        // trajectories (waves) per factor workgroup
 constexpr int KF_LU = 68;      // factor LDS image leading dimension
 
@@ -1467,7 +1477,7 @@ __device__ __forceinline__ int img_tile(const Kn &q, const Im &o, int I, int J)
 // written from the two knots' r (LDS).  The run's last pass forms only the A tiles (and r1)
 // of the first knot of the next run.
 template <typename T, int NW, int NBT>
-__global__ void __launch_bounds__(64 * NW) kb_schur_kernel(KsArgs<T> a)
+__global__ void __launch_bounds__(64 * NW, KS_MIN_BLOCKS) kb_schur_kernel(KsArgs<T> a)
 {
     constexpr int ST = (36 + NW - 1) / NW;
     __shared__ T rbuf[2][KB_RMAX];                 // r of two knots (padded row order)
@@ -1864,6 +1874,14 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_k
 // once per knot; the D2 rows a second time, from L2).
 constexpr int KBW_V = 8 * 64;     // per-wave LDS vector elements
 constexpr int KBW_W = 2080 + 64;  // per-wave LDS image of the packed W (≤ 64×65/2)
+#ifndef KBW_VC_COLS
+#define KBW_VC_COLS 16
+#endif
+#ifndef KBW_RUN
+#define KBW_RUN 32
+#endif
+constexpr int KBW_VC = KBW_VC_COLS;  // columns of Y in flight per lane in the v product
+constexpr int KBW_R = KBW_RUN;       // column-run elements in flight per lane (t, D2ᵀλ)
 
 // Σ_{r<n} p[r]·x[r] for a contiguous run p (global) and x (LDS, broadcast reads), n ≤ 128:
 // every load of a 32-element chunk issued before its FMAs (16-B vector loads when `vec`)
@@ -1873,29 +1891,29 @@ __device__ __forceinline__ T dot_run(const T *p, const T *x, int n, bool vec)
     constexpr int V = 16 / sizeof(T);
     typedef T tv __attribute__((ext_vector_type(V)));
     T s0 = (T)0, s1 = (T)0;
-    for (int r0 = 0; r0 < n; r0 += 32) {
-        T y[32];
-        if (vec && r0 + 32 <= n) {
+    for (int r0 = 0; r0 < n; r0 += KBW_R) {
+        T y[KBW_R];
+        if (vec && r0 + KBW_R <= n) {
 #pragma unroll
-            for (int j = 0; j < 32 / V; ++j) {
+            for (int j = 0; j < KBW_R / V; ++j) {
                 const tv w = *(const tv *)(p + r0 + V * j);
 #pragma unroll
                 for (int e = 0; e < V; ++e) y[V * j + e] = w[e];
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < 32; ++j) y[j] = r0 + j < n ? p[r0 + j] : (T)0;
+            for (int j = 0; j < KBW_R; ++j) y[j] = r0 + j < n ? p[r0 + j] : (T)0;
         }
         // x past n is not data (stale LDS, possibly NaN): never multiply it, even by 0
-        if (r0 + 32 <= n) {
+        if (r0 + KBW_R <= n) {
 #pragma unroll
-            for (int j = 0; j < 32; j += 2) {
+            for (int j = 0; j < KBW_R; j += 2) {
                 s0 = fma(y[j], x[r0 + j], s0);
                 s1 = fma(y[j + 1], x[r0 + j + 1], s1);
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < 32; ++j)
+            for (int j = 0; j < KBW_R; ++j)
                 if (r0 + j < n) s0 = fma(y[j], x[r0 + j], s0);
         }
     }
@@ -2020,19 +2038,19 @@ __global__ void __launch_bounds__(64 * KF_W) kb_bwd_kernel(KbArgs<T> a, int64_t 
             {
                 T s0 = (T)0, s1 = (T)0;
                 const int rl = lane < qj.p1 ? lane : 0;
-                for (int c0 = 0; c0 < qj.w; c0 += 16) {
-                    T y[16];
+                for (int c0 = 0; c0 < qj.w; c0 += KBW_VC) {
+                    T y[KBW_VC];
 #pragma unroll
-                    for (int u = 0; u < 16; ++u) y[u] = c0 + u < qj.w ? Yk[rl + (int64_t)(c0 + u) * qj.rows] : (T)0;
-                    if (c0 + 16 <= qj.w) {
+                    for (int u = 0; u < KBW_VC; ++u) y[u] = c0 + u < qj.w ? Yk[rl + (int64_t)(c0 + u) * qj.rows] : (T)0;
+                    if (c0 + KBW_VC <= qj.w) {
 #pragma unroll
-                        for (int u = 0; u < 16; u += 2) {
+                        for (int u = 0; u < KBW_VC; u += 2) {
                             s0 = fma(y[u], tb[c0 + u], s0);
                             s1 = fma(y[u + 1], tb[c0 + u + 1], s1);
                         }
                     } else {
 #pragma unroll
-                        for (int u = 0; u < 16; ++u)
+                        for (int u = 0; u < KBW_VC; ++u)
                             if (c0 + u < qj.w) s0 = fma(y[u], tb[c0 + u], s0);
                     }
                 }
