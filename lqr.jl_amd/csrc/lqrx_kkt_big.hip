@@ -1574,8 +1574,54 @@ struct KfArgs {
     int32_t *info;
     const int32_t *meta;
     int N, hfac;
+    int kb, ke;                    // knot range of this launch (the state at kb − 1 is in the slab)
     int64_t b0, nb, IMGT, sS;
 };
+
+// W_{k} (packed upper, slab) → C-layout tiles of X (padded P = 16·nt), and λ_k → row layout
+template <typename T>
+__device__ __forceinline__ void kf_resume(acc_t<T> (&X)[10], T (&lam)[4][4], const T *Sk, int P2, int Ps, int nt, int lane)
+{
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = i; j < 4; ++j)
+            if (j < nt) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = 16 * i + Tile<T>::row(lane, r), col = 16 * j + (lane & 15);
+                    X[up4(i, j)][r] = row <= col ? Sk[col * (col + 1) / 2 + row] : (T)0;
+                }
+            }
+    const int oM = P2 * (P2 + 1) / 2 + Ps * (Ps + 1) / 2 + Ps * P2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int e = 16 * i + Tile<T>::row(lane, r);
+            lam[i][r] = e < P2 ? Sk[oM + Ps + e] : (T)0;
+        }
+}
+__device__ __forceinline__ int64_t slab_before(const int32_t *meta, int k)
+{
+    int64_t o = 0;
+    for (int j = 0; j < k; ++j) o += slab_size(r16(meta[8 * j + 1]), r16(meta[8 * j + 2]));
+    return o;
+}
+__device__ __forceinline__ int64_t img_before(const int32_t *meta, int k)
+{
+    int64_t o = 0;
+    for (int j = 0; j < k; ++j) o += img_len(meta, j);
+    return o;
+}
+// info of a launch over knots [kb, ke): the first launch sets it (a non-SPD H_k of the hfac
+// pre-pass, −(k+1), takes precedence); later launches only fill a still-zero entry
+__device__ __forceinline__ void kf_info(int32_t *info, int64_t t, int v, int kb, int hfac)
+{
+    if (!info) return;
+    if (kb == 0 && !hfac) info[t] = v;
+    else if (v && info[t] == 0) info[t] = v;
+}
 
 // In place on the upper tiles X (packed up4) of a P×P SPD matrix (nb ≤ 4 block rows, p real
 // pivots): X ← U⁻¹ with UᵀU = X.  Right-looking by 16 as chol_inv: leaf (LDS, one wave) →
@@ -1687,13 +1733,18 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_k
     const int64_t t = a.b0 + tl;
     const T *imt = a.img + tl * a.IMGT;
     T *St = a.slab + tl * a.sS;
-    int64_t oI = 0, oS = 0;
+    int64_t oI = img_before(a.meta, a.kb), oS = slab_before(a.meta, a.kb);
     acc_t<T> X[10], G[16];
     T lam[4][4];                                     // λ_{k−1}, row layout
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) lam[i][r] = (T)0;
+    if (a.kb > 0) {
+        const int32_t *m = a.meta + 8 * (a.kb - 1);
+        const int P2 = r16(m[2]), Ps = r16(m[1]);
+        kf_resume<T>(X, lam, St + oS - slab_size(Ps, P2), P2, Ps, P2 >> 4, lane);
+    }
     int info = 0;
     // the D or F tiles of knot kn (n1 > 0) into G, every load in flight at once
     auto prefetch_g = [&](int kn, int64_t oIn) __attribute__((always_inline)) {
@@ -1708,7 +1759,7 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_k
             for (int j = 0; j < 4; ++j)
                 if (L < n1n && j < gc) G[L * 4 + j] = gload_tile(Yb + 256 * (L * gc + j), lane);
     };
-    for (int k = 0; k < a.N; ++k) {
+    for (int k = a.kb; k < a.ke; ++k) {
         const Kn q = kn_load(a.meta, k);
         const Im o = img_off(q.P1, q.Ps, q.P2);
         const T *ik = imt + oI;
@@ -1855,13 +1906,129 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_k
         }
         if (bad && !info) info = k + 1;
     }
-    if (lane == 0 && a.info) {
-        if (a.hfac) {
-            if (a.info[t] == 0) a.info[t] = info;   // a non-SPD H_k (−(k+1)) takes precedence
-        } else {
-            a.info[t] = info;
-        }
+    if (lane == 0) kf_info(a.info, t, info, a.kb, a.hfac);
+}
+
+// The interior knots of a trajectory structure (n1 = n2 = 16·NT padded, p = 0) with compile-time
+// tile counts: F̃ = Wᵀ F in place on the F tiles, C −= F̃ᵀF̃, chol + inverse, λ = Wᵀ(d − F̃ᵀλ).  The
+// next knot's F and C tiles (and d) are requested as soon as this knot's copies are dead, so
+// their latency runs under the factorisation.
+template <typename T, int NT>
+__global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_mid_kernel(KfArgs<T> a)
+{
+    extern __shared__ __align__(16) unsigned char kb_lds_raw[];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t tl = (int64_t)blockIdx.x * KF_W + wave;
+    if (tl >= a.nb) return;
+    T *U = (T *)kb_lds_raw + wave * (64 * KF_LU + 64), *vb = U + 64 * KF_LU;
+    const int64_t t = a.b0 + tl;
+    const T *imt = a.img + tl * a.IMGT;
+    T *St = a.slab + tl * a.sS;
+    constexpr int NG = NT * NT, NX = NT * (NT + 1) / 2, PP = 16 * NT;   // X, Cn: up4-packed
+    int64_t oI = img_before(a.meta, a.kb), oS = slab_before(a.meta, a.kb);
+    acc_t<T> X[10], G[16], Cn[10];
+    T lam[4][4], dd[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lam[i][r] = (T)0;
+    {
+        const int32_t *m = a.meta + 8 * (a.kb - 1);
+        kf_resume<T>(X, lam, St + oS - slab_size(r16(m[1]), r16(m[2])), r16(m[2]), r16(m[1]), NT, lane);
     }
+    // the image of an interior knot: F (NT×NT tiles), C (upper), v = d (PP)
+    constexpr Im o = {0, 0, NG, NG, NG, 256 * (NG + NX), 256 * (NG + NX) + PP};
+    auto fetch = [&](const T *ik) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < NG; ++u) G[u] = gload_tile(ik + 256 * (o.F + u), lane);
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+            for (int j = i; j < NT; ++j) Cn[up4(i, j)] = gload_tile(ik + 256 * (o.C + upn(i, j, NT)), lane);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) dd[j] = ik[o.v + 16 * j + (lane & 15)];
+    };
+    fetch(imt + oI);
+    int info = 0;
+    for (int k = a.kb; k < a.ke; ++k) {
+        const int p2 = a.meta[8 * k + 2];
+        T *Sk = St + oS;
+        oI += img_len(a.meta, k);
+        oS += slab_size(0, PP);
+        // F̃ = Ã⁻ᵀF (:57) in place, column of tiles by column
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            acc_t<T> Yc[NT];
+#pragma unroll
+            for (int L = 0; L < NT; ++L) Yc[L] = G[L * NT + j];
+#pragma unroll
+            for (int i = 0; i < NT; ++i) {
+                acc_t<T> g = tzero<T>();
+#pragma unroll
+                for (int L = 0; L <= i; ++L) g = mtn<T>(X[up4(L, i)], Yc[L], g);
+                G[i * NT + j] = g;
+            }
+        }
+        // F̃ᵀλ_{k−1}, then x = d − F̃ᵀλ_{k−1} (column layout)
+        T x[4];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            T sacc = (T)0;
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) sacc = fma(G[i * NT + j][r], lam[i][r], sacc);
+            sacc += __shfl_xor(sacc, 16);
+            sacc += __shfl_xor(sacc, 32);
+            x[j] = dd[j] - sacc;
+        }
+        // C − F̃ᵀF̃ (:61) → X
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+            for (int j = i; j < NT; ++j) {
+                acc_t<T> c = Cn[up4(i, j)];
+#pragma unroll
+                for (int L = 0; L < NT; ++L) c = mtn<T, true>(G[L * NT + i], G[L * NT + j], c);
+                X[up4(i, j)] = c;
+            }
+        // G, Cn, dd are dead: knot k+1's tiles land during the factorisation below
+        if (k + 1 < a.ke) fetch(imt + oI);
+        const int bad = chol_inv_reg<T>(X, NT, p2, U, lane);
+        // λ = C̃⁻ᵀ(d − F̃ᵀλ_{k−1}) (:108-116)
+        T xr[4][4], lc[4];
+        col2row<T>(xr, x, vb, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            T sacc = (T)0;
+            if (j < NT) {
+#pragma unroll
+                for (int i = 0; i <= j; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) sacc = fma(X[up4(i, j)][r], xr[i][r], sacc);
+            }
+            sacc += __shfl_xor(sacc, 16);
+            sacc += __shfl_xor(sacc, 32);
+            lc[j] = sacc;
+        }
+        col2row<T>(lam, lc, vb, lane);
+        // slab: W_k packed upper, λ
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+            for (int j = i; j < NT; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = 16 * i + Tile<T>::row(lane, r), col = 16 * j + (lane & 15);
+                    if (row <= col) Sk[col * (col + 1) / 2 + row] = X[up4(i, j)][r];
+                }
+        if (lane < 16) {
+#pragma unroll
+            for (int j = 0; j < NT; ++j) Sk[PP * (PP + 1) / 2 + 16 * j + lane] = lc[j];
+        }
+        if (bad && !info) info = k + 1;
+    }
+    if (lane == 0) kf_info(a.info, t, info, a.kb, a.hfac);
 }
 
 // ---------------------------------------------------------------- backward sweep (split path)
@@ -2142,8 +2309,15 @@ struct KbPlan {
     int64_t IMGT;                   // split: image elements per trajectory
     int nruns;                      // split: Schur units per trajectory
     int nbt;                        // split: the Schur kernel's block grid (max R / 16)
+    int mid0, mid1, midnt;          // split: knots [mid0, mid1) run on kb_factor_mid_kernel<midnt>
 };
 
+// LQRX_KKT_MID=0 keeps the interior knots on the general factor kernel (A/B checks)
+int kb_mid_env()
+{
+    static const int v = [] { const char *e = std::getenv("LQRX_KKT_MID"); return e && *e ? std::atoi(e) : 1; }();
+    return v;
+}
 // LQRX_KKT_SPLIT=0 keeps every structure on the fused forward kernel (A/B checks)
 int kb_split_env()
 {
@@ -2211,6 +2385,32 @@ bool kb_plan(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_
     P.IMGT = IMGT;
     P.nruns = (a.N + KS_L - 1) / KS_L;
     P.nbt = RM >> 4;
+    // the longest run of interior knots (p = 0, n1 = n2 = one padded size, knot 0 excluded:
+    // the mid kernel resumes from the slab state of the knot before)
+    P.mid0 = P.mid1 = 0;
+    P.midnt = 0;
+    if (P.split && kb_mid_env()) {
+        int best0 = 0, best1 = 0;
+        for (int k = 1; k < a.N;) {
+            const int P2 = r16(n2[k]);
+            if (p[k] == 0 && P2 > 0 && r16(n1[k]) == P2) {
+                int e = k;
+                while (e < a.N && p[e] == 0 && r16(n2[e]) == P2 && r16(n1[e]) == P2) ++e;
+                if (e - k > best1 - best0) {
+                    best0 = k;
+                    best1 = e;
+                }
+                k = e;
+            } else {
+                ++k;
+            }
+        }
+        if (best1 - best0 >= 2) {
+            P.mid0 = best0;
+            P.mid1 = best1;
+            P.midnt = r16(n2[best0]) >> 4;
+        }
+    }
     constexpr size_t LDS_CAP = 160 * 1024;
     return (size_t)P.nf * tsize <= LDS_CAP && (size_t)P.nb * tsize <= LDS_CAP && (size_t)P.nh * tsize <= LDS_CAP;
 }
@@ -2265,8 +2465,12 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
     T *img = P.hfac ? Ui + chunk * P.sU : Z;
     constexpr int KS_NW = 4;
     const size_t lfac = (size_t)KF_W * (64 * KF_LU + 64) * sizeof(T);
-    if (P.split && (e = hipFuncSetAttribute((const void *)kb_factor_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            (int)lfac)) != hipSuccess) {
+    if (P.split && ((e = hipFuncSetAttribute((const void *)kb_factor_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lfac)) != hipSuccess ||
+                    (e = hipFuncSetAttribute((const void *)kb_factor_mid_kernel<T, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfac)) != hipSuccess ||
+                    (e = hipFuncSetAttribute((const void *)kb_factor_mid_kernel<T, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfac)) != hipSuccess ||
+                    (e = hipFuncSetAttribute((const void *)kb_factor_mid_kernel<T, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfac)) != hipSuccess ||
+                    (e = hipFuncSetAttribute((const void *)kb_factor_mid_kernel<T, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfac)) != hipSuccess)) {
         (void)sc.release(s);
         return e;
     }
@@ -2323,7 +2527,27 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
             default: hipLaunchKernelGGL((kb_schur_kernel<T, KS_NW, 8>), gs, bs, 0, s, ks); break;
 #undef KS_L_
             }
-            hipLaunchKernelGGL(kb_factor_kernel<T>, dim3((unsigned)((nb + KF_W - 1) / KF_W)), dim3(64 * KF_W), lfac, s, kf);
+            const dim3 gf((unsigned)((nb + KF_W - 1) / KF_W)), bf(64 * KF_W);
+            auto generic = [&](int k0_, int k1_) {
+                if (k0_ >= k1_) return;
+                kf.kb = k0_;
+                kf.ke = k1_;
+                hipLaunchKernelGGL(kb_factor_kernel<T>, gf, bf, lfac, s, kf);
+            };
+            if (P.mid1 > P.mid0) {
+                generic(0, P.mid0);
+                kf.kb = P.mid0;
+                kf.ke = P.mid1;
+                switch (P.midnt) {
+                case 1: hipLaunchKernelGGL((kb_factor_mid_kernel<T, 1>), gf, bf, lfac, s, kf); break;
+                case 2: hipLaunchKernelGGL((kb_factor_mid_kernel<T, 2>), gf, bf, lfac, s, kf); break;
+                case 3: hipLaunchKernelGGL((kb_factor_mid_kernel<T, 3>), gf, bf, lfac, s, kf); break;
+                default: hipLaunchKernelGGL((kb_factor_mid_kernel<T, 4>), gf, bf, lfac, s, kf); break;
+                }
+                generic(P.mid1, a.N);
+            } else {
+                generic(0, a.N);
+            }
         } else
             hipLaunchKernelGGL(kkt_big_fwd_kernel<T>, dim3((unsigned)nb), dim3(KB_THREADS), lf, s, k);
         if (P.split)
