@@ -86,3 +86,27 @@ def test_graph_ls(lqrx, gpu_ok):
     got, ref = _capture_and_replay(lambda s: ls_solve_device(t, N, stream=s), t, second)
     for k in ("U", "X", "info"):
         assert got[k].equal(ref[k]), k
+
+
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+def test_graph_kkt_big(lqrx, gpu_ok, dt):
+    """The large-block KKT path (split: Schur, general + interior factor, backward kernels) on
+    a caller workspace captured in a hipGraph, fp64 and fp32 (n=16, m=8: 4 + 1 + 1 + 1 kernels
+    per chunk)."""
+    import numpy as np
+    import torch
+    import lqrx.kkt as K
+
+    st, bt = K.trajectory_structure(16, 8, 13), 9
+    keys = ("Y", "y", "H", "g")
+    tdt = torch.float64 if dt == "f64" else torch.float32
+    code = lqrx.F64 if dt == "f64" else lqrx.F32
+    mk = lambda seed: {k: torch.from_numpy(np.ascontiguousarray(getattr(
+        K.random_kkt(st, bt, seed=seed, h_mode=K.H_DIAG, dyn="dense"), k).ravel())).to("cuda", tdt) for k in keys}
+    t = mk(5)
+    t["batch"] = bt
+    ws = torch.empty(K.workspace_size(st, bt, K.H_DIAG, 1, dtype=code), dtype=torch.uint8, device="cuda")
+    got, ref = _capture_and_replay(
+        lambda s: K.kkt_solve_device(st, t, K.H_DIAG, 1, stream=s, workspace=ws), t, mk(6))
+    for k in ("dz", "lam", "info"):
+        assert got[k].equal(ref[k]), k
