@@ -1250,6 +1250,7 @@ __global__ void __launch_bounds__(KB_THREADS, 1) kkt_big_hfac_kernel(KhArgs<T> a
 #define KS_MIN_BLOCKS 4
 #endif
 constexpr int KS_L = KS_L_KNOTS;     // knots per Schur unit (one extra A-only pass per unit)
+constexpr int KS_HG = KB_WMAX + 4;   // staged H⁻¹ / g row: w columns padded to the slice grid
 constexpr int KS_PF = KS_PF_SLICES;  // k-slices in flight per Schur wave
 constexpr int KF_W = 4;        // trajectories (waves) per factor workgroup
 constexpr int KF_LU = 68;      // factor LDS image leading dimension
@@ -1354,8 +1355,8 @@ template <> __device__ __forceinline__ double bload<double>(__amdgpu_buffer_rsrc
 // this wave's upper tiles (q = SI + NW·t) of Y H⁻¹ Yᵀ over the knot's padded row blocks and
 // its rows (v ≡ SI mod NW) of r = Y H⁻¹ g into rn; k-slices of 4 columns, KS_PF in flight
 template <typename T, int NBT, int SI, int NW>
-__device__ __forceinline__ void schur_tiles(const Kn &q, const T *Yt, const T *Ht, const T *gt, bool hinv, bool useg,
-                                            acc_t<T> (&acc)[(36 + NW - 1) / NW], T *rn, int lane)
+__device__ __forceinline__ void schur_tiles(const Kn &q, const T *Yt, const T *hgl, acc_t<T> (&acc)[(36 + NW - 1) / NW],
+                                            T *rn, int lane)
 {
     constexpr int ST = (36 + NW - 1) / NW, NTT = NBT * (NBT + 1) / 2;
     const int i16 = lane & 15, g4 = lane >> 4;
@@ -1386,8 +1387,6 @@ __device__ __forceinline__ void schur_tiles(const Kn &q, const T *Yt, const T *H
     // no address arithmetic and no exec-mask branch per load
     constexpr uint32_t TS = sizeof(T), OOB = 0x80000000u;
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)(Yt + q.oY), (short)0, q.rows * q.w * (int)TS, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void *)(Ht + q.oH), (short)0, q.w * (int)TS, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void *)(gt + q.og), (short)0, q.w * (int)TS, 0x00020000);
     uint32_t vo[NBT];
 #pragma unroll
     for (int v = 0; v < NBT; ++v) vo[v] = i16 < lim[v] ? (uint32_t)((g4 * q.rows + rb[v] + i16) * (int)TS) : OOB;
@@ -1400,11 +1399,11 @@ __device__ __forceinline__ void schur_tiles(const Kn &q, const T *Yt, const T *H
             if constexpr (ks_need(NBT, SI, NW, v)) fr[v] = bload<T>(ry, vo[v], so);
         });
         // raw H and g: the reciprocal is taken in step(), so nothing here waits for a load
-        h = bload<T>(rh, (uint32_t)(g4 * (int)TS), (uint32_t)(4 * s) * TS);
-        g_ = bload<T>(rg, (uint32_t)(g4 * (int)TS), (uint32_t)(4 * s) * TS);
+        h = hgl[4 * s + g4];                       // H⁻¹ (or 1; 0 past w) and g, staged per knot
+        g_ = hgl[KS_HG + 4 * s + g4];
     };
     auto step = [&](const T (&fr)[NBT], T hx, T gx, int s) __attribute__((always_inline)) {
-        const T h = 4 * s + g4 < q.w ? (hinv ? (T)1 / hx : (T)1) : (T)0, g_ = useg ? gx : (T)0;
+        const T h = hx, g_ = gx;
         T fh[NBT];
         sfor<NBT>([&](auto vc) {
             constexpr int v = decltype(vc)::value;
@@ -1449,13 +1448,13 @@ __device__ __forceinline__ void schur_tiles(const Kn &q, const T *Yt, const T *H
 }
 
 template <typename T, int NW, int NBT>
-__device__ __forceinline__ void schur_tiles_d(const Kn &q, int si, const T *Yt, const T *Ht, const T *gt, bool hinv,
-                                              bool useg, acc_t<T> (&acc)[(36 + NW - 1) / NW], T *rn, int lane)
+__device__ __forceinline__ void schur_tiles_d(const Kn &q, int si, const T *Yt, const T *hgl,
+                                              acc_t<T> (&acc)[(36 + NW - 1) / NW], T *rn, int lane)
 {
-    if (si == 0) schur_tiles<T, NBT, 0, NW>(q, Yt, Ht, gt, hinv, useg, acc, rn, lane);
-    else if (si == 1) schur_tiles<T, NBT, 1 % NW, NW>(q, Yt, Ht, gt, hinv, useg, acc, rn, lane);
-    else if (NW > 2 && si == 2) schur_tiles<T, NBT, 2 % NW, NW>(q, Yt, Ht, gt, hinv, useg, acc, rn, lane);
-    else if (NW > 3) schur_tiles<T, NBT, 3 % NW, NW>(q, Yt, Ht, gt, hinv, useg, acc, rn, lane);
+    if (si == 0) schur_tiles<T, NBT, 0, NW>(q, Yt, hgl, acc, rn, lane);
+    else if (si == 1) schur_tiles<T, NBT, 1 % NW, NW>(q, Yt, hgl, acc, rn, lane);
+    else if (NW > 2 && si == 2) schur_tiles<T, NBT, 2 % NW, NW>(q, Yt, hgl, acc, rn, lane);
+    else if (NW > 3) schur_tiles<T, NBT, 3 % NW, NW>(q, Yt, hgl, acc, rn, lane);
 }
 
 // image tile of the global upper tile (I, J) of knot q (−1: an A tile, which belongs to the
@@ -1481,6 +1480,7 @@ __global__ void __launch_bounds__(64 * NW, KS_MIN_BLOCKS) kb_schur_kernel(KsArgs
 {
     constexpr int ST = (36 + NW - 1) / NW;
     __shared__ T rbuf[2][KB_RMAX];                 // r of two knots (padded row order)
+    __shared__ T hgl[2 * KS_HG];                   // H⁻¹ (or 1) | g of the knot, 0 past w
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t u = blockIdx.x, tl = u / a.nruns;
     const int run = (int)(u - tl * a.nruns);
@@ -1520,7 +1520,15 @@ __global__ void __launch_bounds__(64 * NW, KS_MIN_BLOCKS) kb_schur_kernel(KsArgs
         }
         // tiles over the launch's NBT×NBT block grid (the largest knot); rows past this
         // knot's R are zero fragments and their tiles are not stored
-        if (qs.R) schur_tiles_d<T, NW, NBT>(qs, wave, Yt, Ht, gt, a.hinv != 0, a.useg != 0, acc, rbuf[k & 1], lane);
+        // H⁻¹ (one division per column and knot, not per slice and lane) and g into LDS; the
+        // previous knot's readers are past the barriers that closed its iteration
+        for (int c = tid; c < KS_HG; c += 64 * NW) {
+            const bool in = c < q.w;
+            hgl[c] = in ? (a.hinv ? (T)1 / Ht[q.oH + c] : (T)1) : (T)0;
+            hgl[KS_HG + c] = (in && a.useg) ? gt[q.og + c] : (T)0;
+        }
+        __syncthreads();
+        if (qs.R) schur_tiles_d<T, NW, NBT>(qs, wave, Yt, hgl, acc, rbuf[k & 1], lane);
         const int nbt = qs.R >> 4, n1t = qs.P1 >> 4;
         if (!aonly) {
             const Im o = img_off(q.P1, q.Ps, q.P2);
