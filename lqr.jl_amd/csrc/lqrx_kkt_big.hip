@@ -1249,6 +1249,9 @@ __global__ void __launch_bounds__(KB_THREADS, 1) kkt_big_hfac_kernel(KhArgs<T> a
 #ifndef KS_MIN_BLOCKS
 #define KS_MIN_BLOCKS 4
 #endif
+#ifndef KS_MIN_BLOCKS_F64
+#define KS_MIN_BLOCKS_F64 3          // fp64 tiles need ~1.5x the registers: 4 blocks spill (r03g)
+#endif
 constexpr int KS_L = KS_L_KNOTS;     // knots per Schur unit (one extra A-only pass per unit)
 constexpr int KS_HG = KB_WMAX + 4;   // staged H⁻¹ / g row: w columns padded to the slice grid
 constexpr int KS_PF = KS_PF_SLICES;  // k-slices in flight per Schur wave
@@ -1476,7 +1479,8 @@ __device__ __forceinline__ int img_tile(const Kn &q, const Im &o, int I, int J)
 // written from the two knots' r (LDS).  The run's last pass forms only the A tiles (and r1)
 // of the first knot of the next run.
 template <typename T, int NW, int NBT>
-__global__ void __launch_bounds__(64 * NW, KS_MIN_BLOCKS) kb_schur_kernel(KsArgs<T> a)
+__global__ void __launch_bounds__(64 * NW, sizeof(T) == 8 ? KS_MIN_BLOCKS_F64 : KS_MIN_BLOCKS)
+kb_schur_kernel(KsArgs<T> a)
 {
     constexpr int ST = (36 + NW - 1) / NW;
     __shared__ T rbuf[2][KB_RMAX];                 // r of two knots (padded row order)
