@@ -22,6 +22,7 @@
 // The m×m Cholesky + two triangular solves run on the VALU in a lane-per-column layout of
 // the augmented matrix [E | G] (wave-uniform broadcasts via v_readlane), overlapping the
 // MFMA work of the other wave resident on the same SIMD (launch bounds: 2 waves/SIMD).
+#include <cstdlib>
 #include "lqrx_tile.h"
 #include "lqrx_internal.h"
 
@@ -710,6 +711,9 @@ hipError_t dp_launch(const DpArgs &a, hipStream_t s)
     // smallest instantiated tile grid that covers (n, m); padding is exact (zero rows /
     // columns, unit diagonal in R), see tiles_load
     const int nt = (a.n + 15) / 16, mt = (a.m + 15) / 16;
+    // LQRX_DP_BIG=1 sends every shape past the lane kernel to dp_big_kernel (A/B checks)
+    static const bool force_big = [] { const char *e = std::getenv("LQRX_DP_BIG"); return e && *e == '1'; }();
+    if (force_big && dp_big_supported(a.n, a.m)) return dp_big_launch(a, s);
     if (a.dtype == 0) {
         if (nt <= 1 && mt <= 1) return launch_dp_tv<double, 1, 1>(a, s);
         if (nt <= 2 && mt <= 1) return launch_dp_tv<double, 2, 1, LQRX_DP_WAVES, LQRX_DP_VAR>(a, s);
