@@ -1548,6 +1548,8 @@ LQRX_FIL_INST(3, 2, 3, 0, 3)
 LQRX_FIL_INST_DIAG(4, 1, 4, 0, 4)
 LQRX_FILD_INST(6, 3, 6, 1, 6)
 LQRX_FILD_INST(4, 2, 4, 1, 4)
+LQRX_FILD_INST(5, 2, 5, 0, 5)
+LQRX_FILD_INST(7, 3, 7, 0, 7)
 #undef LQRX_FIL_INST
 #undef LQRX_FIL_INST1
 #undef LQRX_FIL_INST_DIAG
@@ -1607,6 +1609,8 @@ static bool fil_dispatch(const KktArgs &a, const int32_t *n1, const int32_t *p, 
     LQRX_FIL_DIAG(4, 1, 4, 0, 4)   // cartpole trajectory problem (test/problems.jl:58-88, device SQP)
     LQRX_FILD(6, 3, 6, 1, 6)       // DoubleIntegrator(3) (test/problems.jl:14-56, test/cholesky_solve.jl)
     LQRX_FILD(4, 2, 4, 1, 4)       // DoubleIntegrator(2)
+    LQRX_FILD(5, 2, 5, 0, 5)       // trajectory_structure(5, 2, N), diagonal H (the SQP problems' shape)
+    LQRX_FILD(7, 3, 7, 0, 7)       // trajectory_structure(7, 3, N), diagonal H
 #undef LQRX_FIL
 #undef LQRX_FIL_SEL
 #undef LQRX_FIL_DIAG

@@ -96,7 +96,8 @@ def test_kkt_alternating_structures(lqrx, gpu_ok):
 
 @pytest.mark.parametrize("model,N,batch", [("dubins", 4, 130), ("dubins", 5, 64), ("dubins", 6, 1),
                                            ("dubins", 101, 16384 + 3), ("cartpole", 6, 130), ("cartpole", 7, 1),
-                                           ("cartpole", 101, 4096 + 5), ("di", 4, 70), ("di", 101, 1000)])
+                                           ("cartpole", 101, 4096 + 5), ("di", 4, 70), ("di", 101, 1000),
+                                           ("t52", 6, 67), ("t52", 101, 4096 + 7), ("t73", 8, 130), ("t73", 101, 1000)])
 @pytest.mark.parametrize("h_mode,ginv", [(2, 1), (0, 1), (2, 0)])
 def test_kkt_fil_shapes(lqrx, gpu_ok, model, N, batch, h_mode, ginv):
     """The compile-time-shaped first/interior/last kernel (lqrx_kkt_fil.hip) at its edge
@@ -107,7 +108,8 @@ def test_kkt_fil_shapes(lqrx, gpu_ok, model, N, batch, h_mode, ginv):
     N = 5 the system is square and a few of the random problems lose 1e-5 to rounding in the
     oracle and the generic kernel alike — measured, tools/kkt_shape_diag.py).
     DoubleIntegrator(3) (the structure of test/cholesky_solve.jl) runs the direct variant
-    kkt_fild_kernel for diagonal H / SOC, the large-block kernel for dense H; at N = 4 its
+    kkt_fild_kernel for diagonal H / SOC, the large-block kernel for dense H, and so do the
+    trajectory structures (5, 2, N) and (7, 3, N) ("t52", "t73"); at N = 4 DoubleIntegrator(3)'s
     S reaches cond ~7e6 and the oracle itself is 4.6e-11 from the exact solution, so the
     trajectories past 1e-10 are held to the refined truth instead (tests/kkt_truth.py)."""
     import lqrx.kkt as K
@@ -117,6 +119,10 @@ def test_kkt_fil_shapes(lqrx, gpu_ok, model, N, batch, h_mode, ginv):
         st = K.dubins_structure(N)
     elif model == "cartpole":
         st = K.trajectory_structure(4, 1, N)
+    elif model == "t52":
+        st = K.trajectory_structure(5, 2, N)
+    elif model == "t73":
+        st = K.trajectory_structure(7, 3, N)
     else:
         st = K.double_integrator_structure(3, N)
     pb = K.random_kkt(st, batch, seed=7 * N + h_mode, h_mode=h_mode)
@@ -165,7 +171,8 @@ def test_kkt_meta_cache_overflow(lqrx, gpu_ok):
 
 @pytest.mark.parametrize("model,N,batch", [("dubins", 4, 1), ("dubins", 5, 130), ("dubins", 101, 16384 + 3),
                                            ("cartpole", 7, 70), ("cartpole", 101, 4096 + 5),
-                                           ("di3", 4, 70), ("di3", 101, 1000), ("di2", 12, 67)])
+                                           ("di3", 4, 70), ("di3", 101, 1000), ("di2", 12, 67),
+                                           ("t52", 101, 1000 + 3), ("t73", 9, 70)])
 @pytest.mark.parametrize("h_mode,ginv", [(2, 1), (0, 1), (1, 1), (2, 0)])
 def test_kkt_layout1_soa(lqrx, gpu_ok, model, N, batch, h_mode, ginv):
     """ABI layout 1 (batch fastest: element e of trajectory t at [e·batch + t]) on the
@@ -176,7 +183,8 @@ def test_kkt_layout1_soa(lqrx, gpu_ok, model, N, batch, h_mode, ginv):
     import lqrx.kkt as K
 
     st = {"dubins": lambda: K.dubins_structure(N), "cartpole": lambda: K.trajectory_structure(4, 1, N),
-          "di3": lambda: K.double_integrator_structure(3, N), "di2": lambda: K.double_integrator_structure(2, N)}[model]()
+          "di3": lambda: K.double_integrator_structure(3, N), "di2": lambda: K.double_integrator_structure(2, N),
+          "t52": lambda: K.trajectory_structure(5, 2, N), "t73": lambda: K.trajectory_structure(7, 3, N)}[model]()
     if model != "dubins" and h_mode != 2 and ginv:
         pb = K.random_kkt(st, 2, seed=1, h_mode=h_mode)            # dense H: no SoA shape
         with pytest.raises(K._lib.LqrxError) as e:
@@ -196,11 +204,11 @@ def test_kkt_layout1_soa(lqrx, gpu_ok, model, N, batch, h_mode, ginv):
 
 
 def test_kkt_layout1_unsupported_shapes(lqrx, gpu_ok):
-    """Layout 1 is served by the compile-time shapes only: other structures (here n = 5, m = 2)
+    """Layout 1 is served by the compile-time shapes only: other structures (here n = 5, m = 3)
     and N < 4 return LQRX_ERR_UNSUPPORTED."""
     import lqrx.kkt as K
 
-    for st in (K.trajectory_structure(5, 2, 12), K.dubins_structure(3)):
+    for st in (K.trajectory_structure(5, 3, 12), K.dubins_structure(3)):
         pb = K.random_kkt(st, 3, seed=2, h_mode=K.H_DIAG)
         with pytest.raises(K._lib.LqrxError) as e:
             K.kkt_solve(pb, layout=1)
