@@ -306,6 +306,27 @@ def check_kkt_dense_sample(out, t, st, idx, bt, threads, f64):
             "oracle": "oracle/lqr_oracle.c (restatement of cholesky_solver.jl _solve!), fp64 on the same inputs"}
 
 
+def check_gathered_P(P, n, m, N, batch, seed, f64, threads, k=8):
+    """Checker for the §8(e) gather: P₁ of a strided sample of the GLOBAL batch (first and
+    last trajectory included, so every shard boundary region of a 2-rank run is crossed) as it
+    arrived on rank 0, against the CPU oracle on the same counter-generated inputs."""
+    import numpy as np
+    import torch
+    import lqrx
+    from oracle import oracle as orc
+
+    idx = _sample_index(batch, k)
+    Pg = P.view(batch, n * n).index_select(0, torch.from_numpy(idx).to(P.device)).double().cpu().numpy()
+    worst = 0.0
+    for j, i in enumerate(idx):
+        d = lqrx.random_batch(n, m, N, 1, seed=seed, traj0=int(i), dtype=lqrx.F64 if f64 else lqrx.F32)
+        ref = orc.dp_solve_abi(d, N, nthreads=threads)["P"].reshape(-1)
+        worst = max(worst, float(np.abs(Pg[j] - ref).max() / max(np.abs(ref).max(), 1e-300)))
+    tol = 1e-10 if f64 else 1e-4
+    return {"trajectories": len(idx), "indices": [int(i) for i in idx], "max_rel_err_P1": worst,
+            "tol": tol, "pass": bool(worst <= tol)}
+
+
 def nonfinite_count(out, keys):
     """Whole-batch scan of the timed launch's outputs on the device."""
     import torch
@@ -363,6 +384,10 @@ def main(argv=None):
     ap.add_argument("--linear", action="store_true",
                     help="dp: linear cost terms q, r, qf (lqrx_dp_solve_linear, SURVEY §8(f) rank 1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process-group backend for N > 1: nccl (= RCCL over xGMI, one GPU per rank) or "
+                         "gloo with host-staged collectives (lets several ranks share one GPU: the "
+                         "multi-rank test on a one-GPU box)")
     ap.add_argument("--no-gather", action="store_true",
                     help="skip the final info + P_1 gather to rank 0 (N > 1)")
     ap.add_argument("--traffic-json", default=None,
@@ -417,8 +442,19 @@ def main(argv=None):
     from lqrx import shard as SH
 
     rank, world, local = SH.dist_env()
+    # one GPU per rank; with fewer visible GPUs than ranks (the gloo rehearsal on a one-GPU
+    # box) ranks share devices round-robin — device_count() does not initialise the GPU
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        raise RuntimeError("bench.py: no GPU visible")
+    local = local % ndev
+    if args.dist_backend == "nccl" and world > ndev:
+        raise RuntimeError(f"bench.py: {world} ranks over {ndev} GPUs needs --dist-backend gloo "
+                           "(RCCL takes one GPU per rank)")
     torch.cuda.set_device(local)
-    SH.init_ranks("nccl", torch.device("cuda", local))
+    SH.init_ranks(args.dist_backend, torch.device("cuda", local))
+    # device of the collectives' tensors: the GPU for RCCL, the host for gloo
+    cdev = torch.device("cuda", local) if args.dist_backend == "nccl" else None
     lib = lqrx.load()
     if lib.lqrx_device_available() != 1:
         raise RuntimeError("liblqrx.so sees no gfx950 device")
@@ -549,7 +585,7 @@ def main(argv=None):
     # non-finite values; a strided sample compared with the CPU oracle (rank 0)
     nonfinite = nonfinite_count(out if args.workload != "sqp" else t,
                                 ("K", "P", "X", "U", "d", "p", "dz", "lam", "Z"))
-    nonfinite, bad = SH.sum_over_ranks([nonfinite, bad], world, dev)
+    nonfinite, bad = SH.sum_over_ranks([nonfinite, bad], world, cdev)
     sampled = None
     if rank == 0 and args.workload in ("dp", "cartpole", "kkt"):
         thr = max(1, min(16, os.cpu_count() or 1))
@@ -569,16 +605,30 @@ def main(argv=None):
     if world > 1 and args.workload in ("dp", "cartpole") and not args.no_gather:
         # a failure here propagates: the rank exits non-zero (spawn_ranks / the launcher
         # report it) instead of printing a line with the error folded into a field
-        g = SH.timed_gather({"info": out["info"], "P": out["P"]}, global_batch, world, sync, dev)
+        fields = {"info": out["info"], "P": out["P"]}
+        if cdev is None:       # gloo: host-staged (the copy is inside the timed gather)
+            fields = {k: v.cpu() for k, v in fields.items()}
+        g = SH.timed_gather(fields, global_batch, world, sync, cdev)
         got = g.pop("got")
         gather = dict(g, what="info + P_1 of every shard to rank 0 (torch.distributed.gather "
                               "= RCCL send/recv); K stays sharded",
+                      backend=args.dist_backend,
                       root_info_nonzero=int((got["info"] != 0).sum().item()) if got is not None else None)
         if got is not None and got["info"].numel() != global_batch:
             raise RuntimeError(f"gather delivered {got['info'].numel()} of {global_batch} trajectories")
+        if got is not None:
+            gather["delivered"] = int(got["info"].numel())
+            if args.workload == "dp":
+                gather["sampled_parity"] = check_gathered_P(got["P"], n, m, N, global_batch, args.seed, f64,
+                                                            max(1, min(16, os.cpu_count() or 1)))
         del got
+    shards = None
+    if world > 1:
+        import torch.distributed as dist
+        shards = [None] * world
+        dist.all_gather_object(shards, (traj0, bt))
 
-    wall = SH.max_over_ranks(wall, world, dev)
+    wall = SH.max_over_ranks(wall, world, cdev)
     total = global_batch * args.steps
     value = total / wall
     ms_per_step = wall / args.steps * 1e3
@@ -605,7 +655,7 @@ def main(argv=None):
             metric = f"{mname} SQP solves/sec (n={n} m={m} N={N}, <=10 steps, L1-merit line search + SOC)"
             workload = f"{mname} SQP around the KKT solve (SURVEY.md 8(f) ranks 2-3)"
             cpu = None
-            if not args.no_cpu_baseline and world == 1:
+            if not args.no_cpu_baseline:
                 sys.path.insert(0, ROOT)
                 import numpy as np
                 from oracle import sqp_oracle as S
@@ -639,7 +689,7 @@ def main(argv=None):
             metric = f"condensed least-squares LQR solves/sec (cartpole n=4 m=1 N={N} B={bt}, Hu=0 as a fresh solver)"
             workload = "LeastSquaresSolver solve! on cartpole (SURVEY.md 8(f) rank 4)"
             cpu = None
-            if not args.no_cpu_baseline and world == 1:
+            if not args.no_cpu_baseline:
                 sys.path.insert(0, ROOT)
                 from oracle import ls_oracle as LO
                 nb, t0c = 0, time.perf_counter()
@@ -682,7 +732,7 @@ def main(argv=None):
             workload = ("large-block banded KKT solve, cholesky_solver.jl _solve! (BASELINE.json configs[4]"
                         + (")" if (n, m, N, args.dtype) == (64, 32, 512, "f32") else " shape family)"))
             cpu = cpu_baseline_kkt_dense(st, target_s=args.cpu_seconds) \
-                if not args.no_cpu_baseline and world == 1 else None
+                if not args.no_cpu_baseline else None
         elif args.workload == "kkt":
             import lqrx.kkt as K
             sY, sy, sH, sg = st.sizes(K.H_DIAG)
@@ -705,7 +755,7 @@ def main(argv=None):
                 metric = f"KKT solves/sec (DoubleIntegrator(3,{N}) n=6 m=3 block-tridiagonal _solve!)"
                 workload = "DoubleIntegrator KKT structure of test/cholesky_solve.jl (non-baseline)"
             cpu = cpu_baseline_kkt(N, target_s=args.cpu_seconds, structure=args.kkt_structure) \
-                if not args.no_cpu_baseline and world == 1 else None
+                if not args.no_cpu_baseline else None
         else:
             flops = dp_flops_per_traj(n, m, N) * bt
             achieved = flops / (kern_ms * 1e-3) / 1e12
@@ -775,7 +825,7 @@ def main(argv=None):
                              "random dense time-invariant LQR") + ", Riccati backward pass + forward rollout"
                             + (" (BASELINE.json configs[4], per GPU)" if cfg5 else " (non-baseline shape)"))
             cpu = cpu_baseline(n, m, N, target_s=args.cpu_seconds, tv=args.tv, linear=args.linear) \
-                if not args.no_cpu_baseline and world == 1 else None
+                if not args.no_cpu_baseline else None
         if tsrc is not None:
             roof.setdefault("traffic_source", tsrc)
         if roof.get("bound") == "hbm":
@@ -794,7 +844,8 @@ def main(argv=None):
                                           "SURVEY.md §8(d) generator)",
             "config": {"workload": workload, "n": n, "m": m, "N": N, "batch_per_gpu": bt,
                        "global_batch": global_batch, "parallelism": f"batch-sharded x{world}",
-                       "shard_rank0": [traj0, bt]},
+                       "shard_rank0": [traj0, bt], "shards": shards,
+                       "dist_backend": args.dist_backend if world > 1 else None},
             "roofline": roof,
             "cpu_baseline": cpu,
             "check": {"nonfinite": nonfinite, "info_nonzero": bad, "sampled_parity": sampled},

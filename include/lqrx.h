@@ -38,8 +38,10 @@
 extern "C" {
 #endif
 
-#define LQRX_ABI_VERSION 3   /* 2: layout 1 (DP, KKT), lqrx_sqp_* (models, stage constraints);
-                                3: lqrx_dp_solve_linear[_host] (linear cost terms) */
+#define LQRX_ABI_VERSION 4   /* 2: layout 1 (DP, KKT), lqrx_sqp_* (models, stage constraints);
+                                3: lqrx_dp_solve_linear[_host] (linear cost terms), and
+                                   dtype LQRX_F32 on the KKT path (large-block kernels);
+                                4: lqrx_scratch_trim (release the library's pooled scratch) */
 
 #define LQRX_F64 0
 #define LQRX_F32 1
@@ -160,7 +162,9 @@ int lqrx_dp_solve_linear_host(const lqrx_dp_desc *desc, const void *A, const voi
  * ------------------------------------------------------------------------------------ */
 typedef struct lqrx_kkt_desc {
     int32_t N;          /* knots                                                  */
-    int32_t dtype;      /* LQRX_F64 only                                          */
+    int32_t dtype;      /* LQRX_F64 (every KKT kernel) or LQRX_F32 (the large-block
+                           MFMA kernels: n1, p, n2 <= 64, padded rows <= 128, w <= 128,
+                           layout 0, every h_mode and ginv; else LQRX_ERR_UNSUPPORTED) */
     int64_t batch;
     const int32_t *n1;  /* [N] host arrays describing the block structure           */
     const int32_t *p;   /* [N]                                                      */
@@ -172,11 +176,12 @@ typedef struct lqrx_kkt_desc {
                            trajectory t's packed array (Y, y, H, g, dz, lam) at
                            [t·len + e];  1 = batch fastest (SoA) at [e·batch + t] —
                            a wave's 64 trajectories read each element as one 512-B
-                           row.  Layout 1 is served by the compile-time shapes only
-                           (Dubins (3,2,3,0,3) every h_mode; cartpole (4,1,4,0,4),
-                           DoubleIntegrator(2)/(3) (4,2,4,1,4)/(6,3,6,1,6) diagonal
-                           H / SOC; N >= 4; arrays < 2 GiB), else
-                           LQRX_ERR_UNSUPPORTED                                       */
+                           row.  Layout 1 is served by the compile-time shapes only,
+                           (n̄, m, p_first, p_interior, p_last) = Dubins (3,2,3,0,3) every
+                           h_mode; cartpole (4,1,4,0,4), DoubleIntegrator(2)/(3)
+                           (4,2,4,1,4)/(6,3,6,1,6), trajectory_structure(5,2,N) /
+                           (7,3,N) (5,2,5,0,5)/(7,3,7,0,7) with diagonal H or ginv = 0;
+                           fp64; N >= 4; arrays < 2 GiB), else LQRX_ERR_UNSUPPORTED    */
     int32_t reserved;
 } lqrx_kkt_desc;
 
@@ -188,7 +193,12 @@ int lqrx_kkt_solve_host(const lqrx_kkt_desc *desc, const void *Y, const void *y,
  * serving loop or a captured hipGraph wants.  lqrx_kkt_workspace_size gives the bytes this
  * structure and batch need (0 for batch 0); lqrx_kkt_solve_ws returns -10 if
  * workspace_bytes is smaller.  One workspace must not be shared by calls in flight on
- * different streams (lqrx_kkt_solve draws stream-ordered scratch from a library pool). */
+ * different streams (lqrx_kkt_solve draws stream-ordered scratch from a library pool).
+ * Large blocks: the slab (+ Schur images) is sized for the batch but capped at
+ * LQRX_KKT_BIG_SLAB_MB (default 40 GiB); a larger batch runs in chunks through it.  Without
+ * a caller workspace that scratch comes from the library pool, whose freed blocks stay
+ * reserved for the next call (up to the cap) until lqrx_scratch_trim; an out-of-memory pool
+ * allocation retries with halved chunks. */
 int lqrx_kkt_workspace_size(const lqrx_kkt_desc *desc, size_t *bytes);
 int lqrx_kkt_solve_ws(const lqrx_kkt_desc *desc, const void *Y, const void *y, const void *H,
                       const void *g, void *dz, void *lam, int32_t *info, void *workspace,
@@ -322,6 +332,10 @@ const char *lqrx_last_error(void);
 int lqrx_get_last_error(char *buf, size_t len);
 /* 1 if the HIP runtime sees a gfx950 device, else 0 (no compute; safe without a GPU) */
 int lqrx_device_available(void);
+/* Return the library pool's unused stream-ordered scratch of `device` (-1: every device
+ * the library has used) to the driver, keeping at most keep_bytes reserved.  Blocks still in
+ * use by enqueued work are not affected.  Returns 0, or LQRX_ERR_HIP. */
+int lqrx_scratch_trim(int32_t device, size_t keep_bytes);
 
 /* Deterministic synthetic random-dense LQR batch: counter-based
  * splitmix64 + Box–Muller keyed by (seed, trajectory, field, element); host memory,

@@ -199,8 +199,8 @@ function kkt_solve!(dz::Matrix{T}, lam::Matrix{T}, info::Vector{Int32},
                     n1::Vector{Int32}, p::Vector{Int32}, n2::Vector{Int32}, w::Vector{Int32},
                     Y::Matrix{T}, y::Matrix{T}, H::Matrix{T}, g::Matrix{T};
                     h_mode::Integer=2, ginv::Integer=1) where {T<:Union{Float64,Float32}}
-    # Float32 runs the large-block MFMA kernels (blocks up to 64 rows, w up to 128; diagonal
-    # H or ginv = 0) — BASELINE configs[4]'s banded KKT
+    # Float32 runs the large-block MFMA kernels (blocks up to 64 rows, w up to 128; dense,
+    # block-diagonal or diagonal H, and ginv = 0) — BASELINE configs[4]'s banded KKT
     batch = size(Y, 2)
     GC.@preserve n1 p n2 w Y y H g dz lam info begin
         d = Ref(KktDesc(length(n1), dtypecode(T), batch, pointer(n1), pointer(p), pointer(n2), pointer(w),

@@ -98,10 +98,11 @@ hipError_t stream_device(hipStream_t s, int *dev)
 // Process-wide state (mutex-guarded, created on first use): one memory pool per device for
 // stream-ordered scratch; freed blocks stay mapped (release threshold ∞), so steady-state
 // calls allocate nothing from the driver.
+static std::mutex pool_mu;
+static std::map<int, hipMemPool_t> pools;
 hipError_t scratch_alloc(void **p, size_t bytes, hipStream_t s)
 {
-    static std::mutex mu;
-    static std::map<int, hipMemPool_t> pools;
+    auto &mu = pool_mu;
     int dev = 0;
     hipError_t e = stream_device(s, &dev);
     if (e != hipSuccess) return e;
@@ -125,6 +126,16 @@ hipError_t scratch_alloc(void **p, size_t bytes, hipStream_t s)
     return hipMallocFromPoolAsync(p, bytes, pool, s);
 }
 hipError_t scratch_free(void *p, hipStream_t s) { return hipFreeAsync(p, s); }
+hipError_t scratch_trim(int device, size_t keep)
+{
+    std::lock_guard<std::mutex> lock(pool_mu);
+    for (auto &kv : pools)
+        if (device < 0 || kv.first == device) {
+            hipError_t e = hipMemPoolTrimTo(kv.second, keep);
+            if (e != hipSuccess) return e;
+        }
+    return hipSuccess;
+}
 } // namespace lqrx
 
 namespace {
@@ -174,6 +185,11 @@ hipError_t dp_launch_soa_staged(const lqrx::DpArgs &a, hipStream_t s)
 extern "C" {
 
 int lqrx_abi_version(void) { return LQRX_ABI_VERSION; }
+int lqrx_scratch_trim(int32_t device, size_t keep_bytes)
+{
+    const hipError_t e = lqrx::scratch_trim(device, keep_bytes);
+    return e == hipSuccess ? 0 : hip_err(e, "hipMemPoolTrimTo");
+}
 
 const char *lqrx_last_error(void) { return g_err.c_str(); }
 
@@ -514,10 +530,12 @@ bool kkt_force_generic()
     static const bool v = [] { const char *e = std::getenv("LQRX_KKT_GENERIC"); return e && *e == '1'; }();
     return v;
 }
-size_t kkt_ws_bytes(const lqrx_kkt_desc *d, const lqrx::KktArgs &a)
+// workspace bytes of the kernel family `route` (kkt_route of the same call: sizing and launch
+// use one routing decision)
+size_t kkt_ws_bytes(const lqrx_kkt_desc *d, const lqrx::KktArgs &a, int route)
 {
     size_t b = 0;
-    switch (kkt_route(d, a)) {
+    switch (route) {
     case KK_FIL: (void)lqrx::kkt_fil_scratch_bytes(a, d->n1, d->p, d->n2, d->w, &b); return b;
     case KK_BIG: return lqrx::kkt_big_scratch_bytes(a, d->n1, d->p, d->n2, d->w);
     case KK_GENERIC: return lqrx::kkt_scratch_bytes(a);
@@ -535,7 +553,12 @@ extern "C" int lqrx_kkt_workspace_size(const lqrx_kkt_desc *d, size_t *bytes)
     int st = kkt_layout(d, L);
     if (st) return st;
     if (!bytes) return set_err(-2, "bytes is NULL");
-    *bytes = d->batch ? kkt_ws_bytes(d, kkt_args(d, L)) : 0;
+    if (d->batch) {
+        const lqrx::KktArgs a = kkt_args(d, L);
+        *bytes = kkt_ws_bytes(d, a, kkt_route(d, a));
+    } else {
+        *bytes = 0;
+    }
     return 0;
 }
 
@@ -583,8 +606,10 @@ int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const v
         a.sel = sel;
         a.nsel = nsel;
     }
+    // one routing decision per call (the large-block plan is an O(N) pass over the structure)
+    const int route = kkt_route(d, a);
     if (ws) {
-        const size_t need = kkt_ws_bytes(d, a);
+        const size_t need = kkt_ws_bytes(d, a, route);
         if (ws_bytes < need) {
             if (meta_tmp) (void)lqrx::scratch_free(meta_tmp, s);
             return set_err(-10, "workspace of %zu bytes < %zu (lqrx_kkt_workspace_size)", ws_bytes, need);
@@ -593,15 +618,14 @@ int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const v
         a.ws_bytes = ws_bytes;
     }
     static const int debug_meta = [] { const char *v = std::getenv("LQRX_DEBUG_META"); return v && *v == '1'; }();
-    const int route = kkt_route(d, a);
     if (route == KK_NONE) {
         if (meta_tmp) (void)lqrx::scratch_free(meta_tmp, s);
         if (d->layout == 1)
             return set_err(LQRX_ERR_UNSUPPORTED, "layout 1 needs a compile-time KKT shape (Dubins; cartpole, "
                                                  "DoubleIntegrator(2|3) with diagonal H) and N >= 4");
-        return set_err(LQRX_ERR_UNSUPPORTED, "no KKT kernel for this structure / options (%s; large blocks need "
-                                             "n1, p, n2 <= 64, padded rows <= 128, w <= 128, layout 0 and a "
-                                             "diagonal H or ginv = 0)",
+        return set_err(LQRX_ERR_UNSUPPORTED, "no KKT kernel for this structure / options (%s; the large-block "
+                                             "kernels need n1, p, n2 <= 64, padded rows <= 128, w <= 128 and "
+                                             "layout 0; every h_mode and ginv is served)",
                        d->dtype == LQRX_F32 ? "fp32" : "fp64");
     }
     if (route == KK_BIG) e = lqrx::kkt_big_launch(a, d->n1, d->p, d->n2, d->w, s);

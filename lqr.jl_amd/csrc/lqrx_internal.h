@@ -71,6 +71,7 @@ int kkt_generic_class(const KktArgs &a);
 // stream-ordered, never shared between calls.  (lqrx_api.cpp)
 hipError_t scratch_alloc(void **p, size_t bytes, hipStream_t s);
 hipError_t scratch_free(void *p, hipStream_t s);
+hipError_t scratch_trim(int device, size_t keep);   // lqrx_scratch_trim
 // a launch's slab: the caller's workspace when one was passed, else a pool block
 struct Scratch {
     void *p = nullptr;

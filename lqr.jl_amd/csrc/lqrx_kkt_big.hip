@@ -1384,10 +1384,13 @@ __device__ __forceinline__ void schur_tiles(const Kn &q, const T *Yt, const T *h
 #pragma unroll
     for (int v = 0; v < NBT; ++v) rp[v] = (T)0;
     const int nks = (q.w + 3) >> 2;
-    // raw buffer loads: the knot's Y block, H and g rows as descriptors whose size bounds the
-    // reads (out-of-range returns 0: columns past w); per lane one byte offset per row block
-    // (rows past the block's real rows get an out-of-range offset), the slice in soffset —
-    // no address arithmetic and no exec-mask branch per load
+    // raw buffer loads: the knot's Y block as a descriptor whose size bounds the reads
+    // (out-of-range returns 0: columns past w, slices past the last); per lane one byte offset
+    // per row block (rows past the block's real rows get an out-of-range offset that stays out
+    // of range when the slice offset is added).  The slice offset must ride in the VGPR
+    // offset: the range check does not cover soffset, so a slice in soffset would read the
+    // next knot's Y (or memory past the caller's allocation at the batch's last knot).  No
+    // exec-mask branch per load.
     constexpr uint32_t TS = sizeof(T), OOB = 0x80000000u;
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)(Yt + q.oY), (short)0, q.rows * q.w * (int)TS, 0x00020000);
     uint32_t vo[NBT];
@@ -1399,7 +1402,7 @@ __device__ __forceinline__ void schur_tiles(const Kn &q, const T *Yt, const T *h
         const uint32_t so = (uint32_t)s * so_col;
         sfor<NBT>([&](auto vc) {
             constexpr int v = decltype(vc)::value;
-            if constexpr (ks_need(NBT, SI, NW, v)) fr[v] = bload<T>(ry, vo[v], so);
+            if constexpr (ks_need(NBT, SI, NW, v)) fr[v] = bload<T>(ry, vo[v] + so, 0u);
         });
         // raw H and g: the reciprocal is taken in step(), so nothing here waits for a load
         h = hgl[4 * s + g4];                       // H⁻¹ (or 1; 0 past w) and g, staged per knot
@@ -2457,9 +2460,16 @@ template <typename T>
 hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
 {
     const size_t per = (size_t)kb_per_traj(a, P) * sizeof(T);
-    const int64_t chunk = kb_chunk(a, P, sizeof(T), a.ws ? a.ws_bytes : kb_slab_cap());
+    int64_t chunk = kb_chunk(a, P, sizeof(T), a.ws ? a.ws_bytes : kb_slab_cap());
     Scratch sc;
     hipError_t e = sc.get(a, (size_t)chunk * per, s);
+    // library scratch (no caller workspace): when the pool cannot hold the cap's chunk, run the
+    // batch in smaller chunks instead of failing — halve until it fits or one trajectory fails
+    while (e == hipErrorOutOfMemory && !a.ws && chunk > 1) {
+        (void)hipGetLastError();
+        chunk = kb_chunk(a, P, sizeof(T), (size_t)((chunk + 1) / 2) * per);
+        e = sc.get(a, (size_t)chunk * per, s);
+    }
     if (e != hipSuccess) return e;
     const size_t lf = (size_t)P.nf * sizeof(T), lb = (size_t)P.nb * sizeof(T);
     const size_t lh = (size_t)P.nh * sizeof(T);

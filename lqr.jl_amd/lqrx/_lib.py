@@ -80,6 +80,7 @@ _SIGS = {
     "lqrx_last_error": (C.c_char_p, []),
     "lqrx_get_last_error": (C.c_int, [C.c_char_p, C.c_size_t]),
     "lqrx_device_available": (C.c_int, []),
+    "lqrx_scratch_trim": (C.c_int, [C.c_int32, C.c_size_t]),
     "lqrx_dp_solve": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 10 + [_VP, _VP]),
     "lqrx_dp_solve_host": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 10 + [_VP]),
     "lqrx_dp_solve_linear": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 6 + [C.POINTER(DpLinear)]

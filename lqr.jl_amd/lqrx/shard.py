@@ -15,7 +15,7 @@ import time
 
 __all__ = ["shard_range", "gather_to_root", "dist_env", "init_ranks", "timed_steps",
            "max_over_ranks", "sum_over_ranks", "timed_gather", "finish_ranks", "spawn_ranks",
-           "rank_partition"]
+           "rank_partition", "profiler_preload"]
 
 
 def _free_port() -> int:
@@ -34,6 +34,23 @@ def _rank_child(rank, world, port, fn, args):
     raise SystemExit(int(rc or 0))
 
 
+_TOOL_ENV = ("ROCP_TOOL_LIBRARIES", "HSA_TOOLS_LIB", "ROCPROFILER_LIBRARY", "ROCP_TOOL_LIB")
+
+
+def profiler_preload() -> str | None:
+    """The profiler / HSA-tool preload active in this process's environment, if any
+    (rocprofv3 sets LD_PRELOAD to its tool library and ROCP_TOOL_LIBRARIES; an HSA tool sets
+    HSA_TOOLS_LIB).  Such a tool initialises the GPU before the program's own code runs."""
+    pre = os.environ.get("LD_PRELOAD", "")
+    for lib in pre.replace(":", " ").split():
+        if "rocprof" in os.path.basename(lib):
+            return f"LD_PRELOAD={lib}"
+    for k in _TOOL_ENV:
+        if os.environ.get(k):
+            return f"{k}={os.environ[k]}"
+    return None
+
+
 def spawn_ranks(nprocs: int, fn, *args, port: int | None = None, timeout: float | None = None) -> int:
     """One process per GPU without an external launcher: start `nprocs` fresh interpreters
     (multiprocessing "spawn": fork + exec of python by THIS process, which must not have
@@ -45,6 +62,12 @@ def spawn_ranks(nprocs: int, fn, *args, port: int | None = None, timeout: float 
     import multiprocessing as mp
     import time as _t
 
+    tool = profiler_preload()
+    if tool:
+        # under rocprofv3 (or any HSA tool preload) this process has been GPU-initialised by
+        # the tool before main() ran; starting ranks from it is the exec this pool forbids
+        raise RuntimeError(f"spawn_ranks: a profiler/tool preload is active ({tool}); profile one "
+                           "rank (--gpus 1) or launch the ranks with torch.distributed.run")
     ctx = mp.get_context("spawn")
     port = port or _free_port()
     procs = [ctx.Process(target=_rank_child, args=(r, nprocs, port, fn, args)) for r in range(nprocs)]

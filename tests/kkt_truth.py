@@ -33,10 +33,12 @@ def _truth_one(os_, pb, t, ginv):
     return x[:NN], x[NN:]
 
 
-def check(st, pb, ginv, got, ref, tol, scale="batch"):
-    """Assert δz and λ match the oracle within tol, or — per offending trajectory — are within
-    C·max(err_oracle, tol) of the refined truth.  scale "batch": errors over the batch-wide max
-    |ref| (test_kkt_gpu's rel); "traj": per trajectory."""
+def check(st, pb, ginv, got, ref, tol, scale="batch", fallback=False):
+    """Assert δz and λ match the oracle within tol.  Only with fallback=True (the documented
+    ill-conditioned case, DoubleIntegrator(3) at N = 4) may an offending trajectory instead be
+    within C·max(err_oracle, tol) of the refined truth; otherwise every trajectory must meet
+    tol flat, so a regression elsewhere cannot pass at a multiple of it.  scale "batch": errors
+    over the batch-wide max |ref| (test_kkt_gpu's rel); "traj": per trajectory."""
     os_ = orc.KktStructure(st.n, st.m, st.N, st.p)
     for key, part in (("dz", 0), ("lam", 1)):
         a = np.asarray(got[key], np.float64).reshape(pb.batch, -1)
@@ -44,6 +46,9 @@ def check(st, pb, ginv, got, ref, tol, scale="batch"):
         den = (np.full(pb.batch, np.abs(b).max()) if scale == "batch" else np.abs(b).max(axis=1))
         den = np.maximum(den, 1e-300)
         e = np.abs(a - b).max(axis=1) / den
+        if not fallback:
+            assert (e <= tol).all(), (key, np.nonzero(e > tol)[0][:8].tolist(), float(e.max()))
+            continue
         for t in np.nonzero(e > tol)[0]:
             tr = _truth_one(os_, pb, int(t), ginv)[part]
             ek = np.abs(a[t] - tr).max() / den[t]

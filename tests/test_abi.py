@@ -18,7 +18,38 @@ def test_exports_every_header_symbol(lqrx):
 
 
 def test_abi_version(lqrx):
-    assert lqrx.load().lqrx_abi_version() == 3
+    assert lqrx.load().lqrx_abi_version() == 4
+
+
+def test_scratch_trim_without_pools(lqrx):
+    """lqrx_scratch_trim before any pool exists (no GPU call made) is a no-op success."""
+    assert lqrx.load().lqrx_scratch_trim(-1, 0) == 0
+
+
+def test_header_kkt_dtype_comment_matches_validation(lqrx):
+    """The header's lqrx_kkt_desc.dtype comment names exactly the dtypes the validation accepts
+    (it said "LQRX_F64 only" after fp32 KKT shipped)."""
+    import os
+    import re
+
+    import lqrx.kkt as K
+    from lqrx import _lib
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hdr = open(os.path.join(root, "include", "lqrx.h")).read()
+    body = hdr[hdr.index("typedef struct lqrx_kkt_desc"):hdr.index("} lqrx_kkt_desc;")]
+    m = re.search(r"int32_t dtype;\s*/\*(.*?)\*/", body, re.S)
+    named = set(re.findall(r"LQRX_F(?:32|64)", m.group(1)))
+    lib = lqrx.load()
+    st = K.trajectory_structure(64, 32, 9)
+    accepted = set()
+    for name, code in (("LQRX_F64", _lib.F64), ("LQRX_F32", _lib.F32)):
+        n = C.c_size_t(0)
+        if lib.lqrx_kkt_workspace_size(C.byref(st.desc(8, K.H_DIAG, 1, 0, code)), C.byref(n)) == 0 and n.value > 0:
+            accepted.add(name)
+    assert named == accepted == {"LQRX_F64", "LQRX_F32"}, (named, accepted)
+    n = C.c_size_t(0)
+    assert lib.lqrx_kkt_workspace_size(C.byref(st.desc(8, K.H_DIAG, 1, 0, 7)), C.byref(n)) == -1
 
 
 @pytest.mark.parametrize("field,val,code", [("n", 0, -1), ("m", 0, -1), ("N", 1, -1),

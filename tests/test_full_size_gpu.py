@@ -98,3 +98,55 @@ def test_cfg5_full_batch_parity_f32(lqrx, oracle, gpu_ok):
     """BASELINE configs[4]: n=64 m=32 N=512 B=8192 fp32 against the fp64 oracle."""
     errs = full_size_case(lqrx, oracle, 64, 32, 512, 8192, False, 48, seed=20260105)
     assert max(errs.values()) <= TOL32_N512
+
+
+def kkt_full_size_case(lqrx, oracle, f64, B, nsample, seed):
+    """configs[4]'s KKT half at its full batch: the trajectory structure n=64 m=32 N=512
+    generated in HBM (206 GB of Y at B=8192 fp32 / B=4096 fp64 — past host memory), solved
+    in ONE lqrx_kkt_solve call on the library's own scratch (no caller workspace: the default
+    slab cap splits the batch into chunks), then a whole-batch device scan for non-finite δz, λ
+    and info ≠ 0, and a strided sample (first and last trajectory included: the last
+    trajectory's Y offset is B·1.26e7 elements, past 2³²) copied back as the kernel saw it and
+    solved by the fp64 C oracle (cholesky_solver.jl _solve!)."""
+    import torch
+    import lqrx.kkt as K
+
+    dev = torch.device("cuda", 0)
+    n, m, N = 64, 32, 512
+    st = K.trajectory_structure(n, m, N)
+    tdt = torch.float64 if f64 else torch.float32
+    t = K.random_kkt_device(st, B, seed, dev, tdt)
+    assert t["Y"].numel() > 2 ** 32
+    out = K.kkt_solve_device(st, t, K.H_DIAG, 1)
+    torch.cuda.synchronize(dev)
+    assert out["rc"] == 0 and int((out["info"] != 0).sum()) == 0
+    assert bool(torch.isfinite(out["dz"]).all()) and bool(torch.isfinite(out["lam"]).all())
+    idx = sample_index(B, nsample)
+    ti = torch.from_numpy(idx).to(dev)
+    pick = lambda x: x.view(B, -1).index_select(0, ti).double().cpu().numpy()
+    Y, y, H, g = (pick(t[k]) for k in ("Y", "y", "H", "g"))
+    dz, lam = pick(out["dz"]), pick(out["lam"])
+    del out, t
+    torch.cuda.empty_cache()
+    ref = oracle.kkt_solve_batch(oracle.KktStructure(n, m, N, st.p), len(idx), Y, y, H, g, h_mode=2,
+                                 nthreads=max(1, min(16, os.cpu_count() or 1)))
+    assert (ref["info"] == 0).all()
+    rel = lambda a, b: float((np.abs(a - b.reshape(a.shape)).max(axis=1)
+                              / np.abs(b.reshape(a.shape)).max(axis=1)).max())
+    e = dict(dz=rel(dz, ref["dz"]), lam=rel(lam, ref["lam"]))
+    print(f"\nfull-size KKT n={n} m={m} N={N} B={B} {'f64' if f64 else 'f32'}: sample {len(idx)} "
+          f"(last {idx[-1]}) rel err dz {e['dz']:.2e} lam {e['lam']:.2e}")
+    return e
+
+
+def test_cfg5_kkt_full_batch_parity_f32(lqrx, oracle, gpu_ok):
+    """BASELINE configs[4]'s banded KKT: n=64 m=32 N=512 B=8192 fp32, 8 sampled trajectories
+    against the fp64 oracle on the same fp32 inputs (1e-4, tests/test_kkt_big_gpu.py)."""
+    e = kkt_full_size_case(lqrx, oracle, False, 8192, 8, seed=4242)
+    assert max(e.values()) <= TOL32_N512
+
+
+def test_cfg5_kkt_full_batch_parity_f64(lqrx, oracle, gpu_ok):
+    """The same KKT shape in fp64 at B=4096 (the same 206 GB of Y), 1e-10."""
+    e = kkt_full_size_case(lqrx, oracle, True, 4096, 8, seed=4243)
+    assert max(e.values()) <= TOL64

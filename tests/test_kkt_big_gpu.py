@@ -311,3 +311,38 @@ def test_big_kkt_fused_and_split_forward(lqrx, gpu_ok, tmp_path, split):
     env = dict(os.environ, LQRX_KKT_SPLIT=split)
     p = subprocess.run([sys.executable, str(f), root], env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
+
+
+@pytest.mark.parametrize("n,m,dt", [(5, 2, "f32"), (6, 3, "f32"), (6, 3, "f64")])
+def test_big_kkt_y_tail_nan(lqrx, gpu_ok, n, m, dt):
+    """Knot widths off the 4-column k-slice (w = n + m interior, w = n at the last knot) on the
+    split Schur kernel, with Y a view followed by NaN-filled memory: the k-slices past a knot's
+    last column must read 0 through the buffer descriptor's bound (the slice offset rides in
+    the range-checked VGPR offset), not the memory after the block — at the batch's last knot
+    that is past the caller's Y (a soffset slice read it, and 0·NaN poisoned the
+    Schur tiles)."""
+    import torch
+    import lqrx.kkt as K
+
+    st = K.trajectory_structure(n, m, 11)
+    bt = 5
+    pb = K.random_kkt(st, bt, seed=n + m, h_mode=K.H_DIAG)
+    f32 = dt == "f32"
+    if f32:
+        pb = _round32(pb)
+    tdt = torch.float32 if f32 else torch.float64
+    dev = torch.device("cuda", 0)
+    sY = pb.Y.size
+    ybuf = torch.full((sY + 4096,), float("nan"), dtype=tdt, device=dev)
+    ybuf[:sY] = torch.from_numpy(pb.Y.ravel()).to(dev, tdt)
+    t = {k: torch.from_numpy(np.ascontiguousarray(getattr(pb, k).ravel())).to(dev, tdt) for k in ("y", "H", "g")}
+    t.update(Y=ybuf[:sY], batch=bt)
+    got = K.kkt_solve_device(st, t, K.H_DIAG)
+    torch.cuda.synchronize()
+    ref = _ref(st, pb)
+    dz = got["dz"].view(bt, -1).double().cpu().numpy()
+    lam = got["lam"].view(bt, -1).double().cpu().numpy()
+    assert np.isfinite(dz).all() and np.isfinite(lam).all()
+    tol = F32_TOL if f32 else TOL
+    assert traj_rel(dz, ref["dz"]) <= tol
+    assert traj_rel(lam, ref["lam"]) <= tol

@@ -129,7 +129,7 @@ def test_kkt_fil_shapes(lqrx, gpu_ok, model, N, batch, h_mode, ginv):
     got = K.kkt_solve(pb, ginv=ginv)
     ref = _ref(st, pb, ginv)
     assert got["rc"] == 0 and (got["info"] == 0).all()
-    check(st, pb, ginv, got, ref, TOL)
+    check(st, pb, ginv, got, ref, TOL, fallback=(model == "di" and N == 4))
 
 
 def test_kkt_workspace_entry(lqrx, gpu_ok):

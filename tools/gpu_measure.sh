@@ -23,6 +23,16 @@ shift
 OUT=gpurun_out/${TAG:-run}
 KREGEX=${KREGEX:-lqrx}
 trim() { find "$OUT" -type f \( -name "*.csv" -o -name "*.json" -o -name "*.db" \) ! -name "*stats.csv" ! -name "*counter_collection.csv" ! -name "bench.json" -delete 2>/dev/null; true; }
+one_rank() {   # rocprofv3 modes profile ONE rank: a --gpus N > 1 bench would start its ranks
+               # from a process the profiler's preload has already GPU-initialised
+    local prev=""
+    for a in "$@"; do
+        if [ "$prev" = "--gpus" ] && [ "$a" != "1" ]; then echo "gpu_measure.sh: $MODE profiles one rank; drop --gpus $a" >&2; exit 1; fi
+        case "$a" in --gpus=*) [ "${a#--gpus=}" != "1" ] && { echo "gpu_measure.sh: $MODE profiles one rank" >&2; exit 1; } ;; esac
+        prev=$a
+    done
+}
+case "$MODE" in prof|pmc) one_rank "$@" ;; esac
 mkdir -p "$OUT"
 nproc > "$OUT/host.txt"
 lscpu | head -20 >> "$OUT/host.txt"

@@ -8,6 +8,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-kb_ab}
 mkdir -p "$OUT"
 ARGS=${KB_ARGS:---workload kkt --kkt-structure dense --n 64 --m 32 --N 512 --batch 8192 --dtype f32}
+case " $ARGS " in *" --gpus "[2-9]*|*" --gpus="[2-9]*) echo "kb_ab.sh: one rank only (rocprofv3 below)" >&2; exit 1 ;; esac
 for v in "" "$@"; do
     name=${v:-base}
     lib=""
