@@ -22,8 +22,10 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ARGS = ["--gpus", "2", "--dist-backend", "gloo", "--n", "32", "--m", "16", "--N", "256",
-        "--batch", "2049", "--steps", "2", "--warmup", "1", "--cpu-seconds", "1"]
+# cfg4's shape (n=32 m=16 N=256 are bench.py's defaults — and must stay implicit: torchrun's
+# own parser would take "--n" for an abbreviation of its --nnodes / --nproc-per-node)
+ARGS = ["--gpus", "2", "--dist-backend", "gloo", "--batch", "2049", "--steps", "2", "--warmup", "1",
+        "--cpu-seconds", "1"]
 
 
 def _free_port():
