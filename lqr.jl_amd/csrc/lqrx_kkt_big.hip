@@ -1384,25 +1384,28 @@ __device__ __forceinline__ void schur_tiles(const Kn &q, const T *Yt, const T *h
 #pragma unroll
     for (int v = 0; v < NBT; ++v) rp[v] = (T)0;
     const int nks = (q.w + 3) >> 2;
-    // raw buffer loads: the knot's Y block as a descriptor whose size bounds the reads
-    // (out-of-range returns 0: columns past w, slices past the last); per lane one byte offset
-    // per row block (rows past the block's real rows get an out-of-range offset that stays out
-    // of range when the slice offset is added).  The slice offset must ride in the VGPR
-    // offset: the range check does not cover soffset, so a slice in soffset would read the
-    // next knot's Y (or memory past the caller's allocation at the batch's last knot).  No
-    // exec-mask branch per load.
+    // raw buffer loads of the knot's Y block: per k-slice a descriptor starting at the slice
+    // whose size is what is left of the block, so the hardware range check (which covers
+    // the VGPR offset, not soffset) returns 0 for columns past w and for the slices past the
+    // last one that the ring prefetches — nothing past the block is read, not even at the
+    // batch's last knot (the end of the caller's Y).  The descriptor is rebuilt per slice on
+    // the SALU; per lane one byte offset per row block, fixed for the knot (rows past a
+    // block's real rows get an out-of-range offset).  No exec-mask branch per load.
     constexpr uint32_t TS = sizeof(T), OOB = 0x80000000u;
-    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)(Yt + q.oY), (short)0, q.rows * q.w * (int)TS, 0x00020000);
+    const char *ybase = (const char *)(Yt + q.oY);
+    const int ybytes = q.rows * q.w * (int)TS;
     uint32_t vo[NBT];
 #pragma unroll
     for (int v = 0; v < NBT; ++v) vo[v] = i16 < lim[v] ? (uint32_t)((g4 * q.rows + rb[v] + i16) * (int)TS) : OOB;
-    const uint32_t so_col = (uint32_t)(4 * q.rows * (int)TS);
+    const int so_col = 4 * q.rows * (int)TS;
     T f[KS_PF][NBT], hh[KS_PF], gg[KS_PF];
     auto load = [&](int s, T (&fr)[NBT], T &h, T &g_) __attribute__((always_inline)) {
-        const uint32_t so = (uint32_t)s * so_col;
+        const int so = s * so_col;
+        const __amdgpu_buffer_rsrc_t ry =
+            __builtin_amdgcn_make_buffer_rsrc((void *)(ybase + so), (short)0, max(ybytes - so, 0), 0x00020000);
         sfor<NBT>([&](auto vc) {
             constexpr int v = decltype(vc)::value;
-            if constexpr (ks_need(NBT, SI, NW, v)) fr[v] = bload<T>(ry, vo[v] + so, 0u);
+            if constexpr (ks_need(NBT, SI, NW, v)) fr[v] = bload<T>(ry, vo[v], 0u);
         });
         // raw H and g: the reciprocal is taken in step(), so nothing here waits for a load
         h = hgl[4 * s + g4];                       // H⁻¹ (or 1; 0 past w) and g, staged per knot
