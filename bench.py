@@ -191,7 +191,7 @@ def cpu_baseline_kkt(N, target_s=12.0, threads=None, structure="dubins"):
                        f"of _solve!), OpenMP {threads} threads, {dt:.1f} s")
 
 
-TRAFFIC_FILES = ("traffic_r03.json", "traffic_r02.json")
+TRAFFIC_FILES = ("traffic_r04.json", "traffic_r03.json", "traffic_r02.json")
 
 
 def traffic_lookup(key, path=None):

@@ -56,8 +56,33 @@
 #ifndef LQRX_DP_TVWAIT
 #define LQRX_DP_TVWAIT 0
 #endif
+#ifndef LQRX_DP_ROLL_FULL
+#define LQRX_DP_ROLL_FULL 1   // exact tile grids: the register-streamed rollout (A/B builds: 0)
+#endif
 
 namespace lqrx {
+
+// wave-level ordering of LDS traffic between the lanes of a one-wave workgroup (the LDS is in
+// order per wave; this is the compiler fence + wave barrier, no s_barrier)
+__device__ __forceinline__ void wsync_w()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// v of lane (lane ^ o): one ds_bpermute per dword with the lane address precomputed (the
+// generic __shfl_xor adds a width test and a select per call)
+__device__ __forceinline__ double xor_shfl(double v, int addr)
+{
+    const long long x = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)(x & 0xffffffffll));
+    const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)(x >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ float xor_shfl(float v, int addr)
+{
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
+}
 
 // Forward LDLᵀ sweep on the augmented matrix [E | G | I] — the factor/solve of
 // chol_solve! (dynamic_programming.jl:28-31: potrf 'U' + potrs 'U'), reorganised so that
@@ -301,7 +326,7 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
                 }
                 T su = s0 + s1;
 #pragma unroll
-                for (int o = MP; o < 64; o <<= 1) su += __shfl_xor(su, o);
+                for (int o = MP; o < 64; o <<= 1) su += xor_shfl(su, (lane ^ o) << 2);
                 if (lane < m) {
                     const T u = LIN ? -(su + dcur) : -su;   // u = −K x (− d)
                     us[lane] = u;
@@ -339,6 +364,162 @@ __device__ __forceinline__ void dp_rollout(const DpArgs &a, int64_t b, T *lds, i
                     }
                 }
                 __syncthreads();
+            }
+        }
+    }
+}
+
+// one global load the compiler's wait-count pass does not track (the caller waits by hand)
+template <typename T, int OFF> __device__ __forceinline__ T gload_asm(const T *p);
+template <> __device__ __forceinline__ double gload_asm<double, 0>(const double *p)
+{
+    double v;
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p));
+    return v;
+}
+template <typename T, int OFF> __device__ __forceinline__ T gload_asm(const T *p)
+{
+    T v;
+    if constexpr (sizeof(T) == 8)
+        asm volatile("global_load_dwordx2 %0, %1, off offset:%2" : "=v"(v) : "v"(p), "n"(OFF));
+    else
+        asm volatile("global_load_dword %0, %1, off offset:%2" : "=v"(v) : "v"(p), "n"(OFF));
+    return v;
+}
+template <> __device__ __forceinline__ float gload_asm<float, 0>(const float *p)
+{
+    float v;
+    asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p));
+    return v;
+}
+// dst[c] = p[c·STR bytes] for c < C (compile-time immediate offsets)
+template <typename T, int C, int STR>
+__device__ __forceinline__ void gload_run(T *dst, const T *p)
+{
+    if constexpr (C > 0) {
+        gload_run<T, C - 1, STR>(dst, p);
+        dst[C - 1] = gload_asm<T, (C - 1) * STR>(p);
+    }
+}
+// s_waitcnt vmcnt(N) that the values r (and d) depend on: their consumers stay after it
+template <int N, typename T, int C>
+__device__ __forceinline__ void vm_wait_regs(T (&r)[C], T &d)
+{
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(d) : "n"(N) : "memory");
+#pragma unroll
+    for (int c = 0; c < C; ++c) asm volatile("" : "+v"(r[c]));
+}
+
+// The same rollout for exact tile grids (n = 16·NT ∈ {16, 32, 64}, m = 16·MT; time-invariant A,
+// B), restructured so that nothing but its arithmetic is left per knot: K_k goes from HBM
+// straight into registers DEPTH knots ahead (no LDS staging, no exec-mask branches), in a lane
+// map where lane l owns row iu = l mod MP of K_k and a contiguous run of CU columns, so
+// u_i = −Σ K[i][j] x_j is one FMA chain per lane plus xor-shuffles over the SU = 64/MP lanes of
+// the row; x_{k+1} = A x + B u with A, B rows in registers (lane l: row l mod NP, a
+// contiguous column run); x and u pass between lanes through LDS, read as contiguous runs;
+// the wave is its own workgroup, so wave-level ordering (wsync) replaces barriers.
+template <typename T, int NT, int MT, int DEPTH, bool LIN>
+__device__ __forceinline__ void dp_rollout_full(const DpArgs &a, int64_t b, T *lds, int lane)
+{
+    constexpr int NP = 16 * NT, MP = 16 * MT;
+    constexpr int SU = 64 / MP, CU = NP / SU;          // lanes per K row, K columns per lane
+    constexpr int SX = 64 / NP, CX = NP / SX, CB = MP / SX;   // lanes per x row; A, B columns per lane
+    static_assert(64 % NP == 0 && 64 % MP == 0, "exact tile grids with 64 % n == 0");
+    const int N = a.N;
+    constexpr size_t mn = (size_t)MP * NP;
+    const T *__restrict__ Kg = (const T *)a.K + (size_t)b * (size_t)(N - 1) * mn;
+    const T *__restrict__ Ag = (const T *)a.A + (size_t)b * NP * NP;
+    const T *__restrict__ Bg = (const T *)a.B + (size_t)b * NP * MP;
+    T *__restrict__ Xg = (T *)a.X + (size_t)b * (size_t)N * NP;
+    T *__restrict__ Ug = (T *)a.U + (size_t)b * (size_t)(N - 1) * MP;
+    const T *Dg = LIN ? (const T *)a.d + (size_t)b * (size_t)(N - 1) * MP : nullptr;
+    T *xs = lds, *us = lds + NP;
+    const int iu = lane % MP, hu = lane / MP, ix = lane % NP, hx = lane / NP;
+    T arow[CX], brow[CB];
+#pragma unroll
+    for (int c = 0; c < CX; ++c) arow[c] = Ag[ix + (size_t)(hx * CX + c) * NP];
+#pragma unroll
+    for (int c = 0; c < CB; ++c) brow[c] = Bg[ix + (size_t)(hx * CB + c) * NP];
+    const T *x0 = (const T *)a.x0 + (size_t)b * NP;
+    if (lane < NP) {
+        const T v = x0[lane];
+        xs[lane] = v;
+        Xg[lane] = v;
+    }
+    // K_kk (knot kk = 1 … N−1; past the end: the last knot again, never used).  The loads are
+    // inline asm, invisible to the compiler's wait-count pass, which would otherwise wait at
+    // the loop header for the loads issued one knot earlier instead of DEPTH knots earlier;
+    // the wait is placed by hand: per knot the wave issues KOPS memory ops (CU loads of K
+    // (+1 of d), then the U and X stores), so knot k's slot is complete once at most
+    // KOPS·(DEPTH−1) are outstanding (fewer in the first DEPTH knots: the bound below is the
+    // smallest such count, i.e. a slight over-wait in the steady state)
+    // (A K slot too large for the 6-bit vmcnt — n = 64, m = 32 — takes compiler-tracked loads.)
+    constexpr int VMW = (CU + (LIN ? 1 : 0)) * (DEPTH - 1);
+    constexpr bool HAND = VMW <= 63 && CU * MP * (int)sizeof(T) <= 4096;
+    T ring[DEPTH][CU], dring[DEPTH];
+    auto issue = [&](int kk, T (&dst)[CU], T &dd) __attribute__((always_inline)) {
+        const T *Kk = Kg + (size_t)(min(kk, N - 1) - 1) * mn + iu + (size_t)hu * CU * MP;
+        const T *Dk = LIN ? Dg + (size_t)(min(kk, N - 1) - 1) * MP + iu : nullptr;
+        if constexpr (HAND) {
+            gload_run<T, CU, MP * (int)sizeof(T)>(dst, Kk);
+            if constexpr (LIN) dd = gload_asm<T, 0>(Dk);
+        } else {
+#pragma unroll
+            for (int c = 0; c < CU; ++c) dst[c] = Kk[(size_t)c * MP];
+            if constexpr (LIN) dd = *Dk;
+        }
+    };
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+        dring[d] = (T)0;
+        issue(1 + d, ring[d], dring[d]);
+    }
+    wsync_w();
+    for (int k0 = 1; k0 <= N - 1; k0 += DEPTH) {
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            const int k = k0 + d;
+            if (k <= N - 1) {
+                if constexpr (HAND) vm_wait_regs<VMW>(ring[d], dring[d]);
+                // u = −K_k x_k (− d_k)   (dynamic_programming.jl:68)
+                T xu[CU];
+#pragma unroll
+                for (int c = 0; c < CU; ++c) xu[c] = xs[hu * CU + c];
+                T s0 = (T)0, s1 = (T)0;
+#pragma unroll
+                for (int c = 0; c < CU; c += 2) {
+                    s0 = fma(ring[d][c], xu[c], s0);
+                    if (c + 1 < CU) s1 = fma(ring[d][c + 1], xu[c + 1], s1);
+                }
+                T su = s0 + s1;
+#pragma unroll
+                for (int o = MP; o < 64; o <<= 1) su += __shfl_xor(su, o);
+                const T u = LIN ? -(su + dring[d]) : -su;
+                T dn = (T)0;
+                issue(k + DEPTH, ring[d], LIN ? dring[d] : dn);
+                if (hu == 0) {
+                    us[iu] = u;
+                    Ug[(size_t)(k - 1) * MP + iu] = u;
+                }
+                wsync_w();
+                // x_{k+1} = A x_k + B u_k   (:69)
+                T t0 = (T)0, t1 = (T)0;
+#pragma unroll
+                for (int c = 0; c < CX; c += 2) {
+                    t0 = fma(arow[c], xs[hx * CX + c], t0);
+                    if (c + 1 < CX) t1 = fma(arow[c + 1], xs[hx * CX + c + 1], t1);
+                }
+#pragma unroll
+                for (int c = 0; c < CB; ++c) t1 = fma(brow[c], us[hx * CB + c], t1);
+                T xn = t0 + t1;
+#pragma unroll
+                for (int o = NP; o < 64; o <<= 1) xn += xor_shfl(xn, (lane ^ o) << 2);
+                wsync_w();
+                if (hx == 0) {
+                    xs[ix] = xn;
+                    Xg[(size_t)k * NP + ix] = xn;
+                }
+                wsync_w();
             }
         }
     }
@@ -667,7 +848,12 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        dp_rollout<T, NT, MT, TV ? LQRX_DP_TVKD : LQRX_DP_KD, TV, LIN>(a, b, lds, lane);
+#if LQRX_DP_ROLL_FULL
+        if constexpr (FULL && !TV && (64 % (16 * NT)) == 0 && (64 % (16 * MT)) == 0)
+            dp_rollout_full<T, NT, MT, LQRX_DP_KD, LIN>(a, b, lds, lane);
+        else
+#endif
+            dp_rollout<T, NT, MT, TV ? LQRX_DP_TVKD : LQRX_DP_KD, TV, LIN>(a, b, lds, lane);
     }
 }
 

@@ -1284,6 +1284,14 @@ __host__ __device__ __forceinline__ int64_t img_len(const int32_t *meta, int k)
     const int32_t *m = meta + 8 * k;
     return (img_off(r16(m[0]), r16(m[1]), r16(m[2])).end + 63) & ~(int64_t)63;
 }
+// image offset of knot k: the knots of a fused interior run [fz0, fz1) have no image
+__host__ __device__ __forceinline__ int64_t img_before(const int32_t *meta, int k, int fz0 = 0, int fz1 = 0)
+{
+    int64_t o = 0;
+    for (int j = 0; j < k; ++j)
+        if (j < fz0 || j >= fz1) o += img_len(meta, j);
+    return o;
+}
 // index of the upper tile (i ≤ j) of an n×n tile grid, row-major over the upper triangle
 __host__ __device__ constexpr int upn(int i, int j, int n) { return i * n - i * (i - 1) / 2 + (j - i); }
 __host__ __device__ constexpr int up4(int i, int j) { return upn(i, j, 4); }
@@ -1333,6 +1341,9 @@ struct KsArgs {
     T *img;
     const int32_t *meta;
     int N, nruns, hinv, useg, yrel;
+    // knot segments: runs [0, nr0) cover knots [0, kend0), the others [kbeg1, N) — with the
+    // fused interior kernel the Schur images of the interior run [kend0, kbeg1) are never made
+    int nr0, kend0, kbeg1;
     int64_t b0, sY, sy, sH, sg, IMGT;   // IMGT: image elements per trajectory
 };
 
@@ -1497,9 +1508,10 @@ kb_schur_kernel(KsArgs<T> a)
     const int64_t t = a.b0 + tl, ty = a.yrel ? tl : t;
     const T *Yt = a.Y + ty * a.sY, *yt = a.y + t * a.sy, *Ht = a.H + t * a.sH, *gt = a.g + ty * a.sg;
     T *img = a.img + tl * a.IMGT;
-    const int k0 = run * KS_L, k1 = min(k0 + KS_L, a.N);
+    const int k0 = run < a.nr0 ? run * KS_L : a.kbeg1 + (run - a.nr0) * KS_L;
+    const int k1 = min(k0 + KS_L, run < a.nr0 ? a.kend0 : a.N);
     int64_t oI = 0, oIp = 0;                       // image offsets of knot k and knot k−1
-    for (int j = 0; j < k0; ++j) oI += img_len(a.meta, j);
+    oI = img_before(a.meta, k0, a.kend0, a.kbeg1);
     acc_t<T> acc[ST];
     Kn qp = kn_load(a.meta, k0);                   // knot k−1
     // v of knot kk (= qp): [c | d + r1 of knot kk+1 (if nx)]
@@ -1593,6 +1605,7 @@ struct KfArgs {
     const int32_t *meta;
     int N, hfac;
     int kb, ke;                    // knot range of this launch (the state at kb − 1 is in the slab)
+    int fz0, fz1;                  // knots without an image (the fused interior run), or 0, 0
     int64_t b0, nb, IMGT, sS;
 };
 
@@ -1624,12 +1637,6 @@ __device__ __forceinline__ int64_t slab_before(const int32_t *meta, int k)
 {
     int64_t o = 0;
     for (int j = 0; j < k; ++j) o += slab_size(r16(meta[8 * j + 1]), r16(meta[8 * j + 2]));
-    return o;
-}
-__device__ __forceinline__ int64_t img_before(const int32_t *meta, int k)
-{
-    int64_t o = 0;
-    for (int j = 0; j < k; ++j) o += img_len(meta, j);
     return o;
 }
 // info of a launch over knots [kb, ke): the first launch sets it (a non-SPD H_k of the hfac
@@ -1751,7 +1758,7 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_k
     const int64_t t = a.b0 + tl;
     const T *imt = a.img + tl * a.IMGT;
     T *St = a.slab + tl * a.sS;
-    int64_t oI = img_before(a.meta, a.kb), oS = slab_before(a.meta, a.kb);
+    int64_t oI = img_before(a.meta, a.kb, a.fz0, a.fz1), oS = slab_before(a.meta, a.kb);
     acc_t<T> X[10], G[16];
     T lam[4][4];                                     // λ_{k−1}, row layout
 #pragma unroll
@@ -1943,7 +1950,7 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_m
     const T *imt = a.img + tl * a.IMGT;
     T *St = a.slab + tl * a.sS;
     constexpr int NG = NT * NT, NX = NT * (NT + 1) / 2, PP = 16 * NT;   // X, Cn: up4-packed
-    int64_t oI = img_before(a.meta, a.kb), oS = slab_before(a.meta, a.kb);
+    int64_t oI = img_before(a.meta, a.kb, a.fz0, a.fz1), oS = slab_before(a.meta, a.kb);
     acc_t<T> X[10], G[16], Cn[10];
     T lam[4][4], dd[4];
 #pragma unroll
@@ -2045,6 +2052,308 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_m
             for (int j = 0; j < NT; ++j) Sk[PP * (PP + 1) / 2 + 16 * j + lane] = lc[j];
         }
         if (bad && !info) info = k + 1;
+    }
+    if (lane == 0) kf_info(a.info, t, info, a.kb, a.hfac);
+}
+
+// ---------------------------------------------------------------- fused interior-knot kernel
+// The interior run [kb, ke) of a trajectory structure (p = 0, n1 = n2 padded to 16·NT) with
+// BOTH halves of the forward sweep in ONE WAVE PER TRAJECTORY — no Schur image is written or
+// read for these knots (the split path's per-knot images and copy_shur!'s read-modify-write
+// alias were 2/3 of its HBM traffic).  Step k:
+//   * cholesky! + forward_substitution! of knot k (cholesky_solve.jl:47-67, 93-117) on the
+//     pivot tiles X = C_k + A_{k+1} − F̃_kᵀF̃_k: X → W_k = C̃_k⁻¹ (kept in LDS), λ_k, the slab;
+//   * shur! (jacobian_blocks.jl:231-242) of knot k+1 — F = D2 H⁻¹ D1ᵀ into G, C = D1 H⁻¹ D1ᵀ
+//     into Cn, r2 — and of knot k+2's D2 rows only: A = D2 H⁻¹ D2ᵀ accumulated straight into
+//     Cn (copy_shur!'s A ≡ previous-C alias, :249-286, in registers) and r1;
+//   * F̃_{k+1} = W_kᵀF_{k+1}, x_{k+1} = d_{k+1} − F̃ᵀλ_k, X ← Cn − F̃ᵀF̃ (:57, :61).
+// Nothing but G and Cn (26 tiles at NT = 4) is live across the streaming, so fp32 runs at 2
+// waves/SIMD; the D2 rows of each knot are streamed twice, one step apart (the second read is
+// the cache's).
+template <typename T>
+struct KuArgs {
+    const T *Y, *y, *H, *g;
+    T *slab;
+    int32_t *info;
+    const int32_t *meta;
+    int N, kb, ke, hinv, useg, yrel, hfac;
+    int64_t b0, nb, sY, sy, sH, sg, sS;
+};
+constexpr int KU_PF = 2;                     // k-slices of Y in flight per wave
+constexpr int KU_LDS = 64 * KF_LU + 64 + 4 * KS_HG;   // per wave: U / W image, vector, 2 H⁻¹|g rows
+
+// H⁻¹ (or 1) and g of knot q into one of the wave's LDS rows (0 past w); earlier reads of the
+// row are ordered before these writes by the wave's in-order LDS (wsync: compiler fence)
+template <typename T>
+__device__ __forceinline__ void fu_stage_hg(T *hgl, const Kn &q, const T *Ht, const T *gt, int hinv, int useg, int lane)
+{
+    wsync();
+#pragma unroll
+    for (int u = 0; u < (KS_HG + 63) / 64; ++u) {
+        const int c = lane + 64 * u;
+        if (c < KS_HG) {
+            const bool in = c < q.w;
+            hgl[c] = in ? (hinv ? (T)1 / Ht[q.oH + c] : (T)1) : (T)0;
+            hgl[KS_HG + c] = (in && useg) ? gt[q.og + c] : (T)0;
+        }
+    }
+    wsync();
+}
+
+// shur! pieces of knot q in one wave.  Row blocks 0..NT−1 are the D2 rows (n1), NT..2NT−1 the
+// D1 rows (n2, after the p stage rows).  MODE 1: F = D2 H⁻¹ D1ᵀ into G and C = D1 H⁻¹ D1ᵀ into
+// Cn (both zeroed here), r2 = D1 H⁻¹ g;  MODE 0: A = D2 H⁻¹ D2ᵀ accumulated into Cn, r1 =
+// D2 H⁻¹ g.  r comes back in column layout (every lane holds r[16v + (lane & 15)]) in rv[v].
+// Y is read by raw buffer loads through a per-slice descriptor bounded by the block's end
+// (columns past w and the slices past the last one read 0: nothing past the block).  FULL:
+// whole 16-row blocks and D1 at row 16·NT — the row-block offsets are immediates of one
+// VGPR offset; otherwise one range-checked offset per row block (rows past a part read 0).
+template <typename T, int NT, int MODE, bool FULL>
+__device__ __forceinline__ void fu_schur(const Kn &q, const T *Yk, const T *hgl, acc_t<T> (&G)[16], acc_t<T> (&Cn)[10],
+                                         T (&rv)[2 * NT], int lane)
+{
+    constexpr int NB = 2 * NT;
+    constexpr int V1 = MODE == 0 ? NT : NB;          // row blocks loaded
+    const int i16 = lane & 15, g4 = lane >> 4;
+    constexpr uint32_t TS = sizeof(T), OOB = 0x80000000u;
+    constexpr int NV = FULL ? 1 : V1;
+    uint32_t vo[NV];
+    if constexpr (FULL) {
+        vo[0] = (uint32_t)((g4 * q.rows + i16) * (int)TS);
+    } else {
+#pragma unroll
+        for (int v = 0; v < V1; ++v) {
+            const int rb = v < NT ? 16 * v : q.p1 + q.ps + 16 * (v - NT);
+            const int lim = v < NT ? q.p1 - 16 * v : q.p2 - 16 * (v - NT);
+            vo[v] = i16 < lim ? (uint32_t)((g4 * q.rows + rb + i16) * (int)TS) : OOB;
+        }
+    }
+    if constexpr (MODE == 1) {
+#pragma unroll
+        for (int u = 0; u < NT * NT; ++u) G[u] = tzero<T>();
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+            for (int j = i; j < NT; ++j) Cn[up4(i, j)] = tzero<T>();
+    }
+    T rp[NB];
+#pragma unroll
+    for (int v = 0; v < NB; ++v) rp[v] = (T)0;
+    const char *ybase = (const char *)Yk;
+    const int ybytes = q.rows * q.w * (int)TS, so_col = 4 * q.rows * (int)TS;
+    const int nks = (q.w + 3) >> 2;
+    T f[KU_PF][NB], hh[KU_PF], gg[KU_PF];
+    auto load = [&](int s, T (&fr)[NB], T &h, T &g_) __attribute__((always_inline)) {
+        const int so = s * so_col;
+        const __amdgpu_buffer_rsrc_t ry =
+            __builtin_amdgcn_make_buffer_rsrc((void *)(ybase + so), (short)0, max(ybytes - so, 0), 0x00020000);
+#pragma unroll
+        for (int v = 0; v < V1; ++v)
+            fr[v] = bload<T>(ry, FULL ? vo[0] + (uint32_t)(16 * v * (int)TS) : vo[FULL ? 0 : v], 0u);
+        h = hgl[4 * s + g4];
+        g_ = hgl[KS_HG + 4 * s + g4];
+    };
+    auto step = [&](const T (&fr)[NB], T h, T g_) __attribute__((always_inline)) {
+        T fh[NB];
+#pragma unroll
+        for (int v = 0; v < V1; ++v) fh[v] = fr[v] * h;
+        if constexpr (MODE == 0) {
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+#pragma unroll
+                for (int j = i; j < NT; ++j) Cn[up4(i, j)] = Tile<T>::mma(fr[i], fh[j], Cn[up4(i, j)]);
+#pragma unroll
+            for (int v = 0; v < NT; ++v) rp[v] = fma(fh[v], g_, rp[v]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j) G[i * NT + j] = Tile<T>::mma(fr[i], fh[NT + j], G[i * NT + j]);
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+#pragma unroll
+                for (int j = i; j < NT; ++j) Cn[up4(i, j)] = Tile<T>::mma(fr[NT + i], fh[NT + j], Cn[up4(i, j)]);
+#pragma unroll
+            for (int v = NT; v < NB; ++v) rp[v] = fma(fh[v], g_, rp[v]);
+        }
+    };
+#pragma unroll
+    for (int u = 0; u < KU_PF; ++u) {
+#pragma unroll
+        for (int v = V1; v < NB; ++v) f[u][v] = (T)0;
+        load(u, f[u], hh[u], gg[u]);
+    }
+    // branch-free ring (slices past the last read 0 and carry h = 0): each step waits only for
+    // its own slice, requested KU_PF steps earlier
+    for (int s0 = 0; s0 < nks; s0 += KU_PF) {
+#pragma unroll
+        for (int u = 0; u < KU_PF; ++u) {
+            step(f[u], hh[u], gg[u]);
+            load(s0 + u + KU_PF, f[u], hh[u], gg[u]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int v = (MODE == 0 ? 0 : NT); v < (MODE == 0 ? NT : NB); ++v) {
+        T x = rp[v];
+        x += __shfl_xor(x, 16);
+        x += __shfl_xor(x, 32);
+        rv[v] = x;
+    }
+}
+
+// F̃ = Wᵀ G in place (:57; the upper tiles of W read from the wave's LDS image, column-major
+// with leading dimension KF_LU), x = xn − F̃ᵀλ (column layout), X ← Cn − F̃ᵀF̃ (:61)
+template <typename T, int NT>
+__device__ __forceinline__ void fu_reduce(acc_t<T> (&X)[10], acc_t<T> (&G)[16], const acc_t<T> (&Cn)[10], const T *Wl,
+                                          const T (&lam)[4][4], const T (&xn)[4], T (&x)[4], int lane)
+{
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int j = i; j < NT; ++j) X[up4(i, j)] = tload(Wl + 16 * i + 16 * j * KF_LU, KF_LU, lane);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        acc_t<T> Yc[NT];
+#pragma unroll
+        for (int L = 0; L < NT; ++L) Yc[L] = G[L * NT + j];
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            acc_t<T> g = tzero<T>();
+#pragma unroll
+            for (int L = 0; L <= i; ++L) g = mtn<T>(X[up4(L, i)], Yc[L], g);
+            G[i * NT + j] = g;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        T sacc = (T)0;
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sacc = fma(G[i * NT + j][r], lam[i][r], sacc);
+        sacc += __shfl_xor(sacc, 16);
+        sacc += __shfl_xor(sacc, 32);
+        x[j] = xn[j] - sacc;
+    }
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int j = i; j < NT; ++j) {
+            acc_t<T> c = Cn[up4(i, j)];
+#pragma unroll
+            for (int L = 0; L < NT; ++L) c = mtn<T, true>(G[L * NT + i], G[L * NT + j], c);
+            X[up4(i, j)] = c;
+        }
+}
+
+// shur! of knot kn (F, C, r2 → xn = r2 − y) and the D2 part of knot kn+1 (A into Cn, r1 added
+// to xn: d_kn = r2 − y + r1 of the next knot, as the image's v)
+template <typename T, int NT, bool FULL>
+__device__ __forceinline__ void fu_stream(const int32_t *meta, int kn, const T *Yt, const T *yt, const T *Ht, const T *gt,
+                                          int hinv, int useg, T *hgl, acc_t<T> (&G)[16], acc_t<T> (&Cn)[10], T (&xn)[4],
+                                          int lane)
+{
+    const Kn q1 = kn_load(meta, kn), q2 = kn_load(meta, kn + 1);
+    T rv[2 * NT];
+    fu_stage_hg<T>(hgl, q1, Ht, gt, hinv, useg, lane);
+    fu_stage_hg<T>(hgl + 2 * KS_HG, q2, Ht, gt, hinv, useg, lane);
+    fu_schur<T, NT, 1, FULL>(q1, Yt + q1.oY, hgl, G, Cn, rv, lane);
+    fu_schur<T, NT, 0, FULL>(q2, Yt + q2.oY, hgl + 2 * KS_HG, G, Cn, rv, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int e = 16 * j + (lane & 15);
+        xn[j] = (j < NT && e < q1.p2) ? (rv[NT + j] - yt[q1.oy + e]) + rv[j] : (T)0;
+    }
+}
+
+template <typename T, int NT, bool FULL>
+__global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_fuse_mid_kernel(KuArgs<T> a)
+{
+    extern __shared__ __align__(16) unsigned char kb_lds_raw[];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t tl = (int64_t)blockIdx.x * KF_W + wave;
+    if (tl >= a.nb) return;                          // whole wave; no workgroup barriers below
+    T *U = (T *)kb_lds_raw + wave * KU_LDS, *vb = U + 64 * KF_LU, *hgl = vb + 64;
+    const int64_t t = a.b0 + tl, ty = a.yrel ? tl : t;
+    const T *Yt = a.Y + ty * a.sY, *yt = a.y + t * a.sy, *Ht = a.H + t * a.sH, *gt = a.g + ty * a.sg;
+    T *St = a.slab + tl * a.sS;
+    constexpr int PP = 16 * NT;
+    int64_t oS = slab_before(a.meta, a.kb);
+    acc_t<T> X[10], G[16], Cn[10];
+    T lam[4][4], x[4], xn[4];
+    {
+        // the state at kb − 1 (W_{kb−1}, λ_{kb−1}, left in the slab by the general kernel)
+        // into the LDS W image the reduction reads
+        const int32_t *m = a.meta + 8 * (a.kb - 1);
+        kf_resume<T>(X, lam, St + oS - slab_size(r16(m[1]), r16(m[2])), r16(m[2]), r16(m[1]), NT, lane);
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+            for (int j = i; j < NT; ++j) tstore(U + 16 * i + 16 * j * KF_LU, KF_LU, X[up4(i, j)], lane);
+    }
+    // prologue: knot kb's F, C, d and knot kb+1's A; then F̃_kb, x_kb, X = C_kb + A_{kb+1} − F̃ᵀF̃
+    fu_stream<T, NT, FULL>(a.meta, a.kb, Yt, yt, Ht, gt, a.hinv, a.useg, hgl, G, Cn, xn, lane);
+    wsync();
+    fu_reduce<T, NT>(X, G, Cn, U, lam, xn, x, lane);
+    int info = 0;
+    for (int k = a.kb; k < a.ke; ++k) {
+        const int p2 = a.meta[8 * k + 2];
+        // C̃_k = chol(X) → X = W_k (:61-62)
+        const int bad = chol_inv_reg<T>(X, NT, p2, U, lane);
+        // λ_k = W_kᵀ x_k (:108-116)
+        T xr[4][4], lc[4];
+        col2row<T>(xr, x, vb, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            T sacc = (T)0;
+            if (j < NT) {
+#pragma unroll
+                for (int i = 0; i <= j; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) sacc = fma(X[up4(i, j)][r], xr[i][r], sacc);
+            }
+            sacc += __shfl_xor(sacc, 16);
+            sacc += __shfl_xor(sacc, 32);
+            lc[j] = sacc;
+        }
+        col2row<T>(lam, lc, vb, lane);
+        // slab: W_k packed upper (column col at col(col+1)/2: the off-diagonal tiles store
+        // unpredicated at a per-lane column base plus immediates; only the diagonal tiles test
+        // row ≤ col, the same four lane masks for every tile), λ_k
+        T *Sk = St + oS;
+        oS += slab_size(0, PP);
+        {
+            const int c = lane & 15;
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                T *cb = Sk + (16 * j + c) * (16 * j + c + 1) / 2;
+#pragma unroll
+                for (int i = 0; i < j; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) cb[16 * i + Tile<T>::row(lane, r)] = X[up4(i, j)][r];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (Tile<T>::row(lane, r) <= c) cb[16 * j + Tile<T>::row(lane, r)] = X[up4(j, j)][r];
+            }
+        }
+        if (lane < 16) {
+#pragma unroll
+            for (int j = 0; j < NT; ++j) Sk[PP * (PP + 1) / 2 + 16 * j + lane] = lc[j];
+        }
+        if (bad && !info) info = k + 1;
+        if (k + 1 < a.ke) {
+            // W_k to the LDS image (chol_inv_reg's scratch is free again): no tile is live
+            // across the streaming but G and Cn
+            wsync();
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+#pragma unroll
+                for (int j = i; j < NT; ++j) tstore(U + 16 * i + 16 * j * KF_LU, KF_LU, X[up4(i, j)], lane);
+            fu_stream<T, NT, FULL>(a.meta, k + 1, Yt, yt, Ht, gt, a.hinv, a.useg, hgl, G, Cn, xn, lane);
+            wsync();
+            fu_reduce<T, NT>(X, G, Cn, U, lam, xn, x, lane);
+        }
     }
     if (lane == 0) kf_info(a.info, t, info, a.kb, a.hfac);
 }
@@ -2328,12 +2637,21 @@ struct KbPlan {
     int nruns;                      // split: Schur units per trajectory
     int nbt;                        // split: the Schur kernel's block grid (max R / 16)
     int mid0, mid1, midnt;          // split: knots [mid0, mid1) run on kb_factor_mid_kernel<midnt>
+    bool fuse;                      // … or on kb_fuse_mid_kernel<midnt> (no Schur images there)
+    bool midfull;                   // fused: n2 of the run a multiple of 16 (whole row blocks)
+    int nr0;                        // Schur runs over knots [0, mid0) (fused) or all runs
 };
 
 // LQRX_KKT_MID=0 keeps the interior knots on the general factor kernel (A/B checks)
 int kb_mid_env()
 {
     static const int v = [] { const char *e = std::getenv("LQRX_KKT_MID"); return e && *e ? std::atoi(e) : 1; }();
+    return v;
+}
+// LQRX_KKT_FUSE=0 runs the interior knots as Schur kernel + kb_factor_mid_kernel (A/B checks)
+int kb_fuse_env()
+{
+    static const int v = [] { const char *e = std::getenv("LQRX_KKT_FUSE"); return e && *e ? std::atoi(e) : 1; }();
     return v;
 }
 // LQRX_KKT_SPLIT=0 keeps every structure on the fused forward kernel (A/B checks)
@@ -2429,6 +2747,16 @@ bool kb_plan(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_
             P.midnt = r16(n2[best0]) >> 4;
         }
     }
+    // fused interior run: the Schur kernel covers [0, mid0) and [mid1, N) only, and the
+    // interior knots get no image
+    P.fuse = P.midnt > 0 && P.mid1 < a.N && kb_fuse_env() != 0;
+    P.midfull = P.fuse && n2[P.mid0] == 16 * P.midnt;
+    P.nr0 = P.nruns;
+    if (P.fuse) {
+        P.nr0 = (P.mid0 + KS_L - 1) / KS_L;
+        P.nruns = P.nr0 + (a.N - P.mid1 + KS_L - 1) / KS_L;
+        for (int k = P.mid0; k < P.mid1; ++k) P.IMGT -= (img_off(r16(n1[k]), r16(p[k]), r16(n2[k])).end + 63) & ~(int64_t)63;
+    }
     constexpr size_t LDS_CAP = 160 * 1024;
     return (size_t)P.nf * tsize <= LDS_CAP && (size_t)P.nb * tsize <= LDS_CAP && (size_t)P.nh * tsize <= LDS_CAP;
 }
@@ -2507,8 +2835,32 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
         ks.img = img; ks.meta = a.meta; ks.N = a.N; ks.nruns = P.nruns;
         ks.hinv = a.ginv && !P.hfac; ks.useg = a.ginv; ks.yrel = P.hfac;
         ks.sY = a.sY; ks.sy = a.sy; ks.sH = a.sH; ks.sg = a.sg; ks.IMGT = P.IMGT;
+        ks.nr0 = P.nr0;
+        ks.kend0 = P.fuse ? P.mid0 : a.N;
+        ks.kbeg1 = P.fuse ? P.mid1 : a.N;
         kf.img = img; kf.slab = slab; kf.info = a.info; kf.meta = a.meta; kf.N = a.N; kf.hfac = P.hfac;
         kf.IMGT = P.IMGT; kf.sS = P.S;
+        kf.fz0 = P.fuse ? P.mid0 : 0;
+        kf.fz1 = P.fuse ? P.mid1 : 0;
+    }
+    KuArgs<T> ku{};
+    const size_t lfu = (size_t)KF_W * KU_LDS * sizeof(T);
+    if (P.fuse) {
+        ku.Y = P.hfac ? Z : (const T *)a.Y; ku.y = (const T *)a.y; ku.H = (const T *)a.H;
+        ku.g = P.hfac ? gz : (const T *)a.g;
+        ku.slab = slab; ku.info = a.info; ku.meta = a.meta; ku.N = a.N; ku.kb = P.mid0; ku.ke = P.mid1;
+        ku.hinv = a.ginv && !P.hfac; ku.useg = a.ginv; ku.yrel = P.hfac; ku.hfac = P.hfac;
+        ku.sY = a.sY; ku.sy = a.sy; ku.sH = a.sH; ku.sg = a.sg; ku.sS = P.S;
+        const void *fk[8] = {(const void *)kb_fuse_mid_kernel<T, 1, false>, (const void *)kb_fuse_mid_kernel<T, 1, true>,
+                             (const void *)kb_fuse_mid_kernel<T, 2, false>, (const void *)kb_fuse_mid_kernel<T, 2, true>,
+                             (const void *)kb_fuse_mid_kernel<T, 3, false>, (const void *)kb_fuse_mid_kernel<T, 3, true>,
+                             (const void *)kb_fuse_mid_kernel<T, 4, false>, (const void *)kb_fuse_mid_kernel<T, 4, true>};
+        for (int i = 0; i < 8 && e == hipSuccess; ++i)
+            e = hipFuncSetAttribute(fk[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfu);
+        if (e != hipSuccess) {
+            (void)sc.release(s);
+            return e;
+        }
     }
     KhArgs<T> h{};
     if (P.hfac) {
@@ -2559,7 +2911,18 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
                 kf.ke = k1_;
                 hipLaunchKernelGGL(kb_factor_kernel<T>, gf, bf, lfac, s, kf);
             };
-            if (P.mid1 > P.mid0) {
+            if (P.fuse) {
+                generic(0, P.mid0);
+                ku.b0 = b0;
+                ku.nb = nb;
+                switch (P.midnt * 2 + (P.midfull ? 1 : 0)) {
+#define KU_L_(NT_, F_) case NT_ * 2 + F_: hipLaunchKernelGGL((kb_fuse_mid_kernel<T, NT_, F_ != 0>), gf, bf, lfu, s, ku); break;
+                KU_L_(1, 0) KU_L_(1, 1) KU_L_(2, 0) KU_L_(2, 1) KU_L_(3, 0) KU_L_(3, 1) KU_L_(4, 0)
+                default: hipLaunchKernelGGL((kb_fuse_mid_kernel<T, 4, true>), gf, bf, lfu, s, ku); break;
+#undef KU_L_
+                }
+                generic(P.mid1, a.N);
+            } else if (P.mid1 > P.mid0) {
                 generic(0, P.mid0);
                 kf.kb = P.mid0;
                 kf.ke = P.mid1;

@@ -276,7 +276,8 @@ sys.path[:0] = [sys.argv[1] + "/lqr.jl_amd", sys.argv[1]]
 import lqrx, lqrx.kkt as K
 from oracle import oracle as orc
 worst = 0.0
-for n, m, N, dt in ((16, 8, 21, lqrx.F64), (64, 32, 9, lqrx.F64), (32, 16, 13, lqrx.F32)):
+for n, m, N, dt in ((16, 8, 21, lqrx.F64), (64, 32, 9, lqrx.F64), (32, 16, 13, lqrx.F32), (8, 4, 17, lqrx.F32),
+                    (40, 12, 11, lqrx.F64), (64, 32, 33, lqrx.F32)):
     st = K.trajectory_structure(n, m, N)
     pb = K.random_kkt(st, 3, seed=n + N, h_mode=K.H_DIAG, dyn="dense")
     if dt == lqrx.F32:
@@ -294,13 +295,14 @@ for n, m, N, dt in ((16, 8, 21, lqrx.F64), (64, 32, 9, lqrx.F64), (32, 16, 13, l
 """
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
-def test_big_kkt_fused_and_split_forward(lqrx, gpu_ok, tmp_path, split):
-    """Both forward sweeps of the large-block path on the trajectory structure: the split
-    Schur-kernel + factor-kernel path (default) and the fused one-workgroup-per-trajectory
-    kernel (LQRX_KKT_SPLIT=0, which every structure with stage constraints at interior knots
-    takes), fp64 and fp32, against the oracle (one child process each: the switch is read
-    once per process)."""
+@pytest.mark.parametrize("split,fuse", [("0", "1"), ("1", "0"), ("1", "1")])
+def test_big_kkt_fused_and_split_forward(lqrx, gpu_ok, tmp_path, split, fuse):
+    """Every forward sweep of the large-block path on the trajectory structure: the split path
+    with the interior knots on the fused one-wave Schur+factor kernel (default), the split path
+    with Schur images + kb_factor_mid_kernel (LQRX_KKT_FUSE=0), and the one-workgroup-per-
+    trajectory kernel (LQRX_KKT_SPLIT=0, which every structure with stage constraints at
+    interior knots takes), fp64 and fp32, against the oracle (one child process each: the
+    switches are read once per process)."""
     import os
     import subprocess
     import sys
@@ -308,7 +310,7 @@ def test_big_kkt_fused_and_split_forward(lqrx, gpu_ok, tmp_path, split):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     f = tmp_path / "fused.py"
     f.write_text(_FUSED_SCRIPT)
-    env = dict(os.environ, LQRX_KKT_SPLIT=split)
+    env = dict(os.environ, LQRX_KKT_SPLIT=split, LQRX_KKT_FUSE=fuse)
     p = subprocess.run([sys.executable, str(f), root], env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
 
