@@ -751,7 +751,7 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
 #pragma unroll
                         for (int j = 0; j < MT; ++j) {
                             X0[i][j] = Xi[i][j];
-                            if (k < N - 2) Xi[i][j] = (T)2 * Xi[i][j] - Xp[i][j];
+                            Xi[i][j] = (T)2 * Xi[i][j] - Xp[i][j];   // = X_{k+1} at k = N−2 (Xp = Xi there)
                         }
                     have = ns_refine<T, MT>(Xi, E, Id, lane);
 #pragma unroll
@@ -780,6 +780,13 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
                 __syncthreads();
                 tiles_zero<T, MT, MT>(Xi);
                 mma_tn<T, MT, MT, MT>(Xi, Wt, DW);                      // X = Wᵀ D⁻¹ W = E⁻¹
+                if (k == N - 1) {
+                    // no extrapolation into knot N−2 (only one inverse exists): 2X − Xp = X
+#pragma unroll
+                    for (int i = 0; i < MT; ++i)
+#pragma unroll
+                        for (int j = 0; j < MT; ++j) Xp[i][j] = Xi[i][j];
+                }
             }
             tiles_zero<T, MT, NT>(Kt);
             mma_tn<T, MT, MT, NT>(Kt, Xi, G);                          // K = XᵀG = E⁻¹G
