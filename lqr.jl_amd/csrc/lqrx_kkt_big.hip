@@ -1257,6 +1257,11 @@ constexpr int KS_HG = KB_WMAX + 4;   // staged H⁻¹ / g row: w columns padded 
 constexpr int KS_PF = KS_PF_SLICES;  // k-slices in flight per Schur wave
 constexpr int KF_W = 4;        // trajectories (waves) per factor workgroup
 constexpr int KF_LU = 68;      // factor LDS image leading dimension
+constexpr int KF_SCR = 4 * KS_HG;                     // per-wave leaf scratch (≥ 64 + 256 + 16)
+constexpr int KF_LDS = 64 * KF_LU + 64 + KF_SCR;      // per wave: U image, vector, scratch
+#ifndef KF_OLD_LEAF
+#define KF_OLD_LEAF 0                                 // 1: the 16-lane readlane leaf (A/B builds)
+#endif
 
 // image of one knot (elements of T from the knot's base): tiles D, F, B, E, C (256 elements
 // each, lane-major C layout: element 4·lane + r = register r of lane `lane`), then
@@ -1648,6 +1653,68 @@ __device__ __forceinline__ void kf_info(int32_t *info, int64_t t, int v, int kb,
     else if (v && info[t] == 0) info[t] = v;
 }
 
+// 16×16 leaf on a C-layout register tile, all 64 lanes (4 elements each): X ← T = U⁻¹ with
+// UᵀU = X (upper; T's strictly-lower part is zero).  potrf 'U' right-looking (dpotf2's order
+// up to rsqrt-multiply; dynamic_programming.jl:29, cholesky_solve.jl:2): pivot i's scaled row
+// U[i][·] (0 at and left of the diagonal) goes through a 64-element LDS row — every row group
+// writes its register holding row i of ITS rows, readers take the group that holds row i — and
+// every lane applies the rank-1 update to its 4 elements unmasked (the zeros confine it to the
+// trailing block).  Then T = U⁻¹ right-looking from the bottom: row k of T = B_k / U_kk is
+// broadcast the same way and B_R −= U[R][k]·T_k with U's strictly-upper columns from an LDS
+// image.  Only the upper triangle of X is read.  q = real pivots (pivots ≥ q are identity
+// padding); returns 1 + the first non-positive pivot, else 0.  scr: KF_SCR elements of LDS.
+template <typename T>
+__device__ __forceinline__ int leaf_chol_inv_t(acc_t<T> &X, T *scr, int q, int lane)
+{
+    T *ub = scr, *ut = scr + 64, *ri = ut + 256;        // row buffer, Uᵀ image, 1/U_ii
+    const int c = lane & 15, g = lane >> 4;
+    constexpr bool F64 = sizeof(T) == 8;
+    int bad = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int gi = F64 ? (i & 3) : (i >> 2), rgi = F64 ? (i >> 2) : (i & 3);
+        const T d = readlane(X[rgi], 16 * gi + i);
+        if (!(d > (T)0) && i < q && !bad) bad = i + 1;
+        const T sc = rsqrt_nr(d);
+        wsync();
+        ub[16 * g + c] = c > i ? X[rgi] * sc : (T)0;
+        if (lane == 0) ri[i] = sc;
+        wsync();
+        const T uc = ub[16 * gi + c];
+        T ur[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ur[r] = ub[16 * gi + Tile<T>::row(lane, r)];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) X[r] = fma(-ur[r], uc, X[r]);
+        ut[16 * c + i] = uc;                             // U[i][c] (c > i) at [c][i]: Uᵀ, column c
+    }
+    // B = I; k = 15 … 0: T_k = B_k / U_kk (broadcast), B_R −= U[R][k] T_k for R < k
+    acc_t<T> B;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) B[r] = Tile<T>::row(lane, r) == c ? (T)1 : (T)0;
+    T rr[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rr[r] = ri[Tile<T>::row(lane, r)];
+#pragma unroll
+    for (int k = 15; k >= 0; --k) {
+        const int gk = F64 ? (k & 3) : (k >> 2), rgk = F64 ? (k >> 2) : (k & 3);
+        const T rk = ri[k];
+        wsync();
+        ub[16 * g + c] = B[rgk] * rk;
+        wsync();
+        const T tk = ub[16 * gk + c];
+        T uk[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) uk[r] = ut[16 * k + Tile<T>::row(lane, r)];   // U[R][k], 0 for R ≥ k
+#pragma unroll
+        for (int r = 0; r < 4; ++r) B[r] = fma(-uk[r], tk, B[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) X[r] = B[r] * rr[r];
+    wsync();
+    return bad;
+}
+
 // In place on the upper tiles X (packed up4) of a P×P SPD matrix (nb ≤ 4 block rows, p real
 // pivots): X ← U⁻¹ with UᵀU = X.  Right-looking by 16 as chol_inv: leaf (LDS, one wave) →
 // panel U_{jb,J} = T_jjᵀ X_{jb,J} → trailing X_IJ −= U_{jb,I}ᵀ U_{jb,J}, all in registers;
@@ -1655,7 +1722,7 @@ __device__ __forceinline__ void kf_info(int32_t *info, int64_t t, int v, int kb,
 // image U (leading dimension KF_LU) the factor phase left there.  Returns 0 or 1 + the
 // first non-positive pivot.
 template <typename T>
-__device__ int chol_inv_reg(acc_t<T> (&X)[10], int nb, int p, T *U, int lane)
+__device__ int chol_inv_reg(acc_t<T> (&X)[10], int nb, int p, T *U, T *scr, int lane)
 {
 #pragma unroll
     for (int jb = 0; jb < 4; ++jb)
@@ -1671,12 +1738,19 @@ __device__ int chol_inv_reg(acc_t<T> (&X)[10], int nb, int p, T *U, int lane)
     for (int jb = 0; jb < 4; ++jb) {
         if (jb < nb) {
             T *Dg = U + 16 * jb * (1 + KF_LU);
+#if KF_OLD_LEAF
             tstore(Dg, KF_LU, X[up4(jb, jb)], lane);
             wsync();
             const int b = leaf_chol_inv<T>(Dg, KF_LU, min(16, p - 16 * jb), lane);
             if (b && !bad) bad = 16 * jb + b;
             wsync();
             X[up4(jb, jb)] = tload(Dg, KF_LU, lane);
+            (void)scr;
+#else
+            const int b = leaf_chol_inv_t<T>(X[up4(jb, jb)], scr, min(16, p - 16 * jb), lane);
+            if (b && !bad) bad = 16 * jb + b;
+            tstore(Dg, KF_LU, X[up4(jb, jb)], lane);     // T_jj for the inverse assembly's reads
+#endif
 #pragma unroll
             for (int J = jb + 1; J < 4; ++J)
                 if (J < nb) {
@@ -1754,7 +1828,7 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_k
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t tl = (int64_t)blockIdx.x * KF_W + wave;
     if (tl >= a.nb) return;                          // whole wave; no workgroup barriers below
-    T *U = (T *)kb_lds_raw + wave * (64 * KF_LU + 64), *vb = U + 64 * KF_LU;
+    T *U = (T *)kb_lds_raw + wave * KF_LDS, *vb = U + 64 * KF_LU, *scr = vb + 64;
     const int64_t t = a.b0 + tl;
     const T *imt = a.img + tl * a.IMGT;
     T *St = a.slab + tl * a.sS;
@@ -1833,7 +1907,7 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_k
                         }
                         X[up4(i, j)] = c;
                     }
-            bad |= chol_inv_reg<T>(X, nst, q.ps, U, lane);
+            bad |= chol_inv_reg<T>(X, nst, q.ps, U, scr, lane);
             // μ = B̃⁻ᵀ(c − D̃ᵀλ_{k−1})  (:101-107)
             T x[4], xr[4][4], mu[4];
 #pragma unroll
@@ -1898,7 +1972,7 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_k
             // Ẽᵀμ for λ while G still holds Ẽ
             T ey[4];
             if (nst) mtv<T, false>(ey, G, mur, nst, n2t);
-            bad |= chol_inv_reg<T>(X, n2t, q.p2, U, lane);
+            bad |= chol_inv_reg<T>(X, n2t, q.p2, U, scr, lane);
             // λ = C̃⁻ᵀ(d − F̃ᵀλ_{k−1} − Ẽᵀμ)  (:108-116)
             T x[4], xr[4][4], lc[4];
 #pragma unroll
@@ -1945,7 +2019,7 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_m
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t tl = (int64_t)blockIdx.x * KF_W + wave;
     if (tl >= a.nb) return;
-    T *U = (T *)kb_lds_raw + wave * (64 * KF_LU + 64), *vb = U + 64 * KF_LU;
+    T *U = (T *)kb_lds_raw + wave * KF_LDS, *vb = U + 64 * KF_LU, *scr = vb + 64;
     const int64_t t = a.b0 + tl;
     const T *imt = a.img + tl * a.IMGT;
     T *St = a.slab + tl * a.sS;
@@ -2019,7 +2093,7 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_factor_m
             }
         // G, Cn, dd are dead: knot k+1's tiles land during the factorisation below
         if (k + 1 < a.ke) fetch(imt + oI);
-        const int bad = chol_inv_reg<T>(X, NT, p2, U, lane);
+        const int bad = chol_inv_reg<T>(X, NT, p2, U, scr, lane);
         // λ = C̃⁻ᵀ(d − F̃ᵀλ_{k−1}) (:108-116)
         T xr[4][4], lc[4];
         col2row<T>(xr, x, vb, lane);
@@ -2080,7 +2154,7 @@ struct KuArgs {
     int64_t b0, nb, sY, sy, sH, sg, sS;
 };
 constexpr int KU_PF = 2;                     // k-slices of Y in flight per wave
-constexpr int KU_LDS = 64 * KF_LU + 64 + 4 * KS_HG;   // per wave: U / W image, vector, 2 H⁻¹|g rows
+constexpr int KU_LDS = KF_LDS;   // per wave: U / W image, vector, 2 H⁻¹|g rows (also the leaf scratch)
 
 // H⁻¹ (or 1) and g of knot q into one of the wave's LDS rows (0 past w); earlier reads of the
 // row are ordered before these writes by the wave's in-order LDS (wsync: compiler fence)
@@ -2300,7 +2374,7 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_fuse_mid
     for (int k = a.kb; k < a.ke; ++k) {
         const int p2 = a.meta[8 * k + 2];
         // C̃_k = chol(X) → X = W_k (:61-62)
-        const int bad = chol_inv_reg<T>(X, NT, p2, U, lane);
+        const int bad = chol_inv_reg<T>(X, NT, p2, U, hgl, lane);
         // λ_k = W_kᵀ x_k (:108-116)
         T xr[4][4], lc[4];
         col2row<T>(xr, x, vb, lane);
@@ -2817,7 +2891,7 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
     T *slab = (T *)sc.p, *Z = slab + chunk * P.S, *gz = Z + chunk * a.sY, *Ui = gz + chunk * a.sg;
     T *img = P.hfac ? Ui + chunk * P.sU : Z;
     constexpr int KS_NW = 4;
-    const size_t lfac = (size_t)KF_W * (64 * KF_LU + 64) * sizeof(T);
+    const size_t lfac = (size_t)KF_W * KF_LDS * sizeof(T);
     if (P.split && ((e = hipFuncSetAttribute((const void *)kb_factor_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                              (int)lfac)) != hipSuccess ||
                     (e = hipFuncSetAttribute((const void *)kb_factor_mid_kernel<T, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfac)) != hipSuccess ||
