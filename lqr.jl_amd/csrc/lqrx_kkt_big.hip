@@ -1746,6 +1746,9 @@ __device__ int chol_inv_reg(acc_t<T> (&X)[10], int nb, int p, T *U, T *scr, int 
             wsync();
             X[up4(jb, jb)] = tload(Dg, KF_LU, lane);
             (void)scr;
+#elif defined(KF_NOLEAF)
+            const int b = 0;       // timing ablation only: no leaf factor (wrong results)
+            (void)scr;
 #else
             const int b = leaf_chol_inv_t<T>(X[up4(jb, jb)], scr, min(16, p - 16 * jb), lane);
             if (b && !bad) bad = 16 * jb + b;
@@ -2152,8 +2155,26 @@ struct KuArgs {
     const int32_t *meta;
     int N, kb, ke, hinv, useg, yrel, hfac;
     int64_t b0, nb, sY, sy, sH, sg, sS;
+    int64_t *prof;                           // KB_PROF builds: per-phase cycles (else unused)
 };
-constexpr int KU_PF = 2;                     // k-slices of Y in flight per wave
+#ifndef KU_PF_SLICES
+#define KU_PF_SLICES 2
+#endif
+#ifndef KU_LEAN
+#define KU_LEAN 1            // H⁻¹/g read at use, λ carried in column layout (fewer live registers)
+#endif
+#ifndef KU_WAVES
+#define KU_WAVES 4           // trajectories (waves) per fused workgroup: 4, or 8 (2 per SIMD in one WG)
+#endif
+#ifndef KU_STAGGER
+#define KU_STAGGER 0         // > 0 (with KU_WAVES 8): waves 4–7 start this many s_sleep units late
+#endif
+#ifndef KU_PRIO
+#define KU_PRIO 1            // the factor phase (latency-bound chain) runs at raised issue priority
+#endif
+// waves per fused workgroup: fp64 stays at 4 (one per SIMD: its LDS and registers)
+template <typename T> constexpr int ku_w() { return sizeof(T) == 4 ? KU_WAVES : 4; }
+constexpr int KU_PF = KU_PF_SLICES;          // k-slices of Y (of both knots) in flight per wave
 constexpr int KU_LDS = KF_LDS;   // per wave: U / W image, vector, 2 H⁻¹|g rows (also the leaf scratch)
 
 // H⁻¹ (or 1) and g of knot q into one of the wave's LDS rows (0 past w); earlier reads of the
@@ -2174,101 +2195,116 @@ __device__ __forceinline__ void fu_stage_hg(T *hgl, const Kn &q, const T *Ht, co
     wsync();
 }
 
-// shur! pieces of knot q in one wave.  Row blocks 0..NT−1 are the D2 rows (n1), NT..2NT−1 the
-// D1 rows (n2, after the p stage rows).  MODE 1: F = D2 H⁻¹ D1ᵀ into G and C = D1 H⁻¹ D1ᵀ into
-// Cn (both zeroed here), r2 = D1 H⁻¹ g;  MODE 0: A = D2 H⁻¹ D2ᵀ accumulated into Cn, r1 =
-// D2 H⁻¹ g.  r comes back in column layout (every lane holds r[16v + (lane & 15)]) in rv[v].
-// Y is read by raw buffer loads through a per-slice descriptor bounded by the block's end
-// (columns past w and the slices past the last one read 0: nothing past the block).  FULL:
-// whole 16-row blocks and D1 at row 16·NT — the row-block offsets are immediates of one
-// VGPR offset; otherwise one range-checked offset per row block (rows past a part read 0).
-template <typename T, int NT, int MODE, bool FULL>
-__device__ __forceinline__ void fu_schur(const Kn &q, const T *Yk, const T *hgl, acc_t<T> (&G)[16], acc_t<T> (&Cn)[10],
-                                         T (&rv)[2 * NT], int lane)
+// shur! pieces of two knots in one pass (one k-slice of each per loop step): of knot q1 the F
+// tiles (D2 H⁻¹ D1ᵀ, into G) and the C tiles (D1 H⁻¹ D1ᵀ, into P) and r2 = D1 H⁻¹ g; of knot
+// q2 = q1 + 1 only the D2 rows: the A tiles (D2 H⁻¹ D2ᵀ) into the SAME P tiles (copy_shur!'s A ≡
+// previous-C alias: q1's pivot block needs C_{q1} + A_{q2}) and r1 = D2 H⁻¹ g.  Row blocks
+// 0..NT−1 are the D2 rows, NT..2NT−1 the D1 rows (after the p stage rows).  G and P are zeroed
+// here; r comes back in column layout (every lane holds r[16v + (lane & 15)]): rv[v] for v ≥ NT
+// of q1, for v < NT of q2.  Y is read by raw buffer loads through per-slice descriptors bounded
+// by each block's end (columns past w and slices past the last one read 0: nothing past a
+// block is read), KU_PF slices in flight.  FULL: whole 16-row blocks and D1 at row 16·NT — the
+// row-block offsets are immediates of one VGPR offset; otherwise one range-checked offset per
+// row block (rows past a part read 0).
+template <typename T, int NT, bool FULL>
+__device__ __forceinline__ void fu_schur2(const Kn &q1, const T *Y1, const T *hg1, const Kn &q2, const T *Y2, const T *hg2,
+                                          acc_t<T> (&G)[16], acc_t<T> (&P)[10], T (&rv)[2 * NT], int lane)
 {
     constexpr int NB = 2 * NT;
-    constexpr int V1 = MODE == 0 ? NT : NB;          // row blocks loaded
     const int i16 = lane & 15, g4 = lane >> 4;
     constexpr uint32_t TS = sizeof(T), OOB = 0x80000000u;
-    constexpr int NV = FULL ? 1 : V1;
-    uint32_t vo[NV];
+    constexpr int NV1 = FULL ? 1 : NB, NV2 = FULL ? 1 : NT;
+    uint32_t vo1[NV1], vo2[NV2];
     if constexpr (FULL) {
-        vo[0] = (uint32_t)((g4 * q.rows + i16) * (int)TS);
+        vo1[0] = (uint32_t)((g4 * q1.rows + i16) * (int)TS);
+        vo2[0] = (uint32_t)((g4 * q2.rows + i16) * (int)TS);
     } else {
 #pragma unroll
-        for (int v = 0; v < V1; ++v) {
-            const int rb = v < NT ? 16 * v : q.p1 + q.ps + 16 * (v - NT);
-            const int lim = v < NT ? q.p1 - 16 * v : q.p2 - 16 * (v - NT);
-            vo[v] = i16 < lim ? (uint32_t)((g4 * q.rows + rb + i16) * (int)TS) : OOB;
+        for (int v = 0; v < NB; ++v) {
+            const int rb = v < NT ? 16 * v : q1.p1 + q1.ps + 16 * (v - NT);
+            const int lim = v < NT ? q1.p1 - 16 * v : q1.p2 - 16 * (v - NT);
+            vo1[v] = i16 < lim ? (uint32_t)((g4 * q1.rows + rb + i16) * (int)TS) : OOB;
         }
+#pragma unroll
+        for (int v = 0; v < NT; ++v)
+            vo2[v] = i16 < q2.p1 - 16 * v ? (uint32_t)((g4 * q2.rows + 16 * v + i16) * (int)TS) : OOB;
     }
-    if constexpr (MODE == 1) {
 #pragma unroll
-        for (int u = 0; u < NT * NT; ++u) G[u] = tzero<T>();
+    for (int u = 0; u < NT * NT; ++u) G[u] = tzero<T>();
 #pragma unroll
-        for (int i = 0; i < NT; ++i)
+    for (int i = 0; i < NT; ++i)
 #pragma unroll
-            for (int j = i; j < NT; ++j) Cn[up4(i, j)] = tzero<T>();
-    }
+        for (int j = i; j < NT; ++j) P[up4(i, j)] = tzero<T>();
     T rp[NB];
 #pragma unroll
     for (int v = 0; v < NB; ++v) rp[v] = (T)0;
-    const char *ybase = (const char *)Yk;
-    const int ybytes = q.rows * q.w * (int)TS, so_col = 4 * q.rows * (int)TS;
-    const int nks = (q.w + 3) >> 2;
-    T f[KU_PF][NB], hh[KU_PF], gg[KU_PF];
-    auto load = [&](int s, T (&fr)[NB], T &h, T &g_) __attribute__((always_inline)) {
-        const int so = s * so_col;
-        const __amdgpu_buffer_rsrc_t ry =
-            __builtin_amdgcn_make_buffer_rsrc((void *)(ybase + so), (short)0, max(ybytes - so, 0), 0x00020000);
+    const char *yb1 = (const char *)Y1, *yb2 = (const char *)Y2;
+    const int yn1 = q1.rows * q1.w * (int)TS, so1 = 4 * q1.rows * (int)TS;
+    const int yn2 = q2.rows * q2.w * (int)TS, so2 = 4 * q2.rows * (int)TS;
+    const int nks = max(q1.w + 3, q2.w + 3) >> 2;
+    T f1[KU_PF][NB], f2[KU_PF][NT], h1[KU_PF], c1[KU_PF], h2[KU_PF], c2[KU_PF];
+    auto load = [&](int s, T (&a1)[NB], T (&a2)[NT], T &hh1, T &gg1, T &hh2, T &gg2) __attribute__((always_inline)) {
+        const int o1 = s * so1, o2 = s * so2;
+        const __amdgpu_buffer_rsrc_t r1 =
+            __builtin_amdgcn_make_buffer_rsrc((void *)(yb1 + o1), (short)0, max(yn1 - o1, 0), 0x00020000);
+        const __amdgpu_buffer_rsrc_t r2 =
+            __builtin_amdgcn_make_buffer_rsrc((void *)(yb2 + o2), (short)0, max(yn2 - o2, 0), 0x00020000);
 #pragma unroll
-        for (int v = 0; v < V1; ++v)
-            fr[v] = bload<T>(ry, FULL ? vo[0] + (uint32_t)(16 * v * (int)TS) : vo[FULL ? 0 : v], 0u);
-        h = hgl[4 * s + g4];
-        g_ = hgl[KS_HG + 4 * s + g4];
-    };
-    auto step = [&](const T (&fr)[NB], T h, T g_) __attribute__((always_inline)) {
-        T fh[NB];
+        for (int v = 0; v < NB; ++v)
+            a1[v] = bload<T>(r1, FULL ? vo1[0] + (uint32_t)(16 * v * (int)TS) : vo1[FULL ? 0 : v], 0u);
 #pragma unroll
-        for (int v = 0; v < V1; ++v) fh[v] = fr[v] * h;
-        if constexpr (MODE == 0) {
-#pragma unroll
-            for (int i = 0; i < NT; ++i)
-#pragma unroll
-                for (int j = i; j < NT; ++j) Cn[up4(i, j)] = Tile<T>::mma(fr[i], fh[j], Cn[up4(i, j)]);
-#pragma unroll
-            for (int v = 0; v < NT; ++v) rp[v] = fma(fh[v], g_, rp[v]);
-        } else {
-#pragma unroll
-            for (int i = 0; i < NT; ++i)
-#pragma unroll
-                for (int j = 0; j < NT; ++j) G[i * NT + j] = Tile<T>::mma(fr[i], fh[NT + j], G[i * NT + j]);
-#pragma unroll
-            for (int i = 0; i < NT; ++i)
-#pragma unroll
-                for (int j = i; j < NT; ++j) Cn[up4(i, j)] = Tile<T>::mma(fr[NT + i], fh[NT + j], Cn[up4(i, j)]);
-#pragma unroll
-            for (int v = NT; v < NB; ++v) rp[v] = fma(fh[v], g_, rp[v]);
+        for (int v = 0; v < NT; ++v)
+            a2[v] = bload<T>(r2, FULL ? vo2[0] + (uint32_t)(16 * v * (int)TS) : vo2[FULL ? 0 : v], 0u);
+        if constexpr (!KU_LEAN) {
+            hh1 = hg1[4 * s + g4];
+            gg1 = hg1[KS_HG + 4 * s + g4];
+            hh2 = hg2[4 * s + g4];
+            gg2 = hg2[KS_HG + 4 * s + g4];
         }
     };
+    auto step = [&](const T (&a1)[NB], const T (&a2)[NT], T hh1, T gg1, T hh2, T gg2, int s) __attribute__((always_inline)) {
+        if constexpr (KU_LEAN) {      // H⁻¹, g of the slice straight from LDS (no ring registers)
+            hh1 = hg1[4 * s + g4];
+            gg1 = hg1[KS_HG + 4 * s + g4];
+            hh2 = hg2[4 * s + g4];
+            gg2 = hg2[KS_HG + 4 * s + g4];
+        }
+        T fh1[NB], fh2[NT];
 #pragma unroll
-    for (int u = 0; u < KU_PF; ++u) {
+        for (int v = NT; v < NB; ++v) fh1[v] = a1[v] * hh1;
 #pragma unroll
-        for (int v = V1; v < NB; ++v) f[u][v] = (T)0;
-        load(u, f[u], hh[u], gg[u]);
-    }
-    // branch-free ring (slices past the last read 0 and carry h = 0): each step waits only for
-    // its own slice, requested KU_PF steps earlier
+        for (int v = 0; v < NT; ++v) fh2[v] = a2[v] * hh2;
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) G[i * NT + j] = Tile<T>::mma(a1[i], fh1[NT + j], G[i * NT + j]);
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+            for (int j = i; j < NT; ++j) P[up4(i, j)] = Tile<T>::mma(a1[NT + i], fh1[NT + j], P[up4(i, j)]);
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+            for (int j = i; j < NT; ++j) P[up4(i, j)] = Tile<T>::mma(a2[i], fh2[j], P[up4(i, j)]);
+#pragma unroll
+        for (int v = NT; v < NB; ++v) rp[v] = fma(fh1[v], gg1, rp[v]);
+#pragma unroll
+        for (int v = 0; v < NT; ++v) rp[v] = fma(fh2[v], gg2, rp[v]);
+    };
+#pragma unroll
+    for (int u = 0; u < KU_PF; ++u) load(u, f1[u], f2[u], h1[u], c1[u], h2[u], c2[u]);
+    // branch-free ring (slices past a block's last read 0 and carry h = 0): each step waits
+    // only for its own slice, requested KU_PF steps earlier
     for (int s0 = 0; s0 < nks; s0 += KU_PF) {
 #pragma unroll
         for (int u = 0; u < KU_PF; ++u) {
-            step(f[u], hh[u], gg[u]);
-            load(s0 + u + KU_PF, f[u], hh[u], gg[u]);
+            step(f1[u], f2[u], h1[u], c1[u], h2[u], c2[u], s0 + u);
+            load(s0 + u + KU_PF, f1[u], f2[u], h1[u], c1[u], h2[u], c2[u]);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
 #pragma unroll
-    for (int v = (MODE == 0 ? 0 : NT); v < (MODE == 0 ? NT : NB); ++v) {
+    for (int v = 0; v < NB; ++v) {
         T x = rp[v];
         x += __shfl_xor(x, 16);
         x += __shfl_xor(x, 32);
@@ -2276,28 +2312,27 @@ __device__ __forceinline__ void fu_schur(const Kn &q, const T *Yk, const T *hgl,
     }
 }
 
-// F̃ = Wᵀ G in place (:57; the upper tiles of W read from the wave's LDS image, column-major
-// with leading dimension KF_LU), x = xn − F̃ᵀλ (column layout), X ← Cn − F̃ᵀF̃ (:61)
+// F̃ = Wᵀ G in place (:57; W's upper tiles from the wave's LDS image, column-major with
+// leading dimension KF_LU, each read once: block rows i from the bottom, so G[L] for L ≤ i is
+// still F when row i is formed), x = xn − F̃ᵀλ (column layout), P ← P − F̃ᵀF̃ (:61)
 template <typename T, int NT>
-__device__ __forceinline__ void fu_reduce(acc_t<T> (&X)[10], acc_t<T> (&G)[16], const acc_t<T> (&Cn)[10], const T *Wl,
-                                          const T (&lam)[4][4], const T (&xn)[4], T (&x)[4], int lane)
+__device__ __forceinline__ void fu_reduce(acc_t<T> (&P)[10], acc_t<T> (&G)[16], const T *Wl, const T (&lam)[4][4],
+                                          const T (&xn)[4], T (&x)[4], int lane)
 {
+    (void)lane;
 #pragma unroll
-    for (int i = 0; i < NT; ++i)
+    for (int i = NT - 1; i >= 0; --i) {
+        acc_t<T> acc[NT];
 #pragma unroll
-        for (int j = i; j < NT; ++j) X[up4(i, j)] = tload(Wl + 16 * i + 16 * j * KF_LU, KF_LU, lane);
+        for (int j = 0; j < NT; ++j) acc[j] = tzero<T>();
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-        acc_t<T> Yc[NT];
+        for (int L = 0; L <= i; ++L) {
+            const acc_t<T> w = tload(Wl + 16 * L + 16 * i * KF_LU, KF_LU, lane);
 #pragma unroll
-        for (int L = 0; L < NT; ++L) Yc[L] = G[L * NT + j];
-#pragma unroll
-        for (int i = 0; i < NT; ++i) {
-            acc_t<T> g = tzero<T>();
-#pragma unroll
-            for (int L = 0; L <= i; ++L) g = mtn<T>(X[up4(L, i)], Yc[L], g);
-            G[i * NT + j] = g;
+            for (int j = 0; j < NT; ++j) acc[j] = mtn<T>(w, G[L * NT + j], acc[j]);
         }
+#pragma unroll
+        for (int j = 0; j < NT; ++j) G[i * NT + j] = acc[j];
     }
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
@@ -2314,26 +2349,23 @@ __device__ __forceinline__ void fu_reduce(acc_t<T> (&X)[10], acc_t<T> (&G)[16], 
     for (int i = 0; i < NT; ++i)
 #pragma unroll
         for (int j = i; j < NT; ++j) {
-            acc_t<T> c = Cn[up4(i, j)];
 #pragma unroll
-            for (int L = 0; L < NT; ++L) c = mtn<T, true>(G[L * NT + i], G[L * NT + j], c);
-            X[up4(i, j)] = c;
+            for (int L = 0; L < NT; ++L) P[up4(i, j)] = mtn<T, true>(G[L * NT + i], G[L * NT + j], P[up4(i, j)]);
         }
 }
 
-// shur! of knot kn (F, C, r2 → xn = r2 − y) and the D2 part of knot kn+1 (A into Cn, r1 added
+// shur! of knot kn (F, C, r2 → xn = r2 − y) and the D2 part of knot kn+1 (A into P, r1 added
 // to xn: d_kn = r2 − y + r1 of the next knot, as the image's v)
 template <typename T, int NT, bool FULL>
 __device__ __forceinline__ void fu_stream(const int32_t *meta, int kn, const T *Yt, const T *yt, const T *Ht, const T *gt,
-                                          int hinv, int useg, T *hgl, acc_t<T> (&G)[16], acc_t<T> (&Cn)[10], T (&xn)[4],
+                                          int hinv, int useg, T *hgl, acc_t<T> (&G)[16], acc_t<T> (&P)[10], T (&xn)[4],
                                           int lane)
 {
     const Kn q1 = kn_load(meta, kn), q2 = kn_load(meta, kn + 1);
     T rv[2 * NT];
     fu_stage_hg<T>(hgl, q1, Ht, gt, hinv, useg, lane);
     fu_stage_hg<T>(hgl + 2 * KS_HG, q2, Ht, gt, hinv, useg, lane);
-    fu_schur<T, NT, 1, FULL>(q1, Yt + q1.oY, hgl, G, Cn, rv, lane);
-    fu_schur<T, NT, 0, FULL>(q2, Yt + q2.oY, hgl + 2 * KS_HG, G, Cn, rv, lane);
+    fu_schur2<T, NT, FULL>(q1, Yt + q1.oY, hgl, q2, Yt + q2.oY, hgl + 2 * KS_HG, G, P, rv, lane);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int e = 16 * j + (lane & 15);
@@ -2342,39 +2374,68 @@ __device__ __forceinline__ void fu_stream(const int32_t *meta, int kn, const T *
 }
 
 template <typename T, int NT, bool FULL>
-__global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_fuse_mid_kernel(KuArgs<T> a)
+__global__ void __launch_bounds__(64 * ku_w<T>(), sizeof(T) == 4 ? 8 / ku_w<T>() : 1) kb_fuse_mid_kernel(KuArgs<T> a)
 {
     extern __shared__ __align__(16) unsigned char kb_lds_raw[];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t tl = (int64_t)blockIdx.x * KF_W + wave;
+    constexpr int KU_W = ku_w<T>();
+    const int64_t tl = (int64_t)blockIdx.x * KU_W + wave;
     if (tl >= a.nb) return;                          // whole wave; no workgroup barriers below
+    if constexpr (KU_W == 8 && KU_STAGGER > 0) {
+        // the two waves sharing a SIMD (w, w + 4) run the same program; offset them so that
+        // one's MFMA-dense streaming overlaps the other's latency-bound factorisation
+        if (wave >= 4)
+            for (int i = 0; i < KU_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+    }
     T *U = (T *)kb_lds_raw + wave * KU_LDS, *vb = U + 64 * KF_LU, *hgl = vb + 64;
     const int64_t t = a.b0 + tl, ty = a.yrel ? tl : t;
     const T *Yt = a.Y + ty * a.sY, *yt = a.y + t * a.sy, *Ht = a.H + t * a.sH, *gt = a.g + ty * a.sg;
     T *St = a.slab + tl * a.sS;
     constexpr int PP = 16 * NT;
     int64_t oS = slab_before(a.meta, a.kb);
-    acc_t<T> X[10], G[16], Cn[10];
-    T lam[4][4], x[4], xn[4];
+    acc_t<T> G[16], P[10];                           // P: pivot tiles; W_k after the factor
+    T lam[4][4], x[4], xn[4], lcol[4];               // λ in row layout, or (KU_LEAN) column layout
     {
         // the state at kb − 1 (W_{kb−1}, λ_{kb−1}, left in the slab by the general kernel)
         // into the LDS W image the reduction reads
         const int32_t *m = a.meta + 8 * (a.kb - 1);
-        kf_resume<T>(X, lam, St + oS - slab_size(r16(m[1]), r16(m[2])), r16(m[2]), r16(m[1]), NT, lane);
+        kf_resume<T>(P, lam, St + oS - slab_size(r16(m[1]), r16(m[2])), r16(m[2]), r16(m[1]), NT, lane);
+        if constexpr (KU_LEAN) {
+            const T *Sk = St + oS - slab_size(r16(m[1]), r16(m[2]));
+            const int P2 = r16(m[2]), Ps = r16(m[1]);
+            const int oM = P2 * (P2 + 1) / 2 + Ps * (Ps + 1) / 2 + Ps * P2;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int e = 16 * j + (lane & 15);
+                lcol[j] = e < P2 ? Sk[oM + Ps + e] : (T)0;
+            }
+        }
 #pragma unroll
         for (int i = 0; i < NT; ++i)
 #pragma unroll
-            for (int j = i; j < NT; ++j) tstore(U + 16 * i + 16 * j * KF_LU, KF_LU, X[up4(i, j)], lane);
+            for (int j = i; j < NT; ++j) tstore(U + 16 * i + 16 * j * KF_LU, KF_LU, P[up4(i, j)], lane);
     }
-    // prologue: knot kb's F, C, d and knot kb+1's A; then F̃_kb, x_kb, X = C_kb + A_{kb+1} − F̃ᵀF̃
-    fu_stream<T, NT, FULL>(a.meta, a.kb, Yt, yt, Ht, gt, a.hinv, a.useg, hgl, G, Cn, xn, lane);
+    // prologue: knot kb's F, C, d and knot kb+1's A; then F̃_kb, x_kb, P = C_kb + A_{kb+1} − F̃ᵀF̃
+    fu_stream<T, NT, FULL>(a.meta, a.kb, Yt, yt, Ht, gt, a.hinv, a.useg, hgl, G, P, xn, lane);
     wsync();
-    fu_reduce<T, NT>(X, G, Cn, U, lam, xn, x, lane);
+    if constexpr (KU_LEAN) col2row<T>(lam, lcol, vb, lane);
+    fu_reduce<T, NT>(P, G, U, lam, xn, x, lane);
     int info = 0;
+#ifdef KB_PROF
+    int64_t kb_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    KB_T0();
+#endif
     for (int k = a.kb; k < a.ke; ++k) {
         const int p2 = a.meta[8 * k + 2];
-        // C̃_k = chol(X) → X = W_k (:61-62)
-        const int bad = chol_inv_reg<T>(X, NT, p2, U, hgl, lane);
+        // C̃_k = chol(P) → P = W_k (:61-62)
+        if constexpr (KU_PRIO) __builtin_amdgcn_s_setprio(2);
+#ifdef KU_NOCHOL
+        const int bad = 0;         // timing ablation only: no factorisation (wrong results)
+        (void)p2;
+#else
+        const int bad = chol_inv_reg<T>(P, NT, p2, U, hgl, lane);
+#endif
+        KB_T(0);
         // λ_k = W_kᵀ x_k (:108-116)
         T xr[4][4], lc[4];
         col2row<T>(xr, x, vb, lane);
@@ -2385,13 +2446,18 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_fuse_mid
 #pragma unroll
                 for (int i = 0; i <= j; ++i)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) sacc = fma(X[up4(i, j)][r], xr[i][r], sacc);
+                    for (int r = 0; r < 4; ++r) sacc = fma(P[up4(i, j)][r], xr[i][r], sacc);
             }
             sacc += __shfl_xor(sacc, 16);
             sacc += __shfl_xor(sacc, 32);
             lc[j] = sacc;
         }
-        col2row<T>(lam, lc, vb, lane);
+        if constexpr (KU_LEAN) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) lcol[j] = lc[j];
+        } else {
+            col2row<T>(lam, lc, vb, lane);
+        }
         // slab: W_k packed upper (column col at col(col+1)/2: the off-diagonal tiles store
         // unpredicated at a per-lane column base plus immediates; only the diagonal tiles test
         // row ≤ col, the same four lane masks for every tile), λ_k
@@ -2405,10 +2471,10 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_fuse_mid
 #pragma unroll
                 for (int i = 0; i < j; ++i)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) cb[16 * i + Tile<T>::row(lane, r)] = X[up4(i, j)][r];
+                    for (int r = 0; r < 4; ++r) cb[16 * i + Tile<T>::row(lane, r)] = P[up4(i, j)][r];
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    if (Tile<T>::row(lane, r) <= c) cb[16 * j + Tile<T>::row(lane, r)] = X[up4(j, j)][r];
+                    if (Tile<T>::row(lane, r) <= c) cb[16 * j + Tile<T>::row(lane, r)] = P[up4(j, j)][r];
             }
         }
         if (lane < 16) {
@@ -2416,19 +2482,25 @@ __global__ void __launch_bounds__(64 * KF_W, sizeof(T) == 4 ? 2 : 1) kb_fuse_mid
             for (int j = 0; j < NT; ++j) Sk[PP * (PP + 1) / 2 + 16 * j + lane] = lc[j];
         }
         if (bad && !info) info = k + 1;
+        if constexpr (KU_PRIO) __builtin_amdgcn_s_setprio(0);
+        KB_T(1);
         if (k + 1 < a.ke) {
             // W_k to the LDS image (chol_inv_reg's scratch is free again): no tile is live
-            // across the streaming but G and Cn
+            // across the streaming but G and P (zeroed there)
             wsync();
 #pragma unroll
             for (int i = 0; i < NT; ++i)
 #pragma unroll
-                for (int j = i; j < NT; ++j) tstore(U + 16 * i + 16 * j * KF_LU, KF_LU, X[up4(i, j)], lane);
-            fu_stream<T, NT, FULL>(a.meta, k + 1, Yt, yt, Ht, gt, a.hinv, a.useg, hgl, G, Cn, xn, lane);
+                for (int j = i; j < NT; ++j) tstore(U + 16 * i + 16 * j * KF_LU, KF_LU, P[up4(i, j)], lane);
+            fu_stream<T, NT, FULL>(a.meta, k + 1, Yt, yt, Ht, gt, a.hinv, a.useg, hgl, G, P, xn, lane);
             wsync();
-            fu_reduce<T, NT>(X, G, Cn, U, lam, xn, x, lane);
+            KB_T(2);
+            if constexpr (KU_LEAN) col2row<T>(lam, lcol, vb, lane);
+            fu_reduce<T, NT>(P, G, U, lam, xn, x, lane);
+            KB_T(3);
         }
     }
+    KB_FLUSH();
     if (lane == 0) kf_info(a.info, t, info, a.kb, a.hfac);
 }
 
@@ -2918,7 +2990,12 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
         kf.fz1 = P.fuse ? P.mid1 : 0;
     }
     KuArgs<T> ku{};
-    const size_t lfu = (size_t)KF_W * KU_LDS * sizeof(T);
+    constexpr int KU_W = ku_w<T>();
+#ifdef KU_SOLO
+    const size_t lfu = std::max((size_t)KU_W * KU_LDS * sizeof(T), (size_t)96 * 1024);   // 1 WG per CU (A/B only)
+#else
+    const size_t lfu = (size_t)KU_W * KU_LDS * sizeof(T);
+#endif
     if (P.fuse) {
         ku.Y = P.hfac ? Z : (const T *)a.Y; ku.y = (const T *)a.y; ku.H = (const T *)a.H;
         ku.g = P.hfac ? gz : (const T *)a.g;
@@ -2959,6 +3036,7 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
     if (!prof) (void)hipMalloc((void **)&prof, 64 * sizeof(int64_t));
     (void)hipMemsetAsync(prof, 0, 64 * sizeof(int64_t), s);
     k.prof = prof;
+    ku.prof = prof;
 #endif
     for (int64_t b0 = 0; b0 < a.batch && e == hipSuccess; b0 += chunk) {
         const int64_t nb = std::min<int64_t>(chunk, a.batch - b0);
@@ -2989,10 +3067,11 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
                 generic(0, P.mid0);
                 ku.b0 = b0;
                 ku.nb = nb;
+                const dim3 gu((unsigned)((nb + KU_W - 1) / KU_W)), bu(64 * KU_W);
                 switch (P.midnt * 2 + (P.midfull ? 1 : 0)) {
-#define KU_L_(NT_, F_) case NT_ * 2 + F_: hipLaunchKernelGGL((kb_fuse_mid_kernel<T, NT_, F_ != 0>), gf, bf, lfu, s, ku); break;
+#define KU_L_(NT_, F_) case NT_ * 2 + F_: hipLaunchKernelGGL((kb_fuse_mid_kernel<T, NT_, F_ != 0>), gu, bu, lfu, s, ku); break;
                 KU_L_(1, 0) KU_L_(1, 1) KU_L_(2, 0) KU_L_(2, 1) KU_L_(3, 0) KU_L_(3, 1) KU_L_(4, 0)
-                default: hipLaunchKernelGGL((kb_fuse_mid_kernel<T, 4, true>), gf, bf, lfu, s, ku); break;
+                default: hipLaunchKernelGGL((kb_fuse_mid_kernel<T, 4, true>), gu, bu, lfu, s, ku); break;
 #undef KU_L_
                 }
                 generic(P.mid1, a.N);
@@ -3025,6 +3104,16 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
         (void)hipStreamSynchronize(s);
         (void)hipMemcpy(h, prof, sizeof h, hipMemcpyDeviceToHost);
         const double steps = (double)a.batch * (a.N + 2);
+        if (P.fuse) {
+            const double kn = (double)a.batch * (P.mid1 - P.mid0);   // wave-knots
+            std::fprintf(stderr, "KB_PROF fused kernel, cycles per knot and wave [chol+inv | lambda+slab | stream | reduce]:");
+            for (int i = 0; i < 4; ++i) {
+                double sum = 0;
+                for (int w = 0; w < 4; ++w) sum += (double)h[16 * w + i];
+                std::fprintf(stderr, " %9.0f", sum / kn);
+            }
+            std::fprintf(stderr, "\n");
+        }
         std::fprintf(stderr, "KB_PROF cycles per step and wave [prefactor factor schur barrier handover | "
                              "F: cholB+E cholC fwdsubst slab Wcopy]:\n");
         for (int w = 0; w < 4; ++w) {
