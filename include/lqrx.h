@@ -41,7 +41,8 @@ extern "C" {
 #define LQRX_ABI_VERSION 4   /* 2: layout 1 (DP, KKT), lqrx_sqp_* (models, stage constraints);
                                 3: lqrx_dp_solve_linear[_host] (linear cost terms), and
                                    dtype LQRX_F32 on the KKT path (large-block kernels);
-                                4: lqrx_scratch_trim (release the library's pooled scratch) */
+                                4: lqrx_scratch_trim (release the library's pooled scratch);
+                                   KKT blocks past 64 rows (up to 512, w up to 1024) */
 
 #define LQRX_F64 0
 #define LQRX_F32 1
@@ -162,9 +163,12 @@ int lqrx_dp_solve_linear_host(const lqrx_dp_desc *desc, const void *A, const voi
  * ------------------------------------------------------------------------------------ */
 typedef struct lqrx_kkt_desc {
     int32_t N;          /* knots                                                  */
-    int32_t dtype;      /* LQRX_F64 (every KKT kernel) or LQRX_F32 (the large-block
-                           MFMA kernels: n1, p, n2 <= 64, padded rows <= 128, w <= 128,
-                           layout 0, every h_mode and ginv; else LQRX_ERR_UNSUPPORTED) */
+    int32_t dtype;      /* LQRX_F64 (every KKT kernel) or LQRX_F32 (layout 0: the
+                           large-block MFMA kernels for n1, p, n2 <= 64, padded rows
+                           <= 128, w <= 128, and the workgroup-per-trajectory kernel
+                           past them; every h_mode and ginv; else
+                           LQRX_ERR_UNSUPPORTED).  Every knot: n1, p, n2 <= 512 and
+                           w <= 1024 (LQRX_ERR_UNSUPPORTED past that)               */
     int64_t batch;
     const int32_t *n1;  /* [N] host arrays describing the block structure           */
     const int32_t *p;   /* [N]                                                      */

@@ -199,8 +199,9 @@ function kkt_solve!(dz::Matrix{T}, lam::Matrix{T}, info::Vector{Int32},
                     n1::Vector{Int32}, p::Vector{Int32}, n2::Vector{Int32}, w::Vector{Int32},
                     Y::Matrix{T}, y::Matrix{T}, H::Matrix{T}, g::Matrix{T};
                     h_mode::Integer=2, ginv::Integer=1) where {T<:Union{Float64,Float32}}
-    # Float32 runs the large-block MFMA kernels (blocks up to 64 rows, w up to 128; dense,
-    # block-diagonal or diagonal H, and ginv = 0) — BASELINE configs[4]'s banded KKT
+    # Float32 runs the large-block MFMA kernels (blocks up to 64 rows, w up to 128 —
+    # BASELINE configs[4]'s banded KKT) and the workgroup-per-trajectory kernel past them;
+    # every H mode and ginv, blocks up to 512 rows and w up to 1024 in either precision
     batch = size(Y, 2)
     GC.@preserve n1 p n2 w Y y H g dz lam info begin
         d = Ref(KktDesc(length(n1), dtypecode(T), batch, pointer(n1), pointer(p), pointer(n2), pointer(w),

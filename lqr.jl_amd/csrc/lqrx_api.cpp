@@ -392,9 +392,10 @@ int kkt_layout(const lqrx_kkt_desc *d, KktLayout &L)
             return set_err(-1, "knot %d: n1 (%d) != n2 of knot %d (%d)", k, n1, k - 1, d->n2[k - 1]);
         if (k == d->N - 1 && n2 != 0) return set_err(-1, "last knot must have n2 == 0");
         int rows = n1 + p + n2;
-        if (n1 > 64 || p > 64 || n2 > 64 || w > 128)
-            return set_err(LQRX_ERR_UNSUPPORTED, "knot %d: block (n1 %d, p %d, n2 %d, w %d) past 64 rows per "
-                                                 "part / 128 columns", k, n1, p, n2, w);
+        if (n1 > lqrx::KW_MAX_BLOCK || p > lqrx::KW_MAX_BLOCK || n2 > lqrx::KW_MAX_BLOCK || w > lqrx::KW_MAX_W)
+            return set_err(LQRX_ERR_UNSUPPORTED, "knot %d: block (n1 %d, p %d, n2 %d, w %d) past %d rows per "
+                                                 "part / %d columns", k, n1, p, n2, w, lqrx::KW_MAX_BLOCK,
+                           lqrx::KW_MAX_W);
         int32_t *m = &L.meta[(size_t)k * 8];
         m[0] = n1; m[1] = p; m[2] = n2; m[3] = w;
         m[4] = (int32_t)L.sY; m[5] = (int32_t)L.sy; m[6] = (int32_t)L.sH; m[7] = (int32_t)L.sg;
@@ -501,20 +502,29 @@ lqrx::KktArgs kkt_args(const lqrx_kkt_desc *d, const KktLayout &L)
     a.dtype = d->dtype == LQRX_F32 ? 1 : 0;
     return a;
 }
-// Kernel family for a call.  fp32: the large-block MFMA kernels only.  fp64: the
-// compile-time shapes (FIL) first, then the LDS-staged / small lane generic kernels, then the
-// large-block kernels (which also replace the scratch-spilling lane<8,8,8,12,16> kernel);
-// LQRX_KKT_BIG=1 forces the large-block kernels wherever they apply, =0 never uses them.
-enum { KK_NONE = 0, KK_FIL, KK_GENERIC, KK_BIG };
+// Kernel family for a call.  fp32: the large-block MFMA kernels, past them the
+// workgroup-per-trajectory kernel.  fp64: the compile-time shapes (FIL) first, then the
+// LDS-staged / small lane generic kernels, then the large-block kernels (which also replace the
+// scratch-spilling lane<8,8,8,12,16> kernel), then the workgroup-per-trajectory kernel (blocks
+// past 64 rows / w past 128).  LQRX_KKT_BIG=1 forces the large-block kernels wherever they
+// apply, =0 never uses them; LQRX_KKT_WG=1 forces the workgroup kernel (layout 0; A/B tests).
+enum { KK_NONE = 0, KK_FIL, KK_GENERIC, KK_BIG, KK_WG };
 int kkt_big_env()
 {
     static const int v = [] { const char *e = std::getenv("LQRX_KKT_BIG"); return e && *e ? std::atoi(e) : -1; }();
     return v;
 }
+int kkt_wg_env()
+{
+    static const int v = [] { const char *e = std::getenv("LQRX_KKT_WG"); return e && *e == '1' ? 1 : 0; }();
+    return v;
+}
 int kkt_route(const lqrx_kkt_desc *d, const lqrx::KktArgs &a)
 {
+    const bool wgk = lqrx::kkt_wg_supported(a, d->n1, d->p, d->n2, d->w);
+    if (kkt_wg_env() && wgk) return KK_WG;
     const bool big = kkt_big_env() != 0 && lqrx::kkt_big_supported(a, d->n1, d->p, d->n2, d->w);
-    if (d->dtype == LQRX_F32) return big ? KK_BIG : KK_NONE;
+    if (d->dtype == LQRX_F32) return big ? KK_BIG : wgk ? KK_WG : KK_NONE;
     if (kkt_big_env() == 1 && big) return KK_BIG;
     size_t b = 0;
     const bool fil = !a.force_lane && !kkt_force_generic() && lqrx::kkt_fil_scratch_bytes(a, d->n1, d->p, d->n2, d->w, &b);
@@ -522,7 +532,7 @@ int kkt_route(const lqrx_kkt_desc *d, const lqrx::KktArgs &a)
     if (fil) return KK_FIL;
     const int gc = lqrx::kkt_generic_class(a);
     if (gc == 1 || gc == 2 || (gc == 3 && (!big || a.force_lane))) return KK_GENERIC;
-    return big ? KK_BIG : KK_NONE;
+    return big ? KK_BIG : wgk ? KK_WG : KK_NONE;
 }
 // LQRX_KKT_GENERIC=1 forces the generic (runtime-shaped) kernel, for A/B checks
 bool kkt_force_generic()
@@ -538,6 +548,7 @@ size_t kkt_ws_bytes(const lqrx_kkt_desc *d, const lqrx::KktArgs &a, int route)
     switch (route) {
     case KK_FIL: (void)lqrx::kkt_fil_scratch_bytes(a, d->n1, d->p, d->n2, d->w, &b); return b;
     case KK_BIG: return lqrx::kkt_big_scratch_bytes(a, d->n1, d->p, d->n2, d->w);
+    case KK_WG: return lqrx::kkt_wg_scratch_bytes(a, d->n1, d->p, d->n2, d->w);
     case KK_GENERIC: return lqrx::kkt_scratch_bytes(a);
     default: return 0;
     }
@@ -623,12 +634,13 @@ int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const v
         if (d->layout == 1)
             return set_err(LQRX_ERR_UNSUPPORTED, "layout 1 needs a compile-time KKT shape (Dubins; cartpole, "
                                                  "DoubleIntegrator(2|3) with diagonal H) and N >= 4");
-        return set_err(LQRX_ERR_UNSUPPORTED, "no KKT kernel for this structure / options (%s; the large-block "
-                                             "kernels need n1, p, n2 <= 64, padded rows <= 128, w <= 128 and "
-                                             "layout 0; every h_mode and ginv is served)",
-                       d->dtype == LQRX_F32 ? "fp32" : "fp64");
+        return set_err(LQRX_ERR_UNSUPPORTED, "no KKT kernel for this structure / options (%s; layout 0 serves "
+                                             "every structure with blocks <= %d rows and w <= %d, every h_mode "
+                                             "and ginv)",
+                       d->dtype == LQRX_F32 ? "fp32" : "fp64", lqrx::KW_MAX_BLOCK, lqrx::KW_MAX_W);
     }
     if (route == KK_BIG) e = lqrx::kkt_big_launch(a, d->n1, d->p, d->n2, d->w, s);
+    else if (route == KK_WG) e = lqrx::kkt_wg_launch(a, d->n1, d->p, d->n2, d->w, s);
     else if (route == KK_GENERIC || !lqrx::kkt_fil_launch(a, d->n1, d->p, d->n2, d->w, s, &e))
         e = lqrx::kkt_launch(a, s);
     if (debug_meta) {   // read the table back before a per-call table is released

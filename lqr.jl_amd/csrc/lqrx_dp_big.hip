@@ -9,10 +9,11 @@
 // products is kept — PB = P·B, E = R + BᵀPB, PA = P·A, K = BᵀPA, potrf 'U' (left-looking, as
 // dpotf2), potrs, APB = AᵀPB, P_ = Q + AᵀPA − APB·K (no symmetric fast form) — the products on
 // fp64/fp32 MFMA tiles (wg_mm: the 4 waves take output tiles round-robin and stream strided
-// operand tiles from L2), the factor, the triangular solves and the rollout on the VALU.
+// operand tiles from L2; lqrx_wg.h), the factor, the triangular solves and the rollout on the VALU.
 // Time-varying knot strides, all-P output, linear cost terms (d, p) as in the other kernels.
 #include "lqrx_internal.h"
 #include "lqrx_tile.h"
+#include "lqrx_wg.h"
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -21,70 +22,10 @@ namespace lqrx {
 
 namespace {
 
-constexpr int BT = 256;
+using wg::BT;
+using wg::Mat;
 
 template <typename T> __device__ __forceinline__ T dsqrt(T x) { return sqrt(x); }
-
-// One 16×16 MFMA C-layout tile of a matrix with general strides: element (row, col) at
-// src[row·rs + col·cs] (column-major: rs = 1, cs = ld; its transpose: rs = ld, cs = 1);
-// zero outside rows × cols.
-template <typename T>
-__device__ __forceinline__ void tile_ld(typename Tile<T>::acc &t, const T *src, int rows, int cols, size_t rs,
-                                        size_t cs, int lane)
-{
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int row = Tile<T>::row(lane, r), col = tcol(lane);
-        const bool ok = row < rows && col < cols;
-        t[r] = ok ? src[(size_t)row * rs + (size_t)col * cs] : (T)0;
-    }
-}
-
-// Strided operand view: element (i, j) at p[i·rs + j·cs]
-template <typename T> struct Mat {
-    const T *p;
-    size_t rs, cs;
-    __device__ const T *at(int i, int j) const { return p + (size_t)i * rs + (size_t)j * cs; }
-};
-
-// Workgroup product on the MFMA pipe: C (r×c, column-major, ldc) = [Cin +] M1ᵀ·Y1 [− M2ᵀ·Y2],
-// M1 kk1×r, Y1 kk1×c (M2 kk2×r, Y2 kk2×c); the 4 waves take the 16×16 output tiles round-robin
-// and stream the k-tiles of their operands from L2 (the per-trajectory scratch / inputs).
-template <typename T, bool SUB>
-__device__ __forceinline__ void wg_mm(T *C, int ldc, int r, int c, const T *Cin, Mat<T> M1, Mat<T> Y1, int kk1,
-                                      Mat<T> M2, Mat<T> Y2, int kk2, int tid)
-{
-    using acc = typename Tile<T>::acc;
-    const int wave = tid >> 6, lane = tid & 63;
-    const int RT = (r + 15) / 16, CT = (c + 15) / 16;
-    for (int ot = wave; ot < RT * CT; ot += BT / 64) {
-        const int it = ot % RT, jt = ot / RT;
-        acc D;
-        if (Cin) tile_ld<T>(D, Cin + it * 16 + (size_t)jt * 16 * ldc, r - it * 16, c - jt * 16, 1, ldc, lane);
-        else D = acc{0, 0, 0, 0};
-        for (int kt = 0; kt < (kk1 + 15) / 16; ++kt) {
-            acc Mt, Yt;
-            tile_ld<T>(Mt, M1.at(kt * 16, it * 16), kk1 - kt * 16, r - it * 16, M1.rs, M1.cs, lane);
-            tile_ld<T>(Yt, Y1.at(kt * 16, jt * 16), kk1 - kt * 16, c - jt * 16, Y1.rs, Y1.cs, lane);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) D = Tile<T>::mma(Mt[q], Yt[q], D);
-        }
-        if constexpr (SUB) {
-            for (int kt = 0; kt < (kk2 + 15) / 16; ++kt) {
-                acc Mt, Yt;
-                tile_ld<T>(Mt, M2.at(kt * 16, it * 16), kk2 - kt * 16, r - it * 16, M2.rs, M2.cs, lane);
-                tile_ld<T>(Yt, Y2.at(kt * 16, jt * 16), kk2 - kt * 16, c - jt * 16, Y2.rs, Y2.cs, lane);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) D = Tile<T>::mma_nega(Mt[q], Yt[q], D);
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int row = it * 16 + Tile<T>::row(lane, q), col = jt * 16 + tcol(lane);
-            if (row < r && col < c) C[row + (size_t)col * ldc] = D[q];
-        }
-    }
-}
 
 template <typename T>
 __global__ __launch_bounds__(BT) void dp_big_kernel(const DpArgs a, T *__restrict__ ws, size_t ws_elems, int64_t b0)
@@ -136,8 +77,8 @@ __global__ __launch_bounds__(BT) void dp_big_kernel(const DpArgs a, T *__restric
         T *K = Kb + (size_t)(k - 1) * nm;
         const Mat<T> Pt{P, (size_t)n, 1}, Am{A, 1, (size_t)n}, Bm{B, 1, (size_t)n}, none{nullptr, 0, 0};
         // :38 PB = P*B  (= (Pᵀ)ᵀ·B) ; :40 PA = P*A
-        wg_mm<T, false>(PB, n, n, m, nullptr, Pt, Bm, n, none, none, 0, tid);
-        wg_mm<T, false>(PA, n, n, n, nullptr, Pt, Am, n, none, none, 0, tid);
+        wg::wg_mm<T, 1, 1>(PB, n, n, m, nullptr, Pt, Bm, n, none, none, 0, tid);
+        wg::wg_mm<T, 1, 1>(PA, n, n, n, nullptr, Pt, Am, n, none, none, 0, tid);
         if (lin) {                                              // w = r + B'p
             const T *r = (const T *)a.r + b * m * kQR + (size_t)(k - 1) * sr;
             for (int c = tid; c < m; c += BT) {
@@ -149,9 +90,9 @@ __global__ __launch_bounds__(BT) void dp_big_kernel(const DpArgs a, T *__restric
         __syncthreads();
         // :39 E = R + B'PB ; :41 K = B'PA ; :50 APB = A'PB
         const Mat<T> PBm{PB, 1, (size_t)n}, PAm{PA, 1, (size_t)n};
-        wg_mm<T, false>(E, m, m, m, R, Bm, PBm, n, none, none, 0, tid);
-        wg_mm<T, false>(K, m, m, n, nullptr, Bm, PAm, n, none, none, 0, tid);
-        wg_mm<T, false>(APB, n, n, m, nullptr, Am, PBm, n, none, none, 0, tid);
+        wg::wg_mm<T, 1, 1>(E, m, m, m, R, Bm, PBm, n, none, none, 0, tid);
+        wg::wg_mm<T, 1, 1>(K, m, m, n, nullptr, Bm, PAm, n, none, none, 0, tid);
+        wg::wg_mm<T, 1, 1>(APB, n, n, m, nullptr, Am, PBm, n, none, none, 0, tid);
         __syncthreads();
         // :29 potrf!('U', E) — left-looking dpotf2; a failed pivot stops the factor (as LAPACK)
         bool failed = false;
@@ -200,7 +141,7 @@ __global__ __launch_bounds__(BT) void dp_big_kernel(const DpArgs a, T *__restric
         // :51 P_ = Q + A'PA − APB*K  (APB·K = (APBᵀ)ᵀ·K)   (and p_ = q + A'p − APB*d)
         {
             const Mat<T> APBt{APB, (size_t)n, 1}, Km{K, 1, (size_t)m};
-            wg_mm<T, true>(Pn, n, n, n, Q, Am, PAm, n, APBt, Km, m, tid);
+            wg::wg_mm<T, 1, -1>(Pn, n, n, n, Q, Am, PAm, n, APBt, Km, m, tid);
         }
         if (lin) {
             const T *q = (const T *)a.q + b * n * kQR + (size_t)(k - 1) * sq;

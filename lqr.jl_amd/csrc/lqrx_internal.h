@@ -106,6 +106,15 @@ size_t kkt_big_scratch_bytes(const KktArgs &a, const int32_t *n1, const int32_t 
 hipError_t kkt_big_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
                           const int32_t *w, hipStream_t s);
 
+// workgroup-per-trajectory KKT kernel (lqrx_kkt_wg.hip): the structures past the large-block
+// kernels (any block > 64 rows or w > 128), every h_mode / ginv, layout 0, fp64 or fp32
+constexpr int KW_MAX_BLOCK = 512, KW_MAX_W = 1024;
+bool kkt_wg_supported(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2, const int32_t *w);
+size_t kkt_wg_scratch_bytes(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
+                            const int32_t *w);
+hipError_t kkt_wg_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
+                         const int32_t *w, hipStream_t s);
+
 // ---- batched trajectory SQP (lqrx_sqp.hip) ----
 enum { SQP_DUBINS = 0, SQP_CARTPOLE = 1, SQP_DI1 = 2, SQP_DI2 = 3, SQP_DI3 = 4 };   // = LQRX_MODEL_*
 struct SqpArgs {

@@ -2512,8 +2512,12 @@ __global__ void __launch_bounds__(64 * ku_w<T>(), sizeof(T) == 4 ? 8 / ku_w<T>()
 // of its column) and lane = row for Y-products (v: coalesced columns); the multipliers pass
 // between lanes through a small per-wave LDS vector area.  Bound by the bytes of Y (read
 // once per knot; the D2 rows a second time, from L2).
-constexpr int KBW_V = 8 * 64;     // per-wave LDS vector elements
-constexpr int KBW_W = 2080 + 64;  // per-wave LDS image of the packed W (≤ 64×65/2)
+// per-wave LDS: vectors x (128), t (128), v, z (= e), λ (64 each), then the packed W image
+// (≤ 64×65/2).  2528 elements: four waves per 40 KB (fp32) workgroup, 4 workgroups (16 waves)
+// per CU; fp64 2 workgroups per CU.  (At 2656 elements LDS held fp32 to 12 waves per CU —
+// configs[4]'s 8192 waves took 3 rounds instead of 2 — and fp64 to 4.)
+constexpr int KBW_V = 7 * 64;
+constexpr int KBW_W = 2080;
 #ifndef KBW_VC_COLS
 #define KBW_VC_COLS 16
 #endif
@@ -2569,7 +2573,8 @@ __global__ void __launch_bounds__(64 * KF_W) kb_bwd_kernel(KbArgs<T> a, int64_t 
     if (tl >= nb) return;
     constexpr int V = 16 / sizeof(T);
     T *xb = (T *)kb_lds_raw + wave * (KBW_V + KBW_W);  // x = [μ_j; λ_j] in Y's row order past D2
-    T *tb = xb + 128, *vb = tb + 128, *zb = vb + 64, *lb = zb + 64, *eb = lb + 64, *wl = xb + KBW_V;
+    // eb (μ − Ẽλ) reuses zb: z is dead once λ = W z is formed (a wave barrier between)
+    T *tb = xb + 128, *vb = tb + 128, *zb = vb + 64, *lb = zb + 64, *eb = zb, *wl = xb + KBW_V;
     const int64_t t = a.b0 + tl, ty = a.yrel ? tl : t;
     const T *Yt = a.Y + ty * a.sY, *Ht = a.H + t * a.sH, *gt = a.g + ty * a.sg;
     T *dzt = a.dz + t * a.sg, *lat = a.lam + t * a.sy;
@@ -2969,7 +2974,9 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
                     (e = hipFuncSetAttribute((const void *)kb_factor_mid_kernel<T, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfac)) != hipSuccess ||
                     (e = hipFuncSetAttribute((const void *)kb_factor_mid_kernel<T, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfac)) != hipSuccess ||
                     (e = hipFuncSetAttribute((const void *)kb_factor_mid_kernel<T, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfac)) != hipSuccess ||
-                    (e = hipFuncSetAttribute((const void *)kb_factor_mid_kernel<T, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfac)) != hipSuccess)) {
+                    (e = hipFuncSetAttribute((const void *)kb_factor_mid_kernel<T, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfac)) != hipSuccess ||
+                    (e = hipFuncSetAttribute((const void *)kb_bwd_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)((size_t)KF_W * (KBW_V + KBW_W) * sizeof(T)))) != hipSuccess)) {
         (void)sc.release(s);
         return e;
     }

@@ -220,3 +220,21 @@ def test_constraint_block_dims(lqrx):
         assert (rows[0], w[0]) == (2 * n, n + m)
         assert (rows[-1], w[-1]) == (2 * n, n)
         assert all(rows[k] == 2 * n + st.p[k] and w[k] == n + m for k in range(1, N - 1))
+
+
+def test_kkt_blocks_past_64_accepted(lqrx):
+    """Blocks past the large-block kernels (n = 96: 96-row blocks, w = 144) route to the
+    workgroup-per-trajectory kernel in fp64 and fp32 (a positive workspace size, no GPU call);
+    past 512 rows the validation returns LQRX_ERR_UNSUPPORTED."""
+    import lqrx.kkt as K
+    from lqrx import _lib
+
+    lib = lqrx.load()
+    st = K.trajectory_structure(96, 48, 64)
+    for code in (_lib.F64, _lib.F32):
+        n = C.c_size_t(0)
+        assert lib.lqrx_kkt_workspace_size(C.byref(st.desc(8, K.H_DIAG, 1, 0, code)), C.byref(n)) == 0
+        assert n.value > 0
+    n = C.c_size_t(0)
+    big = K.trajectory_structure(513, 4, 3)
+    assert lib.lqrx_kkt_workspace_size(C.byref(big.desc(2, K.H_DIAG, 1, 0, _lib.F64)), C.byref(n)) == -101
