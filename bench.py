@@ -49,10 +49,13 @@ def dp_bytes_per_traj(n, m, N, s=8, tv=False):
     return rd * s + ((N - 1) * m * n + N * n + (N - 1) * m + n * n) * s
 
 
-def _dp_kernel_name(n, m, bt, tv):
+def _dp_kernel_name(n, m, bt, tv, lin=False):
     """Which DP kernel lqrx_dp_solve dispatches to (mirrors dp_launch / dp_lane_launch)."""
     if n <= 4 and m <= 4:
         small = os.environ.get("LQRX_DP_SMALL", "")
+        hex_ = not tv and not lin and (small.startswith("h") or (not small[:1] in ("l", "q") and bt <= 8192))
+        if hex_:
+            return "dp_hex_kernel"
         quad = n >= 3 and not tv and (small.startswith("q") or (not small.startswith("l") and bt <= 16384))
         return "dp_quad_kernel" if quad else "dp_lane_kernel"
     if n > 64 or m > 32:
@@ -792,21 +795,22 @@ def main(argv=None):
                         "fp64_tflops": achieved, "fp64_frac": achieved / peak}
             elif n <= 4 and m <= 4:
                 # n ≤ 4 (cfg2 cartpole): AI ≈ 6 flop/B is below the ridge, so the roofline is
-                # HBM — but the launch is latency-bound: 4 (quad) or 1 (lane) lanes per
-                # trajectory give B·lanes/64 waves, at most one per CU for B ≤ 16384, each
-                # running a serial N-knot chain; report that beside the HBM fraction
+                # HBM — but the launch is latency-bound: 16 (hex), 4 (quad) or 1 (lane) lanes
+                # per trajectory give B·lanes/64 waves (cfg2: 1024 = one per SIMD with hex),
+                # each running a serial N-knot chain; report that beside the HBM fraction
                 ab = dp_bytes_per_traj(n, m, N, 8 if f64 else 4, False) * bt
                 hbm = ab / (kern_ms * 1e-3) / 1e9
-                kname = _dp_kernel_name(n, m, bt, False)
-                waves = -(-bt * (4 if kname == "dp_quad_kernel" else 1) // 64)
+                kname = _dp_kernel_name(n, m, bt, False, args.linear)
+                lanes = {"dp_hex_kernel": 16, "dp_quad_kernel": 4}.get(kname, 1)
+                waves = -(-bt * lanes // 64)
                 roof = {"bound": "hbm", "achieved": hbm, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": hbm / PEAK_HBM_GBS, "traffic": traffic, "kernel": kname,
                         "kernel_ms": kern_ms, "alg_bytes_per_launch": ab,
                         "fp64_tflops": achieved, "fp64_frac": achieved / peak,
                         "latency_bound": {"waves": waves, "cus": 256, "waves_per_cu": waves / 256,
                                           "knot_chain_us": kern_ms * 1e3 / N,
-                                          "note": "one serial N-knot chain per wave; the chip holds "
-                                                  "the whole batch at <= 1 wave per CU"}}
+                                          "note": "one serial N-knot chain per trajectory; the chip "
+                                                  "holds the whole batch at once"}}
             headline = (n, m, N, bt, args.dtype) == (32, 16, 256, 65536, "f64") and not args.tv \
                 and not args.linear
             if args.workload == "cartpole":

@@ -42,7 +42,9 @@ extern "C" {
                                 3: lqrx_dp_solve_linear[_host] (linear cost terms), and
                                    dtype LQRX_F32 on the KKT path (large-block kernels);
                                 4: lqrx_scratch_trim (release the library's pooled scratch);
-                                   KKT blocks past 64 rows (up to 512, w up to 1024) */
+                                   KKT blocks past 64 rows (up to 512, w up to 1024);
+                                   KKT layout 1 for every structure (staged);
+                                   lqrx_dp_compute_ctg[_host] (per-knot surface) */
 
 #define LQRX_F64 0
 #define LQRX_F32 1
@@ -104,6 +106,18 @@ int lqrx_dp_solve(const lqrx_dp_desc *desc, const void *A, const void *B, const 
 int lqrx_dp_solve_host(const lqrx_dp_desc *desc, const void *A, const void *B, const void *Q,
                        const void *R, const void *Qf, const void *x0, void *K, void *P,
                        void *X, void *U, int32_t *info);
+
+/* Per-knot DP surface — compute_ctg!(K, solver, prob) (dynamic_programming.jl:45-52, which
+ * runs compute_gain! :34-43 first) for a batch of problems, from P = solver.P (P_{k+1}):
+ *   K  = E⁻¹BᵀPA  with E = R + BᵀPB   (m·n·batch, sol.K[k])
+ *   P_ = Q + AᵀPA − APB·K               (n·n·batch, solver.P_; NULL = compute_gain! only)
+ * A, B, Q, R, P as lqrx_dp_solve's A, B, Q, R, Qf (time-invariant; desc.N, p_mode and the
+ * knot strides are ignored); info as lqrx_dp_solve (1 = E not positive definite).  The same
+ * kernels as lqrx_dp_solve (a 2-knot solve with Qf = P). */
+int lqrx_dp_compute_ctg(const lqrx_dp_desc *desc, const void *A, const void *B, const void *Q,
+                        const void *R, const void *P, void *K, void *P_, int32_t *info, void *stream);
+int lqrx_dp_compute_ctg_host(const lqrx_dp_desc *desc, const void *A, const void *B, const void *Q,
+                             const void *R, const void *P, void *K, void *P_, int32_t *info);
 
 /* ------------------------------------------------------------------------------------
  * DP path with linear cost terms — SURVEY §8(f) rank 1 ("time-varying LQR … and cost
@@ -180,12 +194,15 @@ typedef struct lqrx_kkt_desc {
                            trajectory t's packed array (Y, y, H, g, dz, lam) at
                            [t·len + e];  1 = batch fastest (SoA) at [e·batch + t] —
                            a wave's 64 trajectories read each element as one 512-B
-                           row.  Layout 1 is served by the compile-time shapes only,
+                           row.  Layout 1 is read natively by the compile-time shapes,
                            (n̄, m, p_first, p_interior, p_last) = Dubins (3,2,3,0,3) every
                            h_mode; cartpole (4,1,4,0,4), DoubleIntegrator(2)/(3)
                            (4,2,4,1,4)/(6,3,6,1,6), trajectory_structure(5,2,N) /
                            (7,3,N) (5,2,5,0,5)/(7,3,7,0,7) with diagonal H or ginv = 0;
-                           fp64; N >= 4; arrays < 2 GiB), else LQRX_ERR_UNSUPPORTED    */
+                           fp64; N >= 4.  Every other layout-1 call is staged: the
+                           arrays are transposed to layout 0 in library scratch, solved
+                           by the layout-0 kernels and dz / lam transposed back (2x
+                           the bytes).  Layout 1 arrays < 2 GiB.                      */
     int32_t reserved;
 } lqrx_kkt_desc;
 

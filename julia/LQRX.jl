@@ -82,7 +82,10 @@ end
 "DPSolver(prob): the Julia struct owned the per-knot scratch; here it lives in registers/LDS."
 struct DPSolver{T}
     n::Int; m::Int; N::Int
+    P::Matrix{T}      # solver.P  — the cost-to-go compute_gain!/compute_ctg! start from (zero, as upstream)
+    P_::Matrix{T}     # solver.P_ — what compute_ctg! produces
 end
+DPSolver{T}(n::Integer, m::Integer, N::Integer) where T = DPSolver{T}(n, m, N, zeros(T, n, n), zeros(T, n, n))
 DPSolver(b::LQRBatch{T}) where T = DPSolver{T}(size(b.B, 1), size(b.B, 2), b.N)
 
 """
@@ -147,6 +150,33 @@ function solve!(sol::LQRSolution{T}, solver::DPSolver{T}, prob::LQRProblem{n,m,T
     return solve!(sol, solver, b)
 end
 solve!(sol::LQRSolution{T}, prob::LQRProblem{n,m,T}) where {n,m,T} = solve!(sol, DPSolver(prob), prob)
+
+"""
+    compute_gain!(K, solver, prob);  compute_ctg!(K, solver, prob)
+
+The reference's per-knot surface (src/dynamic_programming.jl:34-52, called by test/dp.jl:16-17
+on `sol.K[1]`): K = (R + BᵀPB)⁻¹BᵀPA from P = solver.P, and for compute_ctg! also
+solver.P_ = Q + AᵀPA − AᵀPB·K — lqrx_dp_compute_ctg_host (the same kernels as solve!, on a
+2-knot problem with Qf = P).
+"""
+function compute_ctg!(K::AbstractMatrix{T}, solver::DPSolver{T}, prob::LQRProblem{n,m,T};
+                      gain_only::Bool=false) where {n,m,T}
+    dense(M, r, c) = reshape(Matrix{T}(M), r, c)
+    A, B, Q, R = dense(prob.A, n, n), dense(prob.B, n, m), dense(prob.Q, n, n), dense(prob.R, m, m)
+    Kd = Matrix{T}(undef, m, n)
+    info = Int32[0]
+    d = Ref(DpDesc(n, m, 2, dtypecode(T), 1, 0, 0, 0, 0))
+    GC.@preserve A B Q R solver Kd info begin
+        rc = ccall((:lqrx_dp_compute_ctg_host, liblqrx), Cint,
+                   (Ref{DpDesc}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{Int32}),
+                   d, A, B, Q, R, solver.P, Kd, gain_only ? Ptr{T}(C_NULL) : pointer(solver.P_), info)
+    end
+    check(rc)
+    K .= Kd
+    return K
+end
+compute_gain!(K::AbstractMatrix{T}, solver::DPSolver{T}, prob::LQRProblem{n,m,T}) where {n,m,T} =
+    compute_ctg!(K, solver, prob; gain_only=true)
 
 # ---- linear cost terms (lqrx_dp_linear; SURVEY §8(f) rank 1, no upstream counterpart) ----
 struct DpLinear
@@ -283,6 +313,7 @@ function sqp_solve!(Z::Matrix{Float64}, lam::Matrix{Float64}, iters::Vector{Int3
 end
 
 export LQRProblem, LQRSolution, LQRBatch, DPSolver, solve!, solve_linear!, kkt_solve!, ls_solve!,
+       compute_gain!, compute_ctg!,
        sqp_solve!, num_vars
 
 end # module

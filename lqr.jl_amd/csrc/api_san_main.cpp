@@ -117,7 +117,7 @@ int main()
     kb = k; kb.n2 = badn2.data();
     CHECK(lqrx_kkt_sizes(&kb, &nY, nullptr, nullptr, nullptr, nullptr) == -1);
     std::vector<int32_t> bigp = p;
-    bigp[50] = 70;                                              // block rows > 64
+    bigp[50] = 600;                                             // block rows > 512
     kb = k; kb.p = bigp.data();
     CHECK(lqrx_kkt_sizes(&kb, &nY, nullptr, nullptr, nullptr, nullptr) == LQRX_ERR_UNSUPPORTED);
     kb = k; kb.w = nullptr;

@@ -343,6 +343,83 @@ int lqrx_dp_solve_host(const lqrx_dp_desc *d, const void *A, const void *B, cons
     return dp_solve_host_impl(d, A, B, Q, R, Qf, x0, nullptr, K, P, X, U, info);
 }
 
+// compute_ctg!(K, solver, prob) / compute_gain!(K, solver, prob) for a batch
+// (dynamic_programming.jl:34-52): one backward knot from P = solver.P.  It is exactly the
+// first backward step of a 2-knot solve with Qf = P, so it runs the same kernel family on a
+// 2-knot descriptor; the rollout's X, U and a zero x0 live in stream-ordered scratch.
+int lqrx_dp_compute_ctg(const lqrx_dp_desc *d, const void *A, const void *B, const void *Q,
+                        const void *R, const void *P, void *K, void *P_, int32_t *info, void *stream)
+{
+    if (!d) return set_err(-1, "desc is NULL");
+    lqrx_dp_desc d2 = *d;
+    d2.N = 2;
+    d2.p_mode = 0;
+    d2.knot_stride_AB = d2.knot_stride_QR = 0;
+    int st = validate_dp(&d2);
+    if (st) return st;
+    if (d2.batch == 0) return 0;
+    const void *in[5] = {A, B, Q, R, P};
+    for (int i = 0; i < 5; ++i)
+        if (!in[i]) return set_err(-(i + 2), "input pointer %d is NULL", i + 2);
+    if (!K) return set_err(-7, "K is NULL");
+    const size_t es = dsize(d2.dtype), bt = (size_t)d2.batch, n = d2.n, m = d2.m;
+    // scratch: x0 (zeros) | X (2n) | U (m) | P_ when the caller passed none (compute_gain!)
+    const size_t ox = 0, oX = ox + ((n * bt * es + 255) & ~(size_t)255);
+    const size_t oU = oX + ((2 * n * bt * es + 255) & ~(size_t)255);
+    const size_t oP = oU + ((m * bt * es + 255) & ~(size_t)255);
+    const size_t tot = oP + (P_ ? 0 : n * n * bt * es);
+    hipStream_t s = (hipStream_t)stream;
+    void *blk = nullptr;
+    hipError_t e = lqrx::scratch_alloc(&blk, tot, s);
+    if (e != hipSuccess) return hip_err(e, "compute_ctg scratch");
+    char *b = (char *)blk;
+    e = hipMemsetAsync(b + ox, 0, n * bt * es, s);
+    if (e != hipSuccess) {
+        (void)lqrx::scratch_free(blk, s);
+        return hip_err(e, "compute_ctg x0");
+    }
+    st = dp_solve_impl(&d2, A, B, Q, R, P, b + ox, nullptr, K, P_ ? P_ : (void *)(b + oP), b + oX, b + oU,
+                       info, stream);
+    e = lqrx::scratch_free(blk, s);
+    if (st) return st;
+    return e == hipSuccess ? 0 : hip_err(e, "compute_ctg scratch free");
+}
+
+int lqrx_dp_compute_ctg_host(const lqrx_dp_desc *d, const void *A, const void *B, const void *Q,
+                             const void *R, const void *P, void *K, void *P_, int32_t *info)
+{
+    if (!d) return set_err(-1, "desc is NULL");
+    lqrx_dp_desc d2 = *d;
+    d2.N = 2;
+    d2.p_mode = 0;
+    d2.knot_stride_AB = d2.knot_stride_QR = 0;
+    int st = validate_dp(&d2);
+    if (st) return st;
+    if (d2.batch == 0) return 0;
+    const void *hin[5] = {A, B, Q, R, P};
+    const size_t es = dsize(d2.dtype), bt = (size_t)d2.batch, n = d2.n, m = d2.m;
+    const size_t szin[5] = {n * n, n * m, n * n, m * m, n * n};
+    DevBuf din[5], dK, dP, dinfo;
+    for (int i = 0; i < 5; ++i) {
+        if (!hin[i]) return set_err(-(i + 2), "input pointer %d is NULL", i + 2);
+        if ((st = dev_alloc(din[i], szin[i] * es * bt, "hipMalloc input"))) return st;
+        const hipError_t e = hipMemcpy(din[i].p, hin[i], szin[i] * es * bt, hipMemcpyHostToDevice);
+        if (e != hipSuccess) return hip_err(e, "H2D");
+    }
+    if (!K) return set_err(-7, "K is NULL");
+    if ((st = dev_alloc(dK, m * n * es * bt, "hipMalloc K"))) return st;
+    if (P_ && (st = dev_alloc(dP, n * n * es * bt, "hipMalloc P_"))) return st;
+    if ((st = dev_alloc(dinfo, 4 * bt, "hipMalloc info"))) return st;
+    st = lqrx_dp_compute_ctg(&d2, din[0].p, din[1].p, din[2].p, din[3].p, din[4].p, dK.p, P_ ? dP.p : nullptr,
+                             (int32_t *)dinfo.p, nullptr);
+    if (st < 0) return st;
+    hipError_t e = hipMemcpy(K, dK.p, m * n * es * bt, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && P_) e = hipMemcpy(P_, dP.p, n * n * es * bt, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && info) e = hipMemcpy(info, dinfo.p, 4 * bt, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_err(e, "D2H");
+    return st;
+}
+
 int lqrx_dp_solve_linear(const lqrx_dp_desc *d, const void *A, const void *B, const void *Q,
                          const void *R, const void *Qf, const void *x0,
                          const lqrx_dp_linear *lin, void *K, void *P, void *X, void *U,
@@ -521,6 +598,12 @@ int kkt_wg_env()
 }
 int kkt_route(const lqrx_kkt_desc *d, const lqrx::KktArgs &a)
 {
+    if (a.layout == 1) {   // SoA read natively by the compile-time shapes (fp64); else staged
+        size_t b = 0;
+        const bool fil = d->dtype == LQRX_F64 && !a.force_lane && !kkt_force_generic() &&
+                         lqrx::kkt_fil_scratch_bytes(a, d->n1, d->p, d->n2, d->w, &b);
+        return fil ? KK_FIL : KK_NONE;
+    }
     const bool wgk = lqrx::kkt_wg_supported(a, d->n1, d->p, d->n2, d->w);
     if (kkt_wg_env() && wgk) return KK_WG;
     const bool big = kkt_big_env() != 0 && lqrx::kkt_big_supported(a, d->n1, d->p, d->n2, d->w);
@@ -528,7 +611,6 @@ int kkt_route(const lqrx_kkt_desc *d, const lqrx::KktArgs &a)
     if (kkt_big_env() == 1 && big) return KK_BIG;
     size_t b = 0;
     const bool fil = !a.force_lane && !kkt_force_generic() && lqrx::kkt_fil_scratch_bytes(a, d->n1, d->p, d->n2, d->w, &b);
-    if (d->layout == 1) return fil ? KK_FIL : KK_NONE;
     if (fil) return KK_FIL;
     const int gc = lqrx::kkt_generic_class(a);
     if (gc == 1 || gc == 2 || (gc == 3 && (!big || a.force_lane))) return KK_GENERIC;
@@ -565,8 +647,13 @@ extern "C" int lqrx_kkt_workspace_size(const lqrx_kkt_desc *d, size_t *bytes)
     if (st) return st;
     if (!bytes) return set_err(-2, "bytes is NULL");
     if (d->batch) {
-        const lqrx::KktArgs a = kkt_args(d, L);
-        *bytes = kkt_ws_bytes(d, a, kkt_route(d, a));
+        lqrx::KktArgs a = kkt_args(d, L);
+        int route = kkt_route(d, a);
+        if (route == KK_NONE && a.layout == 1) {   // staged through layout 0 (kkt_solve_impl)
+            a.layout = 0;
+            route = kkt_route(d, a);
+        }
+        *bytes = kkt_ws_bytes(d, a, route);
     } else {
         *bytes = 0;
     }
@@ -618,7 +705,17 @@ int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const v
         a.nsel = nsel;
     }
     // one routing decision per call (the large-block plan is an O(N) pass over the structure)
-    const int route = kkt_route(d, a);
+    int route = kkt_route(d, a);
+    // layout 1 without a compile-time shape: the SoA arrays are transposed to layout 0 in a
+    // stream-ordered scratch block, solved by the layout-0 kernel family, and dz / λ transposed
+    // back (one extra read + write of every array)
+    bool staged = false;
+    if (route == KK_NONE && a.layout == 1) {
+        a.layout = 0;
+        route = kkt_route(d, a);
+        staged = route != KK_NONE;
+        if (!staged) a.layout = 1;
+    }
     if (ws) {
         const size_t need = kkt_ws_bytes(d, a, route);
         if (ws_bytes < need) {
@@ -631,18 +728,47 @@ int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const v
     static const int debug_meta = [] { const char *v = std::getenv("LQRX_DEBUG_META"); return v && *v == '1'; }();
     if (route == KK_NONE) {
         if (meta_tmp) (void)lqrx::scratch_free(meta_tmp, s);
-        if (d->layout == 1)
-            return set_err(LQRX_ERR_UNSUPPORTED, "layout 1 needs a compile-time KKT shape (Dubins; cartpole, "
-                                                 "DoubleIntegrator(2|3) with diagonal H) and N >= 4");
         return set_err(LQRX_ERR_UNSUPPORTED, "no KKT kernel for this structure / options (%s; layout 0 serves "
                                              "every structure with blocks <= %d rows and w <= %d, every h_mode "
                                              "and ginv)",
                        d->dtype == LQRX_F32 ? "fp32" : "fp64", lqrx::KW_MAX_BLOCK, lqrx::KW_MAX_W);
     }
-    if (route == KK_BIG) e = lqrx::kkt_big_launch(a, d->n1, d->p, d->n2, d->w, s);
+    void *stage = nullptr;
+    const int64_t es = d->dtype == LQRX_F32 ? 4 : 8, B = d->batch;
+    const int64_t S[6] = {L.sY, L.sy, L.sH, L.sg, L.sg, L.sy};   // Y y H g | dz lam
+    size_t soff[6], stot = 0;
+    if (staged) {
+        for (int i = 0; i < 6; ++i) {
+            soff[i] = stot;
+            stot += ((size_t)S[i] * (size_t)B * (size_t)es + 255) & ~(size_t)255;
+        }
+        e = lqrx::scratch_alloc(&stage, stot, s);
+        const void *src[4] = {Y, y, H, g};
+        const double **dst[4] = {&a.Y, &a.y, &a.H, &a.g};
+        for (int i = 0; i < 4 && e == hipSuccess; ++i) {      // [S][B] → [B][S]
+            *dst[i] = (const double *)((char *)stage + soff[i]);
+            e = lqrx::batch_transpose(src[i], (char *)stage + soff[i], S[i], B, (int)es, s);
+        }
+        a.dz = (double *)((char *)stage + soff[4]);
+        a.lam = (double *)((char *)stage + soff[5]);
+        a.sel = nullptr;
+        a.nsel = nullptr;
+    } else {
+        e = hipSuccess;
+    }
+    if (e != hipSuccess) {
+    } else if (route == KK_BIG) e = lqrx::kkt_big_launch(a, d->n1, d->p, d->n2, d->w, s);
     else if (route == KK_WG) e = lqrx::kkt_wg_launch(a, d->n1, d->p, d->n2, d->w, s);
     else if (route == KK_GENERIC || !lqrx::kkt_fil_launch(a, d->n1, d->p, d->n2, d->w, s, &e))
         e = lqrx::kkt_launch(a, s);
+    if (staged && e == hipSuccess) {                          // [B][S] → [S][B]
+        e = lqrx::batch_transpose(a.dz, dz, B, S[4], (int)es, s);
+        if (e == hipSuccess) e = lqrx::batch_transpose(a.lam, lam, B, S[5], (int)es, s);
+    }
+    if (stage) {
+        const hipError_t ef = lqrx::scratch_free(stage, s);
+        if (e == hipSuccess) e = ef;
+    }
     if (debug_meta) {   // read the table back before a per-call table is released
         std::vector<int32_t> back(L.meta.size());
         (void)hipStreamSynchronize(s);

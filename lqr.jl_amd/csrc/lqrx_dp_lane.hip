@@ -721,6 +721,217 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
 #undef PS
 }
 
+// ---------------------------------------------------------------------------------------
+// dp_hex_kernel: SIXTEEN LANES PER TRAJECTORY (one DPP row), n ≤ 4, m ≤ 4, time-invariant.
+// BASELINE cfg2 (cartpole B = 4096) is a 101-knot serial chain per trajectory: with four lanes
+// per trajectory the whole batch is 256 waves, one SIMD in four busy, and each knot a ~100-op
+// dependent chain per lane.  Here lane (i, j) = 4i + j of the row owns ONE element of every
+// n×n quantity, so the per-knot chain is a handful of FMAs between DPP reductions, and the
+// 1024 waves fill every SIMD:
+//   PB[i][c] = Σ_j P[i][j]B[j][c]         quad sum (the 4 lanes of row i are a DPP quad)
+//   PA[i][j] = Σ_l P[i][l]A[l][j]         P[i][l] by quad broadcast
+//   E[c][d]  = R[c][d] + Σ_i B[i][c]PB[i][d]   sum over the 4 quads (row_ror 4, 8)
+//   G[c][j]  = Σ_i PB[i][c]A[i][j]         (= BᵀPA for symmetric P; sum over the quads)
+//   potrf E (replicated), K[:, j] = E⁻¹G[:, j]  (every lane, its column j)
+//   P_[i][j] = Q[i][j] + Σ_l A[l][i](PA[l][j] − Σ_c PB[l][c]K[c][j])   (W from quad l by
+//              row_ror 4s: the same AᵀPA − GᵀK as the quad kernel); the upper triangle then
+//              takes the lower one's values (one bpermute), the symmetric form of the others
+// Rollout: lane (i, j) holds x[j]; u = −Kx and (Ax)[i] are quad sums, B u adds the replicated
+// u, and x_{k+1}[j] comes back from quad j by the same rotations.  The rotation direction is
+// probed once (the quad index itself rotated), so no lane map is assumed.
+template <int CTRL> __device__ __forceinline__ int dppi(int v)
+{
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
+}
+// The replicated sums must be bitwise identical in every lane: with contraction on, the
+// compiler fuses the caller's product into the add (v = a·b; v + dpp(v) → fma(a, b, dpp(v))),
+// which rounds differently in each lane of a pair — PB, E, G and K then differ by an ulp
+// between lanes and the recursion drifts (1e-4 on ill-conditioned cfg2 trajectories).
+template <typename T> __device__ __forceinline__ T qsum(T v)
+{
+#pragma clang fp contract(off)
+    v += qbcast<0xB1>(v);   // quad_perm [1,0,3,2]
+    return v + qbcast<0x4E>(v);   // quad_perm [2,3,0,1]
+}
+// sum over the 4 quads of the row: ror 8 pairs quads (0,2), (1,3), then ror 4 pairs the two
+// partial sums — every lane forms (v0 + v2) + (v1 + v3) in the same association, so E and G
+// (and hence K) are bitwise identical in every quad.  (ror 4 first gives each quad its own
+// association: K then differs by rounding between the rows of W, and the non-stationary
+// P_ = Q + AᵀPA − GᵀK amplified that along ill-conditioned horizons.)
+template <typename T> __device__ __forceinline__ T rsum(T v)
+{
+#pragma clang fp contract(off)
+    v += qbcast<0x128>(v);  // row_ror:8
+    return v + qbcast<0x124>(v);   // row_ror:4
+}
+
+template <typename T, int MP, bool SOA>
+__global__ __launch_bounds__(64) void dp_hex_kernel(const DpArgs a)
+{
+    constexpr int NP = 4;
+    const int64_t b = ((int64_t)blockIdx.x * 64 + threadIdx.x) >> 4;
+    const int r16 = threadIdx.x & 15, i = r16 >> 2, j = r16 & 3;
+    if (b >= a.batch) return;   // whole rows retire together; DPP stays inside the row
+    const int n = a.n, m = a.m, N = a.N;
+    const int64_t nn = (int64_t)n * n, nm = (int64_t)n * m, mm = (int64_t)m * m;
+    const int64_t es = SOA ? a.batch : 1;
+    auto tb = [&](int64_t S) { return SOA ? b : b * S; };
+    const T *Ag = (const T *)a.A + tb(nn), *Bg = (const T *)a.B + tb(nm);
+    const T *Qg = (const T *)a.Q + tb(nn), *Rg = (const T *)a.R + tb(mm);
+    // the quads whose values row_ror 4s delivers to this lane (s = 1, 2, 3)
+    const int q1 = dppi<0x124>(i), q2 = dppi<0x128>(i), q3 = dppi<0x12C>(i);
+    const int qs[4] = {i, q1, q2, q3};
+    auto Ael = [&](int r, int c) { return (r < n && c < n) ? Ag[(r + c * n) * es] : (T)0; };
+    T p = (i < n && j < n) ? ((const T *)a.Qf + tb(nn))[(i + j * n) * es] : (T)0;   // :58 P = Qf
+    const T qij = (i < n && j < n) ? Qg[(i + j * n) * es] : (T)0, aij = Ael(i, j);
+    T Acolj[NP], Acoef[NP];
+#pragma unroll
+    for (int l = 0; l < NP; ++l) {
+        Acolj[l] = Ael(l, j);          // A[l][j]       (PA)
+        Acoef[l] = Ael(qs[l], i);      // A[q_s][i]     (P_, W from quad q_s)
+    }
+    T Bj[MP], Bi[MP], R[MP][MP];
+#pragma unroll
+    for (int c = 0; c < MP; ++c) {
+        Bj[c] = (j < n && c < m) ? Bg[(j + c * n) * es] : (T)0;
+        Bi[c] = (i < n && c < m) ? Bg[(i + c * n) * es] : (T)0;
+#pragma unroll
+        for (int d = 0; d < MP; ++d)
+            R[c][d] = (c < m && d < m) ? Rg[(c + d * m) * es] : (c == d ? (T)1 : (T)0);
+    }
+    T *Kb = (T *)a.K + tb((int64_t)(N - 1) * nm);
+    T *Pall = a.p_all ? (T *)a.P + tb(nn * N) : nullptr;
+    const bool own = i < n && j < n;
+    if (Pall && own) Pall[((int64_t)(N - 1) * nn + i + j * n) * es] = p;
+    int info = 0;
+    for (int k = N - 1; k >= 1; --k) {   // :61
+        T PB[MP];
+#pragma unroll
+        for (int c = 0; c < MP; ++c) PB[c] = qsum(p * Bj[c]);      // :38 PB[i][c]
+        const T P0 = qfrom<0>(p), P1 = qfrom<1>(p), P2 = qfrom<2>(p), P3 = qfrom<3>(p);
+        T pa = P0 * Acolj[0];                                       // :40 PA[i][j]
+        pa = fma(P1, Acolj[1], pa);
+        pa = fma(P2, Acolj[2], pa);
+        pa = fma(P3, Acolj[3], pa);
+        T E[MP][MP], G[MP];
+#pragma unroll
+        for (int c = 0; c < MP; ++c) {
+#pragma unroll
+            for (int d = 0; d <= c; ++d) E[c][d] = R[c][d] + rsum(Bi[c] * PB[d]);   // :39
+            G[c] = rsum(PB[c] * aij);                               // :41 G[c][j]
+        }
+        // :29 potrf 'U' of E (replicated), :30 potrs for column j: K[:, j] = E⁻¹G[:, j]
+        T L[MP][MP], Linv[MP];
+#pragma unroll
+        for (int jj = 0; jj < MP; ++jj) {
+            T d = E[jj][jj];
+#pragma unroll
+            for (int pp = 0; pp < jj; ++pp) d = fma(-L[jj][pp], L[jj][pp], d);
+            if (!(d > (T)0) && info == 0) info = k;
+            const T ri = lane_rsqrt<T>(d);
+            Linv[jj] = ri;
+#pragma unroll
+            for (int ii = jj + 1; ii < MP; ++ii) {
+                T sv = E[ii][jj];
+#pragma unroll
+                for (int pp = 0; pp < jj; ++pp) sv = fma(-L[ii][pp], L[jj][pp], sv);
+                L[ii][jj] = sv * ri;
+            }
+            L[jj][jj] = d * ri;
+        }
+        T y[MP], Kc[MP];
+#pragma unroll
+        for (int ii = 0; ii < MP; ++ii) {
+            T sv = G[ii];
+#pragma unroll
+            for (int pp = 0; pp < ii; ++pp) sv = fma(-L[ii][pp], y[pp], sv);
+            y[ii] = sv * Linv[ii];
+        }
+#pragma unroll
+        for (int ii = MP - 1; ii >= 0; --ii) {
+            T sv = y[ii];
+#pragma unroll
+            for (int pp = ii + 1; pp < MP; ++pp) sv = fma(-L[pp][ii], Kc[pp], sv);
+            Kc[ii] = sv * Linv[ii];
+        }
+        if (i == 0 && j < n) {                                      // sol.K[k] column j
+            T *Kk = Kb + ((int64_t)(k - 1) * nm + j * m) * es;
+#pragma unroll
+            for (int c = 0; c < MP; ++c)
+                if (c < m) Kk[c * es] = Kc[c];
+        }
+        // :51 P_[i][j] = Q[i][j] + Σ_l A[l][i]·W[l][j],  W = PA − PB·K (row l, column j)
+        T wv = pa;
+#pragma unroll
+        for (int c = 0; c < MP; ++c) wv = fma(-PB[c], Kc[c], wv);
+        const T w1 = qbcast<0x124>(wv), w2 = qbcast<0x128>(wv), w3 = qbcast<0x12C>(wv);
+        T pn = fma(Acoef[0], wv, qij);
+        pn = fma(Acoef[1], w1, pn);
+        pn = fma(Acoef[2], w2, pn);
+        pn = fma(Acoef[3], w3, pn);
+        // symmetric form, as the quad / MFMA kernels: the upper triangle mirrors the lower
+        // (left unsymmetrised, rounding asymmetry grows along ill-conditioned horizons)
+        const T pt = __shfl(pn, (int)(threadIdx.x & ~15u) | (4 * j + i), 64);
+        p = own ? (i >= j ? pn : pt) : (T)0;
+        if (Pall && own) Pall[((int64_t)(k - 1) * nn + i + j * n) * es] = p;
+    }
+    if (!a.p_all && own) ((T *)a.P + tb(nn))[(i + j * n) * es] = p;
+    if (a.info && r16 == 0) a.info[b] = info;
+
+    // forward rollout :66-70 — lane (i, j) holds x[j]
+    T *Xb = (T *)a.X + tb((int64_t)N * n), *Ub = (T *)a.U + tb((int64_t)(N - 1) * m);
+    const T *x0 = (const T *)a.x0 + tb(n);
+    T xj = j < n ? x0[j * es] : (T)0;
+    if (i == 0 && j < n) Xb[j * es] = xj;
+    constexpr int RD = 8;
+    T ring[RD][MP];
+    auto fetch = [&](int k, T (&d)[MP]) {   // K_k[:, j]
+        if (k > N - 1) return;
+        const T *Kk = Kb + (int64_t)(k - 1) * nm * es;
+#pragma unroll
+        for (int c = 0; c < MP; ++c) d[c] = (c < m && j < n) ? Kk[(c + j * m) * es] : (T)0;
+    };
+    // K_k was written by lanes (0, j) of this row above: make those stores visible
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#pragma unroll
+    for (int d = 0; d < RD; ++d) fetch(1 + d, ring[d]);
+    const int s_of_j = j == qs[0] ? 0 : j == qs[1] ? 1 : j == qs[2] ? 2 : 3;
+    for (int k0 = 1; k0 <= N - 1; k0 += RD) {
+#pragma unroll
+        for (int d = 0; d < RD; ++d) {
+            const int k = k0 + d;
+            if (k > N - 1) break;
+            T Kc[MP];
+#pragma unroll
+            for (int c = 0; c < MP; ++c) Kc[c] = ring[d][c];
+            fetch(k + RD, ring[d]);
+            T u[MP];
+#pragma unroll
+            for (int c = 0; c < MP; ++c) {
+                u[c] = -qsum(Kc[c] * xj);                           // u = −K x (replicated)
+                if (r16 == c && c < m) Ub[((int64_t)(k - 1) * m + c) * es] = u[c];
+            }
+            T xi = qsum(aij * xj);                                  // (A x)[i]
+#pragma unroll
+            for (int c = 0; c < MP; ++c) xi = fma(Bi[c], u[c], xi); // + (B u)[i]
+            if (j == 0 && i < n) Xb[((int64_t)k * n + i) * es] = xi;
+            const T x1 = qbcast<0x124>(xi), x2 = qbcast<0x128>(xi), x3 = qbcast<0x12C>(xi);
+            xj = s_of_j == 0 ? xi : s_of_j == 1 ? x1 : s_of_j == 2 ? x2 : x3;
+        }
+    }
+}
+
+template <typename T, int MP>
+static hipError_t launch_hex(const DpArgs &a, hipStream_t s)
+{
+    dim3 grid((unsigned)((a.batch * 16 + 63) / 64)), block(64);
+    if (a.layout == 1) hipLaunchKernelGGL((dp_hex_kernel<T, MP, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((dp_hex_kernel<T, MP, false>), grid, block, 0, s, a);
+    return hipGetLastError();
+}
+
 template <typename T, int NP, int MP>
 static hipError_t launch_lane(const DpArgs &a, hipStream_t s)
 {
@@ -761,9 +972,30 @@ static hipError_t launch_quad(const DpArgs &a, hipStream_t s)
     return hipGetLastError();
 }
 
+// hex kernel (16 lanes per trajectory) while 16·batch lanes fit ≤ 2 waves per SIMD; n ≤ 4,
+// m ≤ 4, time-invariant, no linear terms.  LQRX_DP_SMALL=hex forces it (tests).
+static bool use_hex(const DpArgs &a)
+{
+    if (a.tv_AB || a.tv_QR || a.lin || a.n > 4 || a.m > 4) return false;
+    const char *e = std::getenv("LQRX_DP_SMALL");
+    if (e && e[0] == 'h') return true;
+    if (e && (e[0] == 'l' || e[0] == 'q')) return false;
+    return a.batch <= 8192;
+}
+
 hipError_t dp_lane_launch(const DpArgs &a, hipStream_t s)
 {
     const int np = a.n <= 2 ? 2 : 4, mp = a.m <= 1 ? 1 : (a.m <= 2 ? 2 : 4);
+    if (use_hex(a)) {
+        if (a.dtype == 0) {
+            if (mp == 1) return launch_hex<double, 1>(a, s);
+            if (mp == 2) return launch_hex<double, 2>(a, s);
+            return launch_hex<double, 4>(a, s);
+        }
+        if (mp == 1) return launch_hex<float, 1>(a, s);
+        if (mp == 2) return launch_hex<float, 2>(a, s);
+        return launch_hex<float, 4>(a, s);
+    }
     if (use_quad(a)) {
         if (a.dtype == 0) {
             if (mp == 1) return launch_quad<double, 1>(a, s);

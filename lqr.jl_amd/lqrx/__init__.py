@@ -8,10 +8,11 @@ the reference's Julia surface.
 """
 from . import _lib
 from ._lib import F32, F64, LqrxError, load
-from .dp import (DPSolver, LQRBatch, LQRProblem, LQRSolution, dp_solve_device, random_batch,
-                 solve, solve_batch)
+from .dp import (DPSolver, LQRBatch, LQRProblem, LQRSolution, compute_ctg, compute_gain,
+                 dp_solve_device, random_batch, solve, solve_batch)
 from .ls import LeastSquaresSolver, Primals
 
 __all__ = ["F32", "F64", "LqrxError", "load", "DPSolver", "LQRBatch", "LQRProblem",
            "LQRSolution", "solve", "solve_batch", "random_batch", "dp_solve_device",
+           "compute_gain", "compute_ctg",
            "LeastSquaresSolver", "Primals"]

@@ -83,6 +83,8 @@ _SIGS = {
     "lqrx_scratch_trim": (C.c_int, [C.c_int32, C.c_size_t]),
     "lqrx_dp_solve": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 10 + [_VP, _VP]),
     "lqrx_dp_solve_host": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 10 + [_VP]),
+    "lqrx_dp_compute_ctg": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 8 + [_VP]),
+    "lqrx_dp_compute_ctg_host": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 8),
     "lqrx_dp_solve_linear": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 6 + [C.POINTER(DpLinear)]
                              + [_VP] * 4 + [_VP, _VP]),
     "lqrx_dp_solve_linear_host": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 6

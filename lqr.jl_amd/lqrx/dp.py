@@ -6,6 +6,7 @@ Reference surface (Julia, /root/reference/src):
   DPSolver(prob)                                           dynamic_programming.jl:13-23
   LQRSolution (exported, undefined upstream: fields K, X, U as used by :62-69)
   solve!(sol, solver, prob)                                dynamic_programming.jl:54-72
+  compute_gain!(K, solver, prob), compute_ctg!(K, solver, prob)      :34-52 (per knot)
 Extension (no upstream counterpart): linear cost terms q, r, qf on
 LQRProblem / LQRBatch → feedforward d and linear cost-to-go p (lqrx_dp_solve_linear).
 
@@ -24,7 +25,8 @@ import numpy as np
 from . import _lib
 
 __all__ = ["LQRProblem", "LQRSolution", "DPSolver", "solve", "solve_batch", "LQRBatch",
-           "random_batch", "to_abi", "from_abi", "dp_solve_device"]
+           "random_batch", "to_abi", "from_abi", "dp_solve_device", "compute_gain", "compute_ctg",
+           "compute_ctg_batch"]
 
 
 def to_abi(a: np.ndarray) -> np.ndarray:
@@ -110,18 +112,22 @@ class LQRSolution:
 @dataclass
 class DPSolver:
     """DPSolver(prob) (dynamic_programming.jl:13-23).  The Julia struct owns scratch
-    (P, P_, PA, PB, APB, E); here the scratch is registers/LDS inside the kernel, so the
-    solver only records the problem shape and dtype."""
+    (P, P_, PA, PB, APB, E); here the products live in registers/LDS inside the kernel, so
+    the solver records the problem shape and dtype plus the two matrices the reference's
+    per-knot surface reads and writes: P (the cost-to-go compute_gain!/compute_ctg! start
+    from, zero as upstream) and P_ (what compute_ctg! produces)."""
 
     n: int
     m: int
     N: int
     dtype: int = _lib.F64
+    P: np.ndarray | None = None
+    P_: np.ndarray | None = None
 
     @classmethod
     def of(cls, prob: LQRProblem, dtype: int = _lib.F64):
         n, m, N = prob.size()
-        return cls(n, m, N, dtype)
+        return cls(n, m, N, dtype, np.zeros((n, n)), np.zeros((n, n)))
 
 
 @dataclass
@@ -238,6 +244,45 @@ def solve(sol: LQRSolution, solver: DPSolver, prob: LQRProblem) -> LQRSolution:
         sol.d = out["d"][0]
         sol.p = out["p"][0]
     return sol
+
+
+def compute_ctg_batch(A, B, Q, R, P, dtype: int = _lib.F64, gain_only: bool = False):
+    """compute_ctg! (dynamic_programming.jl:45-52; compute_gain! :34-43 with gain_only) for a
+    batch through lqrx_dp_compute_ctg_host: A (batch, n, n), B (batch, n, m), Q, R, and
+    P = solver.P (batch, n, n).  Returns K (batch, m, n), P_ (batch, n, n) (None with
+    gain_only), info (batch,), rc."""
+    lib = _lib.load()
+    A = np.asarray(A)
+    bt, n, m = A.shape[0], A.shape[-1], np.asarray(B).shape[-1]
+    npdt = np.float64 if dtype == _lib.F64 else np.float32
+    ins = [to_abi(np.asarray(x, dtype=npdt)) for x in (A, B, Q, R, P)]
+    K = np.zeros(bt * m * n, npdt)
+    Pn = None if gain_only else np.zeros(bt * n * n, npdt)
+    info = np.zeros(bt, np.int32)
+    d = _lib.DpDesc(n, m, 2, dtype, bt, 0, 0, 0, 0)
+    rc = _lib.check(lib.lqrx_dp_compute_ctg_host(C.byref(d), *[_ptr(a) for a in ins], _ptr(K),
+                                                 None if Pn is None else _ptr(Pn), _ptr(info)))
+    return dict(K=from_abi(K, (bt, m, n)), P_=None if Pn is None else from_abi(Pn, (bt, n, n)),
+                info=info, rc=rc)
+
+
+def compute_gain(K: np.ndarray, solver: DPSolver, prob: LQRProblem) -> np.ndarray:
+    """compute_gain!(K, solver, prob) — dynamic_programming.jl:34-43: K = E⁻¹BᵀPA from
+    P = solver.P (test/dp.jl:16 calls it on a fresh solver, P = 0)."""
+    b = LQRBatch.of([prob])                       # densifies Diagonal Q / R
+    out = compute_ctg_batch(b.A, b.B, b.Q, b.R, np.asarray(solver.P)[None], solver.dtype, gain_only=True)
+    K[...] = out["K"][0]
+    return K
+
+
+def compute_ctg(K: np.ndarray, solver: DPSolver, prob: LQRProblem) -> np.ndarray:
+    """compute_ctg!(K, solver, prob) — dynamic_programming.jl:45-52: the gain as above and
+    solver.P_ = Q + AᵀPA − APB·K."""
+    b = LQRBatch.of([prob])
+    out = compute_ctg_batch(b.A, b.B, b.Q, b.R, np.asarray(solver.P)[None], solver.dtype)
+    K[...] = out["K"][0]
+    solver.P_[...] = out["P_"][0]
+    return K
 
 
 def random_batch(n: int, m: int, N: int, batch: int, seed: int, traj0: int = 0,

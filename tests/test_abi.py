@@ -238,3 +238,18 @@ def test_kkt_blocks_past_64_accepted(lqrx):
     n = C.c_size_t(0)
     big = K.trajectory_structure(513, 4, 3)
     assert lib.lqrx_kkt_workspace_size(C.byref(big.desc(2, K.H_DIAG, 1, 0, _lib.F64)), C.byref(n)) == -101
+
+
+def test_julia_shim_ccalls_resolve(lqrx):
+    """Every `ccall((:sym, liblqrx), …)` in julia/LQRX.jl names a symbol the library exports
+    (Julia is not in this image; this keeps the shim's bindings in step with the ABI)."""
+    import os
+    import re
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = open(os.path.join(root, "julia", "LQRX.jl")).read()
+    syms = set(re.findall(r"ccall\(\(:(\w+),\s*liblqrx\)", src))
+    assert {"lqrx_dp_solve_host", "lqrx_dp_compute_ctg_host", "lqrx_kkt_solve_host"} <= syms
+    lib = lqrx.load()
+    for s in sorted(syms):
+        assert hasattr(lib, s), s

@@ -129,3 +129,52 @@ def test_reference_call_shape_diagonal_costs(lqrx, oracle, gpu_ok):
         assert np.abs(sol.K[k] - K[k]).max() <= TOL64 * np.abs(K[k]).max()
     assert np.abs(sol.X - ref["X"].reshape(N, n)).max() <= TOL64 * np.abs(ref["X"]).max()
     assert np.abs(sol.P - from_abi(ref["P"], (1, n, n))[0]).max() <= TOL64 * np.abs(ref["P"]).max()
+
+
+@pytest.mark.parametrize("n,m,bt", [(4, 2, 5), (3, 1, 70), (12, 5, 9), (32, 16, 3), (80, 40, 2)])
+def test_per_knot_compute_gain_ctg(lqrx, gpu_ok, n, m, bt):
+    """The reference's per-knot surface (test/dp.jl:16-17): compute_gain!(K, solver, prob) and
+    compute_ctg!(K, solver, prob) (dynamic_programming.jl:34-52) through lqrx_dp_compute_ctg —
+    from solver.P = 0 (a fresh solver, as the test calls them) and from a random SPD P, batched
+    over every kernel family (n ≤ 4, register tiles, workgroup) — against the formulas in fp64
+    numpy: K = (R + BᵀPB)⁻¹BᵀPA, P_ = Q + AᵀPA − AᵀPB·K."""
+    from lqrx.dp import abi_to_batch, compute_ctg_batch
+
+    b = abi_to_batch(lqrx.random_batch(n, m, 3, bt, seed=5 + n))
+    rng = np.random.default_rng(n)
+    G = rng.standard_normal((bt, n, n))
+    for P in (np.zeros((bt, n, n)), G @ np.swapaxes(G, 1, 2) / n + np.eye(n)):
+        out = compute_ctg_batch(b.A, b.B, b.Q, b.R, P)
+        assert out["rc"] == 0 and (out["info"] == 0).all()
+        PB, PA = P @ b.B, P @ b.A
+        E = b.R + np.swapaxes(b.B, 1, 2) @ PB
+        K = np.linalg.solve(E, np.swapaxes(b.B, 1, 2) @ PA)
+        Pn = b.Q + np.swapaxes(b.A, 1, 2) @ PA - np.swapaxes(b.A, 1, 2) @ PB @ K
+        assert np.abs(out["K"] - K).max() <= 1e-10 * max(1.0, np.abs(K).max())
+        assert np.abs(out["P_"] - Pn).max() <= 1e-10 * max(1.0, np.abs(Pn).max())
+        g = compute_ctg_batch(b.A, b.B, b.Q, b.R, P, gain_only=True)
+        assert g["P_"] is None and np.array_equal(g["K"], out["K"])
+
+
+def test_per_knot_reference_call_shape(lqrx, gpu_ok):
+    """test/dp.jl:14-17 verbatim in shape: sol = LQRSolution(prob); solver = DPSolver(prob);
+    compute_gain!(sol.K[1], solver, prob); compute_ctg!(sol.K[1], solver, prob) — on a fresh
+    solver (P = 0) the gain is 0 and P_ = Q; with solver.P = Qf it is solve!'s last knot."""
+    n, m, N, dt = 4, 2, 11, 0.1
+    I2 = np.eye(2)
+    A = np.block([[I2, dt * I2], [0 * I2, I2]])
+    B = np.vstack([0.5 * dt * dt * I2, dt * I2])
+    q = np.array([10.0, 10.0, 1.0, 1.0])
+    prob = lqrx.LQRProblem(Qf=10 * q, Q=q, R=np.full(m, 0.1), A=A, B=B, x0=np.array([1.0, -1, 0, 0.5]),
+                           u0=np.zeros(m), tf=1.0, N=N)
+    sol = lqrx.LQRSolution.of(prob)
+    solver = lqrx.DPSolver.of(prob)
+    lqrx.compute_gain(sol.K[0], solver, prob)
+    assert np.abs(sol.K[0]).max() == 0.0
+    lqrx.compute_ctg(sol.K[0], solver, prob)
+    assert np.abs(solver.P_ - np.diag(q)).max() <= 1e-14
+    solver.P[...] = np.diag(10 * q)
+    lqrx.compute_ctg(sol.K[0], solver, prob)
+    full = lqrx.LQRSolution.of(prob)
+    lqrx.solve(full, lqrx.DPSolver.of(prob), prob)
+    assert np.abs(sol.K[0] - full.K[N - 2]).max() <= 1e-12 * np.abs(full.K[N - 2]).max()

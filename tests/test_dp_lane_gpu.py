@@ -112,8 +112,11 @@ def test_lane_cartpole_problem(lqrx, oracle, gpu_ok):
     assert np.abs(got["X"] - ref["X"].reshape(bt, N, 4)).max() <= TOL64
 
 
-def test_lane_non_spd_sets_info(lqrx, gpu_ok):
+@pytest.mark.parametrize("mode", ["lane", "quad", "hex"])
+def test_lane_non_spd_sets_info(lqrx, gpu_ok, monkeypatch, mode):
     from lqrx.dp import abi_to_batch
+
+    monkeypatch.setenv("LQRX_DP_SMALL", mode)
 
     n, m, N, bt = 4, 2, 10, 70
     d = lqrx.random_batch(n, m, N, bt, seed=3)
@@ -162,13 +165,16 @@ def test_time_varying_parity(lqrx, oracle, gpu_ok, n, m, tv_ab, tv_qr, N, bt):
     assert np.abs(got["X"] - refX).max() <= TOL64 * max(1.0, np.abs(refX).max())
 
 
-@pytest.mark.parametrize("mode", ["lane", "quad"])
+@pytest.mark.parametrize("mode", ["lane", "quad", "hex"])
 @pytest.mark.parametrize("n,m,N,batch", [(4, 1, 101, 300), (3, 2, 60, 130), (4, 4, 20, 33),
-                                         (4, 2, 30, 70)])
+                                         (4, 2, 30, 70), (2, 1, 25, 17), (4, 3, 40, 4100)])
 def test_small_kernel_modes(lqrx, oracle, gpu_ok, monkeypatch, mode, n, m, N, batch):
-    """Both small-n kernels — one lane per trajectory (dp_lane_kernel) and one quad per
-    trajectory (dp_quad_kernel, the default for batch ≤ 16384 at n ∈ {3, 4}) — against the
-    oracle; LQRX_DP_SMALL selects the kernel per call."""
+    """The three small-n kernels — one lane per trajectory (dp_lane_kernel), one quad per
+    trajectory (dp_quad_kernel, n ∈ {3, 4}, batch ≤ 16384) and sixteen lanes per trajectory
+    (dp_hex_kernel, the default for batch ≤ 8192) — against the oracle; LQRX_DP_SMALL selects
+    the kernel per call."""
+    if mode == "quad" and n < 3:
+        pytest.skip("the quad kernel serves n in {3, 4}")
     monkeypatch.setenv("LQRX_DP_SMALL", mode)
     seed = 700 + 11 * n + m
     got, ref = run_pair(lqrx, oracle, n, m, N, batch, seed=seed, all_P=True)
@@ -177,7 +183,8 @@ def test_small_kernel_modes(lqrx, oracle, gpu_ok, monkeypatch, mode, n, m, N, ba
 
 
 def test_small_kernel_auto_large_batch(lqrx, oracle, gpu_ok):
-    """batch > 16384 at n = 4 selects the lane kernel (auto)."""
+    """batch > 16384 at n = 4 selects the lane kernel (auto; 8192 < batch ≤ 16384 the quad
+    kernel, below that the hex kernel)."""
     got, ref = run_pair(lqrx, oracle, 4, 1, 12, 16384 + 70, seed=77)
     assert got["rc"] == 0
     assert_parity(got, ref, lqrx.random_batch(4, 1, 12, 16384 + 70, 77), 12)

@@ -186,10 +186,13 @@ def test_kkt_layout1_soa(lqrx, gpu_ok, model, N, batch, h_mode, ginv):
           "di3": lambda: K.double_integrator_structure(3, N), "di2": lambda: K.double_integrator_structure(2, N),
           "t52": lambda: K.trajectory_structure(5, 2, N), "t73": lambda: K.trajectory_structure(7, 3, N)}[model]()
     if model != "dubins" and h_mode != 2 and ginv:
-        pb = K.random_kkt(st, 2, seed=1, h_mode=h_mode)            # dense H: no SoA shape
-        with pytest.raises(K._lib.LqrxError) as e:
-            K.kkt_solve(pb, ginv=ginv, layout=1)
-        assert e.value.code == K._lib.ERR_UNSUPPORTED
+        # dense H: no SoA shape — staged through layout 0 (transpose in, layout-0 kernels,
+        # transpose out): identical to the layout-0 call
+        pb = K.random_kkt(st, 67, seed=1, h_mode=h_mode)
+        got1 = K.kkt_solve(pb, ginv=ginv, layout=1)
+        got0 = K.kkt_solve(pb, ginv=ginv, layout=0)
+        assert got1["rc"] == 0 and (got1["info"] == got0["info"]).all()
+        assert np.array_equal(got1["dz"], got0["dz"]) and np.array_equal(got1["lam"], got0["lam"])
         return
     pb = K.random_kkt(st, batch, seed=11 * N + h_mode, h_mode=h_mode)
     got1 = K.kkt_solve(pb, ginv=ginv, layout=1)
@@ -203,13 +206,30 @@ def test_kkt_layout1_soa(lqrx, gpu_ok, model, N, batch, h_mode, ginv):
     assert rel(got1["lam"][idx], ref["lam"].reshape(len(idx), -1)) <= TOL
 
 
-def test_kkt_layout1_unsupported_shapes(lqrx, gpu_ok):
-    """Layout 1 is served by the compile-time shapes only: other structures (here n = 5, m = 3)
-    and N < 4 return LQRX_ERR_UNSUPPORTED."""
+@pytest.mark.parametrize("case", ["t53", "dubins_N3", "big_f32", "big_f64_dense", "wg_f64"])
+def test_kkt_layout1_staged(lqrx, gpu_ok, case):
+    """Layout 1 outside the compile-time SoA shapes (other structures, N < 4, fp32, the
+    large-block and workgroup kernels) is staged: the SoA arrays are transposed to layout 0 in
+    scratch, solved by the layout-0 kernel family and transposed back — bit-identical to the
+    layout-0 call, and within tolerance of the oracle."""
+    import dataclasses
     import lqrx.kkt as K
 
-    for st in (K.trajectory_structure(5, 3, 12), K.dubins_structure(3)):
-        pb = K.random_kkt(st, 3, seed=2, h_mode=K.H_DIAG)
-        with pytest.raises(K._lib.LqrxError) as e:
-            K.kkt_solve(pb, layout=1)
-        assert e.value.code == K._lib.ERR_UNSUPPORTED
+    st, hm, dt, dyn, tol = {
+        "t53": (K.trajectory_structure(5, 3, 12), K.H_DIAG, lqrx.F64, "small", TOL),
+        "dubins_N3": (K.dubins_structure(3), K.H_DIAG, lqrx.F64, "small", TOL),
+        "big_f32": (K.trajectory_structure(16, 8, 9), K.H_DIAG, lqrx.F32, "dense", 1e-4),
+        "big_f64_dense": (K.trajectory_structure(16, 8, 9), K.H_DENSE, lqrx.F64, "dense", TOL),
+        "wg_f64": (K.trajectory_structure(72, 36, 5), K.H_DIAG, lqrx.F64, "dense", TOL),
+    }[case]
+    pb = K.random_kkt(st, 37, seed=2, h_mode=hm, dyn=dyn)
+    if dt == lqrx.F32:
+        f = lambda a: np.asarray(a, np.float32).astype(np.float64)
+        pb = dataclasses.replace(pb, Y=f(pb.Y), y=f(pb.y), H=f(pb.H), g=f(pb.g))
+    got1 = K.kkt_solve(pb, layout=1, dtype=dt)
+    got0 = K.kkt_solve(pb, layout=0, dtype=dt)
+    assert got1["rc"] == 0 and (got1["info"] == 0).all()
+    assert np.array_equal(got1["dz"], got0["dz"]) and np.array_equal(got1["lam"], got0["lam"])
+    ref = _ref(st, pb, 1)
+    assert rel(got1["dz"], ref["dz"].reshape(pb.batch, -1)) <= tol
+    assert rel(got1["lam"], ref["lam"].reshape(pb.batch, -1)) <= tol

@@ -23,7 +23,7 @@ def _pair(lqrx, b, **kw):
     return a1
 
 
-@pytest.mark.parametrize("mode", ["lane", "quad"])
+@pytest.mark.parametrize("mode", ["lane", "quad", "hex"])
 @pytest.mark.parametrize("n,m,N,bt", [(4, 1, 101, 130), (3, 2, 40, 67), (2, 1, 20, 65), (4, 4, 12, 9)])
 def test_soa_small_kernels(lqrx, oracle, gpu_ok, monkeypatch, mode, n, m, N, bt):
     from lqrx.dp import abi_to_batch, from_abi
