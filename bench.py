@@ -857,6 +857,12 @@ def main(argv=None):
         }
         if gather is not None and "ms" in gather:
             line["value_solve_plus_gather"] = total / (wall + gather["ms"] * 1e-3)
+        try:   # build provenance: the library's compiled-in source hash vs this tree's
+            from lqrx import _lib as _L
+            bi = _L.build_info()
+            line["build"] = {"library": bi["info"], "matches_tree": bi["matches_tree"]}
+        except Exception as exc:   # noqa: BLE001 — reporting only
+            line["build"] = {"error": str(exc)}
         print(json.dumps(line), flush=True)
     SH.finish_ranks(world)
     return 0

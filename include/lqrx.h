@@ -346,6 +346,10 @@ int lqrx_ls_solve_host(const lqrx_ls_desc *desc, const double *A, const double *
  * Utilities
  * ------------------------------------------------------------------------------------ */
 int lqrx_abi_version(void);
+/* "src_sha256=<SHA-256 of the library's sources> abi=<n> arch=gfx950 built=<date time>": the
+ * hash covers lqr.jl_amd/csrc/{*.hip,*.h,*.cpp} (sorted by name) then include/lqrx.h, so a
+ * caller can check that the loaded binary was built from the sources beside it */
+const char *lqrx_build_info(void);
 const char *lqrx_last_error(void);
 /* copy the calling thread's last error message into buf (NUL-terminated, truncated to
  * len-1 bytes); returns the full message length.  For bindings that cannot hold a

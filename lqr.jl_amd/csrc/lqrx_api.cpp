@@ -2,6 +2,8 @@
 // host-pointer convenience wrappers, the synthetic-problem generator.
 #include "../../include/lqrx.h"
 #include "lqrx_internal.h"
+#define LQRX_STR2(x) #x
+#define LQRX_STR(x) LQRX_STR2(x)
 
 #include <hip/hip_runtime.h>
 #include <algorithm>
@@ -185,6 +187,13 @@ hipError_t dp_launch_soa_staged(const lqrx::DpArgs &a, hipStream_t s)
 extern "C" {
 
 int lqrx_abi_version(void) { return LQRX_ABI_VERSION; }
+#ifndef LQRX_SRC_HASH
+#define LQRX_SRC_HASH "unknown"
+#endif
+const char *lqrx_build_info(void)
+{
+    return "src_sha256=" LQRX_SRC_HASH " abi=" LQRX_STR(LQRX_ABI_VERSION) " arch=gfx950 built=" __DATE__ " " __TIME__;
+}
 int lqrx_scratch_trim(int32_t device, size_t keep_bytes)
 {
     const hipError_t e = lqrx::scratch_trim(device, keep_bytes);

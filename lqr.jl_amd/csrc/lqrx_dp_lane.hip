@@ -728,43 +728,23 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
 // dependent chain per lane.  Here lane (i, j) = 4i + j of the row owns ONE element of every
 // n×n quantity, so the per-knot chain is a handful of FMAs between DPP reductions, and the
 // 1024 waves fill every SIMD:
-//   PB[i][c] = Σ_j P[i][j]B[j][c]         quad sum (the 4 lanes of row i are a DPP quad)
-//   PA[i][j] = Σ_l P[i][l]A[l][j]         P[i][l] by quad broadcast
-//   E[c][d]  = R[c][d] + Σ_i B[i][c]PB[i][d]   sum over the 4 quads (row_ror 4, 8)
-//   G[c][j]  = Σ_i PB[i][c]A[i][j]         (= BᵀPA for symmetric P; sum over the quads)
+//   PA[i][j] = Σ_l P[i][l]A[l][j]         P[i][l] by quad broadcast (the 4 lanes of row i
+//                                          are a DPP quad)
+//   PB[i][c] = Σ_l P[i][l]B[l][c]         the same broadcasts, every lane of the quad
+//   E[c][d]  = R[c][d] + Σ_t B[t][c]PB[t][d]   PB[t] by row_newbcast from quad t
+//   G[c][j]  = Σ_t PB[t][c]A[t][j]         (= BᵀPA for symmetric P)
 //   potrf E (replicated), K[:, j] = E⁻¹G[:, j]  (every lane, its column j)
 //   P_[i][j] = Q[i][j] + Σ_l A[l][i](PA[l][j] − Σ_c PB[l][c]K[c][j])   (W from quad l by
 //              row_ror 4s: the same AᵀPA − GᵀK as the quad kernel); the upper triangle then
 //              takes the lower one's values (one bpermute), the symmetric form of the others
-// Rollout: lane (i, j) holds x[j]; u = −Kx and (Ax)[i] are quad sums, B u adds the replicated
-// u, and x_{k+1}[j] comes back from quad j by the same rotations.  The rotation direction is
+// Rollout: lane (i, j) holds x[j]; x and K_k's rows reach every lane of the quad by
+// broadcasts, u = −Kx and (Ax + Bu)[i] are the quad kernel's FMA chains (the same value in
+// every lane of the quad), and x_{k+1}[j] comes back from quad j by the same rotations.  The rotation direction is
 // probed once (the quad index itself rotated), so no lane map is assumed.
 template <int CTRL> __device__ __forceinline__ int dppi(int v)
 {
     return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
 }
-// The replicated sums must be bitwise identical in every lane: with contraction on, the
-// compiler fuses the caller's product into the add (v = a·b; v + dpp(v) → fma(a, b, dpp(v))),
-// which rounds differently in each lane of a pair — PB, E, G and K then differ by an ulp
-// between lanes and the recursion drifts (1e-4 on ill-conditioned cfg2 trajectories).
-template <typename T> __device__ __forceinline__ T qsum(T v)
-{
-#pragma clang fp contract(off)
-    v += qbcast<0xB1>(v);   // quad_perm [1,0,3,2]
-    return v + qbcast<0x4E>(v);   // quad_perm [2,3,0,1]
-}
-// sum over the 4 quads of the row: ror 8 pairs quads (0,2), (1,3), then ror 4 pairs the two
-// partial sums — every lane forms (v0 + v2) + (v1 + v3) in the same association, so E and G
-// (and hence K) are bitwise identical in every quad.  (ror 4 first gives each quad its own
-// association: K then differs by rounding between the rows of W, and the non-stationary
-// P_ = Q + AᵀPA − GᵀK amplified that along ill-conditioned horizons.)
-template <typename T> __device__ __forceinline__ T rsum(T v)
-{
-#pragma clang fp contract(off)
-    v += qbcast<0x128>(v);  // row_ror:8
-    return v + qbcast<0x124>(v);   // row_ror:4
-}
-
 template <typename T, int MP, bool SOA>
 __global__ __launch_bounds__(64) void dp_hex_kernel(const DpArgs a)
 {
@@ -783,17 +763,22 @@ __global__ __launch_bounds__(64) void dp_hex_kernel(const DpArgs a)
     const int qs[4] = {i, q1, q2, q3};
     auto Ael = [&](int r, int c) { return (r < n && c < n) ? Ag[(r + c * n) * es] : (T)0; };
     T p = (i < n && j < n) ? ((const T *)a.Qf + tb(nn))[(i + j * n) * es] : (T)0;   // :58 P = Qf
-    const T qij = (i < n && j < n) ? Qg[(i + j * n) * es] : (T)0, aij = Ael(i, j);
+    const T qij = (i < n && j < n) ? Qg[(i + j * n) * es] : (T)0;
     T Acolj[NP], Acoef[NP];
 #pragma unroll
     for (int l = 0; l < NP; ++l) {
         Acolj[l] = Ael(l, j);          // A[l][j]       (PA)
         Acoef[l] = Ael(qs[l], i);      // A[q_s][i]     (P_, W from quad q_s)
     }
-    T Bj[MP], Bi[MP], R[MP][MP];
+    T Bl[NP][MP], Bi[MP], R[MP][MP], Arow[NP];
+#pragma unroll
+    for (int l = 0; l < NP; ++l) {
+        Arow[l] = Ael(i, l);           // A[i][l]       (rollout)
+#pragma unroll
+        for (int c = 0; c < MP; ++c) Bl[l][c] = (l < n && c < m) ? Bg[(l + c * n) * es] : (T)0;
+    }
 #pragma unroll
     for (int c = 0; c < MP; ++c) {
-        Bj[c] = (j < n && c < m) ? Bg[(j + c * n) * es] : (T)0;
         Bi[c] = (i < n && c < m) ? Bg[(i + c * n) * es] : (T)0;
 #pragma unroll
         for (int d = 0; d < MP; ++d)
@@ -805,20 +790,43 @@ __global__ __launch_bounds__(64) void dp_hex_kernel(const DpArgs a)
     if (Pall && own) Pall[((int64_t)(N - 1) * nn + i + j * n) * es] = p;
     int info = 0;
     for (int k = N - 1; k >= 1; --k) {   // :61
+        const T P0 = qfrom<0>(p), P1 = qfrom<1>(p), P2 = qfrom<2>(p), P3 = qfrom<3>(p);
         T PB[MP];
 #pragma unroll
-        for (int c = 0; c < MP; ++c) PB[c] = qsum(p * Bj[c]);      // :38 PB[i][c]
-        const T P0 = qfrom<0>(p), P1 = qfrom<1>(p), P2 = qfrom<2>(p), P3 = qfrom<3>(p);
+        for (int c = 0; c < MP; ++c) {                              // :38 PB[i][c] (same in the quad)
+            T sv = P0 * Bl[0][c];
+            sv = fma(P1, Bl[1][c], sv);
+            sv = fma(P2, Bl[2][c], sv);
+            PB[c] = fma(P3, Bl[3][c], sv);
+        }
         T pa = P0 * Acolj[0];                                       // :40 PA[i][j]
         pa = fma(P1, Acolj[1], pa);
         pa = fma(P2, Acolj[2], pa);
         pa = fma(P3, Acolj[3], pa);
+        // PB[t][·] of every row t (lane 4t of the DPP row holds it) → E, G by the quad kernel's
+        // FMA chains, the same value in every lane of the row
+        T PBt[NP][MP];
+#pragma unroll
+        for (int c = 0; c < MP; ++c) {
+            PBt[0][c] = qbcast<0x150>(PB[c]);                       // row_newbcast:0
+            PBt[1][c] = qbcast<0x154>(PB[c]);                       // row_newbcast:4
+            PBt[2][c] = qbcast<0x158>(PB[c]);                       // row_newbcast:8
+            PBt[3][c] = qbcast<0x15C>(PB[c]);                       // row_newbcast:12
+        }
         T E[MP][MP], G[MP];
 #pragma unroll
         for (int c = 0; c < MP; ++c) {
 #pragma unroll
-            for (int d = 0; d <= c; ++d) E[c][d] = R[c][d] + rsum(Bi[c] * PB[d]);   // :39
-            G[c] = rsum(PB[c] * aij);                               // :41 G[c][j]
+            for (int d = 0; d <= c; ++d) {                          // :39 E = R + BᵀPB
+                T sv = R[c][d];
+#pragma unroll
+                for (int t = 0; t < NP; ++t) sv = fma(Bl[t][c], PBt[t][d], sv);
+                E[c][d] = sv;
+            }
+            T sv = PBt[0][c] * Acolj[0];                            // :41 G[c][j] = Σ_t PB[t][c]A[t][j]
+#pragma unroll
+            for (int t = 1; t < NP; ++t) sv = fma(PBt[t][c], Acolj[t], sv);
+            G[c] = sv;
         }
         // :29 potrf 'U' of E (replicated), :30 potrs for column j: K[:, j] = E⁻¹G[:, j]
         T L[MP][MP], Linv[MP];
@@ -907,13 +915,23 @@ __global__ __launch_bounds__(64) void dp_hex_kernel(const DpArgs a)
 #pragma unroll
             for (int c = 0; c < MP; ++c) Kc[c] = ring[d][c];
             fetch(k + RD, ring[d]);
+            // x and K_k's rows by quad broadcasts, then the quad kernel's FMA chains: every lane
+            // of the quad forms the same u and (Ax + Bu)[i]
+            const T x0v = qfrom<0>(xj), x1v = qfrom<1>(xj), x2v = qfrom<2>(xj), x3v = qfrom<3>(xj);
             T u[MP];
 #pragma unroll
             for (int c = 0; c < MP; ++c) {
-                u[c] = -qsum(Kc[c] * xj);                           // u = −K x (replicated)
+                T sv = qfrom<0>(Kc[c]) * x0v;                       // u = −K x
+                sv = fma(qfrom<1>(Kc[c]), x1v, sv);
+                sv = fma(qfrom<2>(Kc[c]), x2v, sv);
+                sv = fma(qfrom<3>(Kc[c]), x3v, sv);
+                u[c] = -sv;
                 if (r16 == c && c < m) Ub[((int64_t)(k - 1) * m + c) * es] = u[c];
             }
-            T xi = qsum(aij * xj);                                  // (A x)[i]
+            T xi = Arow[0] * x0v;                                   // (A x)[i]
+            xi = fma(Arow[1], x1v, xi);
+            xi = fma(Arow[2], x2v, xi);
+            xi = fma(Arow[3], x3v, xi);
 #pragma unroll
             for (int c = 0; c < MP; ++c) xi = fma(Bi[c], u[c], xi); // + (B u)[i]
             if (j == 0 && i < n) Xb[((int64_t)k * n + i) * es] = xi;

@@ -77,6 +77,7 @@ class LsDesc(C.Structure):
 _VP = C.c_void_p
 _SIGS = {
     "lqrx_abi_version": (C.c_int, []),
+    "lqrx_build_info": (C.c_char_p, []),
     "lqrx_last_error": (C.c_char_p, []),
     "lqrx_get_last_error": (C.c_int, [C.c_char_p, C.c_size_t]),
     "lqrx_device_available": (C.c_int, []),
@@ -151,3 +152,29 @@ def check(code: int) -> int:
     if code < 0:
         raise LqrxError(code, load().lqrx_last_error().decode())
     return code
+
+
+def source_hash(root: str | None = None) -> str:
+    """SHA-256 of the library sources exactly as the Makefile hashes them (csrc/*.hip, *.h,
+    *.cpp in sorted name order, then include/lqrx.h)."""
+    import glob
+    import hashlib
+
+    root = root or os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    csrc = os.path.join(root, "lqr.jl_amd", "csrc")
+    names = sorted(os.path.basename(f) for pat in ("*.hip", "*.h", "*.cpp")
+                   for f in glob.glob(os.path.join(csrc, pat)))
+    h = hashlib.sha256()
+    for f in [os.path.join(csrc, nm) for nm in names] + [os.path.join(root, "include", "lqrx.h")]:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def build_info() -> dict:
+    """The loaded library's build record and whether it matches the sources in this tree."""
+    info = load().lqrx_build_info().decode()
+    fields = dict(kv.split("=", 1) for kv in info.split(" ") if "=" in kv)
+    tree = source_hash()
+    return {"info": info, "src_sha256": fields.get("src_sha256"), "tree_sha256": tree,
+            "matches_tree": fields.get("src_sha256") == tree}

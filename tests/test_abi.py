@@ -253,3 +253,14 @@ def test_julia_shim_ccalls_resolve(lqrx):
     lib = lqrx.load()
     for s in sorted(syms):
         assert hasattr(lib, s), s
+
+
+def test_library_built_from_these_sources(lqrx):
+    """Build provenance: the loaded liblqrx.so carries the SHA-256 of the
+    sources it was compiled from (lqrx_build_info); it must equal the hash of the sources in
+    this tree, so the binary that travels to the GPU box is the one these sources build."""
+    from lqrx import _lib
+
+    b = _lib.build_info()
+    assert b["src_sha256"] and len(b["src_sha256"]) == 64, b
+    assert b["matches_tree"], b

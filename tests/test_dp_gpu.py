@@ -178,3 +178,13 @@ def test_per_knot_reference_call_shape(lqrx, gpu_ok):
     full = lqrx.LQRSolution.of(prob)
     lqrx.solve(full, lqrx.DPSolver.of(prob), prob)
     assert np.abs(sol.K[0] - full.K[N - 2]).max() <= 1e-12 * np.abs(full.K[N - 2]).max()
+
+
+def test_gpu_run_uses_library_built_from_tree(lqrx, gpu_ok):
+    """On the GPU box: the library these GPU tests load was built from the sources shipped
+    with them (lqrx_build_info's source hash = the tree's; see tests/test_abi.py)."""
+    from lqrx import _lib
+
+    b = _lib.build_info()
+    print(b["info"])
+    assert b["matches_tree"], b
