@@ -53,7 +53,7 @@ def _dp_kernel_name(n, m, bt, tv, lin=False):
     """Which DP kernel lqrx_dp_solve dispatches to (mirrors dp_launch / dp_lane_launch)."""
     if n <= 4 and m <= 4:
         small = os.environ.get("LQRX_DP_SMALL", "")
-        hex_ = not tv and not lin and (small.startswith("h") or (not small[:1] in ("l", "q") and bt <= 8192))
+        hex_ = not tv and not lin and small.startswith("h")
         if hex_:
             return "dp_hex_kernel"
         quad = n >= 3 and not tv and (small.startswith("q") or (not small.startswith("l") and bt <= 16384))

@@ -990,15 +990,15 @@ static hipError_t launch_quad(const DpArgs &a, hipStream_t s)
     return hipGetLastError();
 }
 
-// hex kernel (16 lanes per trajectory) while 16·batch lanes fit ≤ 2 waves per SIMD; n ≤ 4,
-// m ≤ 4, time-invariant, no linear terms.  LQRX_DP_SMALL=hex forces it (tests).
+// hex kernel (16 lanes per trajectory; n ≤ 4, m ≤ 4, time-invariant, no linear terms): an
+// A/B alternative selected by LQRX_DP_SMALL=hex only — measured slower than the quad kernel
+// on cfg2 (0.082 vs 0.055 ms): the replicated m-sized work and the broadcasts
+// leave each lane about as many dependent instructions per knot as the quad's lane has.
 static bool use_hex(const DpArgs &a)
 {
     if (a.tv_AB || a.tv_QR || a.lin || a.n > 4 || a.m > 4) return false;
     const char *e = std::getenv("LQRX_DP_SMALL");
-    if (e && e[0] == 'h') return true;
-    if (e && (e[0] == 'l' || e[0] == 'q')) return false;
-    return a.batch <= 8192;
+    return e && e[0] == 'h';
 }
 
 hipError_t dp_lane_launch(const DpArgs &a, hipStream_t s)

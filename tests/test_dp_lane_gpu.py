@@ -171,7 +171,7 @@ def test_time_varying_parity(lqrx, oracle, gpu_ok, n, m, tv_ab, tv_qr, N, bt):
 def test_small_kernel_modes(lqrx, oracle, gpu_ok, monkeypatch, mode, n, m, N, batch):
     """The three small-n kernels — one lane per trajectory (dp_lane_kernel), one quad per
     trajectory (dp_quad_kernel, n ∈ {3, 4}, batch ≤ 16384) and sixteen lanes per trajectory
-    (dp_hex_kernel, the default for batch ≤ 8192) — against the oracle; LQRX_DP_SMALL selects
+    (dp_hex_kernel, an A/B alternative) — against the oracle; LQRX_DP_SMALL selects
     the kernel per call."""
     if mode == "quad" and n < 3:
         pytest.skip("the quad kernel serves n in {3, 4}")
@@ -183,8 +183,7 @@ def test_small_kernel_modes(lqrx, oracle, gpu_ok, monkeypatch, mode, n, m, N, ba
 
 
 def test_small_kernel_auto_large_batch(lqrx, oracle, gpu_ok):
-    """batch > 16384 at n = 4 selects the lane kernel (auto; 8192 < batch ≤ 16384 the quad
-    kernel, below that the hex kernel)."""
+    """batch > 16384 at n = 4 selects the lane kernel (auto; the quad kernel below)."""
     got, ref = run_pair(lqrx, oracle, 4, 1, 12, 16384 + 70, seed=77)
     assert got["rc"] == 0
     assert_parity(got, ref, lqrx.random_batch(4, 1, 12, 16384 + 70, 77), 12)
