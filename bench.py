@@ -721,9 +721,12 @@ def main(argv=None):
                         "unit": "GB/s", "frac": alg_bytes / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                         "kernel": "kkt_fild_kernel (compile-time direct shape, lqrx_kkt_fil.hip)"}
             else:
+                big = max(n, m) <= 64 and n + m <= 128        # blocks the large-block kernels take
+                kname = ("kb_fuse_mid_kernel (interior knots) + kb_bwd_kernel, kb_schur/kb_factor at the "
+                         "ends (lqrx_kkt_big.hip)" if big else
+                         "kkt_wg_kernel (workgroup per trajectory, blocks past 64 rows, lqrx_kkt_wg.hip)")
                 roof = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                        "frac": achieved / peak,
-                        "kernel": "kb_schur_kernel + kb_factor_kernel + kb_bwd_kernel (split path, lqrx_kkt_big.hip)"}
+                        "frac": achieved / peak, "kernel": kname}
             roof.update({"traffic": traffic, "traffic_source": tsrc, "kernel_ms": kern_ms,
                     "flops_per_traj_minimal": fl_min, "flops_per_traj_reference": fl_ref,
                     "reference_count_tflops": fl_ref * bt / (kern_ms * 1e-3) / 1e12,
