@@ -44,6 +44,31 @@ template <typename T> struct Mat {
 template <typename T> __device__ __forceinline__ Mat<T> cm(const T *p, int ld) { return Mat<T>{p, 1, (size_t)ld}; }
 template <typename T> __device__ __forceinline__ Mat<T> cmt(const T *p, int ld) { return Mat<T>{p, (size_t)ld, 1}; }
 
+// D ±= Mᵀ·Y over kk contraction rows for output tile (it, jt): the operand tiles of k-step
+// kt+1 are loaded before the MFMAs of step kt (their L2 latency overlaps the products)
+template <typename T, int S>
+__device__ __forceinline__ void wg_mm_k(typename Tile<T>::acc &D, Mat<T> M, Mat<T> Y, int kk, int r, int c, int it,
+                                        int jt, int lane)
+{
+    using acc = typename Tile<T>::acc;
+    const int nk = (kk + 15) / 16;
+    if (nk == 0) return;
+    acc Mt, Yt;
+    tile_ld<T>(Mt, M.at(0, it * 16), kk, r - it * 16, M.rs, M.cs, lane);
+    tile_ld<T>(Yt, Y.at(0, jt * 16), kk, c - jt * 16, Y.rs, Y.cs, lane);
+    for (int kt = 0; kt < nk; ++kt) {
+        acc Mn = Mt, Yn = Yt;
+        if (kt + 1 < nk) {
+            tile_ld<T>(Mn, M.at((kt + 1) * 16, it * 16), kk - (kt + 1) * 16, r - it * 16, M.rs, M.cs, lane);
+            tile_ld<T>(Yn, Y.at((kt + 1) * 16, jt * 16), kk - (kt + 1) * 16, c - jt * 16, Y.rs, Y.cs, lane);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) D = S > 0 ? Tile<T>::mma(Mt[q], Yt[q], D) : Tile<T>::mma_nega(Mt[q], Yt[q], D);
+        Mt = Mn;
+        Yt = Yn;
+    }
+}
+
 // Workgroup product on the MFMA pipe: C (r×c, column-major, ldc) = [Cin] + S1·M1ᵀ·Y1 + S2·M2ᵀ·Y2
 // (S1, S2 ∈ {+1, −1}), M1 kk1×r, Y1 kk1×c (M2 kk2×r, Y2 kk2×c; kk = 0 drops a product).  The 4
 // waves take the 16×16 output tiles round-robin and stream the k-tiles of their operands from
@@ -60,20 +85,8 @@ __device__ __forceinline__ void wg_mm(T *C, int ldc, int r, int c, const T *Cin,
         acc D;
         if (Cin) tile_ld<T>(D, Cin + it * 16 + (size_t)jt * 16 * ldc, r - it * 16, c - jt * 16, 1, ldc, lane);
         else D = acc{0, 0, 0, 0};
-        for (int kt = 0; kt < (kk1 + 15) / 16; ++kt) {
-            acc Mt, Yt;
-            tile_ld<T>(Mt, M1.at(kt * 16, it * 16), kk1 - kt * 16, r - it * 16, M1.rs, M1.cs, lane);
-            tile_ld<T>(Yt, Y1.at(kt * 16, jt * 16), kk1 - kt * 16, c - jt * 16, Y1.rs, Y1.cs, lane);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) D = S1 > 0 ? Tile<T>::mma(Mt[q], Yt[q], D) : Tile<T>::mma_nega(Mt[q], Yt[q], D);
-        }
-        for (int kt = 0; kt < (kk2 + 15) / 16; ++kt) {
-            acc Mt, Yt;
-            tile_ld<T>(Mt, M2.at(kt * 16, it * 16), kk2 - kt * 16, r - it * 16, M2.rs, M2.cs, lane);
-            tile_ld<T>(Yt, Y2.at(kt * 16, jt * 16), kk2 - kt * 16, c - jt * 16, Y2.rs, Y2.cs, lane);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) D = S2 > 0 ? Tile<T>::mma(Mt[q], Yt[q], D) : Tile<T>::mma_nega(Mt[q], Yt[q], D);
-        }
+        wg_mm_k<T, S1>(D, M1, Y1, kk1, r, c, it, jt, lane);
+        wg_mm_k<T, S2>(D, M2, Y2, kk2, r, c, it, jt, lane);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int row = it * 16 + Tile<T>::row(lane, q), col = jt * 16 + tcol(lane);
@@ -94,59 +107,104 @@ template <typename T> __device__ __forceinline__ T wsqrt(T x) { return sqrt(x); 
 // A ← U with A = UᵀU (p×p, column-major, ld; only the upper triangle is read or written).
 // Returns 0, or j+1 for the first pivot j that is not positive (LAPACK's info; the factor
 // stops there, as dpotrf does).  The return value is uniform over the workgroup.
+// Per 16-row block: the rows above are subtracted by one wg_mm, then the block row is factored
+// with each thread holding its column's 16 entries in registers; the pivot column of each row
+// is published in LDS (one barrier per row), columns past the first 256 follow without barriers.
 template <typename T> __device__ int wg_potrf(T *A, int ld, int p, int tid)
 {
+    __shared__ T pcol[16 * 16];   // pcol[q + 16j] = U[jb+q][jb+j] (q < j), pcol[j + 16j] = U_jj
     for (int jb = 0; jb < p; jb += 16) {
         const int nb = min(16, p - jb);
         if (jb) {   // block row jb: A[jb:jb+nb, jb:p] −= U[0:jb, jb:jb+nb]ᵀ · U[0:jb, jb:p]
             T *blk = A + jb + (size_t)jb * ld;
             wg_mm1<T, -1>(blk, ld, nb, p - jb, blk, cm(A + (size_t)jb * ld, ld), cm(A + (size_t)jb * ld, ld), jb, tid);
-            __syncthreads();
         }
-        for (int j = jb; j < jb + nb; ++j) {
-            T dj = A[j + (size_t)j * ld];
-            for (int q = jb; q < j; ++q) dj -= A[q + (size_t)j * ld] * A[q + (size_t)j * ld];
-            if (!(dj > (T)0)) {                                 // uniform: every thread saw the same dj
+        __syncthreads();
+        const int c0 = jb + tid;
+        const bool own = c0 < p;
+        T v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = (own && i < nb) ? A[jb + i + (size_t)c0 * ld] : (T)0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (j < nb) {
+                if (tid == j) {                                 // owner of pivot column jb + j
+                    T d = v[j];
+#pragma unroll
+                    for (int q = 0; q < j; ++q) d -= v[q] * v[q];
+                    d = d > (T)0 ? wsqrt(d) : (T)0;             // 0 (or NaN) marks the failure
+                    v[j] = d;
+#pragma unroll
+                    for (int q = 0; q < j; ++q) pcol[q + 16 * j] = v[q];
+                    pcol[j + 16 * j] = d;
+                }
                 __syncthreads();
-                return j + 1;
+                const T dj = pcol[j + 16 * j];
+                if (!(dj > (T)0)) return jb + j + 1;            // uniform: every thread read dj
+                if (own && tid > j) {
+                    T sv = v[j];
+#pragma unroll
+                    for (int q = 0; q < j; ++q) sv -= pcol[q + 16 * j] * v[q];
+                    v[j] = sv / dj;
+                }
             }
-            dj = wsqrt(dj);
-            for (int c = j + 1 + tid; c < p; c += BT) {
-                T s = A[j + (size_t)c * ld];
-                for (int q = jb; q < j; ++q) s -= A[q + (size_t)j * ld] * A[q + (size_t)c * ld];
-                A[j + (size_t)c * ld] = s / dj;
-            }
-            __syncthreads();
-            if (tid == 0) A[j + (size_t)j * ld] = dj;
-            __syncthreads();
         }
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (own && i < nb) A[jb + i + (size_t)c0 * ld] = v[i];
+        for (int c = c0 + BT; c < p; c += BT) {                 // columns past the first BT
+            T u[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) u[i] = i < nb ? A[jb + i + (size_t)c * ld] : (T)0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if (j < nb) {
+                    T sv = u[j];
+#pragma unroll
+                    for (int q = 0; q < j; ++q) sv -= pcol[q + 16 * j] * u[q];
+                    u[j] = sv / pcol[j + 16 * j];
+                }
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if (i < nb) A[jb + i + (size_t)c * ld] = u[i];
+        }
+        __syncthreads();
     }
     return 0;
 }
 
-// X ← U⁻ᵀ·X : U p×p upper (ldu), X p×c (ldx).  Forward substitution by 16-row blocks.
+// X ← U⁻ᵀ·X : U p×p upper (ldu), X p×c (ldx).  Forward substitution by 16-row blocks: the
+// block update on MFMA, the block's 16×16 triangle staged in LDS, each column's 16 unknowns
+// loaded up front into registers.
 template <typename T> __device__ void wg_trsm_ut(const T *U, int ldu, int p, T *X, int ldx, int c, int tid)
 {
+    __shared__ T ub[16 * 16];     // ub[q + 16i] = U[ib+q][ib+i], q ≤ i
     for (int ib = 0; ib < p; ib += 16) {
         const int nb = min(16, p - ib);
-        if (ib) {   // X[ib:ib+nb, :] −= U[0:ib, ib:ib+nb]ᵀ · X[0:ib, :]
+        if (ib)     // X[ib:ib+nb, :] −= U[0:ib, ib:ib+nb]ᵀ · X[0:ib, :]
             wg_mm1<T, -1>(X + ib, ldx, nb, c, X + ib, cm(U + (size_t)ib * ldu, ldu), cm<T>(X, ldx), ib, tid);
-            __syncthreads();
+        for (int e = tid; e < 256; e += BT) {
+            const int q = e & 15, i = e >> 4;
+            ub[e] = (q <= i && i < nb) ? U[ib + q + (size_t)(ib + i) * ldu] : (T)0;
         }
+        __syncthreads();
         for (int col = tid; col < c; col += BT) {
             T *x = X + ib + (size_t)col * ldx;
             T v[16];
 #pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = i < nb ? x[i] : (T)0;
+#pragma unroll
             for (int i = 0; i < 16; ++i) {
                 if (i < nb) {
-                    const T *u = U + ib + (size_t)(ib + i) * ldu;   // column ib+i of U, from row ib
-                    T s = x[i];
+                    T sv = v[i];
 #pragma unroll
-                    for (int q = 0; q < i; ++q) s -= u[q] * v[q];
-                    v[i] = s / u[i];
-                    x[i] = v[i];
+                    for (int q = 0; q < i; ++q) sv -= ub[q + 16 * i] * v[q];
+                    v[i] = sv / ub[i + 16 * i];
                 }
             }
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if (i < nb) x[i] = v[i];
         }
         __syncthreads();
     }
@@ -155,27 +213,35 @@ template <typename T> __device__ void wg_trsm_ut(const T *U, int ldu, int p, T *
 // X ← U⁻¹·X : U p×p upper (ldu), X p×c (ldx).  Backward substitution by 16-row blocks.
 template <typename T> __device__ void wg_trsm_un(const T *U, int ldu, int p, T *X, int ldx, int c, int tid)
 {
+    __shared__ T ub[16 * 16];     // ub[i + 16q] = U[ib+i][ib+q], i ≤ q
     for (int ib = ((p - 1) / 16) * 16; ib >= 0; ib -= 16) {
         const int nb = min(16, p - ib), tail = p - ib - nb;
-        if (tail) { // X[ib:ib+nb, :] −= U[ib:ib+nb, ib+nb:p] · X[ib+nb:p, :]
+        if (tail)   // X[ib:ib+nb, :] −= U[ib:ib+nb, ib+nb:p] · X[ib+nb:p, :]
             wg_mm1<T, -1>(X + ib, ldx, nb, c, X + ib, cmt(U + ib + (size_t)(ib + nb) * ldu, ldu),
                           cm<T>(X + ib + nb, ldx), tail, tid);
-            __syncthreads();
+        for (int e = tid; e < 256; e += BT) {
+            const int i = e & 15, q = e >> 4;
+            ub[e] = (i <= q && q < nb) ? U[ib + i + (size_t)(ib + q) * ldu] : (T)0;
         }
+        __syncthreads();
         for (int col = tid; col < c; col += BT) {
             T *x = X + ib + (size_t)col * ldx;
             T v[16];
 #pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = i < nb ? x[i] : (T)0;
+#pragma unroll
             for (int i = 15; i >= 0; --i) {
                 if (i < nb) {
-                    T s = x[i];
+                    T sv = v[i];
 #pragma unroll
                     for (int q = i + 1; q < 16; ++q)
-                        if (q < nb) s -= U[ib + i + (size_t)(ib + q) * ldu] * v[q];
-                    v[i] = s / U[ib + i + (size_t)(ib + i) * ldu];
-                    x[i] = v[i];
+                        if (q < nb) sv -= ub[i + 16 * q] * v[q];
+                    v[i] = sv / ub[i + 16 * i];
                 }
             }
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if (i < nb) x[i] = v[i];
         }
         __syncthreads();
     }
