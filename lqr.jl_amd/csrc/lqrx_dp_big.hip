@@ -6,10 +6,11 @@
 // trajectory global scratch block (L2-resident working set: 3n² + 2nm + m² elements); the
 // element-wise parts are spread over the workgroup one element per thread-iteration (column-major
 // order, so consecutive threads touch consecutive rows).  The reference's own sequence of
-// products is kept — PB = P·B, E = R + BᵀPB, PA = P·A, K = BᵀPA, potrf 'U' (left-looking, as
-// dpotf2), potrs, APB = AᵀPB, P_ = Q + AᵀPA − APB·K (no symmetric fast form) — the products on
-// fp64/fp32 MFMA tiles (wg_mm: the 4 waves take output tiles round-robin and stream strided
-// operand tiles from L2; lqrx_wg.h), the factor, the triangular solves and the rollout on the VALU.
+// products is kept — PB = P·B, E = R + BᵀPB, PA = P·A, K = BᵀPA, potrf 'U', potrs, APB = AᵀPB,
+// P_ = Q + AᵀPA − APB·K (no symmetric fast form) — the products on fp64/fp32 MFMA tiles (wg_mm:
+// the 4 waves take output tiles round-robin and stream strided operand tiles from L2), the factor
+// and the triangular solves blocked by 16 with their updates on MFMA too (lqrx_wg.h), the rollout
+// on the VALU.
 // Time-varying knot strides, all-P output, linear cost terms (d, p) as in the other kernels.
 #include "lqrx_internal.h"
 #include "lqrx_tile.h"
@@ -25,7 +26,6 @@ namespace {
 using wg::BT;
 using wg::Mat;
 
-template <typename T> __device__ __forceinline__ T dsqrt(T x) { return sqrt(x); }
 
 template <typename T>
 __global__ __launch_bounds__(BT) void dp_big_kernel(const DpArgs a, T *__restrict__ ws, size_t ws_elems, int64_t b0)
@@ -94,50 +94,22 @@ __global__ __launch_bounds__(BT) void dp_big_kernel(const DpArgs a, T *__restric
         wg::wg_mm<T, 1, 1>(K, m, m, n, nullptr, Bm, PAm, n, none, none, 0, tid);
         wg::wg_mm<T, 1, 1>(APB, n, n, m, nullptr, Am, PBm, n, none, none, 0, tid);
         __syncthreads();
-        // :29 potrf!('U', E) — left-looking dpotf2; a failed pivot stops the factor (as LAPACK)
-        bool failed = false;
-        for (int j = 0; j < m; ++j) {
-            T dj = E[j + (size_t)j * m];
-            for (int p = 0; p < j; ++p) dj -= E[p + (size_t)j * m] * E[p + (size_t)j * m];
-            if (!(dj > (T)0)) {
-                failed = true;                                  // uniform: every thread saw the same dj
-                if (tid == 0) {
-                    E[j + (size_t)j * m] = dj;
-                    if (s_info == 0) s_info = k;
-                }
-                break;
-            }
-            dj = dsqrt(dj);
-            for (int c = j + 1 + tid; c < m; c += BT) {
-                T s = E[j + (size_t)c * m];
-                for (int p = 0; p < j; ++p) s -= E[p + (size_t)j * m] * E[p + (size_t)c * m];
-                E[j + (size_t)c * m] = s / dj;
-            }
-            __syncthreads();
-            if (tid == 0) E[j + (size_t)j * m] = dj;
-            __syncthreads();
-        }
-        (void)failed;
+        // :29 potrf!('U', E) — blocked left-looking (lqrx_wg.h); a failed pivot stops the factor
+        // (as LAPACK) and reports this knot
+        const int f = wg::wg_potrf<T>(E, m, m, tid);
+        if (f && tid == 0 && s_info == 0) s_info = k;
+        // :30 potrs!('U', E, K): K ← E⁻¹K by two blocked triangular solves; the linear terms'
+        // w is one more right-hand side (d, written to its output)
+        if (lin)
+            for (int i = tid; i < m; i += BT) db[(size_t)(k - 1) * m + i] = wv[i];
         __syncthreads();
-        // :30 potrs!('U', E, K) — one column per thread (Uᵀy = K[:,j], then U x = y); the linear
-        // terms' w is one more column (d, written to its output)
-        for (int j = tid; j < n + (lin ? 1 : 0); j += BT) {
-            T *x = j < n ? K + (size_t)j * m : db + (size_t)(k - 1) * m;
-            if (j == n) {
-                for (int i = 0; i < m; ++i) x[i] = wv[i];
-            }
-            for (int i = 0; i < m; ++i) {
-                T s = x[i];
-                for (int p = 0; p < i; ++p) s -= E[p + (size_t)i * m] * x[p];
-                x[i] = s / E[i + (size_t)i * m];
-            }
-            for (int i = m - 1; i >= 0; --i) {
-                T s = x[i];
-                for (int p = i + 1; p < m; ++p) s -= E[i + (size_t)p * m] * x[p];
-                x[i] = s / E[i + (size_t)i * m];
-            }
+        wg::wg_trsm_ut<T>(E, m, m, K, m, n, tid);
+        wg::wg_trsm_un<T>(E, m, m, K, m, n, tid);
+        if (lin) {
+            T *x = db + (size_t)(k - 1) * m;
+            wg::wg_trsm_ut<T>(E, m, m, x, m, 1, tid);
+            wg::wg_trsm_un<T>(E, m, m, x, m, 1, tid);
         }
-        __syncthreads();
         // :51 P_ = Q + A'PA − APB*K  (APB·K = (APBᵀ)ᵀ·K)   (and p_ = q + A'p − APB*d)
         {
             const Mat<T> APBt{APB, (size_t)n, 1}, Km{K, 1, (size_t)m};
