@@ -2524,6 +2524,19 @@ constexpr int KBW_W = 2080;
 #ifndef KBW_RUN
 #define KBW_RUN 32
 #endif
+// D2 columns the backward kernel holds in registers between its two uses (fp32; 2 = off, the
+// array is then a dummy).  KBW_NOHOLD=1 restores the second pass over D2 (A/B).
+#ifndef KBW_NOHOLD
+#define KBW_NOHOLD 0
+#endif
+__device__ __forceinline__ float rdlane(float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l)); }
+__device__ __forceinline__ double rdlane(double v, int l)
+{
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+template <typename T> constexpr int kbw_hold() { return (sizeof(T) == 4 && !KBW_NOHOLD) ? 96 : 2; }
 constexpr int KBW_VC = KBW_VC_COLS;  // columns of Y in flight per lane in the v product
 constexpr int KBW_R = KBW_RUN;       // column-run elements in flight per lane (t, D2ᵀλ)
 
@@ -2634,7 +2647,7 @@ __global__ void __launch_bounds__(64 * KF_W) kb_bwd_kernel(KbArgs<T> a, int64_t 
             graw[u] = (c < qj.w && a.ginv) ? gt[qj.og + c] : (T)0;
         }
         // t = [C; D1]ᵀ[μ_j; λ_j] (calc_residual!'s Cᵀμ + D1ᵀλ, :219-231), lane = column
-        T tc[2], hc[2];
+        T tc[2], hc[2], tbv[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int c = lane + 64 * u;
@@ -2643,11 +2656,18 @@ __global__ void __launch_bounds__(64 * KF_W) kb_bwd_kernel(KbArgs<T> a, int64_t 
                 tt = dot_run<T>(Yk + (int64_t)c * qj.rows + qj.p1, xb, nr, vt);
                 h = (a.ginv && !a.hfac) ? (T)1 / hraw[u] : (T)1;
                 tb[c] = tt * h;
+            } else {
+                tb[c] = (T)0;
             }
+            tbv[u] = c < qj.w ? tt * h : (T)0;          // column c's t·h in lane c (held-D2 path)
             tc[u] = tt;
             hc[u] = h;
         }
         wsync();
+        // fp32, w ≤ KBW_HOLD: knot j's D2 rows stay in registers (lane = row) from the v product
+        // to D2ᵀλ_{j−1}, so D2 is read once per knot instead of twice
+        T d2[kbw_hold<T>()];
+        const bool hold = kbw_hold<T>() > 2 && qj.w <= kbw_hold<T>();
         Kn qp = qj;
         if (j > 0) {
             qp = kn_load(a.meta, j - 1);
@@ -2680,7 +2700,24 @@ __global__ void __launch_bounds__(64 * KF_W) kb_bwd_kernel(KbArgs<T> a, int64_t 
                 }
             }
             // v = D2 H⁻¹ t = D_{k+1}μ_{k+1} + F_{k+1}λ_{k+1}, lane = row (coalesced columns, 16 in flight)
-            {
+            if (hold) {
+                // every D2 column in flight at once, and kept in registers for D2ᵀλ_{j−1} below
+                // (the second pass over D2 was ~30 % of this kernel's fabric traffic)
+                const int rl = lane < qj.p1 ? lane : 0;
+                const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+                    (void *)Yk, (short)0, (int)(qj.rows * qj.w * sizeof(T)), 0x00020000);
+                __builtin_amdgcn_sched_barrier(0);       // not hoisted over the W staging above
+#pragma unroll
+                for (int c = 0; c < kbw_hold<T>(); ++c)      // uniform column offset in soffset
+                    d2[c] = bload<T>(yrs, (uint32_t)rl * sizeof(T), (uint32_t)((c < qj.w ? c : 0) * qj.rows * sizeof(T)));
+                T s0 = (T)0, s1 = (T)0;
+#pragma unroll
+                for (int c = 0; c < kbw_hold<T>(); c += 2) {  // tbv is 0 past w (set above)
+                    s0 = fma(d2[c], rdlane(tbv[c >> 6], c & 63), s0);
+                    s1 = fma(d2[c + 1], rdlane(tbv[(c + 1) >> 6], (c + 1) & 63), s1);
+                }
+                vb[lane] = lane < qj.p1 ? s0 + s1 : (T)0;
+            } else {
                 T s0 = (T)0, s1 = (T)0;
                 const int rl = lane < qj.p1 ? lane : 0;
                 for (int c0 = 0; c0 < qj.w; c0 += KBW_VC) {
@@ -2743,12 +2780,40 @@ __global__ void __launch_bounds__(64 * KF_W) kb_bwd_kernel(KbArgs<T> a, int64_t 
             lb[lane] = -nl;
             wsync();
         }
+        if (hold && j > 0) {
+            // D2ᵀλ_{j−1} from the held rows: per-lane products, column sums by a 16-column LDS
+            // transpose (row stride 17: conflict-free both ways) and two lane exchanges; the sums
+            // land in tb (dead since the v product).  W_{j−1} (wl) is dead once λ_{j−1} is formed.
+            const T lr = lane < qj.p1 ? lb[lane] : (T)0;
+            T *red = wl;
+            const int cc = lane & 15, q4 = lane >> 4;
+#pragma unroll
+            for (int c0 = 0; c0 < kbw_hold<T>(); c0 += 16) {
+                if (c0 < qj.w) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) red[lane * 17 + i] = d2[c0 + i] * lr;
+                    wsync();
+                    T s0 = (T)0, s1 = (T)0;
+#pragma unroll
+                    for (int i = 0; i < 16; i += 2) {
+                        s0 += red[(q4 * 16 + i) * 17 + cc];
+                        s1 += red[(q4 * 16 + i + 1) * 17 + cc];
+                    }
+                    T s = s0 + s1;
+                    s += __shfl_xor(s, 16);
+                    s += __shfl_xor(s, 32);
+                    wsync();
+                    if (lane < 16) tb[c0 + lane] = s;
+                }
+            }
+            wsync();
+        }
         // δz_j = −H⁻¹(t + D2ᵀλ_{j−1} + g)  (calc_residual! + calc_primals!, :195-236), lane = column
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int c = lane + 64 * u;
             if (c < qj.w) {
-                const T sd = j > 0 ? dot_run<T>(Yk + (int64_t)c * qj.rows, lb, qj.p1, vs) : (T)0;
+                const T sd = j > 0 ? (hold ? tb[c] : dot_run<T>(Yk + (int64_t)c * qj.rows, lb, qj.p1, vs)) : (T)0;
                 const T res = tc[u] + sd + graw[u];
                 if (a.hfac) tb[c] = res;
                 else dzt[qj.og + c] = -(res * hc[u]);
