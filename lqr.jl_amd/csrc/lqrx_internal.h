@@ -57,6 +57,9 @@ struct KktArgs {
     const int32_t *sel, *nsel;
     void *ws;         // caller's device workspace (lqrx_kkt_solve_ws) or NULL: library pool
     size_t ws_bytes;
+    // runtime (n̄, m, P0, PK, PN) of a trajectory-form structure solved on a padded compile-time
+    // shape (lqrx_kkt_fil.hip, Shape<…, PAD>); unused otherwise
+    int32_t rt[5];
 };
 
 hipError_t kkt_launch(const KktArgs &a, hipStream_t s);

@@ -26,6 +26,7 @@
 #include "lqrx_internal.h"
 #include "lqrx_stage.h"
 #include "lqrx_tile.h"
+#include <cstdlib>
 #include <type_traits>
 
 namespace lqrx {
@@ -52,9 +53,18 @@ using NoCls = Cls<0, 0, 0, 0>;
 
 // SOA = ABI layout 1 (batch fastest): element e of a trajectory's packed array at [e·batch + t],
 // so the 64 trajectories of a wave read one element as a contiguous 512-B row
-template <int NX_, int M_, int P0_, int PK_, int PN_, bool HDIAG_, bool GINV_, bool SOA_ = false> struct Shape {
+// PAD (direct kernel, layout 0): the compile-time sizes are MAXIMA and the structure's own
+// (n̄, m, P0, PK, PN) come at run time (KktArgs::rt, struct Rt below): every block is zero-padded
+// in registers — padded Y rows/columns and g read as 0, padded H as 1, a padded constraint row
+// gets a unit Schur pivot (decoupled: its off-diagonal entries are exact zeros), padded δz/λ
+// entries are never stored.  The real entries see the same operations in the same order as on
+// the exact shape (the padding only adds exact zeros), so one instantiation serves every
+// smaller trajectory structure.
+template <int NX_, int M_, int P0_, int PK_, int PN_, bool HDIAG_, bool GINV_, bool SOA_ = false, bool PAD_ = false>
+struct Shape {
     static constexpr int NX = NX_, M = M_;
-    static constexpr bool HDIAG = HDIAG_, GINV = GINV_, SOA = SOA_;
+    static constexpr bool HDIAG = HDIAG_, GINV = GINV_, SOA = SOA_, PAD = PAD_;
+    static_assert(!PAD_ || !SOA_, "padded shapes read layout 0");
     using F = Cls<0, P0_, NX_, NX_ + M_>;
     using I = Cls<NX_, PK_, NX_, NX_ + M_>;
     using L = Cls<NX_, PN_, 0, NX_>;
@@ -118,6 +128,86 @@ template <class S> struct Off {
     __device__ static int64_t y(int k) { return k == 0 ? 0 : S::template Ly<typename S::F>() + (int64_t)(k - 1) * S::template Ly<typename S::I>(); }
     __device__ static int64_t H(int k) { return k == 0 ? 0 : S::template LH<typename S::F>() + (int64_t)(k - 1) * S::template LH<typename S::I>(); }
     __device__ static int64_t g(int k) { return k == 0 ? 0 : S::template Lg<typename S::F>() + (int64_t)(k - 1) * S::template Lg<typename S::I>(); }
+};
+
+// runtime block sizes of a padded shape (S::PAD): packed offsets of the real structure and the
+// padded → real row / column maps of each knot class (uniform values: scalar registers)
+struct Rt {
+    int nx = 0, m = 0, p0 = 0, pk = 0, pn = 0;
+    int64_t LYF = 0, LYI = 0, LyF = 0, LyI = 0, Lg = 0;
+    // the wave's array bases (trajectory t0) and this lane's byte offsets from them: inputs are
+    // buffer loads with the element offset in the scalar soffset (no per-element address math;
+    // host-checked: 64 trajectories of any array span < 2 GiB)
+    const double *bY = nullptr, *bH = nullptr, *bg = nullptr, *by = nullptr;
+    uint32_t vY = 0, vH = 0, vg = 0, vy = 0;
+    __device__ __forceinline__ void lanes(const KktArgs &a, int64_t t0, int64_t t)
+    {
+        bY = a.Y + t0 * a.sY; bH = a.H + t0 * a.sH; bg = a.g + t0 * a.sg; by = a.y + t0 * a.sy;
+        vY = (uint32_t)((t - t0) * a.sY * 8); vH = (uint32_t)((t - t0) * a.sH * 8);
+        vg = (uint32_t)((t - t0) * a.sg * 8); vy = (uint32_t)((t - t0) * a.sy * 8);
+    }
+    __device__ __forceinline__ void init(const KktArgs &a)
+    {
+        nx = a.rt[0]; m = a.rt[1]; p0 = a.rt[2]; pk = a.rt[3]; pn = a.rt[4];
+        LYF = (int64_t)(p0 + nx) * (nx + m);
+        LYI = (int64_t)(2 * nx + pk) * (nx + m);
+        LyF = p0 + nx;
+        LyI = pk + nx;
+        Lg = nx + m;
+    }
+    // a copy whose sizes the compiler cannot see through: every offset / map derived from it is
+    // recomputed where it is used (scalar ALU, cheap) instead of being hoisted out of the knot
+    // loop into hundreds of live scalar registers (which spilled)
+    __device__ __forceinline__ Rt fresh() const
+    {
+        Rt r = *this;
+        asm volatile("" : "+s"(r.nx), "+s"(r.m), "+s"(r.p0), "+s"(r.pk), "+s"(r.pn));
+        r.LYF = (int64_t)(r.p0 + r.nx) * (r.nx + r.m);
+        r.LYI = (int64_t)(2 * r.nx + r.pk) * (r.nx + r.m);
+        r.LyF = r.p0 + r.nx;
+        r.LyI = r.pk + r.nx;
+        r.Lg = r.nx + r.m;
+        return r;
+    }
+    __device__ __forceinline__ int64_t oY(int k) const { return k == 0 ? 0 : LYF + (int64_t)(k - 1) * LYI; }
+    __device__ __forceinline__ int64_t oy(int k) const { return k == 0 ? 0 : LyF + (int64_t)(k - 1) * LyI; }
+    __device__ __forceinline__ int64_t og(int k) const { return (int64_t)k * Lg; }   // diag H: oH = og
+    // real (p1, ps, p2) of class C of shape S: first (0, P0, n̄), interior (n̄, PK, n̄), last (n̄, PN, 0)
+    template <class S, class C> __device__ __forceinline__ void cls(int &p1, int &ps, int &p2) const
+    {
+        if constexpr (std::is_same<C, typename S::F>::value) { p1 = 0; ps = p0; p2 = nx; }
+        else if constexpr (std::is_same<C, typename S::I>::value) { p1 = nx; ps = pk; p2 = nx; }
+        else { p1 = nx; ps = pn; p2 = 0; }
+    }
+    template <class S, class C> __device__ __forceinline__ int R() const
+    {
+        int p1, ps, p2;
+        cls<S, C>(p1, ps, p2);
+        return p1 + ps + p2;
+    }
+    // padded row i of Y = [D2; C; D1] (class C) → real row, or −1
+    template <class S, class C> __device__ __forceinline__ int row(int i) const
+    {
+        int p1, ps, p2;
+        cls<S, C>(p1, ps, p2);
+        if (i < C::P1) return i < p1 ? i : -1;
+        if (i < C::P1 + C::PS) return i - C::P1 < ps ? p1 + (i - C::P1) : -1;
+        return i - C::P1 - C::PS < p2 ? p1 + ps + (i - C::P1 - C::PS) : -1;
+    }
+    // padded row i of the [μ; λ] chunk (PS + P2 rows) → real row, or −1
+    template <class S, class C> __device__ __forceinline__ int lrow(int i) const
+    {
+        int p1, ps, p2;
+        cls<S, C>(p1, ps, p2);
+        if (i < C::PS) return i < ps ? i : -1;
+        return i - C::PS < p2 ? ps + (i - C::PS) : -1;
+    }
+    // padded column j ([x; u]: NX state then M input columns; the last knot has states only)
+    template <class S, class C> __device__ __forceinline__ int col(int j) const
+    {
+        if (j < S::NX) return j < nx ? j : -1;
+        return j - S::NX < m ? nx + (j - S::NX) : -1;
+    }
 };
 
 using rsrc_t = __amdgpu_buffer_rsrc_t;
@@ -277,6 +367,12 @@ template <int L> struct SImgS {
     }
 };
 
+typedef unsigned int u2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void bstore(double v, rsrc_t r, uint32_t vo, uint32_t so)
+{
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2_t, v), r, vo, so, 0);
+}
+typedef __attribute__((address_space(3))) double lds_dw;
 // Layout-0 output stores (δz, λ): a wave's 64 chunks of L doubles are first written to an LDS
 // image [t][L] (lane t's chunk at t·L), then stored as L instructions, instruction i moving
 // the image's doubles 64i .. 64i+63 — consecutive lanes write consecutive doubles of one
@@ -295,6 +391,18 @@ template <int L> struct StPat {
             const uint32_t tr = p / (uint32_t)L, e = p - tr * (uint32_t)L;
             const uint32_t tg = tr < (uint32_t)nlive ? (sel ? (uint32_t)sel[tr] : tr) : 0u;
             vo[i] = tr < (uint32_t)nlive ? tg * (uint32_t)(s * 8) + 8u * e : 0xFFFFFF00u;
+        }
+    }
+    // padded shapes: a runtime chunk length lr ≤ L (image [t][lr]); instructions past the
+    // image's 64·lr doubles store nothing (out-of-range offset)
+    __device__ __forceinline__ void init_rt(int64_t s, int lane, int nlive, int lr)
+    {
+        const uint32_t l = (uint32_t)(lr > 0 ? lr : 1);
+#pragma unroll
+        for (int i = 0; i < L; ++i) {
+            const uint32_t p = 64u * (uint32_t)i + (uint32_t)lane;
+            const uint32_t tr = p / l, e = p - tr * l;
+            vo[i] = (lr > 0 && tr < (uint32_t)nlive) ? tr * (uint32_t)(s * 8) + 8u * e : 0xFFFFFF00u;
         }
     }
 };
@@ -337,14 +445,47 @@ template <class S> struct Ctx {
     int64_t sgz = 0, slz = 0;                      // per-trajectory strides of dz, lam
     StPat<S::I::W> pz;
     StPat<Z(S::I::PS + S::I::P2)> pl;
+    Rt rt;                                         // S::PAD: the structure's real block sizes
     __device__ __forceinline__ void init_out(const KktArgs &a, double *ost)
     {
         ozi = ost;
         oli = ost + 64 * S::WOUT;
         sgz = a.sg;
         slz = a.sl;
-        pz.init(a.sg, lane, nlive, sel);
-        pl.init(a.sl, lane, nlive, sel);
+        if constexpr (S::PAD) {
+            ozb = (uint32_t)(size_t)(lptr_t)ost;
+            olb = ozb + 64 * S::WOUT * 8;
+            pz.init_rt(a.sg, lane, nlive, (int)rt.Lg);
+            pl.init_rt(a.sl, lane, nlive, (int)rt.LyI);
+        } else {
+            pz.init(a.sg, lane, nlive, sel);
+            pl.init(a.sl, lane, nlive, sel);
+        }
+    }
+    // padded shapes: a chunk of L padded doubles, real length lr, element j at real position
+    // map(j) (−1: padding, not stored); INTERIOR: the precomputed interior pattern applies
+    uint32_t ozb = 0, olb = 0;                     // LDS byte addresses of ozi / oli
+    template <int L, bool INTERIOR, class Map>
+    __device__ __forceinline__ void out_store_pad(const double (&v)[Z(L)], uint32_t b, const StPat<L> *pi,
+                                                  int64_t stride, const double *base, int64_t off, int lr,
+                                                  Map &&map) const
+    {
+#pragma unroll
+        for (int j = 0; j < L; ++j) {
+            const int cj = map(j);
+            if (cj >= 0) *(lds_dw *)(size_t)(b + (lane * lr + cj) * 8) = v[j];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        StPat<L> q;
+        if constexpr (!INTERIOR) q.init_rt(stride, lane, nlive, lr);
+        const StPat<L> &pat = INTERIOR ? *pi : q;
+        const rsrc_t r = make_rsrc(base);
+#pragma unroll
+        for (int i = 0; i < L; ++i) bstore(*(lds_dw *)(size_t)(b + (64 * i + lane) * 8), r, pat.vo[i], (uint32_t)(off * 8));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
     // a chunk of L doubles per trajectory at element offset off: the interior pattern when the
     // length matches, else a one-off pattern (first / last knot)
@@ -438,12 +579,6 @@ template <class S> struct Ctx {
     }
 };
 
-typedef unsigned int u2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void bstore(double v, rsrc_t r, uint32_t vo, uint32_t so)
-{
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2_t, v), r, vo, so, 0);
-}
-typedef __attribute__((address_space(3))) double lds_dw;
 template <int L>
 __device__ __forceinline__ void dense_store(const double (&v)[Z(L)], double *img, const StPat<L> &pat, rsrc_t r,
                                             uint32_t so, int lane)
@@ -1050,7 +1185,15 @@ __device__ __forceinline__ void primal_knot(const Ctx<S> &c, int k, const SlabV<
         double nz[W];
 #pragma unroll
         for (int j = 0; j < W; ++j) nz[j] = -z[j];
-        c.template out_store<W, S::I::W>(nz, c.ozi, c.pz, c.sgz, c.bdz, Off<S>::g(k));
+        if constexpr (S::PAD) {
+            const Rt rt = c.rt.fresh();
+            const int lr = std::is_same<C, typename S::L>::value ? rt.nx : (int)rt.Lg;
+            c.template out_store_pad<W, std::is_same<C, typename S::I>::value>(
+                nz, c.ozb, (const StPat<W> *)(const void *)&c.pz, c.sgz, c.bdz, rt.og(k), lr,
+                [&](int j) { return rt.template col<S, C>(j); });
+        } else {
+            c.template out_store<W, S::I::W>(nz, c.ozi, c.pz, c.sgz, c.bdz, Off<S>::g(k));
+        }
     }
 }
 
@@ -1074,7 +1217,16 @@ __device__ __forceinline__ void store_lam(const Ctx<S> &c, int k, const SlabV<C>
             for (int i = 0; i < C::PS; ++i) lv[i] = v.mu[i];
 #pragma unroll
             for (int i = 0; i < C::P2; ++i) lv[C::PS + i] = v.la[i];
-            c.template out_store<LL, Z(S::I::PS + S::I::P2)>(lv, c.oli, c.pl, c.slz, c.blam, Off<S>::y(k));
+            if constexpr (S::PAD) {
+                const Rt rt = c.rt.fresh();
+                int p1, ps, p2;
+                rt.template cls<S, C>(p1, ps, p2);
+                c.template out_store_pad<LL, std::is_same<C, typename S::I>::value>(
+                    lv, c.olb, (const StPat<LL> *)(const void *)&c.pl, c.slz, c.blam, rt.oy(k), ps + p2,
+                    [&](int i) { return rt.template lrow<S, C>(i); });
+            } else {
+                c.template out_store<LL, Z(S::I::PS + S::I::P2)>(lv, c.oli, c.pl, c.slz, c.blam, Off<S>::y(k));
+            }
         }
     }
 }
@@ -1314,11 +1466,97 @@ __device__ __forceinline__ double gld(const double *base, int64_t t, int64_t len
     }
 }
 
+// padded shapes (S::PAD): element (i, j) of knot k's Y (class C), H's diagonal, g, y — 0
+// (H: 1) at padded positions; uniform branches, the real entries at the structure's offsets
+// A column's rows come as one scalar offset per row segment plus the row in the instruction's
+// immediate offset (a knot needs a few scalar registers, not one per element).  First and
+// interior knots (OVER): a padded row past a segment's real rows reads the real data that
+// follows it — the next segment, column or knot of the same trajectory, always inside the
+// array — and the value is discarded by a uniform select (no branch: the loads stay one
+// cluster).  The last knot has nothing after it: its padded rows are not read (uniform
+// branches).  A padded column reads the knot's first column, discarded the same way.
+template <int S0, int LS, bool OVER>
+__device__ __forceinline__ void pad_seg(double *v, rsrc_t r, uint32_t vo, int64_t base, int ls, bool real)
+{
+    const uint32_t so = (uint32_t)(base * 8);
+#pragma unroll
+    for (int i = 0; i < LS; ++i) {
+        const bool keep = real && i < ls;
+        if constexpr (OVER) {
+            const double x = bload(r, vo + 8u * (uint32_t)i, so);
+            v[S0 + i] = keep ? x : 0.0;
+        } else {
+            double x = 0.0;
+            if (keep) x = bload(r, vo + 8u * (uint32_t)i, so);
+            v[S0 + i] = x;
+        }
+    }
+}
+// rows [0, NR) of padded column j of knot k's Y (class C): NR = C::R, or C::P1 for the head
+template <class S, class C, int NR>
+__device__ __forceinline__ void pad_Ycol(const Rt &rt, int k, int j, double *v)
+{
+    int p1, ps, p2;
+    rt.cls<S, C>(p1, ps, p2);
+    const int cj = rt.col<S, C>(j);
+    const bool real = cj >= 0;
+    const int64_t cb = rt.oY(k) + (real ? (int64_t)cj * (p1 + ps + p2) : 0);
+    const rsrc_t r = make_rsrc(rt.bY);
+    constexpr bool OVER = !std::is_same<C, typename S::L>::value;
+    pad_seg<0, (NR < C::P1 ? NR : C::P1), OVER>(v, r, rt.vY, cb, p1, real);
+    if constexpr (NR > C::P1) {
+        pad_seg<C::P1, C::PS, OVER>(v, r, rt.vY, cb + p1, ps, real);
+        pad_seg<C::P1 + C::PS, C::P2, OVER>(v, r, rt.vY, cb + p1 + ps, p2, real);
+    }
+}
+// H, g: a padded column reads the knot's first column (every knot has one) and discards it
+template <class S, class C>
+__device__ __forceinline__ double pad_H(const KktArgs &, const Rt &rt, int64_t, int k, int j)
+{
+    const int cj = rt.col<S, C>(j);
+    const double x = bload(make_rsrc(rt.bH), rt.vH, (uint32_t)((rt.og(k) + (cj < 0 ? 0 : cj)) * 8));
+    return cj < 0 ? 1.0 : x;
+}
+template <class S, class C>
+__device__ __forceinline__ double pad_g(const KktArgs &, const Rt &rt, int64_t, int k, int j)
+{
+    const int cj = rt.col<S, C>(j);
+    const double x = bload(make_rsrc(rt.bg), rt.vg, (uint32_t)((rt.og(k) + (cj < 0 ? 0 : cj)) * 8));
+    return cj < 0 ? 0.0 : x;
+}
+// y: a padded row of a first / interior knot reads the chunk's first element (non-empty: it
+// holds the knot's D1 rows); the last knot's chunk can be empty, so its padded rows are skipped
+template <class S, class C>
+__device__ __forceinline__ double pad_y(const KktArgs &, const Rt &rt, int64_t, int k, int i)
+{
+    const int ri = rt.lrow<S, C>(i);
+    if constexpr (std::is_same<C, typename S::L>::value) {
+        double x = 0.0;
+        if (ri >= 0) x = bload(make_rsrc(rt.by), rt.vy, (uint32_t)((rt.oy(k) + ri) * 8));
+        return x;
+    } else {
+        const double x = bload(make_rsrc(rt.by), rt.vy, (uint32_t)((rt.oy(k) + (ri < 0 ? 0 : ri)) * 8));
+        return ri < 0 ? 0.0 : x;
+    }
+}
+
 template <class S, class C> struct GIn {          // knot k's inputs (class C) of one trajectory
     double Y[S::template LY<C>()], H[S::template LH<C>()], g[S::template Lg<C>()];
-    __device__ __forceinline__ void load(const KktArgs &a, int64_t t, int k)
+    __device__ __forceinline__ void load(const KktArgs &a, const Rt &rt0, int64_t t, int k)
     {
         using O = Off<S>;
+        if constexpr (S::PAD) {
+            const Rt rt = rt0.fresh();
+#pragma unroll
+            for (int j = 0; j < C::W; ++j) pad_Ycol<S, C, C::R>(rt, k, j, Y + j * C::R);
+            if constexpr (S::GINV) {
+#pragma unroll
+                for (int e = 0; e < S::template LH<C>(); ++e) H[e] = pad_H<S, C>(a, rt, t, k, e);
+#pragma unroll
+                for (int e = 0; e < S::template Lg<C>(); ++e) g[e] = pad_g<S, C>(a, rt, t, k, e);
+            }
+            return;
+        }
 #pragma unroll
         for (int e = 0; e < S::template LY<C>(); ++e) Y[e] = gld<S>(a.Y, t, a.sY, O::Y(k), e, a.batch);
         if constexpr (S::GINV) {
@@ -1338,14 +1576,21 @@ template <class S, class C> struct GIn {          // knot k's inputs (class C) o
 //   REST: everything knot k's own factor reads (the D2×(C, D1) rows and the C, D1 rows).
 // Only one full Schur image is live at a time (plus the p1×p1 head of the next knot).
 template <class S, class C, bool HEAD>
-__device__ __forceinline__ void shur_part(Shur<C> &sc, const KktArgs &a, int64_t t, int k)
+__device__ __forceinline__ void shur_part(Shur<C> &sc, const KktArgs &a, const Rt &rt0, int64_t t, int k)
 {
+    const Rt rt = S::PAD ? rt0.fresh() : rt0;
     static_assert(!S::GINV || S::HDIAG, "direct kernel: diagonal H or the SOC variant");
     constexpr int R = C::R, W = C::W, p1 = C::P1;
     constexpr int lo = 0, hi = HEAD ? p1 : R;                     // rows i in [lo, hi)
     auto Yp = [&](int e) { return gld<S>(a.Y, t, a.sY, Off<S>::Y(k), e, a.batch); };
-    auto Hp = [&](int e) { return gld<S>(a.H, t, a.sH, Off<S>::H(k), e, a.batch); };
-    auto gp = [&](int e) { return gld<S>(a.g, t, a.sg, Off<S>::g(k), e, a.batch); };
+    auto Hp = [&](int e) {
+        if constexpr (S::PAD) return pad_H<S, C>(a, rt, t, k, e);
+        else return gld<S>(a.H, t, a.sH, Off<S>::H(k), e, a.batch);
+    };
+    auto gp = [&](int e) {
+        if constexpr (S::PAD) return pad_g<S, C>(a, rt, t, k, e);
+        else return gld<S>(a.g, t, a.sg, Off<S>::g(k), e, a.batch);
+    };
     auto want = [](int i, int i2) { return HEAD ? (i < p1 && i2 < p1) : !(i < p1 && i2 < p1); };
 #pragma unroll
     for (int i = lo; i < hi; ++i) {
@@ -1353,13 +1598,21 @@ __device__ __forceinline__ void shur_part(Shur<C> &sc, const KktArgs &a, int64_t
 #pragma unroll
         for (int i2 = i; i2 < R; ++i2)
             if (want(i, i2)) sc.S[i][i2] = 0.0;
+        // a padded constraint row of this knot's C or D1 block: unit pivot (its row and column
+        // stay exact zeros); padded D2 rows are the previous knot's D1 rows, pivoted there
+        if constexpr (S::PAD && !HEAD)
+            if (i >= p1 && rt.row<S, C>(i) < 0) sc.S[i][i] = 1.0;
     }
 #pragma unroll
     for (int j = 0; j < W; ++j) {
         double v[R], vh[R];
+        if constexpr (S::PAD) {
+            pad_Ycol<S, C, HEAD ? p1 : R>(rt, k, j, v);
+        } else {
 #pragma unroll
-        for (int i = 0; i < R; ++i)
-            if (!HEAD || i < p1) v[i] = Yp(i + j * R);
+            for (int i = 0; i < R; ++i)
+                if (!HEAD || i < p1) v[i] = Yp(i + j * R);
+        }
         if constexpr (S::GINV) {
             const double h = rcp_nr2(Hp(j));                      // block_cholesky.jl:86 inv
             const double gh = gp(j);
@@ -1381,10 +1634,14 @@ __device__ __forceinline__ void shur_part(Shur<C> &sc, const KktArgs &a, int64_t
 }
 
 template <class S, class C>
-__device__ __forceinline__ void y_direct(double (&yc)[Z(C::PS + C::P2)], const KktArgs &a, int64_t t, int k)
+__device__ __forceinline__ void y_direct(double (&yc)[Z(C::PS + C::P2)], const KktArgs &a, const Rt &rt0, int64_t t, int k)
 {
+    const Rt rt = S::PAD ? rt0.fresh() : rt0;
 #pragma unroll
-    for (int i = 0; i < C::PS + C::P2; ++i) yc[i] = gld<S>(a.y, t, a.sy, Off<S>::y(k), i, a.batch);
+    for (int i = 0; i < C::PS + C::P2; ++i) {
+        if constexpr (S::PAD) yc[i] = pad_y<S, C>(a, rt, t, k, i);
+        else yc[i] = gld<S>(a.y, t, a.sy, Off<S>::y(k), i, a.batch);
+    }
 }
 
 template <class S>
@@ -1413,6 +1670,10 @@ __global__ __launch_bounds__(64) void kkt_fild_kernel(const KktArgs a, double *_
         c.blam = a.lam + t0 * a.sl;
         c.vdz = (uint32_t)(c.lane * a.sg * 8);
         c.vlam = (uint32_t)(c.lane * a.sl * 8);
+        if constexpr (S::PAD) {
+            c.rt.init(a);
+            c.rt.lanes(a, t0, t);
+        }
         c.init_out(a, ost);
     }
     int info = 0;
@@ -1429,19 +1690,19 @@ __global__ __launch_bounds__(64) void kkt_fild_kernel(const KktArgs a, double *_
     {
         Shur<F> s0;
         double y0[Z(F::PS + F::P2)];
-        shur_part<S, F, false>(s0, a, t, 0);                    // F: p1 = 0, REST = all
-        y_direct<S, F>(y0, a, t, 0);
+        shur_part<S, F, false>(s0, a, c.rt, t, 0);                    // F: p1 = 0, REST = all
+        y_direct<S, F>(y0, a, c.rt, t, 0);
         Shur<I> h1;
-        shur_part<S, I, true>(h1, a, t, 1);
+        shur_part<S, I, true>(h1, a, c.rt, t, 1);
         factor_knot<S, F, I>(0, s0, y0, h1, cy, c, info);
     }
     for (int k = 1; k <= N - 3; ++k) {
         Shur<I> sk;
         double yk[Z(I::PS + I::P2)];
-        shur_part<S, I, false>(sk, a, t, k);
-        y_direct<S, I>(yk, a, t, k);
+        shur_part<S, I, false>(sk, a, c.rt, t, k);
+        y_direct<S, I>(yk, a, c.rt, t, k);
         Shur<I> hn;
-        shur_part<S, I, true>(hn, a, t, k + 1);
+        shur_part<S, I, true>(hn, a, c.rt, t, k + 1);
         factor_knot<S, I, I>(k, sk, yk, hn, cy, c, info);   // (knot k's own HEAD went to k−1)
     }
     Shur<L> sL;
@@ -1449,13 +1710,13 @@ __global__ __launch_bounds__(64) void kkt_fild_kernel(const KktArgs a, double *_
     {
         Shur<I> sk;
         double yk[Z(I::PS + I::P2)];
-        shur_part<S, I, false>(sk, a, t, N - 2);
-        y_direct<S, I>(yk, a, t, N - 2);
-        shur_part<S, L, true>(sL, a, t, N - 1);
+        shur_part<S, I, false>(sk, a, c.rt, t, N - 2);
+        y_direct<S, I>(yk, a, c.rt, t, N - 2);
+        shur_part<S, L, true>(sL, a, c.rt, t, N - 1);
         factor_knot<S, I, L>(N - 2, sk, yk, sL, cy, c, info);
     }
-    shur_part<S, L, false>(sL, a, t, N - 1);
-    y_direct<S, L>(yL, a, t, N - 1);
+    shur_part<S, L, false>(sL, a, c.rt, t, N - 1);
+    y_direct<S, L>(yL, a, c.rt, t, N - 1);
     {
         Shur<NoCls> none;
         factor_knot<S, L, NoCls>(N - 1, sL, yL, none, cy, c, info);
@@ -1472,7 +1733,7 @@ __global__ __launch_bounds__(64) void kkt_fild_kernel(const KktArgs a, double *_
     bwd_knot<I, L>(vI, vL);
     {
         GIn<S, L> in;
-        in.load(a, t, N - 1);
+        in.load(a, c.rt, t, N - 1);
         primal_knot<S, L, L::P1>(c, N - 1, vL, vI.la, in.as_in());
     }
     store_lam<S, I>(c, N - 2, vI);
@@ -1480,7 +1741,7 @@ __global__ __launch_bounds__(64) void kkt_fild_kernel(const KktArgs a, double *_
         SlabV<I> v;
         slab_load<S, I>(v, c, j);
         GIn<S, I> in;                                            // knot j+1: F̃_{j+1} and δz_{j+1}
-        in.load(a, t, j + 1);
+        in.load(a, c.rt, t, j + 1);
         recompute_Ft<S, I>(vI.F, v.Cm, in.Y, in.H);
         bwd_knot<I, I>(v, vI);
         primal_knot<S, I, I::P1>(c, j + 1, vI, v.la, in.as_in());
@@ -1491,13 +1752,13 @@ __global__ __launch_bounds__(64) void kkt_fild_kernel(const KktArgs a, double *_
         SlabV<F> v0;
         slab_load<S, F>(v0, c, 0);
         GIn<S, I> in1;
-        in1.load(a, t, 1);
+        in1.load(a, c.rt, t, 1);
         recompute_Ft<S, I>(vI.F, v0.Cm, in1.Y, in1.H);
         bwd_knot<F, I>(v0, vI);
         primal_knot<S, I, I::P1>(c, 1, vI, v0.la, in1.as_in());
         store_lam<S, F>(c, 0, v0);
         GIn<S, F> in0;
-        in0.load(a, t, 0);
+        in0.load(a, c.rt, t, 0);
         double none[1] = {0.0};
         primal_knot<S, F, 0>(c, 0, v0, none, in0.as_in());
     }
@@ -1550,6 +1811,13 @@ LQRX_FILD_INST(6, 3, 6, 1, 6)
 LQRX_FILD_INST(4, 2, 4, 1, 4)
 LQRX_FILD_INST(5, 2, 5, 0, 5)
 LQRX_FILD_INST(7, 3, 7, 0, 7)
+// padded direct variants (layout 0, diagonal H and SOC): every smaller trajectory structure
+#define LQRX_FILP_INST(NX, M, A0, AK, AN)                                                                 \
+    template __global__ void kkt_fild_kernel<Shape<NX, M, A0, AK, AN, true, true, false, true>>(const KktArgs, double *__restrict__); \
+    template __global__ void kkt_fild_kernel<Shape<NX, M, A0, AK, AN, true, false, false, true>>(const KktArgs, double *__restrict__);
+LQRX_FILP_INST(4, 2, 4, 1, 4)
+LQRX_FILP_INST(6, 3, 6, 1, 6)
+#undef LQRX_FILP_INST
 #undef LQRX_FIL_INST
 #undef LQRX_FIL_INST1
 #undef LQRX_FIL_INST_DIAG
@@ -1557,7 +1825,111 @@ LQRX_FILD_INST(7, 3, 7, 0, 7)
 #undef LQRX_FILD_INST
 #undef LQRX_FILD_INST1
 
+// ------------------------------------------------------------------ dense / block-diagonal H
+// (BlockCholesky modes 0/1, block_cholesky.jl:55-77) on the diagonal-H kernels: with H_k = UᵀU,
+// Z = Y U⁻¹ and gz = U⁻ᵀg the KKT system is the same with H = I (S = ZZᵀ = Y H⁻¹ Yᵀ, r = Z gz
+// = Y H⁻¹ g, λ unchanged) and δz = U⁻¹δz'.  The pre-pass writes Z, gz (the packed layouts of Y,
+// g), a unit diagonal H and U (packed upper, inverse diagonal); the diagonal-H kernel solves;
+// the post-pass applies U⁻¹ to δz in place and merges `info` in the order the dense-H sweep
+// reports it (H_k is factored one step before knot k−1's pivots: a non-SPD H_k, −(k+1), wins
+// over a pivot failure at knot ≥ k−1).  One thread per (trajectory, knot), w ≤ WM.
+template <int WM>
+__global__ __launch_bounds__(256) void kkt_hpre_kernel(const KktArgs a, double *__restrict__ Z, double *__restrict__ gz,
+                                                      double *__restrict__ ones, double *__restrict__ Up,
+                                                      int32_t *__restrict__ infoh, int64_t sU)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.batch * a.N) return;
+    const int64_t t = i / a.N;
+    const int k = (int)(i - t * a.N);
+    const int32_t *m = a.meta + 8 * k;
+    const int rows = m[0] + m[1] + m[2], w = m[3];
+    const int64_t oY = m[4], oH = m[6], og = m[7];
+    int64_t oU = 0;                                   // packed-U offset of knot k
+    for (int q = 0; q < k; ++q) oU += (int64_t)a.meta[8 * q + 3] * (a.meta[8 * q + 3] + 1) / 2;
+    const double *H = a.H + t * a.sH + oH;
+    double U[WM][WM];
+#pragma unroll
+    for (int c = 0; c < WM; ++c)
+#pragma unroll
+        for (int r = 0; r <= c; ++r) U[r][c] = (c < w) ? H[r + (int64_t)c * w] : (r == c ? 1.0 : 0.0);
+    const bool ok = potrf_inv<WM>(U);
+    if (!ok) atomicMin(&infoh[t], k);                 // first non-SPD knot (pre-set to N)
+    double x[WM];
+    const double *g = a.g + t * a.sg + og;
+#pragma unroll
+    for (int c = 0; c < WM; ++c) x[c] = c < w ? g[c] : 0.0;
+    trsv_t<WM>(U, x);
+    double *gzt = gz + t * a.sg + og, *on = ones + t * a.sg + og;
+#pragma unroll
+    for (int c = 0; c < WM; ++c)
+        if (c < w) {
+            gzt[c] = x[c];
+            on[c] = 1.0;
+        }
+    const double *Y = a.Y + t * a.sY + oY;
+    double *Zt = Z + t * a.sY + oY;
+    for (int r = 0; r < rows; ++r) {
+#pragma unroll
+        for (int c = 0; c < WM; ++c) x[c] = c < w ? Y[r + (int64_t)c * rows] : 0.0;
+        trsv_t<WM>(U, x);
+#pragma unroll
+        for (int c = 0; c < WM; ++c)
+            if (c < w) Zt[r + (int64_t)c * rows] = x[c];
+    }
+    double *Ut = Up + t * sU + oU;
+    int e = 0;
+#pragma unroll
+    for (int c = 0; c < WM; ++c)
+#pragma unroll
+        for (int r = 0; r <= c; ++r)
+            if (c < w) Ut[e++] = U[r][c];
+}
+
+template <int WM>
+__global__ __launch_bounds__(256) void kkt_hpost_kernel(const KktArgs a, const double *__restrict__ Up,
+                                                       const int32_t *__restrict__ infoh, int64_t sU)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.batch * a.N) return;
+    const int64_t t = i / a.N;
+    const int k = (int)(i - t * a.N);
+    const int32_t *m = a.meta + 8 * k;
+    const int w = m[3];
+    const int64_t og = m[7];
+    int64_t oU = 0;
+    for (int q = 0; q < k; ++q) oU += (int64_t)a.meta[8 * q + 3] * (a.meta[8 * q + 3] + 1) / 2;
+    const double *Ut = Up + t * sU + oU;
+    double U[WM][WM];
+    int e = 0;
+#pragma unroll
+    for (int c = 0; c < WM; ++c)
+#pragma unroll
+        for (int r = 0; r <= c; ++r) U[r][c] = (c < w) ? Ut[e++] : (r == c ? 1.0 : 0.0);
+    double x[WM];
+    double *dz = a.dz + t * a.sg + og;
+#pragma unroll
+    for (int c = 0; c < WM; ++c) x[c] = c < w ? dz[c] : 0.0;
+    trsv_n<WM>(U, x);
+#pragma unroll
+    for (int c = 0; c < WM; ++c)
+        if (c < w) dz[c] = x[c];
+    if (k == 0 && a.info) {
+        const int kh = infoh[t];                      // first non-SPD H knot, or N
+        const int v = a.info[t];                      // pivots: k+1 of the first failing knot
+        if (kh < a.N && (v == 0 || kh <= v)) a.info[t] = -(kh + 1);
+    }
+}
+
 } // namespace fil
+
+// LQRX_KKT_PAD=0 turns off the padded shapes and the dense-H passes (those structures then go
+// to the large-block kernels, as before round 4): A/B and cross-checks
+static bool fil_ext_on()
+{
+    static const bool on = [] { const char *e = std::getenv("LQRX_KKT_PAD"); return !(e && *e == '0'); }();
+    return on;
+}
 
 // Dispatch: the FIL kernel serves a structure iff every knot matches one of the
 // instantiated (n̄, m, P0, PK, PN) shapes; otherwise the generic kernel (lqrx_kkt.hip) runs.
@@ -1574,9 +1946,9 @@ static bool fil_dispatch(const KktArgs &a, const int32_t *n1, const int32_t *p, 
         if (n1[k] != nx || n2[k] != nx || p[k] != PK || w[k] != nx + m) return false;
     const bool diag = a.h_mode == 2, ginv = a.ginv != 0, soa = a.layout == 1;
 #define LQRX_FIL_SEL(NX, M, A0, AK, AN, SOA)                                                             \
-    if (diag && ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true, SOA>{}, std::false_type{});           \
-    else if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, false, true, SOA>{}, std::false_type{});             \
-    else fn(fil::Shape<NX, M, A0, AK, AN, true, false, SOA>{}, std::false_type{});
+    if (diag && ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true, SOA>{}, std::false_type{}, a);        \
+    else if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, false, true, SOA>{}, std::false_type{}, a);          \
+    else fn(fil::Shape<NX, M, A0, AK, AN, true, false, SOA>{}, std::false_type{}, a);
 #define LQRX_FIL(NX, M, A0, AK, AN)                                                                      \
     if (nx == NX && m == M && P0 == A0 && PK == AK && PN == AN) {                                        \
         if (soa) { LQRX_FIL_SEL(NX, M, A0, AK, AN, true) }                                               \
@@ -1586,22 +1958,22 @@ static bool fil_dispatch(const KktArgs &a, const int32_t *n1, const int32_t *p, 
 #define LQRX_FIL_DIAG(NX, M, A0, AK, AN)                                                                 \
     if (nx == NX && m == M && P0 == A0 && PK == AK && PN == AN && (diag || !ginv)) {                     \
         if (soa) {                                                                                       \
-            if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true, true>{}, std::false_type{});          \
-            else fn(fil::Shape<NX, M, A0, AK, AN, true, false, true>{}, std::false_type{});              \
+            if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true, true>{}, std::false_type{}, a);       \
+            else fn(fil::Shape<NX, M, A0, AK, AN, true, false, true>{}, std::false_type{}, a);           \
         } else {                                                                                         \
-            if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true>{}, std::false_type{});                \
-            else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{}, std::false_type{});                    \
+            if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true>{}, std::false_type{}, a);             \
+            else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{}, std::false_type{}, a);                 \
         }                                                                                                \
         return true;                                                                                     \
     }
 #define LQRX_FILD(NX, M, A0, AK, AN)                                                                     \
     if (nx == NX && m == M && P0 == A0 && PK == AK && PN == AN && (diag || !ginv)) {                     \
         if (soa) {                                                                                       \
-            if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true, true>{}, std::true_type{});           \
-            else fn(fil::Shape<NX, M, A0, AK, AN, true, false, true>{}, std::true_type{});               \
+            if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true, true>{}, std::true_type{}, a);        \
+            else fn(fil::Shape<NX, M, A0, AK, AN, true, false, true>{}, std::true_type{}, a);            \
         } else {                                                                                         \
-            if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true>{}, std::true_type{});                 \
-            else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{}, std::true_type{});                     \
+            if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true>{}, std::true_type{}, a);              \
+            else fn(fil::Shape<NX, M, A0, AK, AN, true, false>{}, std::true_type{}, a);                  \
         }                                                                                                \
         return true;                                                                                     \
     }
@@ -1611,6 +1983,22 @@ static bool fil_dispatch(const KktArgs &a, const int32_t *n1, const int32_t *p, 
     LQRX_FILD(4, 2, 4, 1, 4)       // DoubleIntegrator(2)
     LQRX_FILD(5, 2, 5, 0, 5)       // trajectory_structure(5, 2, N), diagonal H (the SQP problems' shape)
     LQRX_FILD(7, 3, 7, 0, 7)       // trajectory_structure(7, 3, N), diagonal H
+    // any other trajectory structure up to a padded bin (layout 0; layout 1 is staged): the
+    // smallest bin that holds it, its own sizes at run time (Shape PAD, Rt).  LQRX_KKT_PAD=0
+    // sends them to the large-block kernels instead (A/B)
+    if (fil_ext_on() && !soa && (diag || !ginv) && nx >= 1 && m >= 0 && P0 >= 0 && PK >= 0 && PN >= 0) {
+        KktArgs b = a;
+        b.rt[0] = nx; b.rt[1] = m; b.rt[2] = P0; b.rt[3] = PK; b.rt[4] = PN;
+#define LQRX_FILP(NX, M, A0, AK, AN)                                                                     \
+        if (nx <= NX && m <= M && P0 <= A0 && PK <= AK && PN <= AN) {                                    \
+            if (ginv) fn(fil::Shape<NX, M, A0, AK, AN, true, true, false, true>{}, std::true_type{}, b);  \
+            else fn(fil::Shape<NX, M, A0, AK, AN, true, false, false, true>{}, std::true_type{}, b);     \
+            return true;                                                                                 \
+        }
+        LQRX_FILP(4, 2, 4, 1, 4)
+        LQRX_FILP(6, 3, 6, 1, 6)
+#undef LQRX_FILP
+    }
 #undef LQRX_FIL
 #undef LQRX_FIL_SEL
 #undef LQRX_FIL_DIAG
@@ -1618,16 +2006,99 @@ static bool fil_dispatch(const KktArgs &a, const int32_t *n1, const int32_t *p, 
     return false;
 }
 
+// Dense / block-diagonal H (ginv, layout 0) on a structure whose diagonal-H form a FIL shape
+// serves: the pre-pass / diagonal kernel / post-pass of fil::kkt_hpre_kernel.  Scratch: Z | gz |
+// unit H | packed U | H-failure knots | the diagonal kernel's slab.
+namespace {
+constexpr int FILH_WM = 10;                           // w ≤ 10: every FIL shape and padded bin
+struct FilH {
+    int64_t sU = 0;
+    size_t oZ = 0, ogz = 0, oon = 0, oU = 0, oinf = 0, oslab = 0, slab = 0, total = 0;
+};
+bool filh_plan(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2, const int32_t *w,
+               KktArgs &b, FilH &P)
+{
+    // (not for a trajectory subset: the pre/post passes cover the whole batch)
+    if (!fil_ext_on() || a.h_mode == 2 || !a.ginv || a.layout != 0 || a.maxw > FILH_WM || a.batch <= 0 || a.sel)
+        return false;
+    b = a;
+    b.h_mode = 2;
+    b.sH = a.sg;                                      // unit diagonal H, g's packing
+    size_t sb = 0;
+    if (!fil_dispatch(b, n1, p, n2, w, [&](auto shape, auto, const KktArgs &c) { sb = fil::slab_bytes<decltype(shape)>(c); }))
+        return false;
+    for (int k = 0; k < a.N; ++k) P.sU += (int64_t)w[k] * (w[k] + 1) / 2;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t B = (size_t)a.batch;
+    P.oZ = 0;
+    P.ogz = P.oZ + al(B * (size_t)a.sY * 8);
+    P.oon = P.ogz + al(B * (size_t)a.sg * 8);
+    P.oU = P.oon + al(B * (size_t)a.sg * 8);
+    P.oinf = P.oU + al(B * (size_t)P.sU * 8);
+    P.oslab = P.oinf + al(B * 4);
+    P.slab = sb;
+    P.total = P.oslab + sb;
+    return true;
+}
+} // namespace
+
 bool kkt_fil_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
                     const int32_t *w, hipStream_t s, hipError_t *err)
 {
-    return fil_dispatch(a, n1, p, n2, w, [&](auto shape, auto direct) { *err = fil::launch<decltype(shape), decltype(direct)::value>(a, s); });
+    if (fil_dispatch(a, n1, p, n2, w, [&](auto shape, auto direct, const KktArgs &b) {
+            *err = fil::launch<decltype(shape), decltype(direct)::value>(b, s);
+        }))
+        return true;
+    KktArgs b;
+    FilH P;
+    if (!filh_plan(a, n1, p, n2, w, b, P)) return false;
+    Scratch sc;
+    hipError_t e = sc.get(a, P.total, s);
+    if (e != hipSuccess) {
+        *err = e;
+        return true;
+    }
+    char *base = (char *)sc.p;
+    double *Z = (double *)(base + P.oZ), *gz = (double *)(base + P.ogz), *on = (double *)(base + P.oon),
+           *Up = (double *)(base + P.oU);
+    int32_t *infoh = (int32_t *)(base + P.oinf);
+    const int64_t nt = a.batch * a.N;
+    const unsigned grid = (unsigned)((nt + 255) / 256);
+    // H-failure knots start at N ("none"): 0x7f7f7f7f ≥ N for every accepted structure
+    e = hipMemsetAsync(infoh, 0x7f, (size_t)a.batch * 4, s);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL((fil::kkt_hpre_kernel<FILH_WM>), dim3(grid), dim3(256), 0, s, a, Z, gz, on, Up, infoh, P.sU);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) {
+        b.Y = Z; b.g = gz; b.H = on;
+        b.ws = base + P.oslab;
+        b.ws_bytes = P.slab;
+        hipError_t e2 = hipSuccess;
+        (void)fil_dispatch(b, n1, p, n2, w, [&](auto shape, auto direct, const KktArgs &c) {
+            e2 = fil::launch<decltype(shape), decltype(direct)::value>(c, s);
+        });
+        e = e2;
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL((fil::kkt_hpost_kernel<FILH_WM>), dim3(grid), dim3(256), 0, s, a, Up, infoh, P.sU);
+        e = hipGetLastError();
+    }
+    hipError_t er = sc.release(s);
+    *err = e != hipSuccess ? e : er;
+    return true;
 }
 
 bool kkt_fil_scratch_bytes(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2,
                            const int32_t *w, size_t *bytes)
 {
-    return fil_dispatch(a, n1, p, n2, w, [&](auto shape, auto) { *bytes = fil::slab_bytes<decltype(shape)>(a); });
+    if (fil_dispatch(a, n1, p, n2, w, [&](auto shape, auto, const KktArgs &b) { *bytes = fil::slab_bytes<decltype(shape)>(b); }))
+        return true;
+    KktArgs b;
+    FilH P;
+    if (!filh_plan(a, n1, p, n2, w, b, P)) return false;
+    *bytes = P.total;
+    return true;
 }
 
 } // namespace lqrx

@@ -104,9 +104,12 @@ def test_kkt_fil_shapes(lqrx, gpu_ok, model, N, batch, h_mode, ginv):
     cases: the shortest horizon it serves (N = 4), one trajectory, ragged last waves, the
     full cfg3 batch; Ginv = 0 is the second-order-correction variant.  The cartpole shape
     (n 4, m 1; the device SQP's structure) is instantiated for diagonal H (dense H → the
-    generic kernel, also checked here); N ≥ 6 (N = 4 is over-constrained: 20 rows, 19 vars; at
-    N = 5 the system is square and a few of the random problems lose 1e-5 to rounding in the
-    oracle and the generic kernel alike — measured, tools/kkt_shape_diag.py).
+    H = UᵀU pre-pass around that kernel, round 4; the generic kernel before); N ≥ 6 (N = 4 is
+    over-constrained: 20 rows, 19 vars; at N = 5 the system is square and a few of the random
+    problems lose 1e-5 to rounding in the oracle and the generic kernel alike — measured,
+    tools/kkt_shape_diag.py; at N = 6, 7 it is near-square — 28 rows, 29 vars at N = 6 — and
+    with dense H the Z = YU⁻¹ form and the oracle's H⁻¹Yᵀ form round apart by up to ~2e-10, so
+    those trajectories are held to the refined truth as below).
     DoubleIntegrator(3) (the structure of test/cholesky_solve.jl) runs the direct variant
     kkt_fild_kernel for diagonal H / SOC, the large-block kernel for dense H, and so do the
     trajectory structures (5, 2, N) and (7, 3, N) ("t52", "t73"); at N = 4 DoubleIntegrator(3)'s
@@ -129,7 +132,8 @@ def test_kkt_fil_shapes(lqrx, gpu_ok, model, N, batch, h_mode, ginv):
     got = K.kkt_solve(pb, ginv=ginv)
     ref = _ref(st, pb, ginv)
     assert got["rc"] == 0 and (got["info"] == 0).all()
-    check(st, pb, ginv, got, ref, TOL, fallback=(model == "di" and N == 4))
+    check(st, pb, ginv, got, ref, TOL,
+          fallback=(model == "di" and N == 4) or (model == "cartpole" and N <= 7 and h_mode == 0))
 
 
 def test_kkt_workspace_entry(lqrx, gpu_ok):
