@@ -170,7 +170,7 @@ def cpu_baseline_kkt_dense(st, target_s=12.0, threads=None):
                        f"{threads} threads, {dt:.1f} s")
 
 
-def cpu_baseline_kkt(N, target_s=12.0, threads=None, structure="dubins"):
+def cpu_baseline_kkt(N, target_s=12.0, threads=None, structure="dubins", h_mode=2):
     """CPU oracle (C restatement of cholesky_solver.jl _solve!) on a bounded sample."""
     import lqrx.kkt as K
     from oracle import oracle as orc
@@ -179,14 +179,14 @@ def cpu_baseline_kkt(N, target_s=12.0, threads=None, structure="dubins"):
     st = kkt_structure(structure, N)
     os_ = orc.KktStructure(st.n, st.m, st.N, st.p)
     probe = 256
-    pb = K.random_kkt(st, probe, seed=1, h_mode=K.H_DIAG)
+    pb = K.random_kkt(st, probe, seed=1, h_mode=h_mode)
     t0 = time.perf_counter()
-    orc.kkt_solve_batch(os_, probe, pb.Y, pb.y, pb.H, pb.g, h_mode=2, nthreads=threads)
+    orc.kkt_solve_batch(os_, probe, pb.Y, pb.y, pb.H, pb.g, h_mode=h_mode, nthreads=threads)
     per = (time.perf_counter() - t0) / probe
     sample = int(max(probe, min(1 << 18, target_s / max(per, 1e-9))))
-    pb = K.random_kkt(st, sample, seed=2, h_mode=K.H_DIAG)
+    pb = K.random_kkt(st, sample, seed=2, h_mode=h_mode)
     t0 = time.perf_counter()
-    orc.kkt_solve_batch(os_, sample, pb.Y, pb.y, pb.H, pb.g, h_mode=2, nthreads=threads)
+    orc.kkt_solve_batch(os_, sample, pb.Y, pb.y, pb.H, pb.g, h_mode=h_mode, nthreads=threads)
     dt = time.perf_counter() - t0
     return dict(value=sample / dt, unit="trajectories/s", cores=threads, kind="port",
                 sample=f"{sample} {'Dubins' if structure == 'dubins' else 'DoubleIntegrator(3)'} KKT solves "
@@ -274,7 +274,7 @@ def check_kkt_sample(out, pb, st, idx, bt, threads):
     dz = out["dz"].view(bt, -1).index_select(0, ti).cpu().numpy()
     lam = out["lam"].view(bt, -1).index_select(0, ti).cpu().numpy()
     ref = orc.kkt_solve_batch(orc.KktStructure(st.n, st.m, st.N, st.p), s, pb.Y[idx], pb.y[idx],
-                              pb.H[idx], pb.g[idx], h_mode=2, nthreads=threads)
+                              pb.H[idx], pb.g[idx], h_mode=pb.h_mode, nthreads=threads)
     rel = lambda a, b: float((np.abs(a - b.reshape(a.shape)).max(axis=1)
                               / np.maximum(1e-300, np.abs(b.reshape(a.shape)).max(axis=1))).max())
     e = dict(dz=rel(dz, ref["dz"]), lam=rel(lam, ref["lam"]))
@@ -399,6 +399,9 @@ def main(argv=None):
                     help="kkt workload: Dubins (configs[2]), DoubleIntegrator(3,N) (test/problems.jl), or "
                          "dense: the trajectory structure at --n/--m with dense dynamics, generated in HBM "
                          "(configs[4]: --n 64 --m 32 --N 512 --batch 8192 --dtype f32)")
+    ap.add_argument("--kkt-hmode", type=int, choices=[0, 1, 2], default=2,
+                    help="kkt workload (dubins / di): BlockCholesky mode of H — 2 diagonal (default), 1 "
+                         "block-diagonal, 0 dense (block_cholesky.jl:19-159)")
     ap.add_argument("--kkt-layout", type=int, choices=[0, 1], default=0,
                     help="kkt workload: ABI layout 0 (per trajectory, the reference's blocks) or 1 "
                          "(batch fastest, SoA)")
@@ -562,7 +565,8 @@ def main(argv=None):
     else:
         import lqrx.kkt as K
         st = kkt_structure(args.kkt_structure, N)
-        pb = K.random_kkt(st, bt, seed=args.seed + rank, h_mode=K.H_DIAG)
+        hm = args.kkt_hmode
+        pb = K.random_kkt(st, bt, seed=args.seed + rank, h_mode=hm)
         kl = args.kkt_layout
         # layout 1: the same data as [element][batch] (transposed on the device, untimed)
         t = {k: (torch.from_numpy(getattr(pb, k)).to(dev).t().contiguous().view(-1) if kl else
@@ -570,11 +574,11 @@ def main(argv=None):
         t["batch"] = bt
         # caller-owned workspace (lqrx_kkt_solve_ws): a step is the kernel alone, as a serving
         # loop would run it (the pool path adds ~0.05 ms of stream-ordered alloc/free per call)
-        ws = torch.empty(K.workspace_size(st, bt, K.H_DIAG, 1, kl), dtype=torch.uint8, device=dev)
-        out = K.kkt_solve_device(st, t, K.H_DIAG, 1, stream=sh, workspace=ws, layout=kl)
+        ws = torch.empty(K.workspace_size(st, bt, hm, 1, kl), dtype=torch.uint8, device=dev)
+        out = K.kkt_solve_device(st, t, hm, 1, stream=sh, workspace=ws, layout=kl)
 
         def step():
-            K.kkt_solve_device(st, t, K.H_DIAG, 1, stream=sh, out=out, workspace=ws, layout=kl)
+            K.kkt_solve_device(st, t, hm, 1, stream=sh, out=out, workspace=ws, layout=kl)
 
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -744,13 +748,17 @@ def main(argv=None):
                 if not args.no_cpu_baseline else None
         elif args.workload == "kkt":
             import lqrx.kkt as K
-            sY, sy, sH, sg = st.sizes(K.H_DIAG)
+            hm = args.kkt_hmode
+            sY, sy, sH, sg = st.sizes(hm)
             alg_bytes = (sY + sy + sH + sg + sg + sy) * 8 * bt     # inputs + dz + λ
             achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
             traffic, tsrc = traffic_lookup(f"kkt_{args.kkt_structure}_N{N}_B{bt}_f64"
-                                           + ("_soa" if args.kkt_layout else ""), args.traffic_json)
+                                           + ("_soa" if args.kkt_layout else "")
+                                           + (f"_h{hm}" if hm != 2 else ""), args.traffic_json)
             kname = ("kkt_fil_kernel" if args.kkt_structure == "dubins" else "kkt_fild_kernel") if N >= 4 \
                 else "kkt_staged_kernel"
+            if hm != 2 and args.kkt_structure == "di" and N >= 4:
+                kname = "kkt_hpre_kernel + kkt_fild_kernel + kkt_hpost_kernel (dense H = UᵀU passes)"
             roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": tsrc,
                     "kernel": kname,
@@ -763,7 +771,10 @@ def main(argv=None):
             else:
                 metric = f"KKT solves/sec (DoubleIntegrator(3,{N}) n=6 m=3 block-tridiagonal _solve!)"
                 workload = "DoubleIntegrator KKT structure of test/cholesky_solve.jl (non-baseline)"
-            cpu = cpu_baseline_kkt(N, target_s=args.cpu_seconds, structure=args.kkt_structure) \
+            if hm != 2:
+                metric = metric[:-1] + f", {('dense', 'block-diagonal')[hm]} H)"
+                workload += f", BlockCholesky mode {hm}"
+            cpu = cpu_baseline_kkt(N, target_s=args.cpu_seconds, structure=args.kkt_structure, h_mode=hm) \
                 if not args.no_cpu_baseline else None
         else:
             flops = dp_flops_per_traj(n, m, N) * bt
