@@ -1828,13 +1828,14 @@ LQRX_FILP_INST(6, 3, 6, 1, 6)
 // ------------------------------------------------------------------ dense / block-diagonal H
 // (BlockCholesky modes 0/1, block_cholesky.jl:55-77) on the diagonal-H kernels: with H_k = UᵀU,
 // Z = Y U⁻¹ and gz = U⁻ᵀg the KKT system is the same with H = I (S = ZZᵀ = Y H⁻¹ Yᵀ, r = Z gz
-// = Y H⁻¹ g, λ unchanged) and δz = U⁻¹δz'.  The pre-pass writes Z, gz (the packed layouts of Y,
-// g), a unit diagonal H and U (packed upper, inverse diagonal); the diagonal-H kernel solves;
+// = Y H⁻¹ g, λ unchanged) and δz = U⁻¹δz'.  The pre-pass writes gz (g's packing), a unit
+// diagonal H and U (packed upper, inverse diagonal), the Z kernel Z (Y's packing) one row per
+// thread; the diagonal-H kernel solves;
 // the post-pass applies U⁻¹ to δz in place and merges `info` in the order the dense-H sweep
 // reports it (H_k is factored one step before knot k−1's pivots: a non-SPD H_k, −(k+1), wins
 // over a pivot failure at knot ≥ k−1).  One thread per (trajectory, knot), w ≤ WM.
 template <int WM>
-__global__ __launch_bounds__(256) void kkt_hpre_kernel(const KktArgs a, double *__restrict__ Z, double *__restrict__ gz,
+__global__ __launch_bounds__(256) void kkt_hpre_kernel(const KktArgs a, double *__restrict__ gz,
                                                       double *__restrict__ ones, double *__restrict__ Up,
                                                       int32_t *__restrict__ infoh, int64_t sU)
 {
@@ -1843,10 +1844,11 @@ __global__ __launch_bounds__(256) void kkt_hpre_kernel(const KktArgs a, double *
     const int64_t t = i / a.N;
     const int k = (int)(i - t * a.N);
     const int32_t *m = a.meta + 8 * k;
-    const int rows = m[0] + m[1] + m[2], w = m[3];
-    const int64_t oY = m[4], oH = m[6], og = m[7];
-    int64_t oU = 0;                                   // packed-U offset of knot k
-    for (int q = 0; q < k; ++q) oU += (int64_t)a.meta[8 * q + 3] * (a.meta[8 * q + 3] + 1) / 2;
+    const int w = m[3];
+    const int64_t oH = m[6], og = m[7];
+    // packed-U offset of knot k: every knot before the last has knot 0's w (trajectory form)
+    const int w0 = a.meta[3];
+    const int64_t oU = (int64_t)k * (w0 * (w0 + 1) / 2);
     const double *H = a.H + t * a.sH + oH;
     double U[WM][WM];
 #pragma unroll
@@ -1867,16 +1869,6 @@ __global__ __launch_bounds__(256) void kkt_hpre_kernel(const KktArgs a, double *
             gzt[c] = x[c];
             on[c] = 1.0;
         }
-    const double *Y = a.Y + t * a.sY + oY;
-    double *Zt = Z + t * a.sY + oY;
-    for (int r = 0; r < rows; ++r) {
-#pragma unroll
-        for (int c = 0; c < WM; ++c) x[c] = c < w ? Y[r + (int64_t)c * rows] : 0.0;
-        trsv_t<WM>(U, x);
-#pragma unroll
-        for (int c = 0; c < WM; ++c)
-            if (c < w) Zt[r + (int64_t)c * rows] = x[c];
-    }
     double *Ut = Up + t * sU + oU;
     int e = 0;
 #pragma unroll
@@ -1884,6 +1876,52 @@ __global__ __launch_bounds__(256) void kkt_hpre_kernel(const KktArgs a, double *
 #pragma unroll
         for (int r = 0; r <= c; ++r)
             if (c < w) Ut[e++] = U[r][c];
+}
+
+// Z = Y U⁻¹ row by row: one thread per (trajectory, knot, row of Y) — the rows of a knot are
+// consecutive threads (their Y loads and Z stores are one contiguous run per column, their U
+// loads the same addresses); the trajectory form's row counts give the knot in closed form
+template <int WM>
+__global__ __launch_bounds__(256) void kkt_hz_kernel(const KktArgs a, double *__restrict__ Z,
+                                                    const double *__restrict__ Up, int64_t sU)
+{
+    const int N = a.N;
+    const int R0 = a.meta[0] + a.meta[1] + a.meta[2], R1 = a.meta[8] + a.meta[9] + a.meta[10];
+    const int RL = a.meta[8 * (N - 1)] + a.meta[8 * (N - 1) + 1] + a.meta[8 * (N - 1) + 2];
+    const int64_t Rt = (int64_t)R0 + (int64_t)(N - 2) * R1 + RL;     // Y rows per trajectory
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.batch * Rt) return;
+    const int64_t t = i / Rt;
+    int j = (int)(i - t * Rt), k;
+    if (j < R0) {
+        k = 0;
+    } else if (j < R0 + (N - 2) * R1) {
+        j -= R0;
+        k = 1 + j / R1;
+        j -= (k - 1) * R1;
+    } else {
+        j -= R0 + (N - 2) * R1;
+        k = N - 1;
+    }
+    const int32_t *m = a.meta + 8 * k;
+    const int rows = m[0] + m[1] + m[2], w = m[3];
+    const int w0 = a.meta[3];
+    const double *Ut = Up + t * sU + (int64_t)k * (w0 * (w0 + 1) / 2);
+    double U[WM][WM];
+    int e = 0;
+#pragma unroll
+    for (int c = 0; c < WM; ++c)
+#pragma unroll
+        for (int r = 0; r <= c; ++r) U[r][c] = (c < w) ? Ut[e++] : (r == c ? 1.0 : 0.0);
+    const double *Y = a.Y + t * a.sY + m[4] + j;
+    double x[WM];
+#pragma unroll
+    for (int c = 0; c < WM; ++c) x[c] = c < w ? Y[(int64_t)c * rows] : 0.0;
+    trsv_t<WM>(U, x);
+    double *Zt = Z + t * a.sY + m[4] + j;
+#pragma unroll
+    for (int c = 0; c < WM; ++c)
+        if (c < w) Zt[(int64_t)c * rows] = x[c];
 }
 
 template <int WM>
@@ -1897,8 +1935,9 @@ __global__ __launch_bounds__(256) void kkt_hpost_kernel(const KktArgs a, const d
     const int32_t *m = a.meta + 8 * k;
     const int w = m[3];
     const int64_t og = m[7];
-    int64_t oU = 0;
-    for (int q = 0; q < k; ++q) oU += (int64_t)a.meta[8 * q + 3] * (a.meta[8 * q + 3] + 1) / 2;
+    // packed-U offset of knot k: every knot before the last has knot 0's w (trajectory form)
+    const int w0 = a.meta[3];
+    const int64_t oU = (int64_t)k * (w0 * (w0 + 1) / 2);
     const double *Ut = Up + t * sU + oU;
     double U[WM][WM];
     int e = 0;
@@ -2067,7 +2106,14 @@ bool kkt_fil_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const
     // H-failure knots start at N ("none"): 0x7f7f7f7f ≥ N for every accepted structure
     e = hipMemsetAsync(infoh, 0x7f, (size_t)a.batch * 4, s);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL((fil::kkt_hpre_kernel<FILH_WM>), dim3(grid), dim3(256), 0, s, a, Z, gz, on, Up, infoh, P.sU);
+        hipLaunchKernelGGL((fil::kkt_hpre_kernel<FILH_WM>), dim3(grid), dim3(256), 0, s, a, gz, on, Up, infoh, P.sU);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) {
+        int64_t Rt = 0;
+        for (int k = 0; k < a.N; ++k) Rt += n1[k] + p[k] + n2[k];
+        hipLaunchKernelGGL((fil::kkt_hz_kernel<FILH_WM>), dim3((unsigned)((a.batch * Rt + 255) / 256)), dim3(256), 0, s,
+                           a, Z, Up, P.sU);
         e = hipGetLastError();
     }
     if (e == hipSuccess) {
