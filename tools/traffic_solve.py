@@ -37,7 +37,7 @@ tj[key] = {
     "per_kernel_per_solve": kern, "solves_in_pmc_run": solves,
     "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes, every dispatch of "
               f"'{ks}' summed per solve; FETCH_SIZE x2 (gfx950 wide-read undercount, MI355X_MICROARCH.md "
-              "HBM section; not calibrated for 4-B-per-lane loads), KiB->bytes x1024",
+              "HBM section; calibrated at 0.500 of the bytes read for 4-, 8- and 16-B-per-lane coalesced loads: profiles/r04/m/kkt_cfg4_sq_and_fetch_calib.txt), KiB->bytes x1024",
     "source": f"{fdir}, {wdir}",
     "measured_at_head": os.environ.get("GIT_HEAD"),
 }
