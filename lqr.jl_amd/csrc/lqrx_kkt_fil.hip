@@ -1817,6 +1817,7 @@ LQRX_FILD_INST(7, 3, 7, 0, 7)
     template __global__ void kkt_fild_kernel<Shape<NX, M, A0, AK, AN, true, false, false, true>>(const KktArgs, double *__restrict__);
 LQRX_FILP_INST(4, 2, 4, 1, 4)
 LQRX_FILP_INST(6, 3, 6, 1, 6)
+LQRX_FILP_INST(8, 4, 8, 1, 8)
 #undef LQRX_FILP_INST
 #undef LQRX_FIL_INST
 #undef LQRX_FIL_INST1
@@ -2036,6 +2037,7 @@ static bool fil_dispatch(const KktArgs &a, const int32_t *n1, const int32_t *p, 
         }
         LQRX_FILP(4, 2, 4, 1, 4)
         LQRX_FILP(6, 3, 6, 1, 6)
+        LQRX_FILP(8, 4, 8, 1, 8)
 #undef LQRX_FILP
     }
 #undef LQRX_FIL

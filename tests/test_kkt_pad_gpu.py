@@ -1,6 +1,6 @@
 """GPU parity: trajectory-form KKT structures outside the compile-time shapes, on the padded
 direct kernel (kkt_fild_kernel<Shape<…, PAD>>, lqrx_kkt_fil.hip) — blocks zero-padded in
-registers up to a bin (4,2,4,1,4) / (6,3,6,1,6), the structure's own sizes at run time.
+registers up to a bin (4,2,4,1,4) / (6,3,6,1,6) / (8,4,8,1,8), the structure's own sizes at run time.
 
 Reference: the block structure ConstraintBlocks builds (conblocks.jl:403-425) for any (n, m)
 and stage constraints; the solve is cholesky_solver.jl:166-236 on it.  Oracle: oracle/
@@ -53,6 +53,9 @@ CASES = [
     (6, 3, 40, "traj", 17),
     (5, 3, 12, "stage", 40),
     (6, 1, 4, "nogoal", 9),
+    (8, 4, 21, "traj", 66),              # bin (8,4,8,1,8)
+    (7, 2, 12, "stage", 31),
+    (8, 3, 5, "nogoal", 5),
 ]
 
 
