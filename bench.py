@@ -720,8 +720,8 @@ def main(argv=None):
             traffic, tsrc = traffic_lookup(f"kkt_dense_n{n}_m{m}_N{N}_B{bt}_{args.dtype}", args.traffic_json)
             # fp64 trajectory structures with a compile-time direct-kernel shape (lqrx_kkt_fil.hip
             # fil_dispatch) run kkt_fild_kernel, HBM-bound; everything else the large-block path
-            # (the other small ones, up to n=6 m=3, the padded direct kernel: Shape<…, PAD>)
-            padded = f64 and N >= 4 and n <= 6 and m <= 3 and (n, m) not in ((5, 2), (7, 3))
+            # (the other small ones, up to n=8 m=4, the padded direct kernel: Shape<…, PAD>)
+            padded = f64 and N >= 4 and n <= 8 and m <= 4 and (n, m) not in ((5, 2), (7, 3))
             if f64 and N >= 4 and ((n, m) in ((5, 2), (7, 3)) or padded):
                 roof = {"bound": "hbm", "achieved": alg_bytes / (kern_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
                         "unit": "GB/s", "frac": alg_bytes / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
