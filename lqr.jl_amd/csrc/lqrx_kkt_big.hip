@@ -2524,8 +2524,9 @@ constexpr int KBW_W = 2080;
 #ifndef KBW_RUN
 #define KBW_RUN 32
 #endif
-// D2 columns the backward kernel holds in registers between its two uses (fp32; 2 = off, the
-// array is then a dummy).  KBW_NOHOLD=1 restores the second pass over D2 (A/B).
+// D2 columns the backward kernel holds in registers between its two uses (fp32 96, fp64 32:
+// wider knots hold their first columns and read the rest twice; 2 = off, the array is then a
+// dummy).  KBW_NOHOLD=1 restores the second pass over every D2 column (A/B).
 #ifndef KBW_NOHOLD
 #define KBW_NOHOLD 0
 #endif
@@ -2536,7 +2537,7 @@ __device__ __forceinline__ double rdlane(double v, int l)
     const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
-template <typename T> constexpr int kbw_hold() { return (sizeof(T) == 4 && !KBW_NOHOLD) ? 96 : 2; }
+template <typename T> constexpr int kbw_hold() { return KBW_NOHOLD ? 2 : sizeof(T) == 4 ? 96 : 32; }
 constexpr int KBW_VC = KBW_VC_COLS;  // columns of Y in flight per lane in the v product
 constexpr int KBW_R = KBW_RUN;       // column-run elements in flight per lane (t, D2ᵀλ)
 
@@ -2667,7 +2668,8 @@ __global__ void __launch_bounds__(64 * KF_W) kb_bwd_kernel(KbArgs<T> a, int64_t 
         // fp32, w ≤ KBW_HOLD: knot j's D2 rows stay in registers (lane = row) from the v product
         // to D2ᵀλ_{j−1}, so D2 is read once per knot instead of twice
         T d2[kbw_hold<T>()];
-        const bool hold = kbw_hold<T>() > 2 && qj.w <= kbw_hold<T>();
+        constexpr int KH = kbw_hold<T>();
+        const bool hold = KH > 2;                  // columns [0, min(w, KH)) held
         Kn qp = qj;
         if (j > 0) {
             qp = kn_load(a.meta, j - 1);
@@ -2715,6 +2717,14 @@ __global__ void __launch_bounds__(64 * KF_W) kb_bwd_kernel(KbArgs<T> a, int64_t 
                 for (int c = 0; c < kbw_hold<T>(); c += 2) {  // tbv is 0 past w (set above)
                     s0 = fma(d2[c], rdlane(tbv[c >> 6], c & 63), s0);
                     s1 = fma(d2[c + 1], rdlane(tbv[(c + 1) >> 6], (c + 1) & 63), s1);
+                }
+                for (int c0 = KH; c0 < qj.w; c0 += KBW_VC) {    // columns past the held ones
+                    T y[KBW_VC];
+#pragma unroll
+                    for (int u = 0; u < KBW_VC; ++u) y[u] = c0 + u < qj.w ? Yk[rl + (int64_t)(c0 + u) * qj.rows] : (T)0;
+#pragma unroll
+                    for (int u = 0; u < KBW_VC; ++u)
+                        if (c0 + u < qj.w) s0 = fma(y[u], tb[c0 + u], s0);
                 }
                 vb[lane] = lane < qj.p1 ? s0 + s1 : (T)0;
             } else {
@@ -2813,7 +2823,7 @@ __global__ void __launch_bounds__(64 * KF_W) kb_bwd_kernel(KbArgs<T> a, int64_t 
         for (int u = 0; u < 2; ++u) {
             const int c = lane + 64 * u;
             if (c < qj.w) {
-                const T sd = j > 0 ? (hold ? tb[c] : dot_run<T>(Yk + (int64_t)c * qj.rows, lb, qj.p1, vs)) : (T)0;
+                const T sd = j > 0 ? ((hold && c < KH) ? tb[c] : dot_run<T>(Yk + (int64_t)c * qj.rows, lb, qj.p1, vs)) : (T)0;
                 const T res = tc[u] + sd + graw[u];
                 if (a.hfac) tb[c] = res;
                 else dzt[qj.og + c] = -(res * hc[u]);
