@@ -1829,62 +1829,22 @@ LQRX_FILP_INST(8, 4, 8, 1, 8)
 // ------------------------------------------------------------------ dense / block-diagonal H
 // (BlockCholesky modes 0/1, block_cholesky.jl:55-77) on the diagonal-H kernels: with H_k = UᵀU,
 // Z = Y U⁻¹ and gz = U⁻ᵀg the KKT system is the same with H = I (S = ZZᵀ = Y H⁻¹ Yᵀ, r = Z gz
-// = Y H⁻¹ g, λ unchanged) and δz = U⁻¹δz'.  The pre-pass writes gz (g's packing), a unit
-// diagonal H and U (packed upper, inverse diagonal), the Z kernel Z (Y's packing) one row per
-// thread; the diagonal-H kernel solves;
+// = Y H⁻¹ g, λ unchanged) and δz = U⁻¹δz'.  The pre-pass (kkt_hz_kernel) writes Z (Y's
+// packing) one row per thread, gz (g's packing), a unit diagonal H and U (packed upper, inverse
+// diagonal); the diagonal-H kernel solves;
 // the post-pass applies U⁻¹ to δz in place and merges `info` in the order the dense-H sweep
 // reports it (H_k is factored one step before knot k−1's pivots: a non-SPD H_k, −(k+1), wins
 // over a pivot failure at knot ≥ k−1).  One thread per (trajectory, knot), w ≤ WM.
+// One thread per (trajectory, knot, row of Y): the rows of a knot are consecutive threads, so
+// their Y loads and Z stores are one contiguous run per column and their H loads the same
+// addresses; every thread factors H_k = UᵀU itself (w ≤ 10: cheaper than a pass that stores U
+// for the others to re-read), forms z = y U⁻¹ of its row, and the knot's row-0 thread also
+// writes gz = U⁻ᵀg, the unit diagonal, the packed U for the post-pass and the H-failure knot.
+// The trajectory form's row counts give the knot in closed form.
 template <int WM>
-__global__ __launch_bounds__(256) void kkt_hpre_kernel(const KktArgs a, double *__restrict__ gz,
-                                                      double *__restrict__ ones, double *__restrict__ Up,
-                                                      int32_t *__restrict__ infoh, int64_t sU)
-{
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= a.batch * a.N) return;
-    const int64_t t = i / a.N;
-    const int k = (int)(i - t * a.N);
-    const int32_t *m = a.meta + 8 * k;
-    const int w = m[3];
-    const int64_t oH = m[6], og = m[7];
-    // packed-U offset of knot k: every knot before the last has knot 0's w (trajectory form)
-    const int w0 = a.meta[3];
-    const int64_t oU = (int64_t)k * (w0 * (w0 + 1) / 2);
-    const double *H = a.H + t * a.sH + oH;
-    double U[WM][WM];
-#pragma unroll
-    for (int c = 0; c < WM; ++c)
-#pragma unroll
-        for (int r = 0; r <= c; ++r) U[r][c] = (c < w) ? H[r + (int64_t)c * w] : (r == c ? 1.0 : 0.0);
-    const bool ok = potrf_inv<WM>(U);
-    if (!ok) atomicMin(&infoh[t], k);                 // first non-SPD knot (pre-set to N)
-    double x[WM];
-    const double *g = a.g + t * a.sg + og;
-#pragma unroll
-    for (int c = 0; c < WM; ++c) x[c] = c < w ? g[c] : 0.0;
-    trsv_t<WM>(U, x);
-    double *gzt = gz + t * a.sg + og, *on = ones + t * a.sg + og;
-#pragma unroll
-    for (int c = 0; c < WM; ++c)
-        if (c < w) {
-            gzt[c] = x[c];
-            on[c] = 1.0;
-        }
-    double *Ut = Up + t * sU + oU;
-    int e = 0;
-#pragma unroll
-    for (int c = 0; c < WM; ++c)
-#pragma unroll
-        for (int r = 0; r <= c; ++r)
-            if (c < w) Ut[e++] = U[r][c];
-}
-
-// Z = Y U⁻¹ row by row: one thread per (trajectory, knot, row of Y) — the rows of a knot are
-// consecutive threads (their Y loads and Z stores are one contiguous run per column, their U
-// loads the same addresses); the trajectory form's row counts give the knot in closed form
-template <int WM>
-__global__ __launch_bounds__(256) void kkt_hz_kernel(const KktArgs a, double *__restrict__ Z,
-                                                    const double *__restrict__ Up, int64_t sU)
+__global__ __launch_bounds__(256) void kkt_hz_kernel(const KktArgs a, double *__restrict__ Z, double *__restrict__ gz,
+                                                    double *__restrict__ ones, double *__restrict__ Up,
+                                                    int32_t *__restrict__ infoh, int64_t sU)
 {
     const int N = a.N;
     const int R0 = a.meta[0] + a.meta[1] + a.meta[2], R1 = a.meta[8] + a.meta[9] + a.meta[10];
@@ -1906,14 +1866,13 @@ __global__ __launch_bounds__(256) void kkt_hz_kernel(const KktArgs a, double *__
     }
     const int32_t *m = a.meta + 8 * k;
     const int rows = m[0] + m[1] + m[2], w = m[3];
-    const int w0 = a.meta[3];
-    const double *Ut = Up + t * sU + (int64_t)k * (w0 * (w0 + 1) / 2);
+    const double *H = a.H + t * a.sH + m[6];
     double U[WM][WM];
-    int e = 0;
 #pragma unroll
     for (int c = 0; c < WM; ++c)
 #pragma unroll
-        for (int r = 0; r <= c; ++r) U[r][c] = (c < w) ? Ut[e++] : (r == c ? 1.0 : 0.0);
+        for (int r = 0; r <= c; ++r) U[r][c] = (c < w) ? H[r + (int64_t)c * w] : (r == c ? 1.0 : 0.0);
+    const bool ok = potrf_inv<WM>(U);
     const double *Y = a.Y + t * a.sY + m[4] + j;
     double x[WM];
 #pragma unroll
@@ -1923,6 +1882,30 @@ __global__ __launch_bounds__(256) void kkt_hz_kernel(const KktArgs a, double *__
 #pragma unroll
     for (int c = 0; c < WM; ++c)
         if (c < w) Zt[(int64_t)c * rows] = x[c];
+    if (j == 0) {
+        if (!ok) atomicMin(&infoh[t], k);             // first non-SPD knot (pre-set to N)
+        const int64_t og = m[7];
+        const double *g = a.g + t * a.sg + og;
+#pragma unroll
+        for (int c = 0; c < WM; ++c) x[c] = c < w ? g[c] : 0.0;
+        trsv_t<WM>(U, x);
+        double *gzt = gz + t * a.sg + og, *on = ones + t * a.sg + og;
+#pragma unroll
+        for (int c = 0; c < WM; ++c)
+            if (c < w) {
+                gzt[c] = x[c];
+                on[c] = 1.0;
+            }
+        // packed-U offset of knot k: every knot before the last has knot 0's w (trajectory form)
+        const int w0 = a.meta[3];
+        double *Ut = Up + t * sU + (int64_t)k * (w0 * (w0 + 1) / 2);
+        int e = 0;
+#pragma unroll
+        for (int c = 0; c < WM; ++c)
+#pragma unroll
+            for (int r = 0; r <= c; ++r)
+                if (c < w) Ut[e++] = U[r][c];
+    }
 }
 
 template <int WM>
@@ -2048,7 +2031,7 @@ static bool fil_dispatch(const KktArgs &a, const int32_t *n1, const int32_t *p, 
 }
 
 // Dense / block-diagonal H (ginv, layout 0) on a structure whose diagonal-H form a FIL shape
-// serves: the pre-pass / diagonal kernel / post-pass of fil::kkt_hpre_kernel.  Scratch: Z | gz |
+// serves: the pre-pass / diagonal kernel / post-pass of fil::kkt_hz_kernel.  Scratch: Z | gz |
 // unit H | packed U | H-failure knots | the diagonal kernel's slab.
 namespace {
 constexpr int FILH_WM = 10;                           // w ≤ 10: every FIL shape and padded bin
@@ -2108,14 +2091,10 @@ bool kkt_fil_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const
     // H-failure knots start at N ("none"): 0x7f7f7f7f ≥ N for every accepted structure
     e = hipMemsetAsync(infoh, 0x7f, (size_t)a.batch * 4, s);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL((fil::kkt_hpre_kernel<FILH_WM>), dim3(grid), dim3(256), 0, s, a, gz, on, Up, infoh, P.sU);
-        e = hipGetLastError();
-    }
-    if (e == hipSuccess) {
         int64_t Rt = 0;
         for (int k = 0; k < a.N; ++k) Rt += n1[k] + p[k] + n2[k];
         hipLaunchKernelGGL((fil::kkt_hz_kernel<FILH_WM>), dim3((unsigned)((a.batch * Rt + 255) / 256)), dim3(256), 0, s,
-                           a, Z, Up, P.sU);
+                           a, Z, gz, on, Up, infoh, P.sU);
         e = hipGetLastError();
     }
     if (e == hipSuccess) {
