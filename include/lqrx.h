@@ -177,7 +177,11 @@ int lqrx_dp_solve_linear_host(const lqrx_dp_desc *desc, const void *A, const voi
  * ------------------------------------------------------------------------------------ */
 typedef struct lqrx_kkt_desc {
     int32_t N;          /* knots                                                  */
-    int32_t dtype;      /* LQRX_F64 (every KKT kernel) or LQRX_F32 (layout 0: the
+    int32_t dtype;      /* LQRX_F64 (every KKT kernel: the compile-time shapes, the
+                           padded bins for trajectory structures up to n̄ <= 8, m <= 4
+                           — dense / block-diagonal H on both through an H = UᵀU
+                           pre/post pass — then the large-block and workgroup kernels)
+                           or LQRX_F32 (layout 0: the
                            large-block MFMA kernels for n1, p, n2 <= 64, padded rows
                            <= 128, w <= 128, and the workgroup-per-trajectory kernel
                            past them; every h_mode and ginv; else
