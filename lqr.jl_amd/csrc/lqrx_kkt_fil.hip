@@ -26,6 +26,8 @@
 #include "lqrx_internal.h"
 #include "lqrx_stage.h"
 #include "lqrx_tile.h"
+#include <algorithm>
+#include <climits>
 #include <cstdlib>
 #include <type_traits>
 
@@ -2009,7 +2011,11 @@ static bool fil_dispatch(const KktArgs &a, const int32_t *n1, const int32_t *p, 
     // any other trajectory structure up to a padded bin (layout 0; layout 1 is staged): the
     // smallest bin that holds it, its own sizes at run time (Shape PAD, Rt).  LQRX_KKT_PAD=0
     // sends them to the large-block kernels instead (A/B)
-    if (fil_ext_on() && !soa && (diag || !ginv) && nx >= 1 && m >= 0 && P0 >= 0 && PK >= 0 && PN >= 0) {
+    // (per-lane byte offsets from a wave's base are 32-bit and the buffer range 2 GiB: 64
+    // trajectories of every array must span less)
+    const int64_t smax = std::max(std::max(a.sY, a.sy), std::max(a.sH, a.sg));
+    if (fil_ext_on() && !soa && (diag || !ginv) && nx >= 1 && m >= 0 && P0 >= 0 && PK >= 0 && PN >= 0 &&
+        smax * 8 * 64 < (int64_t)INT32_MAX) {
         KktArgs b = a;
         b.rt[0] = nx; b.rt[1] = m; b.rt[2] = P0; b.rt[3] = PK; b.rt[4] = PN;
 #define LQRX_FILP(NX, M, A0, AK, AN)                                                                     \
