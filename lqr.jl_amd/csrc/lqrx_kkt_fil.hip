@@ -40,6 +40,9 @@ namespace fil {
                          // hand-placed VMEM waits, 32 no forward slab stores, 64 no δz/λ
                          // stores — timing bounds only, results wrong)
 #endif
+#ifndef LQRX_FIL_RING
+#define LQRX_FIL_RING 1  // layout-0 δz/λ of interior knots through the LDS output ring (0: direct stores)
+#endif
 #ifndef LQRX_FIL_N12
 #define LQRX_FIL_N12 1   // 12-byte LDS-DMA pieces for the short chunks (0: dwords only)
 #endif
@@ -1137,7 +1140,7 @@ template <class S, class C> struct KnotIn {      // a staged knot's Y, H, g in r
 
 template <class S, class C, int NLP>
 __device__ __forceinline__ void primal_knot(const Ctx<S> &c, int k, const SlabV<C> &v, const double (&lp)[Z(NLP)],
-                                            const KnotIn<S, C> &in)
+                                            const KnotIn<S, C> &in, uint32_t ring = 0)
 {
     constexpr int R = C::R, W = C::W;
     static_assert(NLP == C::P1, "λ_{k-1} has n1[k] entries");
@@ -1187,7 +1190,10 @@ __device__ __forceinline__ void primal_knot(const Ctx<S> &c, int k, const SlabV<
         double nz[W];
 #pragma unroll
         for (int j = 0; j < W; ++j) nz[j] = -z[j];
-        if constexpr (S::PAD) {
+        if (ring) {                                               // output ring (layout 0, interior)
+#pragma unroll
+            for (int j = 0; j < W; ++j) *(lds_dw *)(size_t)(ring + 8u * j) = nz[j];
+        } else if constexpr (S::PAD) {
             const Rt rt = c.rt.fresh();
             const int lr = std::is_same<C, typename S::L>::value ? rt.nx : (int)rt.Lg;
             c.template out_store_pad<W, std::is_same<C, typename S::I>::value>(
@@ -1200,7 +1206,7 @@ __device__ __forceinline__ void primal_knot(const Ctx<S> &c, int k, const SlabV<
 }
 
 template <class S, class C>
-__device__ __forceinline__ void store_lam(const Ctx<S> &c, int k, const SlabV<C> &v)
+__device__ __forceinline__ void store_lam(const Ctx<S> &c, int k, const SlabV<C> &v, uint32_t ring = 0)
 {
     if constexpr ((LQRX_FIL_ABL & 64) != 0) return;
     if constexpr (S::SOA) {
@@ -1219,7 +1225,10 @@ __device__ __forceinline__ void store_lam(const Ctx<S> &c, int k, const SlabV<C>
             for (int i = 0; i < C::PS; ++i) lv[i] = v.mu[i];
 #pragma unroll
             for (int i = 0; i < C::P2; ++i) lv[C::PS + i] = v.la[i];
-            if constexpr (S::PAD) {
+            if (ring) {
+#pragma unroll
+                for (int i = 0; i < LL; ++i) *(lds_dw *)(size_t)(ring + 8u * i) = lv[i];
+            } else if constexpr (S::PAD) {
                 const Rt rt = c.rt.fresh();
                 int p1, ps, p2;
                 rt.template cls<S, C>(p1, ps, p2);
@@ -1246,6 +1255,41 @@ __device__ __forceinline__ void fwd_wait()
     vm_wait<S::template Dmin<Cnn>() + Sprev>();
 }
 
+// ------------------------------------------------------------------ layout-0 output ring
+// The layout-0 δz / λ chunks of one knot are 40-B pieces 4 KB apart (one per trajectory); L2
+// writes their lines back partially before the neighbouring knots fill them.  Interior steps of
+// the staged kernel instead put their chunks into an LDS image of a group of OR_G knots —
+// per trajectory the group's δz run ([t][OR_G·W]) and λ run ([t][OR_G·L]), in memory order — and
+// the image of the previous group leaves during the next group's steps, W + L store instructions
+// per step (exactly the count of the direct stores it replaces, so the hand-counted vmcnt bounds
+// are unchanged; the first group's steps issue out-of-range stores).  Instruction f moves
+// the image's doubles 64f … 64f + 63: consecutive lanes write consecutive doubles of one
+// trajectory's OR_G-knot run.
+constexpr int OR_G = 4;
+template <class S> constexpr int or_w() { return S::I::W; }
+template <class S> constexpr int or_l() { return S::I::PS + S::I::P2; }
+template <class S> constexpr int or_doubles() { return OR_G * 64 * (or_w<S>() + or_l<S>()); }   // one group image
+// flush instructions f ∈ [f0, f0 + NF) of the group image at LDS byte address img whose δz run
+// starts at element offset oz and λ run at ol; valid = false: out-of-range stores (dropped)
+template <class S, int NF>
+__device__ __forceinline__ void or_flush(const Ctx<S> &c, uint32_t img, int f0, int64_t oz, int64_t ol, bool valid)
+{
+    constexpr int RZ = OR_G * or_w<S>(), RL = OR_G * or_l<S>();
+    const rsrc_t rz = make_rsrc(c.bdz), rl = make_rsrc(c.blam);
+#pragma unroll
+    for (int u = 0; u < NF; ++u) {
+        const int f = f0 + u;
+        const bool isz = f < RZ;
+        const uint32_t p = 64u * (uint32_t)(isz ? f : f - RZ) + (uint32_t)c.lane;
+        const uint32_t run = isz ? (uint32_t)RZ : (uint32_t)RL;
+        const uint32_t tr = p / run, e = p - tr * run;
+        const double v = *(lds_dw *)(size_t)(img + 8u * (isz ? p : 64u * RZ + p));
+        const uint32_t vo = (valid && tr < (uint32_t)c.nlive)
+                                ? tr * (uint32_t)((isz ? c.sgz : c.slz) * 8) + 8u * e : 0xFFFFFF00u;
+        bstore(v, isz ? rz : rl, vo, (uint32_t)((isz ? oz : ol) * 8));
+    }
+}
+
 // ------------------------------------------------------------------ the kernel
 template <class S>
 __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__restrict__ scratch)
@@ -1256,6 +1300,10 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     __shared__ __attribute__((aligned(16))) double stg[3 * S::BUF];
     __shared__ __attribute__((aligned(16))) double sl[3 * SLB<S>];
     __shared__ __attribute__((aligned(16))) double ost[S::SOA ? 1 : 64 * (S::WOUT + S::LOUT)];
+    // the layout-0 output ring (two group images), where the static LDS allows it
+    constexpr bool RING = !S::SOA && LQRX_FIL_RING &&
+                          (3 * S::BUF + 3 * SLB<S> + 64 * (S::WOUT + S::LOUT) + 2 * or_doubles<S>()) * 8 <= 160 * 1024;
+    __shared__ __attribute__((aligned(16))) double oring[RING ? 2 * or_doubles<S>() : 1];
     const int N = a.N;                                          // ≥ 4 (host-checked)
     const int64_t t0 = (int64_t)blockIdx.x * 64;
     Ctx<S> c;
@@ -1400,6 +1448,13 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
         primal_knot<S, L, L::P1>(c, N - 1, vL, vI.la, in);
     }
     store_lam<S, I>(c, N - 2, vI);
+    // output ring: interior steps q = N−3−j in whole groups of OR_G (q < nq) write to the ring; a
+    // trailing partial group stores directly; the last group image leaves after the loop
+    const bool ring_on = RING && !c.sel;
+    const int nq = ring_on ? ((N - 3) / OR_G) * OR_G : 0;
+    const uint32_t rbase = (uint32_t)(size_t)(lptr_t)oring;
+    constexpr uint32_t RB = (uint32_t)or_doubles<S>() * 8u;            // bytes per group image
+    constexpr int RZ = OR_G * or_w<S>(), RL = OR_G * or_l<S>();
     for (int j = N - 3; j >= 1; --j) {
         // slab j, knot j+1 were issued at step j+2; after them: stores of step j+2, the DMA
         // of step j+1 (knot j; slab j-1 only when j ≥ 2) and its stores.
@@ -1422,9 +1477,35 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
         else c.stage_any(a, 0, stg, false);
         recompute_Ft<S, I>(vI.F, v.Cm, in.Y, in.H);
         bwd_knot<I, I>(v, vI);
-        primal_knot<S, I, I::P1>(c, j + 1, vI, v.la, in);
-        store_lam<S, I>(c, j, v);
+        const int q = N - 3 - j;
+        if (q < nq) {
+            const int g = q / OR_G, sl_ = q % OR_G;
+            // 1/OR_G of the previous group's image leaves (group g−1: δz of knots kz … kz+OR_G−1,
+            // λ of knots kz−1 …, lowest first in memory)
+            const uint32_t prev = rbase + (uint32_t)((g + 1) & 1) * RB;
+            const int kz = N - 1 - OR_G * g, kl = kz - 1;
+            or_flush<S, or_w<S>() + or_l<S>()>(c, prev, sl_ * (or_w<S>() + or_l<S>()), Off<S>::g(kz), Off<S>::y(kl), g > 0);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t cur = rbase + (uint32_t)(g & 1) * RB;
+            const int pos = OR_G - 1 - sl_;                    // this step's knots in memory order
+            primal_knot<S, I, I::P1>(c, j + 1, vI, v.la, in, cur + 8u * (uint32_t)(c.lane * RZ + pos * or_w<S>()));
+            store_lam<S, I>(c, j, v, cur + 8u * (uint32_t)(64 * RZ + c.lane * RL + pos * or_l<S>()));
+        } else {
+            primal_knot<S, I, I::P1>(c, j + 1, vI, v.la, in);
+            store_lam<S, I>(c, j, v);
+        }
         vI = v;
+    }
+    if (nq > 0) {
+        // the last ring group leaves whole
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int gl = nq / OR_G - 1;
+        const int kz = N - 2 - OR_G * gl - (OR_G - 1), kl = kz - 1;
+        or_flush<S, RZ + RL>(c, rbase + (uint32_t)(gl & 1) * RB, 0, Off<S>::g(kz), Off<S>::y(kl), true);
     }
     {
         // step 0: multipliers of knot 0 (its class-F slab is the wider one: a register load,
