@@ -454,8 +454,14 @@ __device__ __forceinline__ void dp_rollout_full(const DpArgs &a, int64_t b, T *l
     // KOPS·(DEPTH−1) are outstanding (fewer in the first DEPTH knots: the bound below is the
     // smallest such count, i.e. a slight over-wait in the steady state)
     // (A K slot too large for the 6-bit vmcnt — n = 64, m = 32 — takes compiler-tracked loads.)
+    // Not with linear terms: there the compiler copied an in-flight d register (the asm load's
+    // destination, which it sees as already written) into another register before the hand
+    // wait, so u_k now and then used the load's address bits (an intermittent wrong X/U in
+    // tests/test_dp_linear_gpu.py::test_dp_linear_device_stream; the copy is visible in the
+    // gfx950 assembly of dp_riccati_kernel<double,2,1,2,64,true>).  The LIN variants take
+    // compiler-tracked loads, whose waits the compiler places itself.
     constexpr int VMW = (CU + (LIN ? 1 : 0)) * (DEPTH - 1);
-    constexpr bool HAND = VMW <= 63 && CU * MP * (int)sizeof(T) <= 4096;
+    constexpr bool HAND = !LIN && VMW <= 63 && CU * MP * (int)sizeof(T) <= 4096;
     T ring[DEPTH][CU], dring[DEPTH];
     auto issue = [&](int kk, T (&dst)[CU], T &dd) __attribute__((always_inline)) {
         const T *Kk = Kg + (size_t)(min(kk, N - 1) - 1) * mn + iu + (size_t)hu * CU * MP;
