@@ -73,3 +73,60 @@ def test_dma_unit_leaves_m0_to_the_dma_blocks(unit, tmp_path):
             bad.append(t)
     assert dma > 0, "no LDS-DMA blocks found (kernel changed?)"
     assert not bad, f"compiler uses M0 outside the DMA blocks: {bad[:5]}"
+
+
+def _regs(text):
+    out = set()
+    for a, b in re.findall(r"v\[(\d+):(\d+)\]", text):
+        out.update(range(int(a), int(b) + 1))
+    for a in re.findall(r"\bv(\d+)\b", re.sub(r"v\[\d+:\d+\]", "", text)):
+        out.add(int(a))
+    return out
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_dp_rollout_asm_loads_not_read_before_their_wait(tmp_path):
+    """The DP rollout (lqrx_dp.hip dp_rollout_full) issues its K loads as inline asm, invisible
+    to the compiler's wait-count pass, and waits for them by hand.  The compiler treats an asm
+    output register as written at the asm statement, so it may copy it (or read it otherwise)
+    before the hand wait — a race it cannot see: round 4 found one in the linear-terms variant
+    (an in-flight d_k register copied before the wait; intermittently wrong X/U).  Guard: in the
+    compiled gfx950 assembly of every dp_riccati_kernel, no instruction outside the inline-asm
+    blocks reads a register an inline-asm load wrote before an s_waitcnt vmcnt follows it."""
+    out = tmp_path / "dp.s"
+    subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-munsafe-fp-atomics",
+                    "-I" + os.path.join(ROOT, "include"), "--cuda-device-only", "-S",
+                    os.path.join(CSRC, "lqrx_dp.hip"), "-o", str(out)], check=True, timeout=900)
+    text = open(out).read()
+    bad, kernels, asm_loads = [], 0, 0
+    for m in re.finditer(r"^(_ZN4lqrx17dp_riccati_kernel\w+):", text, re.M):
+        kernels += 1
+        body = text[m.end():text.find(".Lfunc_end", m.end())]
+        inasm, pend = False, {}
+        for ln in body.split("\n"):
+            s = ln.strip()
+            if s.startswith(";;#ASMSTART"):
+                inasm = True
+                continue
+            if s.startswith(";;#ASMEND"):
+                inasm = False
+                continue
+            if not s or s.startswith(";") or s.startswith("."):
+                continue
+            if "s_waitcnt" in s and "vmcnt" in s:
+                pend = {}
+                continue
+            if inasm:
+                lm = re.match(r"global_load_dword\w*\s+(v\[\d+:\d+\]|v\d+)", s)
+                if lm:
+                    asm_loads += 1
+                    for r in _regs(lm.group(1)):
+                        pend[r] = s
+                continue
+            if s.startswith("s_"):
+                continue
+            hit = _regs(s) & set(pend)
+            if hit:
+                bad.append((m.group(1)[-48:], s, pend[min(hit)]))
+    assert kernels > 0 and asm_loads > 0, (kernels, asm_loads)
+    assert not bad, bad[:5]
