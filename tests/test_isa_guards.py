@@ -37,6 +37,25 @@ def _dma_units():
 DMA_UNITS = _dma_units()
 
 
+@pytest.fixture(scope="module")
+def asm_of(tmp_path_factory):
+    """gfx950 assembly of every unit these guards read, compiled once and concurrently (each
+    unit is a multi-minute hipcc run; the CPU suite runs serially)."""
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    d = tmp_path_factory.mktemp("isa")
+    units = sorted(set(DMA_UNITS) | {"lqrx_dp.hip"})
+    procs = {}
+    for u in units:
+        procs[u] = subprocess.Popen([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-munsafe-fp-atomics",
+                                     "-I" + os.path.join(ROOT, "include"), "--cuda-device-only", "-S",
+                                     os.path.join(CSRC, u), "-o", str(d / (u + ".s"))],
+                                    stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    for u, pr in procs.items():
+        assert pr.wait(timeout=1200) == 0, f"hipcc failed on {u}"
+    return lambda u: (d / (u + ".s")).read_text()
+
+
 def test_dma_units_found():
     assert "lqrx_kkt_fil.hip" in DMA_UNITS, DMA_UNITS
 
@@ -50,15 +69,10 @@ def test_dma_unit_source_has_no_m0_users(unit):
     assert not hits, f"{unit} uses M0-writing constructs beside dma_lds: {hits}"
 
 
-@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 @pytest.mark.parametrize("unit", DMA_UNITS)
-def test_dma_unit_leaves_m0_to_the_dma_blocks(unit, tmp_path):
-    out = tmp_path / (unit + ".s")
-    subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-munsafe-fp-atomics",
-                    "-I" + os.path.join(ROOT, "include"), "--cuda-device-only", "-S",
-                    os.path.join(CSRC, unit), "-o", str(out)], check=True, timeout=900)
+def test_dma_unit_leaves_m0_to_the_dma_blocks(unit, asm_of):
     inasm, bad, dma = False, [], 0
-    for line in out.read_text().splitlines():
+    for line in asm_of(unit).splitlines():
         t = line.strip()
         if t.startswith(";;#ASMSTART"):
             inasm = True
@@ -84,8 +98,7 @@ def _regs(text):
     return out
 
 
-@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-def test_dp_rollout_asm_loads_not_read_before_their_wait(tmp_path):
+def test_dp_rollout_asm_loads_not_read_before_their_wait(asm_of):
     """The DP rollout (lqrx_dp.hip dp_rollout_full) issues its K loads as inline asm, invisible
     to the compiler's wait-count pass, and waits for them by hand.  The compiler treats an asm
     output register as written at the asm statement, so it may copy it (or read it otherwise)
@@ -93,11 +106,7 @@ def test_dp_rollout_asm_loads_not_read_before_their_wait(tmp_path):
     (an in-flight d_k register copied before the wait; intermittently wrong X/U).  Guard: in the
     compiled gfx950 assembly of every dp_riccati_kernel, no instruction outside the inline-asm
     blocks reads a register an inline-asm load wrote before an s_waitcnt vmcnt follows it."""
-    out = tmp_path / "dp.s"
-    subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-munsafe-fp-atomics",
-                    "-I" + os.path.join(ROOT, "include"), "--cuda-device-only", "-S",
-                    os.path.join(CSRC, "lqrx_dp.hip"), "-o", str(out)], check=True, timeout=900)
-    text = open(out).read()
+    text = asm_of("lqrx_dp.hip")
     bad, kernels, asm_loads = [], 0, 0
     for m in re.finditer(r"^(_ZN4lqrx17dp_riccati_kernel\w+):", text, re.M):
         kernels += 1
