@@ -399,6 +399,8 @@ def main(argv=None):
                     help="kkt workload: Dubins (configs[2]), DoubleIntegrator(3,N) (test/problems.jl), or "
                          "dense: the trajectory structure at --n/--m with dense dynamics, generated in HBM "
                          "(configs[4]: --n 64 --m 32 --N 512 --batch 8192 --dtype f32)")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay one captured HIP graph per step (no per-call host work in the timed loop)")
     ap.add_argument("--kkt-hmode", type=int, choices=[0, 1, 2], default=2,
                     help="kkt workload (dubins / di): BlockCholesky mode of H — 2 diagonal (default), 1 "
                          "block-diagonal, 0 dense (block_cholesky.jl:19-159)")
@@ -580,6 +582,16 @@ def main(argv=None):
         def step():
             K.kkt_solve_device(st, t, hm, 1, stream=sh, out=out, workspace=ws, layout=kl)
 
+    if args.graph:
+        # one step captured as a HIP graph (torch.cuda.graph on the launch stream) and replayed
+        # per step: the serving form, same kernels and work, none of the per-call host work
+        # (ctypes marshalling, ~8 µs) that outlasts a sub-0.1-ms kernel in the timed loop
+        step()
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            step()
+        step = graph.replay
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     sync = lambda: torch.cuda.synchronize(dev)
@@ -866,7 +878,8 @@ def main(argv=None):
             "config": {"workload": workload, "n": n, "m": m, "N": N, "batch_per_gpu": bt,
                        "global_batch": global_batch, "parallelism": f"batch-sharded x{world}",
                        "shard_rank0": [traj0, bt], "shards": shards,
-                       "dist_backend": args.dist_backend if world > 1 else None},
+                       "dist_backend": args.dist_backend if world > 1 else None,
+                       "hip_graph": bool(args.graph)},
             "roofline": roof,
             "cpu_baseline": cpu,
             "check": {"nonfinite": nonfinite, "info_nonzero": bad, "sampled_parity": sampled},
