@@ -595,6 +595,7 @@ __device__ __forceinline__ void stage_knot(const KktArgs &a, const KMeta &km, in
 {
     const int rows = km.n1 + km.p + km.n2;
     const int LH = a.h_mode == 2 ? km.w : km.w * km.w;
+    dma_group();                                                 // one knot: one DMA group
     stage_chunk(a.Y, a.sY, km.oY, rows * km.w, t0, a.batch, buf, lane);
     stage_chunk(a.y, a.sy, km.oy, km.p + km.n2, t0, a.batch, buf + 64 * LYm, lane);
     stage_chunk(a.H, a.sH, km.oH, LH, t0, a.batch, buf + 64 * (LYm + Lym), lane);
@@ -609,11 +610,12 @@ __device__ __forceinline__ void dma_wait()
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 // wait for everything but the N most recent vector-memory ops (the previous knot's slab
-// stores, issued after the DMA being waited for)
+// stores, issued after the DMA being waited for: the most recent DMA group, g=1 — checked on
+// the compiled instruction stream by tests/isa_vmcnt.py)
 template <int NST> __device__ __forceinline__ void dma_wait_but()
 {
     static_assert(NST >= 0 && NST < 64, "vmcnt range");
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NST) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0) ; lqrx.wait g=1" ::"n"(NST) : "memory");
 }
 
 #ifndef LQRX_KKT_DMACHECK
@@ -689,6 +691,9 @@ __global__ __launch_bounds__(64) void kkt_staged_kernel(const KktArgs a, const i
     for (int i = 0; i < PM * PM; ++i) Ua[i] = 0.0;
 #pragma unroll
     for (int i = 0; i < PM; ++i) lprev[i] = 0.0;
+    // knot 1 landed (its DMA ran under knot 0's Schur pieces) — here rather than at the loop's
+    // k = 0 step, so the loop's hand bound below holds on every compiled path
+    dma_wait();
 
     for (int k = 0; k < N; ++k) {
         const int p1 = km.n1, ps = km.p, p2 = km.n2;
@@ -697,9 +702,9 @@ __global__ __launch_bounds__(64) void kkt_staged_kernel(const KktArgs a, const i
         if (k + 1 < N) {
             kn = kmeta(meta, k + 1);
             // knot k+1 has landed (the previous knot's slab stores may still fly) and every
-            // ds_read of the buffer about to be restaged has returned (WAR vs the DMA)
-            if (k == 0) dma_wait();
-            else dma_wait_but<SL::SIZE>();
+            // ds_read of the buffer about to be restaged has returned (WAR vs the DMA); at k = 0
+            // everything already has (the wait before the loop)
+            dma_wait_but<SL::SIZE>();
             if (k + 2 < N) stage_knot(a, kmeta(meta, k + 2), t0, stg + (k & 1) * SC::SIZE, LYm, Lym, LHm, lane);
             asm volatile("" ::: "memory");                      // keep the DMAs before the stores
             const int b = (k + 1) & 1;

@@ -445,6 +445,7 @@ template <class S> struct Ctx {
     const int32_t *sel = nullptr;                  // layout 0, selected trajectories (a.sel + t0) or null
     uint32_t vsoa = 0, rowb = 0;                   // SOA: lane's row-pair offset, bytes per element row
     uint32_t limY = 0, limy = 0, limH = 0, limg = 0; // SOA: bytes from the wave base to each array's end
+    uint32_t lpad = 0;                             // LDS byte address of the DMA filler's 256-B target
     // layout 0: LDS images of the coalesced δz / λ stores (dense_store), interior patterns
     double *ozi = nullptr, *oli = nullptr;
     int64_t sgz = 0, slz = 0;                      // per-trajectory strides of dz, lam
@@ -574,13 +575,39 @@ template <class S> struct Ctx {
             qg.issue(make_rsrc4(bg), O::g(k), buf + S::OFF_g / 8);
         }
     }
+    // A first / last knot stages fewer DMA instructions than an interior one when its blocks
+    // are smaller: it then issues filler DMAs (an out-of-range source — nothing is read — into
+    // a 256-B LDS area nothing reads) up to the interior count.  Every staging group then issues
+    // at least the interior count on every path, so the hand-counted vmcnt bounds, which count
+    // interior groups, hold also on the compiled paths a static check cannot rule out (a last-
+    // knot stage followed by an interior step's wait).
+    template <class C>
+    __device__ __forceinline__ void stage_fill(bool fwd) const
+    {
+        constexpr int nf = S::template Dmin<I>() - S::template Dmin<C>();
+        constexpr int nb = S::template Dbwd<I>() - S::template Dbwd<C>();
+        const u4_t r = make_rsrc4(bY);
+        if (fwd) {
+#pragma unroll
+            for (int i = 0; i < nf; ++i) dma_lds<4>(r, 0xFFFFFF00u, 0u, lpad);
+        } else {
+#pragma unroll
+            for (int i = 0; i < nb; ++i) dma_lds<4>(r, 0xFFFFFF00u, 0u, lpad);
+        }
+    }
     // any knot into its ring buffer (stg + (k mod 3)·BUF)
     __device__ __forceinline__ void stage_any(const KktArgs &a, int k, double *stg, bool fwd) const
     {
         double *buf = stg + (k % 3) * S::BUF;
-        if (k == 0) stage<typename S::F>(a, 0, buf, fwd);
-        else if (k == a.N - 1) stage<typename S::L>(a, k, buf, fwd);
-        else stage_I(k, buf, fwd);
+        if (k == 0) {
+            stage<typename S::F>(a, 0, buf, fwd);
+            stage_fill<typename S::F>(fwd);
+        } else if (k == a.N - 1) {
+            stage<typename S::L>(a, k, buf, fwd);
+            stage_fill<typename S::L>(fwd);
+        } else {
+            stage_I(k, buf, fwd);
+        }
     }
 };
 
@@ -615,15 +642,27 @@ __device__ __forceinline__ double bload(rsrc_t r, uint32_t vo, uint32_t so)
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
 }
 
-// wait until at most N vector-memory ops are outstanding (N ≤ 63) and all LDS ops are done
-template <int N> __device__ __forceinline__ void vm_wait()
+// wait until at most N vector-memory ops are outstanding (N ≤ 63) and all LDS ops are done.
+// G names the DMA group the wait is for — the G-th most recent `dma_group()` — so that
+// tests/isa_vmcnt.py can check N against the compiled instruction stream (N > 0 needs a G).
+// LQRX_FIL_WAIT_SLACK (test-only negative control, never in the library build) loosens every
+// bound by that many ops.
+#ifndef LQRX_FIL_WAIT_SLACK
+#define LQRX_FIL_WAIT_SLACK 0
+#endif
+template <int N, int G = 0> __device__ __forceinline__ void vm_wait()
 {
-    constexpr int n = N > 63 ? 63 : (N < 0 ? 0 : N);
+    static_assert(N <= 0 || G > 0, "a hand vmcnt bound names its target DMA group");
+    constexpr int n0 = N > 0 ? N + LQRX_FIL_WAIT_SLACK : N;
+    constexpr int n = n0 > 63 ? 63 : (n0 < 0 ? 0 : n0);
 #if LQRX_FIL_ABL & 16
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // ablation: no VMEM waits (wrong results)
     (void)n;
 #else
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(n) : "memory");
+    if constexpr (G > 0)
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0) ; lqrx.wait g=%1" ::"n"(n), "n"(G) : "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(n) : "memory");
 #endif
 }
 
@@ -984,11 +1023,14 @@ template <class S> constexpr int SLB = slab_dma_instrs<S>() * 128;     // double
 // DMA instructions that stage one knot's slab chunk of class C (two fields per instruction)
 template <class S, class C> constexpr int slab_dma_of() { return (S::template slab<C>() + 1) / 2; }
 
+// slab k into its ring slot (k mod 3); k < 1: the same DMA, from slab 1, into the slot a slab k
+// would take — a slot nothing reads again (the backward sweep's last steps), so every step
+// issues the same number of DMAs and the hand-counted waits hold on every compiled path
 template <class S, class C>
 __device__ __forceinline__ void stage_slab(const Ctx<S> &c, int k, double *ring)
 {
     const u4_t r = make_rsrc4(c.bS);
-    const uint32_t so = slab_so<S>(k, 0), l0 = lds_addr(ring + (k % 3) * SLB<S>);
+    const uint32_t so = slab_so<S>(k < 1 ? 1 : k, 0), l0 = lds_addr(ring + ((k + 3) % 3) * SLB<S>);
 #pragma unroll
     for (int i = 0; i < slab_dma_of<S, C>(); ++i) dma_lds<16>(r, 2u * c.vS, so + 1024u * i, l0 + 1024u * i);
 }
@@ -1182,10 +1224,11 @@ __device__ __forceinline__ void primal_knot(const Ctx<S> &c, int k, const SlabV<
     }
     if constexpr ((LQRX_FIL_ABL & 64) != 0) return;
     if constexpr (S::SOA) {                                       // coalesced 512-B rows
-        if (c.live) {
+        // every lane stores (a dead lane's offset is past the buffer's range: dropped), so no
+        // exec branch changes the count of vector-memory ops the hand-placed vmcnt bounds rely on
+        const uint32_t vo = c.live ? c.vdz : 0xFFFFFF00u;
 #pragma unroll
-            for (int j = 0; j < W; ++j) bstore(-z[j], make_rsrc(c.bdz), c.vdz, (uint32_t)(Off<S>::g(k) + j) * c.rowb);
-        }
+        for (int j = 0; j < W; ++j) bstore(-z[j], make_rsrc(c.bdz), vo, (uint32_t)(Off<S>::g(k) + j) * c.rowb);
     } else {                                                      // dense image, every lane
         double nz[W];
 #pragma unroll
@@ -1209,13 +1252,12 @@ template <class S, class C>
 __device__ __forceinline__ void store_lam(const Ctx<S> &c, int k, const SlabV<C> &v, uint32_t ring = 0)
 {
     if constexpr ((LQRX_FIL_ABL & 64) != 0) return;
-    if constexpr (S::SOA) {
-        if (!c.live) return;
-        const uint32_t r0 = (uint32_t)Off<S>::y(k);
+    if constexpr (S::SOA) {                                       // (dead lanes: out of range)
+        const uint32_t r0 = (uint32_t)Off<S>::y(k), vo = c.live ? c.vlam : 0xFFFFFF00u;
 #pragma unroll
-        for (int i = 0; i < C::PS; ++i) bstore(v.mu[i], make_rsrc(c.blam), c.vlam, (r0 + i) * c.rowb);
+        for (int i = 0; i < C::PS; ++i) bstore(v.mu[i], make_rsrc(c.blam), vo, (r0 + i) * c.rowb);
 #pragma unroll
-        for (int i = 0; i < C::P2; ++i) bstore(v.la[i], make_rsrc(c.blam), c.vlam, (r0 + C::PS + i) * c.rowb);
+        for (int i = 0; i < C::P2; ++i) bstore(v.la[i], make_rsrc(c.blam), vo, (r0 + C::PS + i) * c.rowb);
         return;
     } else {                                                      // [μ_k; λ_k], dense image
         constexpr int LL = C::PS + C::P2;
@@ -1246,13 +1288,14 @@ __device__ __forceinline__ void store_lam(const Ctx<S> &c, int k, const SlabV<C>
 // After its DMA (issued at step k-2) came the slab stores of step k-2 (not counted:
 // conservative), the DMA of knot k+2 (≥ Dmin<Cnn> instructions) and the slab stores of
 // step k-1 (single-double stores, ≥ the smaller of the F / C slab sizes).  Step 0 has no
-// stores before it.  Then knot k+3 is restaged into knot k's (consumed) buffer.
-template <class S, class C, class Cnn, bool FIRST>
+// stores before it.  Then knot k+3 is restaged into knot k's (consumed) buffer.  G: knot k+1's
+// group counted from the most recent (2 while a step restages knot k+3; 1 after the last one).
+template <class S, class C, class Cnn, bool FIRST, int G = 2>
 __device__ __forceinline__ void fwd_wait()
 {
     constexpr int sF = S::template slab<typename S::F>(), sC = S::template slab<C>();
     constexpr int Sprev = FIRST ? 0 : (sF < sC ? sF : sC);
-    vm_wait<S::template Dmin<Cnn>() + Sprev>();
+    vm_wait<S::template Dmin<Cnn>() + Sprev, G>();
 }
 
 // ------------------------------------------------------------------ layout-0 output ring
@@ -1301,13 +1344,16 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     __shared__ __attribute__((aligned(16))) double sl[3 * SLB<S>];
     __shared__ __attribute__((aligned(16))) double ost[S::SOA ? 1 : 64 * (S::WOUT + S::LOUT)];
     // the layout-0 output ring (two group images), where the static LDS allows it
+    __shared__ __attribute__((aligned(16))) uint32_t dpad[64];   // stage_fill's target
     constexpr bool RING = !S::SOA && LQRX_FIL_RING &&
-                          (3 * S::BUF + 3 * SLB<S> + 64 * (S::WOUT + S::LOUT) + 2 * or_doubles<S>()) * 8 <= 160 * 1024;
+                          (3 * S::BUF + 3 * SLB<S> + 64 * (S::WOUT + S::LOUT) + 2 * or_doubles<S>()) * 8 + 256 <=
+                              160 * 1024;
     __shared__ __attribute__((aligned(16))) double oring[RING ? 2 * or_doubles<S>() : 1];
     const int N = a.N;                                          // ≥ 4 (host-checked)
     const int64_t t0 = (int64_t)blockIdx.x * 64;
     Ctx<S> c;
     c.lane = threadIdx.x;
+    c.lpad = lds_addr(dpad);
     // a.sel (layout 0): wave w solves the trajectories sel[64w ..) of the *nsel selected ones
     // (the SQP's second-order-correction subset); waves past the end leave at once (uniform)
     const int64_t nb = (!S::SOA && a.sel) ? (int64_t)*a.nsel : a.batch;
@@ -1356,10 +1402,13 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     int info = 0;
 
     // ---------------- forward ----------------
+    dma_group();
     c.stage_any(a, 0, stg, true);
+    dma_group();
     c.stage_I(1, stg + S::BUF, true);
+    dma_group();
     c.stage_I(2, stg + 2 * S::BUF, true);               // N ≥ 4: knot 2 is interior
-    vm_wait<S::template Dmin<I>() * 2>();
+    vm_wait<S::template Dmin<I>() * 2, 3>();            // knot 0
     Shur<F> s0;
     double y0[Z(F::PS + F::P2)];
     {
@@ -1384,6 +1433,7 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     Shur<I> sI;
     double yI[Z(I::PS + I::P2)];
     fwd_wait<S, F, I, true>();
+    dma_group();
     c.stage_any(a, 3, stg, true);
     fwd_step<S, F, I, I, true>(a, c, 0, stg, s0, y0, sI, yI, cy, info);
     for (int k = 1; k <= N - 3; ++k) {
@@ -1394,6 +1444,7 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
             fwd_step<S, I, I, L>(a, c, k, stg, sI, yI, sn, yn, cy, info);
         } else {
             fwd_wait<S, I, I, false>();
+            dma_group();
             c.stage_any(a, k + 3, stg, true);
             fwd_step<S, I, I, I>(a, c, k, stg, sI, yI, sn, yn, cy, info);
         }
@@ -1403,7 +1454,7 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     }
     Shur<L> sL;
     double yL[Z(L::PS + L::P2)];
-    fwd_wait<S, I, NoCls, false>();
+    fwd_wait<S, I, NoCls, false, 1>();
     fwd_step<S, I, L, NoCls>(a, c, N - 2, stg, sI, yI, sL, yL, cy, info);
     {
         Shur<NoCls> none;
@@ -1424,22 +1475,26 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     constexpr int nS = slab_dma_of<S, I>(), nK = S::template Dbwd<I>();
     constexpr int stL = L::PS + L::P2, stI = I::PS + I::P2;             // store_lam
     vm_wait<0>();                                               // forward slab stores landed
+    dma_group();
     stage_slab<S, L>(c, N - 1, sl);
+    dma_group();
     stage_slab<S, I>(c, N - 2, sl);
     c.stage_any(a, N - 1, stg, false);
-    vm_wait<nS + S::template Dbwd<L>()>();                      // slab N-1
+    vm_wait<nS + S::template Dbwd<L>(), 2>();                   // slab N-1
     SlabV<L> vL;
     slab_read<S, L>(vL, c, N - 1, sl);
+    dma_group();
     stage_slab<S, I>(c, N - 3, sl);                             // N-3 ≥ 1: interior
     c.stage_I(N - 2, stg + ((N - 2) % 3) * S::BUF, false);
     SlabV<NoCls> vnone;
     bwd_knot<L, NoCls>(vL, vnone);                              // step N-1 (no primal)
     store_lam<S, L>(c, N - 1, vL);
     // step N-2: slab N-2, knot N-1 (issued before step N-1's DMA and stores)
-    vm_wait<nS + nK + stL>();
+    vm_wait<nS + nK + stL, 2>();
     SlabV<I> vI;
     slab_read<S, I>(vI, c, N - 2, sl);
-    if (N - 4 >= 1) stage_slab<S, I>(c, N - 4, sl);
+    dma_group();
+    stage_slab<S, I>(c, N - 4, sl);                             // (N = 4: the k < 1 filler)
     c.stage_I(N - 3, stg + ((N - 3) % 3) * S::BUF, false);
     bwd_knot<I, L>(vI, vL);                                     // class L: no F̃ (p2 = 0)
     {
@@ -1457,22 +1512,23 @@ __global__ __launch_bounds__(64) void kkt_fil_kernel(const KktArgs a, double *__
     constexpr int RZ = OR_G * or_w<S>(), RL = OR_G * or_l<S>();
     for (int j = N - 3; j >= 1; --j) {
         // slab j, knot j+1 were issued at step j+2; after them: stores of step j+2, the DMA
-        // of step j+1 (knot j; slab j-1 only when j ≥ 2) and its stores.
-        // Lower bounds: the slab of step N-2 is not counted at j = N-3.
+        // of step j+1 (slab j-1 — the filler when j < 2 — and knot j) and its stores.
         constexpr int stp = stI + I::W;                         // stores of an interior step
-        if (j == N - 3) vm_wait<stL + nK + L::W + stI>();
-        else if (j == N - 4) {
-            if (j >= 2) vm_wait<L::W + stI + nS + nK + stp>();
-            else vm_wait<L::W + stI + nK + stp>();
-        } else {
-            if (j >= 2) vm_wait<stp + nS + nK + stp>();
-            else vm_wait<stp + nK + stp>();
-        }
+        // (target: the group of step j+2, the second most recent; every group carries a slab
+        // DMA — stage_slab's k < 1 filler at the last steps).  At j = N−3 the ops after it are
+        // stL + nS + nK + L::W + stI, at j = N−4 L::W + stI + nS + nK + stp, later stp + nS + nK
+        // + stp: ONE wait at the smallest of the three (it waits for a few more of step j+2's
+        // stores in the steady state) — one bound per loop, so it holds on every compiled path,
+        // also those a static check cannot rule out (the loop entering at a later case)
+        constexpr int b0 = stL + nS + nK + L::W + stI, b1 = L::W + stI + nS + nK + stp, b2 = stp + nS + nK + stp;
+        constexpr int bw = b0 < b1 ? (b0 < b2 ? b0 : b2) : (b1 < b2 ? b1 : b2);
+        vm_wait<bw, 2>();
         SlabV<I> v;
         slab_read<S, I>(v, c, j, sl);
         KnotIn<S, I> in;                                        // knot j+1: F̃_{j+1} and δz_{j+1}
         in.load(Buf<S>{stg + ((j + 1) % 3) * S::BUF}, c.lane);
-        if (j - 2 >= 1) stage_slab<S, I>(c, j - 2, sl);
+        dma_group();
+        stage_slab<S, I>(c, j - 2, sl);                         // (j − 2 < 1: the filler)
         if (j - 1 >= 1) c.stage_I(j - 1, stg + ((j - 1) % 3) * S::BUF, false);
         else c.stage_any(a, 0, stg, false);
         recompute_Ft<S, I>(vI.F, v.Cm, in.Y, in.H);

@@ -105,6 +105,13 @@ __device__ __forceinline__ void dma_lds(u4_t r, uint32_t vo, uint32_t so, uint32
 }
 __device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(size_t)(lptr_t)p; }
 
+// Source marker (an assembly comment, no instruction): the LDS-DMA issued from here up to the
+// next marker form one group — the unit a hand-placed wait names as its target
+// (`s_waitcnt vmcnt(N) … ; lqrx.wait g=G`: the G-th most recent group must have landed).
+// tests/isa_vmcnt.py checks every such bound against the compiled gfx950 instruction stream:
+// at least N vector-memory instructions issued after the target group's last DMA, on every path.
+__device__ __forceinline__ void dma_group() { asm volatile("; lqrx.grp"); }
+
 // number of DMA instructions stage_chunk issues for a chunk of L doubles (same rule)
 __host__ __device__ constexpr int stage_instrs(int L, bool wide) { return L <= 0 ? 0 : (wide ? L / 2 : 2 * L); }
 

@@ -171,6 +171,63 @@ def source_hash(root: str | None = None) -> str:
     return h.hexdigest()
 
 
+def _code_digest(path: str) -> str:
+    """SHA-256 (16 hex) of a C/C++/HIP source with its comments and blank space removed: an edit
+    of the documentation keeps the digest, an edit of the code changes it."""
+    import hashlib
+
+    with open(path) as fh:
+        src = fh.read()
+    src = re.sub(r"/\*.*?\*/", " ", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", " ", src)
+    src = re.sub(r"\s+", " ", src).strip()
+    return hashlib.sha256(src.encode()).hexdigest()[:16]
+
+
+def _root(root: str | None) -> str:
+    return root or os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def kernel_unit(kernel: str, root: str | None = None) -> str | None:
+    """The csrc/*.hip translation unit that defines the __global__ function `kernel` (its base
+    name, e.g. ``kb_fuse_mid_kernel``), relative to the repository root, or None."""
+    import glob
+
+    root = _root(root)
+    base = re.findall(r"(\w+)", kernel.split("<")[0])[-1]
+    for f in sorted(glob.glob(os.path.join(root, "lqr.jl_amd", "csrc", "*.hip"))):
+        with open(f) as fh:
+            src = fh.read()
+        if re.search(r"__global__[^;{}]*?\b" + re.escape(base) + r"\s*\(", src, re.S):
+            return os.path.relpath(f, root)
+    return None
+
+
+def kernel_source_digest(units, root: str | None = None) -> dict:
+    """{path: code digest} of the given translation units and every local header they include
+    (recursively; ``lqrx.h`` resolves to include/) — the sources a measured kernel's code comes
+    from.  Recorded with each PMC traffic figure (tools/traffic_json.py) and recomputed by
+    bench.py, which drops a figure whose kernel's code has changed since."""
+    root = _root(root)
+    out, todo = {}, list(units)
+    while todo:
+        rel = todo.pop()
+        if rel in out:
+            continue
+        path = os.path.join(root, rel)
+        if not os.path.exists(path):
+            out[rel] = None
+            continue
+        out[rel] = _code_digest(path)
+        with open(path) as fh:
+            for inc in re.findall(r'#\s*include\s*"([^"]+)"', fh.read()):
+                cand = os.path.normpath(os.path.join(os.path.dirname(rel), inc))
+                if os.path.basename(inc) == "lqrx.h":
+                    cand = os.path.join("include", "lqrx.h")
+                todo.append(cand)
+    return dict(sorted(out.items()))
+
+
 def build_info() -> dict:
     """The loaded library's build record and whether it matches the sources in this tree."""
     info = load().lqrx_build_info().decode()

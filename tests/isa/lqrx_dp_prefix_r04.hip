@@ -1,3 +1,9 @@
+// TEST-ONLY NEGATIVE CONTROL — never built into liblqrx.so.
+// lqr.jl_amd/csrc/lqrx_dp.hip as it stood before commit 53f4b95 (round 4), whose linear-terms
+// rollout waited for its inline-asm K/d loads by hand: the compiler copied an in-flight d
+// register before that wait (an intermittent wrong X/U).  tests/test_isa_guards.py compiles
+// this file (device code only, the one LIN kernel instantiated below) and requires
+// tests/isa_vmcnt.py to report the hazard.  Only the launcher at the end is cut.
 // lqrx_dp.hip — batched finite-horizon LQR (Riccati backward pass + forward rollout) on
 // gfx950.  Replaces, for a whole batch per launch, the reference's per-knot LAPACK/BLAS
 // calls in solve!(sol, ::DPSolver, ::LQRProblem)  /root/reference/src/dynamic_programming.jl:54-72.
@@ -454,14 +460,8 @@ __device__ __forceinline__ void dp_rollout_full(const DpArgs &a, int64_t b, T *l
     // KOPS·(DEPTH−1) are outstanding (fewer in the first DEPTH knots: the bound below is the
     // smallest such count, i.e. a slight over-wait in the steady state)
     // (A K slot too large for the 6-bit vmcnt — n = 64, m = 32 — takes compiler-tracked loads.)
-    // Not with linear terms: there the compiler copied an in-flight d register (the asm load's
-    // destination, which it sees as already written) into another register before the hand
-    // wait, so u_k now and then used the load's address bits (an intermittent wrong X/U in
-    // tests/test_dp_linear_gpu.py::test_dp_linear_device_stream; the copy is visible in the
-    // gfx950 assembly of dp_riccati_kernel<double,2,1,2,64,true>).  The LIN variants take
-    // compiler-tracked loads, whose waits the compiler places itself.
     constexpr int VMW = (CU + (LIN ? 1 : 0)) * (DEPTH - 1);
-    constexpr bool HAND = !LIN && VMW <= 63 && CU * MP * (int)sizeof(T) <= 4096;
+    constexpr bool HAND = VMW <= 63 && CU * MP * (int)sizeof(T) <= 4096;
     T ring[DEPTH][CU], dring[DEPTH];
     auto issue = [&](int kk, T (&dst)[CU], T &dd) __attribute__((always_inline)) {
         const T *Kk = Kg + (size_t)(min(kk, N - 1) - 1) * mn + iu + (size_t)hu * CU * MP;
@@ -481,70 +481,54 @@ __device__ __forceinline__ void dp_rollout_full(const DpArgs &a, int64_t b, T *l
         issue(1 + d, ring[d], dring[d]);
     }
     wsync_w();
-    // one knot: slot d holds K_k (issued DEPTH knots earlier); NEXT: refill the slot with knot
-    // k + DEPTH (the main loop) or not (the tail)
-    auto knot = [&](int k, T (&rk)[CU], T &dk, bool next) __attribute__((always_inline)) {
-        // u = −K_k x_k (− d_k)   (dynamic_programming.jl:68)
-        T xu[CU];
-#pragma unroll
-        for (int c = 0; c < CU; ++c) xu[c] = xs[hu * CU + c];
-        T s0 = (T)0, s1 = (T)0;
-#pragma unroll
-        for (int c = 0; c < CU; c += 2) {
-            s0 = fma(rk[c], xu[c], s0);
-            if (c + 1 < CU) s1 = fma(rk[c + 1], xu[c + 1], s1);
-        }
-        T su = s0 + s1;
-#pragma unroll
-        for (int o = MP; o < 64; o <<= 1) su += __shfl_xor(su, o);
-        const T u = LIN ? -(su + dk) : -su;
-        T dn = (T)0;
-        if (next) issue(k + DEPTH, rk, LIN ? dk : dn);
-        if (hu == 0) {
-            us[iu] = u;
-            Ug[(size_t)(k - 1) * MP + iu] = u;
-        }
-        wsync_w();
-        // x_{k+1} = A x_k + B u_k   (:69)
-        T t0 = (T)0, t1 = (T)0;
-#pragma unroll
-        for (int c = 0; c < CX; c += 2) {
-            t0 = fma(arow[c], xs[hx * CX + c], t0);
-            if (c + 1 < CX) t1 = fma(arow[c + 1], xs[hx * CX + c + 1], t1);
-        }
-#pragma unroll
-        for (int c = 0; c < CB; ++c) t1 = fma(brow[c], us[hx * CB + c], t1);
-        T xn = t0 + t1;
-#pragma unroll
-        for (int o = NP; o < 64; o <<= 1) xn += xor_shfl(xn, (lane ^ o) << 2);
-        wsync_w();
-        if (hx == 0) {
-            xs[ix] = xn;
-            Xg[(size_t)k * NP + ix] = xn;
-        }
-        wsync_w();
-    };
-    // Whole groups of DEPTH knots: every slot is waited for, consumed and refilled on every
-    // path through the loop body, so the hand bound VMW holds on every path the compiled code
-    // has (tests/isa_vmcnt.py checks it on the gfx950 assembly; a body that skipped knots past
-    // N−1 had compiled paths with fewer loads between a slot's issue and its wait).
-    int k0 = 1;
-    for (; k0 + DEPTH - 1 <= N - 1; k0 += DEPTH) {
+    for (int k0 = 1; k0 <= N - 1; k0 += DEPTH) {
 #pragma unroll
         for (int d = 0; d < DEPTH; ++d) {
-            if constexpr (HAND) vm_wait_regs<VMW>(ring[d], dring[d]);
-            knot(k0 + d, ring[d], dring[d], true);
+            const int k = k0 + d;
+            if (k <= N - 1) {
+                if constexpr (HAND) vm_wait_regs<VMW>(ring[d], dring[d]);
+                // u = −K_k x_k (− d_k)   (dynamic_programming.jl:68)
+                T xu[CU];
+#pragma unroll
+                for (int c = 0; c < CU; ++c) xu[c] = xs[hu * CU + c];
+                T s0 = (T)0, s1 = (T)0;
+#pragma unroll
+                for (int c = 0; c < CU; c += 2) {
+                    s0 = fma(ring[d][c], xu[c], s0);
+                    if (c + 1 < CU) s1 = fma(ring[d][c + 1], xu[c + 1], s1);
+                }
+                T su = s0 + s1;
+#pragma unroll
+                for (int o = MP; o < 64; o <<= 1) su += __shfl_xor(su, o);
+                const T u = LIN ? -(su + dring[d]) : -su;
+                T dn = (T)0;
+                issue(k + DEPTH, ring[d], LIN ? dring[d] : dn);
+                if (hu == 0) {
+                    us[iu] = u;
+                    Ug[(size_t)(k - 1) * MP + iu] = u;
+                }
+                wsync_w();
+                // x_{k+1} = A x_k + B u_k   (:69)
+                T t0 = (T)0, t1 = (T)0;
+#pragma unroll
+                for (int c = 0; c < CX; c += 2) {
+                    t0 = fma(arow[c], xs[hx * CX + c], t0);
+                    if (c + 1 < CX) t1 = fma(arow[c + 1], xs[hx * CX + c + 1], t1);
+                }
+#pragma unroll
+                for (int c = 0; c < CB; ++c) t1 = fma(brow[c], us[hx * CB + c], t1);
+                T xn = t0 + t1;
+#pragma unroll
+                for (int o = NP; o < 64; o <<= 1) xn += xor_shfl(xn, (lane ^ o) << 2);
+                wsync_w();
+                if (hx == 0) {
+                    xs[ix] = xn;
+                    Xg[(size_t)k * NP + ix] = xn;
+                }
+                wsync_w();
+            }
         }
     }
-    // the last < DEPTH knots: their K is in the ring already; drain every load first (also
-    // the clamped refills past N−1, so no load is in flight when the rollout returns)
-    if constexpr (HAND) {
-#pragma unroll
-        for (int d = 0; d < DEPTH; ++d) vm_wait_regs<0>(ring[d], dring[d]);
-    }
-#pragma unroll
-    for (int d = 0; d < DEPTH - 1; ++d)
-        if (k0 + d <= N - 1) knot(k0 + d, ring[d], dring[d], false);
 }
 
 // Kernel variants (compile-time VAR bits):
@@ -918,38 +902,7 @@ static hipError_t launch_dp(const DpArgs &a, hipStream_t s)
         hipLaunchKernelGGL((dp_riccati_kernel<T, NT, MT, WAVES, VAR, false>), grid, block, 0, s, a);
     return hipGetLastError();
 }
-
-hipError_t dp_launch(const DpArgs &a, hipStream_t s)
-{
-    // n ≤ 4: one lane per trajectory (a 16×16 MFMA tile would be mostly padding)
-    if (dp_lane_supported(a.n, a.m)) return dp_lane_launch(a, s);
-    // smallest instantiated tile grid that covers (n, m); padding is exact (zero rows /
-    // columns, unit diagonal in R), see tiles_load
-    const int nt = (a.n + 15) / 16, mt = (a.m + 15) / 16;
-    // LQRX_DP_BIG=1 sends every shape past the lane kernel to dp_big_kernel (A/B checks)
-    static const bool force_big = [] { const char *e = std::getenv("LQRX_DP_BIG"); return e && *e == '1'; }();
-    if (force_big && dp_big_supported(a.n, a.m)) return dp_big_launch(a, s);
-    if (a.dtype == 0) {
-        if (nt <= 1 && mt <= 1) return launch_dp_tv<double, 1, 1>(a, s);
-        if (nt <= 2 && mt <= 1) return launch_dp_tv<double, 2, 1, LQRX_DP_WAVES, LQRX_DP_VAR>(a, s);
-        if (nt <= 2 && mt <= 2) return launch_dp_tv<double, 2, 2>(a, s);
-        if (nt <= 4 && mt <= 2) return launch_dp_tv<double, 4, 2, 1>(a, s);   // n ≤ 64: 1 wave/SIMD
-    } else {
-        if (nt <= 1 && mt <= 1) return launch_dp_tv<float, 1, 1>(a, s);
-        if (nt <= 2 && mt <= 1) return launch_dp_tv<float, 2, 1>(a, s);
-        if (nt <= 2 && mt <= 2) return launch_dp_tv<float, 2, 2>(a, s);
-        if (nt <= 4 && mt <= 2) return launch_dp_tv<float, 4, 2, 1>(a, s);    // cfg5: n=64 m=32
-    }
-    return dp_big_launch(a, s);     // past the register tiles: workgroup per trajectory
-}
-
-bool dp_supported(int dtype, int n, int m, bool tv)
-{
-    (void)dtype;
-    (void)tv;
-    if (dp_lane_supported(n, m)) return true;
-    const int nt = (n + 15) / 16, mt = (m + 15) / 16;
-    return (n >= 1 && m >= 1 && nt <= 4 && mt <= 2) || dp_big_supported(n, m);
-}
+// (launcher cut) the kernel the round-4 race was found in, cfg4's shape with linear terms
+template __global__ void dp_riccati_kernel<double, 2, 1, 2, VAR_LIN, true>(const DpArgs);
 
 } // namespace lqrx

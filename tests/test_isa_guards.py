@@ -1,5 +1,16 @@
 """Guards on the compiled gfx950 assembly (CPU: hipcc cross-compiles, nothing runs).
 
+Hand-placed vmcnt waits (tests/isa_vmcnt.py models s_waitcnt vmcnt(N) by issue order over each
+kernel's control-flow graph):
+  * the DP rollout's inline-asm K loads: no instruction outside the asm blocks may name a
+    register whose load has not provably landed (every dp_riccati_kernel);
+  * the KKT LDS-DMA rings: every hand bound names its target DMA group and at least N vector-
+    memory instructions follow that group's last DMA on every path (every DMA kernel);
+  * negative controls: the round-4 pre-fix linear-terms rollout (tests/isa/lqrx_dp_prefix_r04.hip)
+    must be flagged, and so must the FIL kernels built with every bound loosened
+    (-DLQRX_FIL_WAIT_SLACK, a test-only build);
+  * every csrc unit that places a vmcnt wait by hand is covered.
+
 The KKT kernels' LDS-DMA blocks (lqr.jl_amd/csrc/lqrx_stage.h dma_lds) set M0 and do not
 restore it.  That is only sound while the compiler itself never uses M0 in the translation
 units that issue them.  For every csrc/*.hip that calls dma_lds this test
@@ -13,6 +24,8 @@ import re
 import subprocess
 
 import pytest
+
+import isa_vmcnt as V
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "lqr.jl_amd", "csrc")
@@ -35,6 +48,22 @@ def _dma_units():
 
 
 DMA_UNITS = _dma_units()
+PREFIX = os.path.join(ROOT, "tests", "isa", "lqrx_dp_prefix_r04.hip")
+
+
+def _wait_units():
+    """csrc units that place a vmcnt wait by hand (an asm string naming vmcnt)."""
+    out = []
+    for f in sorted(os.listdir(CSRC)):
+        if f.endswith((".hip", ".h")):
+            src = open(os.path.join(CSRC, f)).read()
+            src = re.sub(r"//[^\n]*", "", re.sub(r"/\*.*?\*/", "", src, flags=re.S))
+            if re.search(r'asm\s+volatile\s*\(\s*"[^"]*vmcnt', src):
+                out.append(f)
+    return out
+
+
+WAIT_UNITS = [u for u in _wait_units() if u.endswith(".hip")]
 
 
 @pytest.fixture(scope="module")
@@ -44,12 +73,15 @@ def asm_of(tmp_path_factory):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
     d = tmp_path_factory.mktemp("isa")
-    units = sorted(set(DMA_UNITS) | {"lqrx_dp.hip"})
+    # name → (source, extra flags): the library units as built, plus the negative controls
+    jobs = {u: (os.path.join(CSRC, u), []) for u in sorted(set(DMA_UNITS) | set(WAIT_UNITS) | {"lqrx_dp.hip"})}
+    jobs["prefix_r04"] = (PREFIX, ["-I" + CSRC])
+    jobs["fil_slack"] = (os.path.join(CSRC, "lqrx_kkt_fil.hip"), ["-DLQRX_FIL_WAIT_SLACK=4"])
     procs = {}
-    for u in units:
+    for u, (src, extra) in jobs.items():
         procs[u] = subprocess.Popen([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-munsafe-fp-atomics",
-                                     "-I" + os.path.join(ROOT, "include"), "--cuda-device-only", "-S",
-                                     os.path.join(CSRC, u), "-o", str(d / (u + ".s"))],
+                                     "-I" + os.path.join(ROOT, "include"), *extra, "--cuda-device-only", "-S",
+                                     src, "-o", str(d / (u + ".s"))],
                                     stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     for u, pr in procs.items():
         assert pr.wait(timeout=1200) == 0, f"hipcc failed on {u}"
@@ -89,53 +121,114 @@ def test_dma_unit_leaves_m0_to_the_dma_blocks(unit, asm_of):
     assert not bad, f"compiler uses M0 outside the DMA blocks: {bad[:5]}"
 
 
-def _regs(text):
-    out = set()
-    for a, b in re.findall(r"v\[(\d+):(\d+)\]", text):
-        out.update(range(int(a), int(b) + 1))
-    for a in re.findall(r"\bv(\d+)\b", re.sub(r"v\[\d+:\d+\]", "", text)):
-        out.add(int(a))
-    return out
+def test_every_hand_wait_unit_is_checked():
+    """The units (and headers) with hand-placed vmcnt waits are exactly the ones checked below:
+    the DP rollout, the FIL/fild kernels (waits in lqrx_kkt_fil.hip), the runtime-shaped staged
+    kernel (lqrx_kkt.hip).  A new hand wait elsewhere must be added to the guards."""
+    assert set(_wait_units()) <= {"lqrx_dp.hip", "lqrx_kkt_fil.hip", "lqrx_kkt.hip"}, _wait_units()
+    assert {"lqrx_dp.hip", "lqrx_kkt_fil.hip", "lqrx_kkt.hip"} <= set(WAIT_UNITS), WAIT_UNITS
 
 
-def test_dp_rollout_asm_loads_not_read_before_their_wait(asm_of):
-    """The DP rollout (lqrx_dp.hip dp_rollout_full) issues its K loads as inline asm, invisible
-    to the compiler's wait-count pass, and waits for them by hand.  The compiler treats an asm
-    output register as written at the asm statement, so it may copy it (or read it otherwise)
-    before the hand wait — a race it cannot see: round 4 found one in the linear-terms variant
-    (an in-flight d_k register copied before the wait; intermittently wrong X/U).  Guard: in the
-    compiled gfx950 assembly of every dp_riccati_kernel, no instruction outside the inline-asm
-    blocks reads a register an inline-asm load wrote before an s_waitcnt vmcnt follows it."""
-    text = asm_of("lqrx_dp.hip")
-    bad, kernels, asm_loads = [], 0, 0
-    for m in re.finditer(r"^(_ZN4lqrx17dp_riccati_kernel\w+):", text, re.M):
-        kernels += 1
-        body = text[m.end():text.find(".Lfunc_end", m.end())]
-        inasm, pend = False, {}
-        for ln in body.split("\n"):
-            s = ln.strip()
-            if s.startswith(";;#ASMSTART"):
-                inasm = True
-                continue
-            if s.startswith(";;#ASMEND"):
-                inasm = False
-                continue
-            if not s or s.startswith(";") or s.startswith("."):
-                continue
-            if "s_waitcnt" in s and "vmcnt" in s:
-                pend = {}
-                continue
-            if inasm:
-                lm = re.match(r"global_load_dword\w*\s+(v\[\d+:\d+\]|v\d+)", s)
-                if lm:
-                    asm_loads += 1
-                    for r in _regs(lm.group(1)):
-                        pend[r] = s
-                continue
-            if s.startswith("s_"):
-                continue
-            hit = _regs(s) & set(pend)
-            if hit:
-                bad.append((m.group(1)[-48:], s, pend[min(hit)]))
-    assert kernels > 0 and asm_loads > 0, (kernels, asm_loads)
-    assert not bad, bad[:5]
+DP_HEADLINE = "_ZN4lqrx17dp_riccati_kernelIdLi2ELi1ELi2ELi0ELb1EEEvNS_6DpArgsE"   # cfg4: <double,2,1,2,0,true>
+
+
+def test_dp_rollout_hand_waits_by_issue_order(asm_of):
+    """Every dp_riccati_kernel: no compiler instruction names a register of an inline-asm K load
+    that has not provably landed — vmcnt(N) retires only loads with ≥ N younger VMEM ops on
+    every path (the round-4 guard cleared every pending load at any vmcnt)."""
+    findings, stats = V.analyse(asm_of("lqrx_dp.hip"), r"_ZN4lqrx17dp_riccati_kernel\w+")
+    hand = {k: v for k, v in stats.items() if v["asm_loads"]}
+    assert DP_HEADLINE in hand and hand[DP_HEADLINE]["hand_waits"] > 0, sorted(hand)
+    assert len(hand) >= 6, sorted(hand)                    # fp64 / fp32 × 1×1, 2×1, 2×2 grids
+    assert not findings, findings[:5]
+
+
+def test_dp_negative_control_prefix_r04(asm_of):
+    """The round-4 linear-terms rollout before commit 53f4b95 (hand-waited K/d loads): the
+    compiler copies an in-flight d register (v_mov) ahead of the hand wait — the race behind the
+    intermittent wrong X/U.  The model must report it."""
+    findings, stats = V.analyse(asm_of("prefix_r04"), r"_ZN4lqrx17dp_riccati_kernel\w+")
+    assert stats and all(v["asm_loads"] for v in stats.values()), stats
+    copies = [f for f in findings if f[0] == "hazard" and f[3].startswith("v_mov")]
+    assert copies, findings[:5]
+
+
+def test_kkt_dma_hand_bounds(asm_of):
+    """Every KKT kernel that stages by LDS-DMA: every hand vmcnt bound names its target group
+    (`; lqrx.wait g=G`) and at least N VMEM instructions follow that group's last DMA on every
+    path of the compiled gfx950 code."""
+    n_dma = 0
+    for unit, pat in (("lqrx_kkt_fil.hip", r"_ZN4lqrx\w*kkt_\w+"), ("lqrx_kkt.hip", r"_ZN4lqrx\w*kkt_\w+")):
+        findings, stats = V.analyse(asm_of(unit), pat)
+        dma = {k: v for k, v in stats.items() if v["dma"]}
+        n_dma += len(dma)
+        assert dma, unit
+        for k, v in dma.items():
+            assert v["hand_waits"] == v["tagged_waits"] > 0 or (v["hand_waits"] == 0 and unit == "lqrx_kkt.hip"), (k, v)
+        assert not findings, (unit, findings[:5])
+    assert n_dma >= 11, n_dma
+
+
+def test_kkt_negative_control_slack(asm_of):
+    """The same FIL kernels built with every hand bound loosened by 4 ops
+    (-DLQRX_FIL_WAIT_SLACK=4, test-only): the model must report bounds past their groups."""
+    findings, _ = V.analyse(asm_of("fil_slack"), r"_ZN4lqrx\w*kkt_\w+")
+    assert sum(f[0] == "bound" for f in findings) >= 10, findings[:3]
+
+
+# ---- the model itself, on hand-written instruction streams (fast) ----
+def _fn(body):
+    return "k:\n" + "\n".join("\t" + l for l in body.strip().split("\n")) + "\n.Lfunc_end0:\n"
+
+
+def _asm(ins):
+    return ";;#ASMSTART\n" + ins + "\n;;#ASMEND"
+
+
+def test_model_counts_by_issue_order():
+    """vmcnt(N) retires a load only when ≥ N VMEM ops were issued after it: vmcnt(2) after two
+    younger stores clears it, vmcnt(3) does not (the old clear-on-any-wait model passed both)."""
+    base = [_asm("global_load_dwordx2 v[4:5], v[0:1], off"),
+            "global_store_dword v[2:3], v6, off", "global_store_dword v[2:3], v7, off"]
+    ok = _fn("\n".join(base + [_asm("s_waitcnt vmcnt(2)"), "v_add_f64 v[8:9], v[4:5], v[4:5]", "s_endpgm"]))
+    bad = _fn("\n".join(base + [_asm("s_waitcnt vmcnt(3)"), "v_add_f64 v[8:9], v[4:5], v[4:5]", "s_endpgm"]))
+    assert not V.analyse(ok, "k")[0]
+    f = V.analyse(bad, "k")[0]
+    assert f and f[0][0] == "hazard", f
+    # a copy before the wait is a hazard whatever the wait says
+    cp = _fn("\n".join([base[0], "v_mov_b32 v10, v4", _asm("s_waitcnt vmcnt(0)"), "s_endpgm"]))
+    assert V.analyse(cp, "k")[0]
+
+
+def test_model_loops_and_groups():
+    """A loop back edge carries pending loads (a 2-deep ring is fine at vmcnt(1), not at
+    vmcnt(2)), and a tagged DMA wait is checked against its group."""
+    def ring(n):                                   # two slots, each refilled after its use
+        return _fn("\n".join([
+            _asm("global_load_dwordx2 v[4:5], v[0:1], off"),
+            _asm("global_load_dwordx2 v[6:7], v[0:1], off offset:8"),
+            ".LBB0_1:",
+            _asm(f"s_waitcnt vmcnt({n})"),
+            "v_add_f64 v[8:9], v[4:5], v[8:9]",
+            _asm("global_load_dwordx2 v[4:5], v[0:1], off"),
+            _asm(f"s_waitcnt vmcnt({n})"),
+            "v_add_f64 v[8:9], v[6:7], v[8:9]",
+            _asm("global_load_dwordx2 v[6:7], v[0:1], off offset:8"),
+            "s_cbranch_scc1 .LBB0_1",
+            _asm("s_waitcnt vmcnt(0)"),
+            "s_endpgm"]))
+    assert not V.analyse(ring(1), "k")[0]
+    f = V.analyse(ring(2), "k")[0]
+    assert f and all(x[0] == "hazard" and x[3].startswith("v_add") for x in f), f
+
+    def dma(n, g):
+        return _fn("\n".join([
+            _asm("; lqrx.grp"), _asm("buffer_load_dword v1, s[0:3], 0 offen lds"),
+            _asm("; lqrx.grp"), _asm("buffer_load_dword v1, s[0:3], 0 offen lds"),
+            _asm("buffer_load_dword v1, s[0:3], 0 offen lds"),
+            "buffer_store_dword v2, v1, s[4:7], 0 offen",
+            _asm(f"s_waitcnt vmcnt({n}) lgkmcnt(0) ; lqrx.wait g={g}"), "s_endpgm"]))
+    assert not V.analyse(dma(3, 2), "k")[0]          # 3 ops after group 1's DMA
+    assert V.analyse(dma(4, 2), "k")[0][0][0] == "bound"
+    assert not V.analyse(dma(1, 1), "k")[0]          # 1 op (the store) after group 2's last DMA
+    assert V.analyse(dma(2, 1), "k")[0][0][0] == "bound"

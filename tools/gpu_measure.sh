@@ -14,7 +14,7 @@
 #
 # $OUT = gpurun_out/$TAG.  Every mode writes $OUT/RECIPE.txt: the exact command, the commit it
 # was launched from (GIT_HEAD, passed in by the caller: the box has no .git), the library's
-# compiled-in source hash and the SHA-256 of every kernel source in the tree — the provenance
+# compiled-in source hash and the code digest of every kernel source in the tree — the provenance
 # tools/traffic_json.py stamps into profiles/traffic_*.json and bench.py checks before it
 # reports a traffic figure.  KREGEX (default "lqrx") restricts the PMC passes to the library's
 # kernels; only the stats / counter CSVs are kept (gpurun copies back ≤ 64 MiB).  Every GPU step
@@ -44,14 +44,19 @@ provenance() {   # $OUT/RECIPE.txt + $OUT/sources.json
         echo "date_utc: $(date -u +%FT%TZ)"
     } > "$OUT/RECIPE.txt"
     python - "$OUT/sources.json" >> "$OUT/RECIPE.txt" <<'EOF'
-import ctypes, glob, hashlib, json, os, sys
+import ctypes, glob, hashlib, importlib.util, json, os, sys
+spec = importlib.util.spec_from_file_location("lqrx_lib", "lqr.jl_amd/lqrx/_lib.py")
+L = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(L)
 srcs = sorted(glob.glob("lqr.jl_amd/csrc/*.hip") + glob.glob("lqr.jl_amd/csrc/*.h")
               + glob.glob("lqr.jl_amd/csrc/*.cpp") + ["include/lqrx.h"])
-h = {s: hashlib.sha256(open(s, "rb").read()).hexdigest()[:16] for s in srcs}
 lib = ctypes.CDLL("lqr.jl_amd/lqrx/liblqrx.so")
 lib.lqrx_build_info.restype = ctypes.c_char_p
 info = lib.lqrx_build_info().decode()
-json.dump({"library_build_info": info, "git_head": os.environ.get("GIT_HEAD"), "sources": h},
+json.dump({"library_build_info": info, "git_head": os.environ.get("GIT_HEAD"),
+           "library_matches_tree": info.split(" ")[0] == "src_sha256=" + L.source_hash("."),
+           "code_digests": {s: L._code_digest(s) for s in srcs},
+           "sha256": {s: hashlib.sha256(open(s, "rb").read()).hexdigest()[:16] for s in srcs}},
           open(sys.argv[1], "w"), indent=1)
 print("library: " + info)
 EOF
@@ -93,6 +98,10 @@ recipe_evidence() {   # traffic at HEAD for the non-headline lines + cfg2 SQ cou
 }
 recipe_kktsq() {   # configs[4] KKT half: prof + SQ counters of the fused interior-knot kernel
     sub kkt32 prof $CFG4KKT && KREGEX=kb_ PMC="$SQ1;$SQ2" sub kkt32sq pmc $CFG4KKT
+}
+recipe_check() {   # after a kernel change: the -m gpu suite + smoke, then the lines it touches
+    sub t tests && sub cfg4 kt && sub cfg3 kt --workload kkt && sub cfg3soa kt --workload kkt --kkt-layout 1 &&
+    sub lin kt --linear && sub cfg2 kt --workload cartpole && sub di kt --workload kkt --kkt-structure di
 }
 recipe_list() { declare -F | sed -n 's/^declare -f recipe_//p'; }
 
