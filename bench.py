@@ -22,6 +22,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -194,14 +195,15 @@ def cpu_baseline_kkt(N, target_s=12.0, threads=None, structure="dubins", h_mode=
                        f"of _solve!), OpenMP {threads} threads, {dt:.1f} s")
 
 
-TRAFFIC_FILES = ("traffic_r04.json", "traffic_r03.json", "traffic_r02.json")
+TRAFFIC_FILES = ("traffic_r05.json", "traffic_r04.json", "traffic_r03.json", "traffic_r02.json")
 
 
 def traffic_lookup(key, path=None):
     """roofline.traffic: PMC HBM bytes per launch of this exact workload from the committed
     profiles/traffic_*.json (FETCH_SIZE×2 + WRITE_SIZE passes, tools/traffic_json.py), newest
-    round first, with where it came from — the file, the key, the commit it was measured at and
-    the PMC run — so a stale figure is visible in the line itself."""
+    round first, with where it came from — the file, the key, the commit it was measured at, the
+    PMC run, the kernels measured and their sources' code digests; traffic_validate() below
+    drops a figure that no longer describes the line's kernel."""
     paths = [path] if path else [os.path.join(ROOT, "profiles", f) for f in TRAFFIC_FILES]
     for p in paths:
         if not os.path.exists(p):
@@ -213,8 +215,41 @@ def traffic_lookup(key, path=None):
         if e and e.get("hbm_bytes_per_launch"):
             return e["hbm_bytes_per_launch"], {"file": os.path.relpath(p, ROOT), "key": key,
                                                "measured_at_head": e.get("measured_at_head"),
-                                               "pmc_source": e.get("source")}
+                                               "pmc_source": e.get("source"),
+                                               "kernels": e.get("kernels"), "sources": e.get("sources")}
     return None, {"file": None, "key": key, "note": "no PMC FETCH/WRITE pass recorded for this workload"}
+
+
+def traffic_validate(roof):
+    """Keep roofline.traffic only while it describes the kernel this line timed: the entry must
+    name its measured kernels and the code digests of their sources (round 5 on), the line's
+    dominant kernel must be one of them, and the tree's code digests of those sources must still
+    match.  Otherwise traffic is null and traffic_source says why (the stale figure is kept
+    beside it as stale_bytes_per_launch)."""
+    tsrc = roof.get("traffic_source")
+    if not isinstance(tsrc, dict) or roof.get("traffic") is None:
+        return
+    kernels, sources = tsrc.pop("kernels", None), tsrc.pop("sources", None)
+    why = None
+    if not kernels or not sources:
+        why = "entry records no measured kernels / source digests (measured before round 5)"
+    else:
+        want = re.findall(r"\b(\w+_kernel)\b", roof.get("kernel") or "")[:1]
+        bases = {re.findall(r"(\w+)", k.split("<")[0])[-1] for k in kernels}
+        if want and want[0] not in bases:
+            why = f"measured kernels {sorted(bases)} do not include this line's {want[0]}"
+        else:
+            from lqrx import _lib as _L
+            now = _L.kernel_source_digest(list(sources), ROOT)
+            changed = sorted(f for f, d in sources.items() if now.get(f) != d)
+            if changed:
+                why = "kernel code changed since the measurement: " + ", ".join(changed)
+    if why:
+        tsrc["stale"] = why
+        tsrc["stale_bytes_per_launch"] = roof["traffic"]
+        roof["traffic"] = None
+    else:
+        tsrc["verified"] = "kernel and source code digests match the measurement"
 
 
 def _sample_index(batch, k=64):
@@ -394,13 +429,16 @@ def main(argv=None):
     ap.add_argument("--no-gather", action="store_true",
                     help="skip the final info + P_1 gather to rank 0 (N > 1)")
     ap.add_argument("--traffic-json", default=None,
-                    help="PMC traffic table (default: profiles/traffic_r03.json, then traffic_r02.json)")
+                    help="PMC traffic table (default: profiles/traffic_r05.json, then the older rounds'; a "
+                         "figure is reported only while its kernel's code is unchanged, see traffic_validate)")
     ap.add_argument("--kkt-structure", choices=["dubins", "di", "dense"], default="dubins",
                     help="kkt workload: Dubins (configs[2]), DoubleIntegrator(3,N) (test/problems.jl), or "
                          "dense: the trajectory structure at --n/--m with dense dynamics, generated in HBM "
                          "(configs[4]: --n 64 --m 32 --N 512 --batch 8192 --dtype f32)")
     ap.add_argument("--graph", action="store_true",
-                    help="replay one captured HIP graph per step (no per-call host work in the timed loop)")
+                    help="replay one captured HIP graph per step (no per-call host work in the timed loop); "
+                         "dp, cartpole, kkt and ls workloads — the sqp step synchronises with the host "
+                         "every pass and cannot be captured")
     ap.add_argument("--kkt-hmode", type=int, choices=[0, 1, 2], default=2,
                     help="kkt workload (dubins / di): BlockCholesky mode of H — 2 diagonal (default), 1 "
                          "block-diagonal, 0 dense (block_cholesky.jl:19-159)")
@@ -417,6 +455,9 @@ def main(argv=None):
                          "sqp = Dubins SQP around the KKT solve (SURVEY §8(f) ranks 2-3, B=16384); "
                          "ls = condensed least-squares LQR on cartpole (SURVEY §8(f) rank 4, B=4096)")
     args = ap.parse_args(argv)
+    if args.graph and args.workload == "sqp":
+        ap.error("--graph: the sqp workload reads its active count back to the host every loop pass "
+                 "(lqrx_sqp.hip), which a HIP graph capture cannot contain; use dp, cartpole, kkt or ls")
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         # no launcher: spawn one rank per GPU now, before this process touches a GPU
@@ -861,6 +902,7 @@ def main(argv=None):
                 if not args.no_cpu_baseline else None
         if tsrc is not None:
             roof.setdefault("traffic_source", tsrc)
+        traffic_validate(roof)
         if roof.get("bound") == "hbm":
             # beside the 8 TB/s spec: the measured achievable streaming rate
             # (MI355X_MICROARCH.md: float4 copy, 6.29 TB/s); peak and frac stay on the spec

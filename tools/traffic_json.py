@@ -65,7 +65,17 @@ prov = json.load(open(os.path.join(a.run_dir, "sources.json")))
 units = sorted({u for u in (L.kernel_unit(k, ROOT) for k in kern) if u})
 # digests as measured: the run's own per-file digests for every file the kernels' units pull in
 files = L.kernel_source_digest(units, ROOT)
-measured = {f: prov["code_digests"].get(f) for f in files}
+if "code_digests" in prov:
+    measured = {f: prov["code_digests"].get(f) for f in files}
+else:   # a run recorded before code digests (raw SHA-256/16 only): valid while the file is unchanged
+    import hashlib
+    raw = prov.get("sources", {})
+    measured = {}
+    for f in files:
+        now = hashlib.sha256(open(os.path.join(ROOT, f), "rb").read()).hexdigest()[:16]
+        if raw.get(f) != now:
+            raise SystemExit(f"{f} changed since {a.run_dir} was measured (no code digest recorded)")
+        measured[f] = files[f]
 tj = json.load(open(a.out)) if os.path.exists(a.out) else {}
 tj[a.key] = {
     "hbm_bytes_per_launch": sum(v["fetch_x2_bytes"] + v["write_bytes"] for v in kern.values()),
