@@ -113,7 +113,13 @@ int lqrx_dp_solve_host(const lqrx_dp_desc *desc, const void *A, const void *B, c
  *   P_ = Q + AᵀPA − APB·K               (n·n·batch, solver.P_; NULL = compute_gain! only)
  * A, B, Q, R, P as lqrx_dp_solve's A, B, Q, R, Qf (time-invariant; desc.N, p_mode and the
  * knot strides are ignored); info as lqrx_dp_solve (1 = E not positive definite).  The same
- * kernels as lqrx_dp_solve (a 2-knot solve with Qf = P). */
+ * kernels as lqrx_dp_solve (a 2-knot solve with Qf = P).
+ * Precondition: P and Q symmetric, as every cost-to-go and cost Hessian of the recursion is.
+ * The n ≥ 5 and n ≤ 4 kernel families use the symmetric fast form (P_ = Q + AᵀPA − GᵀK on the
+ * lower triangle, mirrored), the n > 64 workgroup kernel the reference's operation order, so
+ * for a non-symmetric P or Q the result depends on the family.  The host wrappers (Python
+ * lqrx.compute_ctg*, Julia compute_ctg!) reject P or Q whose asymmetry exceeds 1e-10 of the
+ * matrix's largest entry. */
 int lqrx_dp_compute_ctg(const lqrx_dp_desc *desc, const void *A, const void *B, const void *Q,
                         const void *R, const void *P, void *K, void *P_, int32_t *info, void *stream);
 int lqrx_dp_compute_ctg_host(const lqrx_dp_desc *desc, const void *A, const void *B, const void *Q,
@@ -223,7 +229,10 @@ int lqrx_kkt_solve_host(const lqrx_kkt_desc *desc, const void *Y, const void *y,
  * LQRX_KKT_BIG_SLAB_MB (default 40 GiB); a larger batch runs in chunks through it.  Without
  * a caller workspace that scratch comes from the library pool, whose freed blocks stay
  * reserved for the next call (up to the cap) until lqrx_scratch_trim; an out-of-memory pool
- * allocation retries with halved chunks. */
+ * allocation retries with halved chunks.  A layout-1 call whose structure has no native SoA
+ * kernel is staged through layout 0: its six transposed arrays (Y y H g, δz λ) are part of
+ * the workspace too (counted by lqrx_kkt_workspace_size, carved from its front), so a _ws call
+ * draws no pool scratch in any layout. */
 int lqrx_kkt_workspace_size(const lqrx_kkt_desc *desc, size_t *bytes);
 int lqrx_kkt_solve_ws(const lqrx_kkt_desc *desc, const void *Y, const void *y, const void *H,
                       const void *g, void *dz, void *lam, int32_t *info, void *workspace,

@@ -157,12 +157,17 @@ solve!(sol::LQRSolution{T}, prob::LQRProblem{n,m,T}) where {n,m,T} = solve!(sol,
 The reference's per-knot surface (src/dynamic_programming.jl:34-52, called by test/dp.jl:16-17
 on `sol.K[1]`): K = (R + BᵀPB)⁻¹BᵀPA from P = solver.P, and for compute_ctg! also
 solver.P_ = Q + AᵀPA − AᵀPB·K — lqrx_dp_compute_ctg_host (the same kernels as solve!, on a
-2-knot problem with Qf = P).
+2-knot problem with Qf = P).  P = solver.P and Q must be symmetric (the kernels' symmetric
+fast form, include/lqrx.h): an asymmetry above 1e-10 of the largest entry throws.
 """
 function compute_ctg!(K::AbstractMatrix{T}, solver::DPSolver{T}, prob::LQRProblem{n,m,T};
                       gain_only::Bool=false) where {n,m,T}
     dense(M, r, c) = reshape(Matrix{T}(M), r, c)
     A, B, Q, R = dense(prob.A, n, n), dense(prob.B, n, m), dense(prob.Q, n, n), dense(prob.R, m, m)
+    for (nm, M) in (("P", solver.P), ("Q", Q))
+        maximum(abs, M - transpose(M); init=zero(T)) > 1e-10 * max(maximum(abs, M; init=zero(T)), floatmin(T)) &&
+            throw(ArgumentError("compute_ctg!: $nm must be symmetric (lqrx_dp_compute_ctg precondition)"))
+    end
     Kd = Matrix{T}(undef, m, n)
     info = Int32[0]
     d = Ref(DpDesc(n, m, 2, dtypecode(T), 1, 0, 0, 0, 0))

@@ -644,6 +644,19 @@ size_t kkt_ws_bytes(const lqrx_kkt_desc *d, const lqrx::KktArgs &a, int route)
     default: return 0;
     }
 }
+// a layout-1 call staged through layout 0: the six transposed arrays (Y y H g | dz λ), each
+// 256-B aligned — part of the call's workspace (lqrx_kkt_workspace_size counts them)
+size_t kkt_stage_bytes(const lqrx_kkt_desc *d, const KktLayout &L, size_t soff[6] = nullptr)
+{
+    const size_t es = d->dtype == LQRX_F32 ? 4 : 8, B = (size_t)d->batch;
+    const int64_t S[6] = {L.sY, L.sy, L.sH, L.sg, L.sg, L.sy};
+    size_t tot = 0;
+    for (int i = 0; i < 6; ++i) {
+        if (soff) soff[i] = tot;
+        tot += ((size_t)S[i] * B * es + 255) & ~(size_t)255;
+    }
+    return tot;
+}
 int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const void *H, const void *g,
                    void *dz, void *lam, int32_t *info, void *ws, size_t ws_bytes, void *stream,
                    bool null_sync = true, const int32_t *sel = nullptr, const int32_t *nsel = nullptr);
@@ -658,11 +671,13 @@ extern "C" int lqrx_kkt_workspace_size(const lqrx_kkt_desc *d, size_t *bytes)
     if (d->batch) {
         lqrx::KktArgs a = kkt_args(d, L);
         int route = kkt_route(d, a);
+        size_t stage = 0;
         if (route == KK_NONE && a.layout == 1) {   // staged through layout 0 (kkt_solve_impl)
             a.layout = 0;
             route = kkt_route(d, a);
+            if (route != KK_NONE) stage = kkt_stage_bytes(d, L);
         }
-        *bytes = kkt_ws_bytes(d, a, route);
+        *bytes = stage + kkt_ws_bytes(d, a, route);
     } else {
         *bytes = 0;
     }
@@ -725,14 +740,18 @@ int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const v
         staged = route != KK_NONE;
         if (!staged) a.layout = 1;
     }
+    // the staged arrays: at the front of the caller's workspace (counted by
+    // lqrx_kkt_workspace_size: a _ws call draws nothing from the pool), else from the pool
+    size_t soff[6];
+    const size_t stot = staged ? kkt_stage_bytes(d, L, soff) : 0;
     if (ws) {
-        const size_t need = kkt_ws_bytes(d, a, route);
+        const size_t need = stot + kkt_ws_bytes(d, a, route);
         if (ws_bytes < need) {
             if (meta_tmp) (void)lqrx::scratch_free(meta_tmp, s);
             return set_err(-10, "workspace of %zu bytes < %zu (lqrx_kkt_workspace_size)", ws_bytes, need);
         }
-        a.ws = ws;
-        a.ws_bytes = ws_bytes;
+        a.ws = (char *)ws + stot;
+        a.ws_bytes = ws_bytes - stot;
     }
     static const int debug_meta = [] { const char *v = std::getenv("LQRX_DEBUG_META"); return v && *v == '1'; }();
     if (route == KK_NONE) {
@@ -742,16 +761,17 @@ int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const v
                                              "and ginv)",
                        d->dtype == LQRX_F32 ? "fp32" : "fp64", lqrx::KW_MAX_BLOCK, lqrx::KW_MAX_W);
     }
-    void *stage = nullptr;
+    void *stage = nullptr, *pooled = nullptr;
     const int64_t es = d->dtype == LQRX_F32 ? 4 : 8, B = d->batch;
     const int64_t S[6] = {L.sY, L.sy, L.sH, L.sg, L.sg, L.sy};   // Y y H g | dz lam
-    size_t soff[6], stot = 0;
     if (staged) {
-        for (int i = 0; i < 6; ++i) {
-            soff[i] = stot;
-            stot += ((size_t)S[i] * (size_t)B * (size_t)es + 255) & ~(size_t)255;
+        if (ws) {
+            stage = ws;
+            e = hipSuccess;
+        } else {
+            e = lqrx::scratch_alloc(&pooled, stot, s);
+            stage = pooled;
         }
-        e = lqrx::scratch_alloc(&stage, stot, s);
         const void *src[4] = {Y, y, H, g};
         const double **dst[4] = {&a.Y, &a.y, &a.H, &a.g};
         for (int i = 0; i < 4 && e == hipSuccess; ++i) {      // [S][B] → [B][S]
@@ -774,8 +794,8 @@ int kkt_solve_impl(const lqrx_kkt_desc *d, const void *Y, const void *y, const v
         e = lqrx::batch_transpose(a.dz, dz, B, S[4], (int)es, s);
         if (e == hipSuccess) e = lqrx::batch_transpose(a.lam, lam, B, S[5], (int)es, s);
     }
-    if (stage) {
-        const hipError_t ef = lqrx::scratch_free(stage, s);
+    if (pooled) {
+        const hipError_t ef = lqrx::scratch_free(pooled, s);
         if (e == hipSuccess) e = ef;
     }
     if (debug_meta) {   // read the table back before a per-call table is released

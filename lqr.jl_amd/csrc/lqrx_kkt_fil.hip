@@ -2077,9 +2077,10 @@ __global__ __launch_bounds__(256) void kkt_hpost_kernel(const KktArgs a, const d
     for (int c = 0; c < WM; ++c)
         if (c < w) dz[c] = x[c];
     if (k == 0 && a.info) {
+        // a non-SPD H_k wins over any Schur pivot failure, as in the reference order (every
+        // H_k is factored in shur! before cholesky! sees a pivot) and the oracle / the other routes
         const int kh = infoh[t];                      // first non-SPD H knot, or N
-        const int v = a.info[t];                      // pivots: k+1 of the first failing knot
-        if (kh < a.N && (v == 0 || kh <= v)) a.info[t] = -(kh + 1);
+        if (kh < a.N) a.info[t] = -(kh + 1);
     }
 }
 

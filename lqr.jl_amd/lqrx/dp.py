@@ -254,6 +254,12 @@ def compute_ctg_batch(A, B, Q, R, P, dtype: int = _lib.F64, gain_only: bool = Fa
     lib = _lib.load()
     A = np.asarray(A)
     bt, n, m = A.shape[0], A.shape[-1], np.asarray(B).shape[-1]
+    # the kernels' symmetric fast form needs symmetric P and Q (include/lqrx.h precondition)
+    for name, M in (("P", P), ("Q", Q)):
+        M = np.asarray(M, dtype=np.float64)
+        if np.abs(M - np.swapaxes(M, -1, -2)).max(initial=0.0) > 1e-10 * max(np.abs(M).max(initial=0.0), 1e-300):
+            raise ValueError(f"compute_ctg: {name} must be symmetric (the Riccati cost-to-go / cost "
+                             "Hessian; lqrx_dp_compute_ctg precondition)")
     npdt = np.float64 if dtype == _lib.F64 else np.float32
     ins = [to_abi(np.asarray(x, dtype=npdt)) for x in (A, B, Q, R, P)]
     K = np.zeros(bt * m * n, npdt)

@@ -264,3 +264,22 @@ def test_library_built_from_these_sources(lqrx):
     b = _lib.build_info()
     assert b["src_sha256"] and len(b["src_sha256"]) == 64, b
     assert b["matches_tree"], b
+
+
+def test_compute_ctg_rejects_asymmetric_cost():
+    """lqrx_dp_compute_ctg's precondition (include/lqrx.h): P and Q symmetric — the host
+    wrapper refuses a clearly asymmetric one before any device call (no GPU needed)."""
+    import numpy as np
+    from lqrx.dp import compute_ctg_batch
+
+    rng = np.random.default_rng(0)
+    A, B = rng.standard_normal((2, 5, 5)), rng.standard_normal((2, 5, 2))
+    Q, R = np.tile(np.eye(5), (2, 1, 1)), np.tile(np.eye(2), (2, 1, 1))
+    P = np.tile(np.eye(5), (2, 1, 1))
+    P[1, 0, 3] = 0.5                                  # asymmetric
+    with pytest.raises(ValueError, match="P must be symmetric"):
+        compute_ctg_batch(A, B, Q, R, P)
+    Q2 = Q.copy()
+    Q2[0, 4, 1] = 1e-3
+    with pytest.raises(ValueError, match="Q must be symmetric"):
+        compute_ctg_batch(A, B, Q2, R, np.tile(np.eye(5), (2, 1, 1)))

@@ -237,3 +237,31 @@ def test_kkt_layout1_staged(lqrx, gpu_ok, case):
     ref = _ref(st, pb, 1)
     assert rel(got1["dz"], ref["dz"].reshape(pb.batch, -1)) <= tol
     assert rel(got1["lam"], ref["lam"].reshape(pb.batch, -1)) <= tol
+
+
+@pytest.mark.parametrize("case", ["t53", "big_f64"])
+def test_kkt_layout1_staged_workspace(lqrx, gpu_ok, case):
+    """A staged layout-1 call through lqrx_kkt_solve_ws takes its transposed arrays from the
+    caller's workspace (lqrx_kkt_workspace_size counts them: more than the layout-0 call needs),
+    gives the pool call's result bit for bit, and a workspace short of the staged arrays is
+    rejected with -10."""
+    import torch
+    import lqrx.kkt as K
+
+    st, dyn = {"t53": (K.trajectory_structure(5, 3, 12), "small"),
+               "big_f64": (K.trajectory_structure(16, 8, 9), "dense")}[case]
+    bt = 37
+    pb = K.random_kkt(st, bt, seed=3, h_mode=K.H_DIAG, dyn=dyn)
+    t = {k: torch.from_numpy(getattr(pb, k)).cuda().t().contiguous().view(-1) for k in ("Y", "y", "H", "g")}
+    t["batch"] = bt
+    n1 = K.workspace_size(st, bt, K.H_DIAG, 1, 1)
+    n0 = K.workspace_size(st, bt, K.H_DIAG, 1, 0)
+    assert n1 > n0
+    a = K.kkt_solve_device(st, t, K.H_DIAG, 1, layout=1)
+    ws = torch.empty(n1, dtype=torch.uint8, device="cuda")
+    b = K.kkt_solve_device(st, t, K.H_DIAG, 1, workspace=ws, layout=1)
+    torch.cuda.synchronize()
+    assert torch.equal(a["dz"], b["dz"]) and torch.equal(a["lam"], b["lam"])
+    with pytest.raises(lqrx.LqrxError) as e:
+        K.kkt_solve_device(st, t, K.H_DIAG, 1, workspace=ws[: n1 - 256], layout=1)
+    assert e.value.code == -10

@@ -161,3 +161,24 @@ def test_kkt_dense_h_info(lqrx, gpu_ok, knot):
     assert got["rc"] == 1
     assert int(got["info"][3]) == -(knot + 1)
     assert (np.delete(got["info"], 3) == 0).all()
+
+
+def test_kkt_dense_h_info_wins_over_earlier_pivot(lqrx, gpu_ok):
+    """A Schur pivot failure at knot 2 (a zero stage-constraint row) AND a non-SPD H_10: the H
+    failure is reported, −11, as the oracle (and the reference, which factors every H_k in
+    shur! before cholesky! meets a pivot) and the large-block / workgroup routes report it."""
+    import lqrx.kkt as K
+
+    st = K.double_integrator_structure(3, 21)
+    pb = K.random_kkt(st, 6, seed=12, h_mode=0)
+    rows, w = st.n1 + st.p + st.n2, st.w
+    oY = int(np.sum(rows[:2] * w[:2]))                    # knot 2's Y block, column-major rows × w
+    for c in range(int(w[2])):
+        pb.Y[3, oY + c * int(rows[2]) + int(st.n1[2])] = 0.0   # its stage row (C, after D2)
+    oH = int(np.sum(w[:10] * w[:10]))
+    pb.H[3, oH:oH + int(w[10]) ** 2] *= -1.0
+    got = K.kkt_solve(pb)
+    ref = _ref(st, pb, 1)
+    assert int(ref["info"][3]) == -11
+    assert int(got["info"][3]) == -11
+    assert (np.delete(got["info"], 3) == 0).all()
