@@ -67,6 +67,155 @@ template <typename T> __device__ __forceinline__ Knot<T> kw_knot(const int32_t *
     return K;
 }
 
+// ---- diagonal H (and the SOC, where H⁻¹ → I): the Schur pieces straight from Y ----------------
+// shur!/copy_shur! (jacobian_blocks.jl:231-286) need Y·H⁻¹·Yᵀ by blocks of Y = [D2; C; D1]: A = D2
+// H⁻¹D2ᵀ (added into knot k−1's C), D, F = D2 H⁻¹[Cᵀ | D1ᵀ], B, E = C H⁻¹[Cᵀ | D1ᵀ], C = D1 H⁻¹D1ᵀ —
+// the upper block triangle of one Gram matrix over the rows in segment order.  With a diagonal
+// H it is formed with no H⁻¹Yᵀ transient: Y is streamed in 4-column k-slices, every lane holds
+// one element of each of a super-tile's row blocks (16 rows), the column side scaled by h⁻¹ on
+// the fly; each wave owns 4×4 super-tiles of 16×16 output tiles (round-robin), so one slice of
+// ≤ 8 row blocks feeds ≤ 16 MFMAs.  The k order (16-column k-tiles, Tile<T>::row's k index per
+// MFMA) is wg_mm_k's, so the results equal the transient path's bit for bit.
+template <typename T> __device__ __forceinline__ T kw_bload(__amdgpu_buffer_rsrc_t r, uint32_t vo)
+{
+    if constexpr (sizeof(T) == 8)
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)vo, 0, 0));
+    else
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo, 0, 0));
+}
+struct KwBlk {
+    int seg, r0, nv, off;          // segment (0 D2, 1 C, 2 D1), first Y row, valid rows, row offset in the segment
+};
+template <typename T> __device__ __forceinline__ KwBlk kw_blk(const Knot<T> &K, int b)
+{
+    const int n0 = (K.p1 + 15) >> 4, n1 = (K.ps + 15) >> 4;
+    if (b < n0) return KwBlk{0, 16 * b, min(16, K.p1 - 16 * b), 16 * b};
+    if (b < n0 + n1) return KwBlk{1, K.p1 + 16 * (b - n0), min(16, K.ps - 16 * (b - n0)), 16 * (b - n0)};
+    const int c = b - n0 - n1;
+    return KwBlk{2, K.p1 + K.ps + 16 * c, min(16, K.p2 - 16 * c), 16 * c};
+}
+// destination of the (si, sj) block of the Gram matrix (si ≤ sj); null: not needed
+template <typename T>
+__device__ __forceinline__ T *kw_dst(const Knot<T> &K, const Knot<T> *Kp, int si, int sj, int &ld, bool &add)
+{
+    add = false;
+    if (si == 0 && sj == 0) { ld = K.p1; add = true; return Kp ? Kp->C : nullptr; }   // A ≡ prev C (+=)
+    if (si == 0 && sj == 1) { ld = K.p1; return K.DF; }                                // D
+    if (si == 0) { ld = K.p1; return K.DF + (size_t)K.p1 * K.ps; }                     // F
+    if (si == 1 && sj == 1) { ld = K.ps; return K.B; }
+    if (si == 1) { ld = K.ps; return K.Emu; }                                          // E
+    ld = K.p2;
+    return K.C;
+}
+
+// one super-tile: row blocks 4·GI … 4·GI+3 × column blocks RJ·GJ … (all RJ·4 tiles are
+// accumulated; only the upper ones, bi ≤ bj, are stored)
+template <typename T> constexpr int kw_rj() { return sizeof(T) == 8 ? 2 : 4; }
+template <typename T>
+__device__ __forceinline__ void kw_gram_st(const Knot<T> &K, const Knot<T> *Kp, const T *Yk, const T *hs, int GI,
+                                           int GJ, int NB, int lane)
+{
+    using acc = typename Tile<T>::acc;
+    constexpr int RJ = kw_rj<T>();
+    constexpr uint32_t TS = sizeof(T), OOB = 0x80000000u;
+    const int i16 = lane & 15, rows = K.rows, w = K.w;
+    // this lane's k index within a 16-column k-tile for the slice q = s mod 4: Tile<T>::row(lane, q)
+    const int kl = Tile<T>::row(lane, 0), kq = Tile<T>::row(lane, 1) - kl;   // row(lane, q) = kl + q·kq
+    KwBlk bI[4], bJ[RJ];
+    uint32_t vI[4], vJ[RJ];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int b = 4 * GI + i;
+        bI[i] = b < NB ? kw_blk<T>(K, b) : KwBlk{-1, 0, 0, 0};
+        vI[i] = i16 < bI[i].nv ? (uint32_t)((bI[i].r0 + i16 + kl * rows) * (int)TS) : OOB;
+    }
+#pragma unroll
+    for (int j = 0; j < RJ; ++j) {
+        const int c = RJ * GJ + j;
+        bJ[j] = c < NB ? kw_blk<T>(K, c) : KwBlk{-1, 0, 0, 0};
+        vJ[j] = i16 < bJ[j].nv ? (uint32_t)((bJ[j].r0 + i16 + kl * rows) * (int)TS) : OOB;
+    }
+    acc D[4][RJ];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < RJ; ++j) {
+            D[i][j] = acc{0, 0, 0, 0};
+            // the A tiles (D2·D2ᵀ) add into knot k−1's C: start from it
+            if (Kp && bI[i].seg == 0 && bJ[j].seg == 0 && 4 * GI + i <= RJ * GJ + j)
+                wg::tile_ld<T>(D[i][j], Kp->C + bI[i].off + (size_t)bJ[j].off * K.p1, bI[i].nv, bJ[j].nv, 1, K.p1, lane);
+        }
+    const char *yb = (const char *)Yk;
+    const int yn = rows * w * (int)TS, nks = (w + 3) >> 2;
+    // slice s: columns 16(s/4) + row(lane, s mod 4) — descriptor base at the slice's first column
+    auto base = [&](int s) { return 16 * (s >> 2) + kq * (s & 3); };
+    constexpr int PF = 2;
+    T aI[PF][4], aJ[PF][RJ];
+    auto load = [&](int s, T (&xi)[4], T (&xj)[RJ]) __attribute__((always_inline)) {
+        const int o = base(s) * rows * (int)TS;
+        const __amdgpu_buffer_rsrc_t r =
+            __builtin_amdgcn_make_buffer_rsrc((void *)(yb + o), (short)0, max(yn - o, 0), 0x00020000);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xi[i] = kw_bload<T>(r, vI[i]);
+#pragma unroll
+        for (int j = 0; j < RJ; ++j) xj[j] = kw_bload<T>(r, vJ[j]);
+    };
+#pragma unroll
+    for (int u = 0; u < PF; ++u) load(u, aI[u], aJ[u]);
+    for (int s0 = 0; s0 < nks; s0 += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            const int s = s0 + u;
+            const T h = hs[base(s) + kl];             // 0 past w (and the loads read 0 there)
+            T fj[RJ];
+#pragma unroll
+            for (int j = 0; j < RJ; ++j) fj[j] = aJ[u][j] * h;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < RJ; ++j) D[i][j] = Tile<T>::mma(aI[u][i], fj[j], D[i][j]);
+            load(s + PF, aI[u], aJ[u]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // store: the upper tiles (bi ≤ bj) into their block's destination; a same-segment off-
+    // diagonal tile also transposed (the symmetric blocks stay full, as the transient path left them)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < RJ; ++j) {
+            const KwBlk &P = bI[i], &Q = bJ[j];
+            if (P.seg < 0 || Q.seg < 0 || 4 * GI + i > RJ * GJ + j) continue;
+            int ld;
+            bool add;
+            T *dst = kw_dst<T>(K, Kp, P.seg, Q.seg, ld, add);
+            if (!dst) continue;
+            const bool mirror = P.seg == Q.seg && P.off != Q.off;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = Tile<T>::row(lane, r), col = tcol(lane);
+                if (row < P.nv && col < Q.nv) {
+                    dst[P.off + row + (size_t)(Q.off + col) * ld] = D[i][j][r];
+                    if (mirror) dst[Q.off + col + (size_t)(P.off + row) * ld] = D[i][j][r];
+                }
+            }
+        }
+}
+
+// the Schur pieces of knot k from Y with column scale hs (LDS, ≥ w + 16 entries, 0 past w):
+// the waves take the super-tiles that hold an upper tile round-robin
+template <typename T>
+__device__ void kw_gram(const Knot<T> &K, const Knot<T> *Kp, const T *Yk, const T *hs, int tid)
+{
+    constexpr int RJ = kw_rj<T>();
+    const int NB = ((K.p1 + 15) >> 4) + ((K.ps + 15) >> 4) + ((K.p2 + 15) >> 4);
+    const int GR = (NB + 3) >> 2, GC = (NB + RJ - 1) / RJ, wave = tid >> 6, lane = tid & 63;
+    int idx = 0;
+    for (int GI = 0; GI < GR; ++GI)
+        for (int GJ = (4 * GI) / RJ; GJ < GC; ++GJ, ++idx)       // first column group with a tile bj ≥ 4·GI
+            if (idx % (BT / 64) == wave) kw_gram_st<T>(K, Kp, Yk, hs, GI, GJ, NB, lane);
+}
+
 // cholesky_solve.jl:47-67 and :93-117 for knot j (its Schur pieces complete), Kp = knot j−1
 // (its C factored: the A factor of this knot; its λ final from the forward sweep)
 template <typename T>
@@ -104,7 +253,7 @@ __device__ void kw_factor_fwd(const Knot<T> &K, const Knot<T> *Kp, int j, int *s
 }
 
 template <typename T>
-__global__ __launch_bounds__(BT) void kkt_wg_kernel(const KktArgs a, T *__restrict__ ws, size_t ws_elems, int64_t b0)
+__global__ __launch_bounds__(BT, 2) void kkt_wg_kernel(const KktArgs a, T *__restrict__ ws, size_t ws_elems, int64_t b0)
 {
     const int64_t b = b0 + blockIdx.x;          // trajectory; scratch slot blockIdx.x
     if (b >= a.batch) return;
@@ -116,6 +265,7 @@ __global__ __launch_bounds__(BT) void kkt_wg_kernel(const KktArgs a, T *__restri
     T *w0 = ws + (size_t)blockIdx.x * ws_elems;
     T *JYt = w0, *vt = JYt + (size_t)a.maxw * a.maxrows, *per = vt + std::max(a.maxw, a.maxrows);
     __shared__ int s_hinfo, s_finfo;
+    __shared__ T hs_l[KW_MAX_W + 16], hg_l[KW_MAX_W];      // diagonal H: h⁻¹ (or 1), h⁻¹·g
     if (tid == 0) { s_hinfo = 0; s_finfo = 0; }
     __syncthreads();
 
@@ -129,42 +279,59 @@ __global__ __launch_bounds__(BT) void kkt_wg_kernel(const KktArgs a, T *__restri
             const int w = K.w, rows = K.rows;
             // H_k factor (block_cholesky.jl:55-91,145-153): potrf, or 1/h for a diagonal H
             const T *Hk = Hb + K.oH;
+            const T *Yk = Yb + K.oY;
+            const int p1 = K.p1, ps = K.ps, p2 = K.p2, o2 = p1 + ps;
             if (hm == 2) {
-                for (int i = tid; i < w; i += BT) K.Hf[i] = (T)1 / Hk[i];
-                __syncthreads();                                         // JYt below reads all of it
+                // no H⁻¹Yᵀ transient: the Schur pieces straight from Y (kw_gram), r = Y·(h⁻¹g)
+                const T *gk = gb + K.og;
+                for (int i = tid; i < w + 16; i += BT) {
+                    const T hi = i < w ? (T)1 / Hk[i] : (T)0;
+                    if (i < w) K.Hf[i] = hi;
+                    hs_l[i] = i < w ? (ginv ? hi : (T)1) : (T)0;
+                    if (ginv && i < w) hg_l[i] = hi * gk[i];
+                }
+                __syncthreads();
+                kw_gram<T>(K, k > 0 ? &Kp : nullptr, Yk, hs_l, tid);
+                if (ginv) {
+                    for (int i = tid; i < rows; i += BT) {
+                        T s0 = (T)0, s1 = (T)0;
+                        int q = 0;
+                        for (; q + 1 < w; q += 2) {
+                            s0 = fma(Yk[i + (size_t)q * rows], hg_l[q], s0);
+                            s1 = fma(Yk[i + (size_t)(q + 1) * rows], hg_l[q + 1], s1);
+                        }
+                        if (q < w) s0 = fma(Yk[i + (size_t)q * rows], hg_l[q], s0);
+                        vt[i] = s0 + s1;
+                    }
+                }
+                __syncthreads();
             } else {
                 for (int e = tid; e < w * w; e += BT) K.Hf[e] = Hk[e];
                 __syncthreads();
                 const int f = wg::wg_potrf<T>(K.Hf, w, w, tid);
                 if (f && tid == 0 && s_hinfo == 0) s_hinfo = -(k + 1);
-            }
-            // jacobian_blocks.jl:232-236  JYt = H⁻¹Yᵀ (w × rows), r = JYtᵀg
-            const T *Yk = Yb + K.oY;
-            for (int e = tid; e < w * rows; e += BT) {
-                const int i = e / w, j = e - i * w;
-                T v = Yk[i + (size_t)j * rows];
-                if (ginv && hm == 2) v *= K.Hf[j];
-                JYt[j + (size_t)i * w] = v;
-            }
-            __syncthreads();
-            if (ginv && hm != 2) {                                       // potrs
-                wg::wg_trsm_ut<T>(K.Hf, w, w, JYt, w, rows, tid);
-                wg::wg_trsm_un<T>(K.Hf, w, w, JYt, w, rows, tid);
-            }
-            if (ginv) {
-                wg::wg_mm1<T, 1>(vt, rows, rows, 1, nullptr, cm<T>(JYt, w), cm<T>(gb + K.og, w), w, tid);
+                // jacobian_blocks.jl:232-236  JYt = H⁻¹Yᵀ (w × rows), r = JYtᵀg
+                for (int e = tid; e < w * rows; e += BT) {
+                    const int i = e / w, j = e - i * w;
+                    JYt[j + (size_t)i * w] = Yk[i + (size_t)j * rows];
+                }
                 __syncthreads();
+                if (ginv) {                                              // potrs
+                    wg::wg_trsm_ut<T>(K.Hf, w, w, JYt, w, rows, tid);
+                    wg::wg_trsm_un<T>(K.Hf, w, w, JYt, w, rows, tid);
+                    wg::wg_mm1<T, 1>(vt, rows, rows, 1, nullptr, cm<T>(JYt, w), cm<T>(gb + K.og, w), w, tid);
+                    __syncthreads();
+                }
+                // :240 Y·JYt by blocks, copy_shur! (:271-286): rows [0,p1) D2, [p1,p1+ps) C, [p1+ps,rows) D1
+                auto Ym = [&](int i0) { return cmt<T>(Yk + i0, rows); };  // (q, i) → Y[i0+i, q]
+                auto Jm = [&](int j0) { return cm<T>(JYt + (size_t)j0 * w, w); };
+                if (k > 0 && p1) wg::wg_mm1<T, 1>(Kp.C, p1, p1, p1, Kp.C, Ym(0), Jm(0), w, tid);   // A ≡ prev C
+                wg::wg_mm1<T, 1>(K.B, ps, ps, ps, nullptr, Ym(p1), Jm(p1), w, tid);
+                wg::wg_mm1<T, 1>(K.C, p2, p2, p2, nullptr, Ym(o2), Jm(o2), w, tid);
+                wg::wg_mm1<T, 1>(K.DF, p1, p1, ps, nullptr, Ym(0), Jm(p1), w, tid);
+                wg::wg_mm1<T, 1>(K.DF + (size_t)p1 * ps, p1, p1, p2, nullptr, Ym(0), Jm(o2), w, tid);
+                wg::wg_mm1<T, 1>(K.Emu, ps, ps, p2, nullptr, Ym(p1), Jm(o2), w, tid);
             }
-            // :240 Y·JYt by blocks, copy_shur! (:271-286): rows [0,p1) D2, [p1,p1+ps) C, [p1+ps,rows) D1
-            const int p1 = K.p1, ps = K.ps, p2 = K.p2, o2 = p1 + ps;
-            auto Ym = [&](int i0) { return cmt<T>(Yk + i0, rows); };      // (q, i) → Y[i0+i, q]
-            auto Jm = [&](int j0) { return cm<T>(JYt + (size_t)j0 * w, w); };
-            if (k > 0 && p1) wg::wg_mm1<T, 1>(Kp.C, p1, p1, p1, Kp.C, Ym(0), Jm(0), w, tid);   // A ≡ prev C
-            wg::wg_mm1<T, 1>(K.B, ps, ps, ps, nullptr, Ym(p1), Jm(p1), w, tid);
-            wg::wg_mm1<T, 1>(K.C, p2, p2, p2, nullptr, Ym(o2), Jm(o2), w, tid);
-            wg::wg_mm1<T, 1>(K.DF, p1, p1, ps, nullptr, Ym(0), Jm(p1), w, tid);
-            wg::wg_mm1<T, 1>(K.DF + (size_t)p1 * ps, p1, p1, p2, nullptr, Ym(0), Jm(o2), w, tid);
-            wg::wg_mm1<T, 1>(K.Emu, ps, ps, p2, nullptr, Ym(p1), Jm(o2), w, tid);
             // c = r_C − y_c, d = r_D1 − y_d ; d_{k−1} += r_D2 (:251)
             const T *yk = yb + K.oy;
             T *mu = K.mu();

@@ -2,6 +2,7 @@
 # gpu_measure.sh — the measurement recipe behind profiles/ (run on the GPU box via gpurun).
 #
 #   TAG=r05a tools/gpu_measure.sh tests                 full `-m gpu` parity suite + smoke()
+#   TAG=r05a tools/gpu_measure.sh pytest FILES…         a subset of the -m gpu suite
 #   TAG=r05a tools/gpu_measure.sh bench  [bench args]   one bench.py line → $OUT/bench.json
 #   TAG=r05a tools/gpu_measure.sh kt     [bench args]   bench line, then rocprofv3 --kernel-trace
 #                                                       --stats of the same command
@@ -103,6 +104,9 @@ recipe_check() {   # after a kernel change: the -m gpu suite + smoke, then the l
     sub t tests && sub cfg4 kt && sub cfg3 kt --workload kkt && sub cfg3soa kt --workload kkt --kkt-layout 1 &&
     sub lin kt --linear && sub cfg2 kt --workload cartpole && sub di kt --workload kkt --kkt-structure di
 }
+recipe_wg() {   # the workgroup KKT kernel (blocks past 64 rows): its tests, then the n=96 line
+    sub t pytest tests/test_kkt_wg_gpu.py tests/test_dp_big_gpu.py && sub wg96 prof $WG96
+}
 recipe_list() { declare -F | sed -n 's/^declare -f recipe_//p'; }
 
 case "$MODE" in
@@ -115,6 +119,13 @@ tests)
     [ $rc -eq 0 ] || exit $rc
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -20 "$OUT/smoke.log"; exit 7; }
     tail -2 "$OUT/smoke.log" ;;
+pytest)        # a subset of the -m gpu suite: the test files / -k expression given
+    provenance "$@"
+    timeout -k 10 900 python -u -m pytest "$@" -m gpu -x -q --timeout 300 --timeout-method thread \
+        > "$OUT/gpu_tests.log" 2>&1
+    rc=$?
+    tail -5 "$OUT/gpu_tests.log"
+    exit $rc ;;
 bench)
     provenance "$@"
     bench_line "$@" || exit 2 ;;
