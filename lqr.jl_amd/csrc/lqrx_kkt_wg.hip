@@ -229,7 +229,7 @@ __device__ void kw_factor_fwd(const Knot<T> &K, const Knot<T> *Kp, int j, int *s
         wg::wg_trsm_ut<T>(Kp->C, p1, p1, K.DF, p1, ps + p2, tid);
         const Mat<T> lp = cm<T>(Kp->lam, p1);
         // :50-53 B − DᵀD ; :59 E − DᵀF ; :100-105 c − Dᵀλ_{j−1}, d − Fᵀλ_{j−1}
-        wg::wg_mm1<T, -1>(K.B, ps, ps, ps, K.B, Dm, Dm, p1, tid);
+        wg::wg_mm<T, -1, 1>(K.B, ps, ps, ps, K.B, Dm, Dm, p1, Dm, Dm, 0, tid, true);   // (upper, as C)
         wg::wg_mm1<T, -1>(K.Emu, ps, ps, p2, K.Emu, Dm, Fm, p1, tid);
         wg::wg_mm1<T, -1>(mu, ps, ps, 1, mu, Dm, lp, p1, tid);
         wg::wg_mm1<T, -1>(K.lam, p2, p2, 1, K.lam, Fm, lp, p1, tid);
@@ -243,7 +243,8 @@ __device__ void kw_factor_fwd(const Knot<T> &K, const Knot<T> *Kp, int j, int *s
     if (p2) {
         // :61-62 C − FᵀF − ẼᵀẼ ; :108-112 d − Ẽᵀμ
         const Mat<T> Em = cm<T>(K.Emu, ps), mum = cm<T>(mu, ps);
-        wg::wg_mm<T, -1, -1>(K.C, p2, p2, p2, K.C, Fm, Fm, p1, Em, Em, ps, tid);
+        // (upper tiles only: potrf and the triangular solves read C's upper triangle)
+        wg::wg_mm<T, -1, -1>(K.C, p2, p2, p2, K.C, Fm, Fm, p1, Em, Em, ps, tid, true);
         wg::wg_mm1<T, -1>(K.lam, p2, p2, 1, K.lam, Em, mum, ps, tid);
         __syncthreads();
         const int f = wg::wg_potrf<T>(K.C, p2, p2, tid);                // :62
@@ -434,7 +435,11 @@ size_t kw_elems(const KktArgs &a, const int32_t *n1, const int32_t *p, const int
 
 int64_t kw_chunk(const KktArgs &a, size_t per_bytes)
 {
-    int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(a.batch, ((int64_t)4 << 30) / (int64_t)per_bytes));
+    // up to 24 GiB of per-trajectory scratch per launch (n = 96: ~10 MB per trajectory — the
+    // B = 2048 batch in one launch instead of five under-filled ones), chunks evened out
+    const int64_t cap = std::max<int64_t>(1, ((int64_t)24 << 30) / (int64_t)per_bytes);
+    const int64_t nl = (a.batch + cap - 1) / cap;
+    int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(a.batch, (a.batch + nl - 1) / nl));
     if (const char *ev = std::getenv("LQRX_KKT_WG_CHUNK"))   // tests: force the multi-chunk path
         chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, std::atoll(ev)));
     return chunk;

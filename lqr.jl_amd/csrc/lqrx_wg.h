@@ -69,29 +69,101 @@ __device__ __forceinline__ void wg_mm_k(typename Tile<T>::acc &D, Mat<T> M, Mat<
     }
 }
 
+// D[a][b] ±= Mᵀ·Y for the 2×2 output tiles (it0 + a, jt0 + b): every k-step loads two M and two Y
+// tiles and feeds four accumulators (half the operand loads of four single tiles); k-step kt+1's
+// tiles are loaded before the MFMAs of step kt.  Tiles past the matrix read zeros.
+template <typename T, int S>
+__device__ __forceinline__ void wg_mm_k22(typename Tile<T>::acc (&D)[2][2], Mat<T> M, Mat<T> Y, int kk, int r, int c,
+                                          int it0, int jt0, int lane)
+{
+    using acc = typename Tile<T>::acc;
+    const int nk = (kk + 15) / 16;
+    if (nk == 0) return;
+    acc Mt[2], Yt[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        tile_ld<T>(Mt[a], M.at(0, (it0 + a) * 16), kk, r - (it0 + a) * 16, M.rs, M.cs, lane);
+        tile_ld<T>(Yt[a], Y.at(0, (jt0 + a) * 16), kk, c - (jt0 + a) * 16, Y.rs, Y.cs, lane);
+    }
+    for (int kt = 0; kt < nk; ++kt) {
+        acc Mn[2] = {Mt[0], Mt[1]}, Yn[2] = {Yt[0], Yt[1]};
+        if (kt + 1 < nk) {
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                tile_ld<T>(Mn[a], M.at((kt + 1) * 16, (it0 + a) * 16), kk - (kt + 1) * 16, r - (it0 + a) * 16, M.rs,
+                           M.cs, lane);
+                tile_ld<T>(Yn[a], Y.at((kt + 1) * 16, (jt0 + a) * 16), kk - (kt + 1) * 16, c - (jt0 + a) * 16, Y.rs,
+                           Y.cs, lane);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    D[a][b] = S > 0 ? Tile<T>::mma(Mt[a][q], Yt[b][q], D[a][b]) : Tile<T>::mma_nega(Mt[a][q], Yt[b][q], D[a][b]);
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            Mt[a] = Mn[a];
+            Yt[a] = Yn[a];
+        }
+    }
+}
+
 // Workgroup product on the MFMA pipe: C (r×c, column-major, ldc) = [Cin] + S1·M1ᵀ·Y1 + S2·M2ᵀ·Y2
 // (S1, S2 ∈ {+1, −1}), M1 kk1×r, Y1 kk1×c (M2 kk2×r, Y2 kk2×c; kk = 0 drops a product).  The 4
-// waves take the 16×16 output tiles round-robin and stream the k-tiles of their operands from
-// L2.  Cin may alias C (each tile is read, then written, by the wave that owns it).
+// waves take the output tiles round-robin — 2×2 blocks of them (shared operand loads) when there
+// are more than 8 tiles, single tiles otherwise (so a thin product still spreads over the waves)
+// — and stream the k-tiles of their operands from L2.  UPPER: only the tiles on or above the
+// diagonal (it ≤ jt) are computed and stored (a symmetric result whose consumers read the upper
+// triangle).  Cin may alias C (each tile is read, then written, by the wave that owns it).
 template <typename T, int S1, int S2>
 __device__ __forceinline__ void wg_mm(T *C, int ldc, int r, int c, const T *Cin, Mat<T> M1, Mat<T> Y1, int kk1,
-                                      Mat<T> M2, Mat<T> Y2, int kk2, int tid)
+                                      Mat<T> M2, Mat<T> Y2, int kk2, int tid, bool upper = false)
 {
     using acc = typename Tile<T>::acc;
     const int wave = tid >> 6, lane = tid & 63;
     const int RT = (r + 15) / 16, CT = (c + 15) / 16;
-    for (int ot = wave; ot < RT * CT; ot += BT / 64) {
-        const int it = ot % RT, jt = ot / RT;
-        acc D;
-        if (Cin) tile_ld<T>(D, Cin + it * 16 + (size_t)jt * 16 * ldc, r - it * 16, c - jt * 16, 1, ldc, lane);
-        else D = acc{0, 0, 0, 0};
-        wg_mm_k<T, S1>(D, M1, Y1, kk1, r, c, it, jt, lane);
-        wg_mm_k<T, S2>(D, M2, Y2, kk2, r, c, it, jt, lane);
+    auto store = [&](const acc &D, int it, int jt) __attribute__((always_inline)) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int row = it * 16 + Tile<T>::row(lane, q), col = jt * 16 + tcol(lane);
             if (row < r && col < c) C[row + (size_t)col * ldc] = D[q];
         }
+    };
+    auto init = [&](acc &D, int it, int jt) __attribute__((always_inline)) {
+        if (Cin) tile_ld<T>(D, Cin + it * 16 + (size_t)jt * 16 * ldc, r - it * 16, c - jt * 16, 1, ldc, lane);
+        else D = acc{0, 0, 0, 0};
+    };
+    if (RT * CT > 8) {
+        const int RB = (RT + 1) / 2, CB = (CT + 1) / 2;
+        for (int ob = wave; ob < RB * CB; ob += BT / 64) {
+            const int it0 = 2 * (ob % RB), jt0 = 2 * (ob / RB);
+            if (upper && it0 > jt0 + 1) continue;
+            acc D[2][2];
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) init(D[a][b], it0 + a, jt0 + b);
+            wg_mm_k22<T, S1>(D, M1, Y1, kk1, r, c, it0, jt0, lane);
+            wg_mm_k22<T, S2>(D, M2, Y2, kk2, r, c, it0, jt0, lane);
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    if (!upper || it0 + a <= jt0 + b) store(D[a][b], it0 + a, jt0 + b);
+        }
+        return;
+    }
+    for (int ot = wave; ot < RT * CT; ot += BT / 64) {
+        const int it = ot % RT, jt = ot / RT;
+        if (upper && it > jt) continue;
+        acc D;
+        init(D, it, jt);
+        wg_mm_k<T, S1>(D, M1, Y1, kk1, r, c, it, jt, lane);
+        wg_mm_k<T, S2>(D, M2, Y2, kk2, r, c, it, jt, lane);
+        store(D, it, jt);
     }
 }
 // one product: C = [Cin] + S·M1ᵀ·Y1

@@ -105,7 +105,8 @@ recipe_check() {   # after a kernel change: the -m gpu suite + smoke, then the l
     sub lin kt --linear && sub cfg2 kt --workload cartpole && sub di kt --workload kkt --kkt-structure di
 }
 recipe_wg() {   # the workgroup KKT kernel (blocks past 64 rows): its tests, then the n=96 line
-    sub t pytest tests/test_kkt_wg_gpu.py tests/test_dp_big_gpu.py && sub wg96 prof $WG96
+    sub t pytest tests/test_kkt_wg_gpu.py tests/test_dp_big_gpu.py && sub wg96 prof $WG96 &&
+    sub big128 kt --n 128 --m 64 --N 64 --batch 2048
 }
 recipe_list() { declare -F | sed -n 's/^declare -f recipe_//p'; }
 
