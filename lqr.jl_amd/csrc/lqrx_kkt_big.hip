@@ -1262,6 +1262,9 @@ constexpr int KF_LDS = 64 * KF_LU + 64 + KF_SCR;      // per wave: U image, vect
 #ifndef KF_OLD_LEAF
 #define KF_OLD_LEAF 0                                 // 1: the 16-lane readlane leaf (A/B builds)
 #endif
+#ifndef KF_INV_SWEEP
+#define KF_INV_SWEEP 0                                // 1: the round-4 leaf inverse sweep (A/B builds)
+#endif
 
 // image of one knot (elements of T from the knot's base): tiles D, F, B, E, C (256 elements
 // each, lane-major C layout: element 4·lane + r = register r of lane `lane`), then
@@ -1715,6 +1718,51 @@ __device__ __forceinline__ int leaf_chol_inv_t(acc_t<T> &X, T *scr, int q, int l
     return bad;
 }
 
+// The same leaf with the inverse carried along (round 5): the factor's row operations — row i
+// scaled by 1/U_ii, rows r > i minus U[i][r]·(scaled row i) — applied to E = I as well turn it
+// into U⁻ᵀ (the operations compose to U⁻ᵀ, since U⁻ᵀ·X = U), so each of the 16 steps broadcasts
+// the scaled row i of E beside the pivot row (one LDS round trip for both) and the separate
+// 16-step back-substitution chain of leaf_chol_inv_t disappears.  T = U⁻¹ = Eᵀ goes through the
+// caller's image Dg (column-major, KF_LU; where leaf_chol_inv_t's caller stored T): E is written
+// transposed and read back as X.  Returns 1 + the first non-positive pivot (< q), else 0.
+template <typename T>
+__device__ __forceinline__ int leaf_chol_inv_e(acc_t<T> &X, T *scr, T *Dg, int q, int lane)
+{
+    T *ub = scr, *eb = scr + 64;                        // pivot row of U, scaled row of E
+    const int c = lane & 15, g = lane >> 4;
+    constexpr bool F64 = sizeof(T) == 8;
+    int bad = 0;
+    acc_t<T> E;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) E[r] = Tile<T>::row(lane, r) == c ? (T)1 : (T)0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int gi = F64 ? (i & 3) : (i >> 2), rgi = F64 ? (i >> 2) : (i & 3);
+        const T d = readlane(X[rgi], 16 * gi + i);
+        if (!(d > (T)0) && i < q && !bad) bad = i + 1;
+        const T sc = rsqrt_nr(d);
+        wsync();
+        ub[16 * g + c] = c > i ? X[rgi] * sc : (T)0;
+        eb[16 * g + c] = E[rgi] * sc;
+        wsync();
+        const T uc = ub[16 * gi + c], ec = eb[16 * gi + c];
+        T ur[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ur[r] = ub[16 * gi + Tile<T>::row(lane, r)];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            X[r] = fma(-ur[r], uc, X[r]);
+            E[r] = Tile<T>::row(lane, r) == i ? ec : fma(-ur[r], ec, E[r]);
+        }
+    }
+    wsync();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Dg[c + Tile<T>::row(lane, r) * KF_LU] = E[r];   // T = Eᵀ, column-major
+    wsync();
+    X = tload(Dg, KF_LU, lane);
+    return bad;
+}
+
 // In place on the upper tiles X (packed up4) of a P×P SPD matrix (nb ≤ 4 block rows, p real
 // pivots): X ← U⁻¹ with UᵀU = X.  Right-looking by 16 as chol_inv: leaf (LDS, one wave) →
 // panel U_{jb,J} = T_jjᵀ X_{jb,J} → trailing X_IJ −= U_{jb,I}ᵀ U_{jb,J}, all in registers;
@@ -1749,10 +1797,14 @@ __device__ int chol_inv_reg(acc_t<T> (&X)[10], int nb, int p, T *U, T *scr, int 
 #elif defined(KF_NOLEAF)
             const int b = 0;       // timing ablation only: no leaf factor (wrong results)
             (void)scr;
-#else
+#elif KF_INV_SWEEP
+            // A/B: the round-4 leaf (inverse by a second 16-step back-substitution sweep)
             const int b = leaf_chol_inv_t<T>(X[up4(jb, jb)], scr, min(16, p - 16 * jb), lane);
             if (b && !bad) bad = 16 * jb + b;
             tstore(Dg, KF_LU, X[up4(jb, jb)], lane);     // T_jj for the inverse assembly's reads
+#else
+            const int b = leaf_chol_inv_e<T>(X[up4(jb, jb)], scr, Dg, min(16, p - 16 * jb), lane);
+            if (b && !bad) bad = 16 * jb + b;            // (T_jj is in Dg for the inverse assembly)
 #endif
 #pragma unroll
             for (int J = jb + 1; J < 4; ++J)

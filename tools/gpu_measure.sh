@@ -108,6 +108,10 @@ recipe_wg() {   # the workgroup KKT kernel (blocks past 64 rows): its tests, the
     sub t pytest tests/test_kkt_wg_gpu.py tests/test_dp_big_gpu.py && sub wg96 prof $WG96 &&
     sub big128 kt --n 128 --m 64 --N 64 --batch 2048
 }
+recipe_kkt() {   # the large-block KKT path (configs[4]'s KKT half): its tests, then the fp32 / fp64 lines
+    sub t pytest tests/test_kkt_big_gpu.py tests/test_full_size_gpu.py tests/test_kkt_pad_gpu.py &&
+    sub kkt32 kt $CFG4KKT && sub kkt64 kt $CFG4KKT64
+}
 recipe_list() { declare -F | sed -n 's/^declare -f recipe_//p'; }
 
 case "$MODE" in
