@@ -1769,9 +1769,19 @@ __device__ __forceinline__ int leaf_chol_inv_e(acc_t<T> &X, T *scr, T *Dg, int q
 // then W_IJ = −T_I Σ_{L=I+1..J} U_IL W_LJ with U_ILᵀ and T_Iᵀ read transposed from the LDS
 // image U (leading dimension KF_LU) the factor phase left there.  Returns 0 or 1 + the
 // first non-positive pivot.
+// kbc (KB_PROF timing builds only, else null): cycles of the leaves, the panel / trailing
+// updates and the inverse assembly added to kbc[0..2]
 template <typename T>
-__device__ int chol_inv_reg(acc_t<T> (&X)[10], int nb, int p, T *U, T *scr, int lane)
+__device__ int chol_inv_reg(acc_t<T> (&X)[10], int nb, int p, T *U, T *scr, int lane, int64_t *kbc = nullptr)
 {
+    int64_t kc0 = kbc ? clock64() : 0;
+    auto kct = [&](int i) {
+        if (kbc) {
+            const int64_t t = clock64();
+            kbc[i] += t - kc0;
+            kc0 = t;
+        }
+    };
 #pragma unroll
     for (int jb = 0; jb < 4; ++jb)
         if (jb < nb) {
@@ -1806,6 +1816,7 @@ __device__ int chol_inv_reg(acc_t<T> (&X)[10], int nb, int p, T *U, T *scr, int 
             const int b = leaf_chol_inv_e<T>(X[up4(jb, jb)], scr, Dg, min(16, p - 16 * jb), lane);
             if (b && !bad) bad = 16 * jb + b;            // (T_jj is in Dg for the inverse assembly)
 #endif
+            kct(0);
 #pragma unroll
             for (int J = jb + 1; J < 4; ++J)
                 if (J < nb) {
@@ -1817,6 +1828,7 @@ __device__ int chol_inv_reg(acc_t<T> (&X)[10], int nb, int p, T *U, T *scr, int 
 #pragma unroll
                 for (int J = I; J < 4; ++J)
                     if (J < nb) X[up4(I, J)] = mtn<T, true>(X[up4(jb, I)], X[up4(jb, J)], X[up4(I, J)]);
+            kct(1);
         }
     }
     wsync();
@@ -1832,6 +1844,7 @@ __device__ int chol_inv_reg(acc_t<T> (&X)[10], int nb, int p, T *U, T *scr, int 
                 X[up4(I, J)] = mtn<T, true>(tload_t(U + 16 * I * (1 + KF_LU), KF_LU, lane), s, tzero<T>());
             }
         }
+    kct(2);
     return bad;
 }
 
@@ -2210,7 +2223,7 @@ struct KuArgs {
     int64_t *prof;                           // KB_PROF builds: per-phase cycles (else unused)
 };
 #ifndef KU_PF_SLICES
-#define KU_PF_SLICES 2
+#define KU_PF_SLICES 0       // 0: per precision (ku_pf)
 #endif
 #ifndef KU_LEAN
 #define KU_LEAN 1            // H⁻¹/g read at use, λ carried in column layout (fewer live registers)
@@ -2226,7 +2239,10 @@ struct KuArgs {
 #endif
 // waves per fused workgroup: fp64 stays at 4 (one per SIMD: its LDS and registers)
 template <typename T> constexpr int ku_w() { return sizeof(T) == 4 ? KU_WAVES : 4; }
-constexpr int KU_PF = KU_PF_SLICES;          // k-slices of Y (of both knots) in flight per wave
+// k-slices of Y (of both knots) in flight per wave: fp64 runs one wave per SIMD (512 registers),
+// where a third slice fits and gains (stream 86 k → 82 k cycles per knot, profiles/r05/h; fp32's
+// 2 waves/SIMD spill with three)
+template <typename T> constexpr int ku_pf() { return KU_PF_SLICES ? KU_PF_SLICES : (sizeof(T) == 8 ? 3 : 2); }
 constexpr int KU_LDS = KF_LDS;   // per wave: U / W image, vector, 2 H⁻¹|g rows (also the leaf scratch)
 
 // H⁻¹ (or 1) and g of knot q into one of the wave's LDS rows (0 past w); earlier reads of the
@@ -2294,6 +2310,7 @@ __device__ __forceinline__ void fu_schur2(const Kn &q1, const T *Y1, const T *hg
     const int yn1 = q1.rows * q1.w * (int)TS, so1 = 4 * q1.rows * (int)TS;
     const int yn2 = q2.rows * q2.w * (int)TS, so2 = 4 * q2.rows * (int)TS;
     const int nks = max(q1.w + 3, q2.w + 3) >> 2;
+    constexpr int KU_PF = ku_pf<T>();
     T f1[KU_PF][NB], f2[KU_PF][NT], h1[KU_PF], c1[KU_PF], h2[KU_PF], c2[KU_PF];
     auto load = [&](int s, T (&a1)[NB], T (&a2)[NT], T &hh1, T &gg1, T &hh2, T &gg2) __attribute__((always_inline)) {
         const int o1 = s * so1, o2 = s * so2;
@@ -2485,7 +2502,11 @@ __global__ void __launch_bounds__(64 * ku_w<T>(), sizeof(T) == 4 ? 8 / ku_w<T>()
         const int bad = 0;         // timing ablation only: no factorisation (wrong results)
         (void)p2;
 #else
+#ifdef KB_PROF
+        const int bad = chol_inv_reg<T>(P, NT, p2, U, hgl, lane, kb_acc + 4);
+#else
         const int bad = chol_inv_reg<T>(P, NT, p2, U, hgl, lane);
+#endif
 #endif
         KB_T(0);
         // λ_k = W_kᵀ x_k (:108-116)
@@ -2589,7 +2610,10 @@ __device__ __forceinline__ double rdlane(double v, int l)
     const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
-template <typename T> constexpr int kbw_hold() { return KBW_NOHOLD ? 2 : sizeof(T) == 4 ? 96 : 32; }
+#ifndef KBW_HOLD64
+#define KBW_HOLD64 32        // fp64 D2 columns held (A/B: 64, 96 take the kernel to one wave per SIMD)
+#endif
+template <typename T> constexpr int kbw_hold() { return KBW_NOHOLD ? 2 : sizeof(T) == 4 ? 96 : KBW_HOLD64; }
 constexpr int KBW_VC = KBW_VC_COLS;  // columns of Y in flight per lane in the v product
 constexpr int KBW_R = KBW_RUN;       // column-run elements in flight per lane (t, D2ᵀλ)
 
@@ -3167,8 +3191,8 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
     }
 #ifdef KB_PROF
     static int64_t *prof = nullptr;
-    if (!prof) (void)hipMalloc((void **)&prof, 64 * sizeof(int64_t));
-    (void)hipMemsetAsync(prof, 0, 64 * sizeof(int64_t), s);
+    if (!prof) (void)hipMalloc((void **)&prof, 128 * sizeof(int64_t));   // ≤ 8 waves × 16 phases
+    (void)hipMemsetAsync(prof, 0, 128 * sizeof(int64_t), s);
     k.prof = prof;
     ku.prof = prof;
 #endif
@@ -3234,16 +3258,17 @@ hipError_t kb_launch_t(const KktArgs &a, const KbPlan &P, hipStream_t s)
     }
 #ifdef KB_PROF
     {
-        int64_t h[64];
+        int64_t h[128];
         (void)hipStreamSynchronize(s);
         (void)hipMemcpy(h, prof, sizeof h, hipMemcpyDeviceToHost);
         const double steps = (double)a.batch * (a.N + 2);
         if (P.fuse) {
             const double kn = (double)a.batch * (P.mid1 - P.mid0);   // wave-knots
-            std::fprintf(stderr, "KB_PROF fused kernel, cycles per knot and wave [chol+inv | lambda+slab | stream | reduce]:");
-            for (int i = 0; i < 4; ++i) {
+            std::fprintf(stderr, "KB_PROF fused kernel, cycles per knot and wave [chol+inv | lambda+slab | stream | reduce"
+                                 " || chol: leaves | panel+trailing | inverse assembly]:");
+            for (int i = 0; i < 7; ++i) {
                 double sum = 0;
-                for (int w = 0; w < 4; ++w) sum += (double)h[16 * w + i];
+                for (int w = 0; w < 8; ++w) sum += (double)h[16 * w + i];
                 std::fprintf(stderr, " %9.0f", sum / kn);
             }
             std::fprintf(stderr, "\n");
