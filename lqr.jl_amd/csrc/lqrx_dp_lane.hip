@@ -434,14 +434,20 @@ __device__ __forceinline__ float qbcast(float v)
 template <int R, typename T>
 __device__ __forceinline__ T qfrom(T v) { return qbcast<R | (R << 2) | (R << 4) | (R << 6)>(v); }
 
-template <typename T, int MP, bool SOA, bool LIN = false>
+#ifndef LQRX_QUAD_PB_REPL
+#define LQRX_QUAD_PB_REPL 0     // A/B: 1 = PB = P·B replicated in every lane of the quad (round 4)
+#endif
+// EX (exact shape: n = 4, m = MP, trajectory-contiguous layout): every stride and padding test
+// is a compile-time constant — the rollout's K loads become immediate offsets of one pointer
+template <typename T, int MP, bool SOA, bool LIN = false, bool EX = false>
 __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
 {
     constexpr int NP = 4;
+    static_assert(!EX || !SOA, "EX: trajectory-contiguous layout only");
     const int64_t b = ((int64_t)blockIdx.x * 64 + threadIdx.x) >> 2;
     const int q = threadIdx.x & 3;
     if (b >= a.batch) return;   // whole quads retire together; DPP stays inside the quad
-    const int n = a.n, m = a.m, N = a.N;
+    const int n = EX ? NP : a.n, m = EX ? MP : a.m, N = a.N;
     const int64_t nn = (int64_t)n * n, nm = (int64_t)n * m, mm = (int64_t)m * m;
     const int64_t es = SOA ? a.batch : 1;                      // as dp_lane_kernel
     auto tb = [&](int64_t S) { return SOA ? b : b * S; };
@@ -495,17 +501,39 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
         qq = q < n ? qg[q * es] : (T)0;
         if (pall && q < n) pall[((int64_t)(N - 1) * n + q) * es] = qf[q * es];
     }
+    // this lane's column of P (row q by symmetry): P_N = Qf, then the P_[:,q] the knot forms
+    T Pcol[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) Pcol[i] = (i < n && q < n) ? ((const T *)a.Qf + tb(nn))[(i + q * n) * es] : (T)0;
     for (int k = N - 1; k >= 1; --k) {   // :61
         T PB[NP][MP];
+        if constexpr (LQRX_QUAD_PB_REPL || sizeof(T) == 4) {
 #pragma unroll
-        for (int i = 0; i < NP; ++i)
+            for (int i = 0; i < NP; ++i)
 #pragma unroll
-            for (int c = 0; c < MP; ++c) {                       // :38 PB = P B
+                for (int c = 0; c < MP; ++c) {                       // :38 PB = P B
+                    T s = (T)0;
+#pragma unroll
+                    for (int l = 0; l < NP; ++l) s = fma(PS(i, l), B[l][c], s);
+                    PB[i][c] = s;
+                }
+        } else {
+            // :38 PB = P B split by rows (fp64): lane q forms row q from its own column P_[:,q] (the
+            // upper-triangle part of that row differs from the symmetrised P by rounding only), the
+            // quad broadcasts hand every lane the same PB — NP·MP FMAs per lane instead of NP²·MP.
+            // fp32 keeps the replicated form: there the mixed-triangle row measurably loosens the
+            // random-problem parity bound (tests/test_dp_lane_gpu.py::test_lane_parity_f32)
+#pragma unroll
+            for (int c = 0; c < MP; ++c) {
                 T s = (T)0;
 #pragma unroll
-                for (int l = 0; l < NP; ++l) s = fma(PS(i, l), B[l][c], s);
-                PB[i][c] = s;
+                for (int l = 0; l < NP; ++l) s = fma(Pcol[l], B[l][c], s);
+                PB[0][c] = qfrom<0>(s);
+                PB[1][c] = qfrom<1>(s);
+                PB[2][c] = qfrom<2>(s);
+                PB[3][c] = qfrom<3>(s);
             }
+        }
         T PAc[NP];
 #pragma unroll
         for (int i = 0; i < NP; ++i) {                           // :40 PA[:,q] = P A[:,q]
@@ -624,6 +652,8 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
             for (int l = 0; l < NP; ++l) s = fma(A[l][i], wv[l], s);
             Pn[i] = s;
         }
+#pragma unroll
+        for (int i = 0; i < NP; ++i) Pcol[i] = Pn[i];
         // re-replicate the lower triangle: P[i][r] (i ≥ r) from lane r
 #pragma unroll
         for (int i = 0; i < NP; ++i) P[i][0] = qfrom<0>(Pn[i]);
@@ -652,21 +682,29 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
 #pragma unroll
     for (int i = 0; i < NP; ++i) x[i] = i < n ? x0[i * es] : (T)0;
     if (q < n) Xb[q * es] = q == 0 ? x[0] : (q == 1 ? x[1] : (q == 2 ? x[2] : x[3]));
+    if (N < 2) return;                 // no controls (the clamped fetches below need knot 1)
     constexpr int RD = 8;
     T ring[RD][MP][NP], dring[LIN ? RD : 1];
-    auto fetch = [&](int k, T (&d)[MP][NP]) {
-        if (k > N - 1) return;
-        const T *Kk = Kb + (int64_t)(k - 1) * nm * es;
+    const int64_t kst = nm * es, dst = (int64_t)m * es;     // knot strides of K and d
+    // The ring: slot d of a group holds knot k0 + d; its refill fetches knot k0 + d + RD from
+    // the group's base pointer (scalar offsets d·stride, no per-knot index arithmetic), or —
+    // in the one group whose refills run past the last knot — from knot min(k, N − 1).
+    // Unconditional loads with nothing applied to them until the knot uses them, so the
+    // compiler's waits count the ring instead of draining it at every knot: a padding entry
+    // (i ≥ m or j ≥ n) reads another element of K_k (an index clamp, not a select the compiler
+    // could turn into a branch) — finite — and only ever meets a zero (x[j ≥ n] = 0;
+    // u[i ≥ m] meets Brow[i] = 0 and is not stored).
+    auto fetch = [&](const T *Kk, T (&d)[MP][NP]) {
 #pragma unroll
         for (int j = 0; j < NP; ++j)
 #pragma unroll
-            for (int i = 0; i < MP; ++i) d[i][j] = (i < m && j < n) ? Kk[(i + j * m) * es] : (T)0;
+            for (int i = 0; i < MP; ++i) d[i][j] = Kk[min(i + j * m, (int)nm - 1) * es];
     };
-    auto fetch_d = [&](int k, T &d) {   // lane q < m: d_k[q]
-        if constexpr (LIN) {
-            if (k <= N - 1) d = q < m ? db[((int64_t)(k - 1) * m + q) * es] : (T)0;
-        }
+    auto fetch_d = [&](const T *dk, T &d) {   // lane q < m: d_k[q] (q ≥ m: unused)
+        if constexpr (LIN) d = dk[min(q, m - 1) * es];
     };
+    auto kat = [&](int k) { return Kb + (int64_t)(min(k, N - 1) - 1) * kst; };
+    auto dat = [&](int k) { return db + (int64_t)(min(k, N - 1) - 1) * dst; };
     // K_k was written by this quad's own lanes above; make those stores visible to the
     // quad's loads (other lanes' stores: complete them and drop any stale L1 line, once)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -674,50 +712,66 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #pragma unroll
     for (int d = 0; d < RD; ++d) {
-        fetch(1 + d, ring[d]);
-        fetch_d(1 + d, dring[LIN ? d : 0]);
+        fetch(kat(1 + d), ring[d]);
+        if constexpr (LIN) fetch_d(dat(1 + d), dring[d]);
     }
-    for (int k0 = 1; k0 <= N - 1; k0 += RD) {
+    // knot k from ring slot d; REFILL 1: the slot then fetches knot k + RD at (Kr, Dr)
+    auto knot = [&](int k, T (&slot)[MP][NP], T &dslot, bool refill, const T *Kr, const T *Dr)
+        __attribute__((always_inline)) {
+        T Kc[MP][NP], dq = (T)0;
 #pragma unroll
-        for (int d = 0; d < RD; ++d) {
-            const int k = k0 + d;
-            if (k > N - 1) break;
-            T Kc[MP][NP], dq = (T)0;
+        for (int j = 0; j < NP; ++j)
 #pragma unroll
-            for (int j = 0; j < NP; ++j)
+            for (int i = 0; i < MP; ++i) Kc[i][j] = slot[i][j];
+        if constexpr (LIN) dq = dslot;
+        if (refill) {
+            fetch(Kr, slot);
+            fetch_d(Dr, dslot);
+        }
+        T u[MP];
 #pragma unroll
-                for (int i = 0; i < MP; ++i) Kc[i][j] = ring[d][i][j];
-            fetch(k + RD, ring[d]);
-            if constexpr (LIN) {
-                dq = dring[d];
-                fetch_d(k + RD, dring[d]);
-            }
-            T u[MP];
-#pragma unroll
-            for (int i = 0; i < MP; ++i) {
-                T s = (T)0;
-#pragma unroll
-                for (int j = 0; j < NP; ++j) s = fma(Kc[i][j], x[j], s);
-                if constexpr (LIN) {   // u = −(K x + d), d_k[i] from lane i
-                    const T di = i == 0 ? qfrom<0>(dq) : i == 1 ? qfrom<1>(dq) : i == 2 ? qfrom<2>(dq) : qfrom<3>(dq);
-                    u[i] = -(s + di);
-                } else {
-                    u[i] = -s;
-                }
-                if (q == 0 && i < m) Ub[((int64_t)(k - 1) * m + i) * es] = u[i];
-            }
+        for (int i = 0; i < MP; ++i) {
             T s = (T)0;
 #pragma unroll
-            for (int j = 0; j < NP; ++j) s = fma(Arow[j], x[j], s);
-#pragma unroll
-            for (int c = 0; c < MP; ++c) s = fma(Brow[c], u[c], s);
-            if (q < n) Xb[((int64_t)k * n + q) * es] = s;
-            x[0] = qfrom<0>(s);
-            x[1] = qfrom<1>(s);
-            x[2] = qfrom<2>(s);
-            x[3] = qfrom<3>(s);
+            for (int j = 0; j < NP; ++j) s = fma(Kc[i][j], x[j], s);
+            if constexpr (LIN) {   // u = −(K x + d), d_k[i] from lane i
+                const T di = i == 0 ? qfrom<0>(dq) : i == 1 ? qfrom<1>(dq) : i == 2 ? qfrom<2>(dq) : qfrom<3>(dq);
+                u[i] = -(s + di);
+            } else {
+                u[i] = -s;
+            }
+            if (q == 0 && i < m) Ub[((int64_t)(k - 1) * m + i) * es] = u[i];
         }
+        T s = (T)0;
+#pragma unroll
+        for (int j = 0; j < NP; ++j) s = fma(Arow[j], x[j], s);
+#pragma unroll
+        for (int c = 0; c < MP; ++c) s = fma(Brow[c], u[c], s);
+        if (q < n) Xb[((int64_t)k * n + q) * es] = s;
+        x[0] = qfrom<0>(s);
+        x[1] = qfrom<1>(s);
+        x[2] = qfrom<2>(s);
+        x[3] = qfrom<3>(s);
+    };
+    // whole groups of RD knots (no per-knot exit test) whose refills stay inside the horizon,
+    // then at most one group with clamped refills, then the < RD remaining knots
+    int k0 = 1;
+    for (; k0 + 2 * RD - 1 <= N - 1; k0 += RD) {
+        const T *Kg = Kb + (int64_t)(k0 + RD - 1) * kst;
+        const T *Dg = LIN ? db + (int64_t)(k0 + RD - 1) * dst : nullptr;
+#pragma unroll
+        for (int d = 0; d < RD; ++d)
+            knot(k0 + d, ring[d], dring[LIN ? d : 0], true, Kg + d * kst, LIN ? Dg + d * dst : nullptr);
     }
+    if (k0 + RD - 1 <= N - 1) {
+#pragma unroll
+        for (int d = 0; d < RD; ++d)
+            knot(k0 + d, ring[d], dring[LIN ? d : 0], true, kat(k0 + d + RD), LIN ? dat(k0 + d + RD) : nullptr);
+        k0 += RD;
+    }
+#pragma unroll
+    for (int d = 0; d < RD - 1; ++d)
+        if (k0 + d <= N - 1) knot(k0 + d, ring[d], dring[LIN ? d : 0], false, nullptr, nullptr);
 #undef PS
 }
 
@@ -986,6 +1040,7 @@ static hipError_t launch_quad(const DpArgs &a, hipStream_t s)
     if (a.lin && a.layout == 1) hipLaunchKernelGGL((dp_quad_kernel<T, MP, true, true>), grid, block, 0, s, a);
     else if (a.lin) hipLaunchKernelGGL((dp_quad_kernel<T, MP, false, true>), grid, block, 0, s, a);
     else if (a.layout == 1) hipLaunchKernelGGL((dp_quad_kernel<T, MP, true>), grid, block, 0, s, a);
+    else if (a.n == 4 && a.m == MP) hipLaunchKernelGGL((dp_quad_kernel<T, MP, false, false, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((dp_quad_kernel<T, MP, false>), grid, block, 0, s, a);
     return hipGetLastError();
 }
