@@ -56,6 +56,9 @@
 #ifndef LQRX_DP_TVWAIT
 #define LQRX_DP_TVWAIT 0
 #endif
+#ifndef LQRX_DP_WG4
+#define LQRX_DP_WG4 1         // fp64 n = 64: the four-wave kernel (A/B builds: 0 = one wave)
+#endif
 #ifndef LQRX_DP_ROLL_FULL
 #define LQRX_DP_ROLL_FULL 1   // exact tile grids: the register-streamed rollout (A/B builds: 0)
 #endif
@@ -886,6 +889,265 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
     }
 }
 
+// ------------------------------------------------------------------ four waves per trajectory
+// dp_wg4_kernel<T, MT> — fp64 n = 64, m = 16·MT (time-invariant, no linear terms): the shape
+// whose tile grid does not fit one wave (A alone is 128 fp64 registers; the one-wave kernel
+// spills ~2–3 KB per lane there).  One 256-thread workgroup per trajectory, one wave per SIMD,
+// the same fast form and the same Newton–Schulz / exact-sweep inverse as dp_riccati_kernel,
+// with the knot's products split by the n-dimension's 16-column tiles (wave w ↔ tile column w):
+//   :38  PB[w][:] = P[:, w]ᵀ·B            (P tiles from the LDS image, B in registers)
+//   :40  PA[:, w] = Pᵀ·A[:, w]             (all of P from LDS, A[:, w] in registers)
+//   :39  E tile (w mod MT, w / MT) = R + BᵀPB   (PB from its LDS image; one tile per wave)
+//   :41  G[:, w] = Bᵀ·PA[:, w]             (registers only; also to an LDS image)
+//   :42  X ≈ E⁻¹ (every wave, bitwise alike), K[:, w] = XᵀG[:, w], stored to sol.K
+//   :51  P_ tiles (i, w), i from wave w's row list — the ten tiles of the symmetric 4×4 grid
+//        as 3, 3, 2, 2 per wave: Q + A[:, i]ᵀPA[:, w] − G[:, i]ᵀK[:, w], written to the P image
+//        at (i, w) and mirrored to (w, i) (diagonal tiles from their lower triangle), so the
+//        image stays exactly symmetric as tiles_symmetrize_lower keeps the one-wave P.
+// Three workgroup barriers per knot (after PB/PA, after E/G, after P_).  Registers per wave:
+// the A columns its P_ rows need (3 × 4 tiles, the first is A[:, w]), B, Q's P_ tiles, R's E
+// tile — time-invariant, loaded once.  The rollout (:66-70) is dp_rollout_full on wave 0.
+template <typename T, int MT>
+struct Wg4Cfg {
+    static constexpr int NT = 4, NP = 64, MP = 16 * MT;
+    static constexpr int PL = NP + 2;                    // P image column stride (bank spread)
+    static constexpr int CS = MP + 2;                    // PB / E / G images, aug sweep
+    static constexpr int P_EL = NP * PL;
+    static constexpr int AUG = 2 * MP * CS + 64 + MP;   // [E | I] sweep image + row/rinv
+    static constexpr int PB_EL = (MP * CS > AUG ? MP * CS : AUG) > NP * CS ? (MP * CS > AUG ? MP * CS : AUG) : NP * CS;
+    static constexpr int E_EL = MP * CS, G_EL = NP * CS;
+    static constexpr int B_EL = MP * PL;                                 // B image (NP × MP)
+    static constexpr int LDS = 2 * P_EL + B_EL + PB_EL + E_EL + G_EL + 8;   // P, Q, B images
+};
+// row tile of wave w's t-th P_ tile (column tile w), −1: none
+__host__ __device__ constexpr int wg4_pn_row(int w, int t)
+{
+    constexpr int tab[4][3] = {{0, 1, 2}, {1, 2, 3}, {2, 3, -1}, {3, 0, -1}};
+    return tab[w][t];
+}
+
+template <typename T>
+__device__ __forceinline__ typename Tile<T>::acc wg4_tload(const T *X, int ld, int lane)
+{
+    typename Tile<T>::acc c;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) c[r] = X[Tile<T>::row(lane, r) + tcol(lane) * ld];
+    return c;
+}
+template <typename T>
+__device__ __forceinline__ void wg4_tstore(T *X, int ld, const typename Tile<T>::acc &c, int lane)
+{
+#pragma unroll
+    for (int r = 0; r < 4; ++r) X[Tile<T>::row(lane, r) + tcol(lane) * ld] = c[r];
+}
+// D += Mᵀ·Y (one 16×16×16 tile product, 4 MFMAs)
+template <typename T, bool NEG = false>
+__device__ __forceinline__ void wg4_mtn(typename Tile<T>::acc &D, const typename Tile<T>::acc &M,
+                                        const typename Tile<T>::acc &Y)
+{
+#pragma unroll
+    for (int r = 0; r < 4; ++r) D = NEG ? Tile<T>::mma_nega(M[r], Y[r], D) : Tile<T>::mma(M[r], Y[r], D);
+}
+
+template <typename T, int MT>
+__global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
+{
+    using C = Wg4Cfg<T, MT>;
+    using acc = typename Tile<T>::acc;
+    constexpr int NT = C::NT, NP = C::NP, MP = C::MP, PL = C::PL, CS = C::CS;
+    __shared__ T lds[C::LDS];
+    T *Pim = lds, *Qim = Pim + C::P_EL, *Bim = Qim + C::P_EL, *PBim = Bim + C::B_EL, *Eim = PBim + C::PB_EL;
+    T *Gim = Eim + C::E_EL;
+    int *flag = (int *)(Gim + C::G_EL);
+    T *aug = PBim;                       // the exact sweep reuses the PB image (read before it)
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t b = blockIdx.x;
+    if (b >= a.batch) return;            // whole workgroup
+    const int N = a.N;
+    constexpr size_t nn = (size_t)NP * NP, nm = (size_t)NP * MP, mm = (size_t)MP * MP;
+    const T *Ab = (const T *)a.A + b * nn, *Bb = (const T *)a.B + b * nm;
+    const T *Qb = (const T *)a.Q + b * nn, *Rb = (const T *)a.R + b * mm;
+
+    // time-invariant register operands
+    acc Ar[3][NT], Rw = acc{0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        const int i = wg4_pn_row(w, t) < 0 ? 0 : wg4_pn_row(w, t);
+#pragma unroll
+        for (int k = 0; k < NT; ++k) Ar[t][k] = wg4_tload(Ab + 16 * k + (size_t)16 * i * NP, NP, lane);  // A[k][i]
+    }
+    auto Bt = [&](int kk, int j) { return wg4_tload(Bim + 16 * kk + 16 * j * PL, PL, lane); };   // B[kk][j]
+    const int ei = w % MT, ej = w / MT;          // this wave's E tile (w < MT²)
+    if (w < MT * MT) Rw = wg4_tload(Rb + 16 * ei + (size_t)16 * ej * MP, MP, lane);
+    // P = Qf (:58) into the image; Q (the P_ accumulators' start) into its own
+    for (int e = tid; e < NP * NP; e += 256) {
+        Pim[(e % NP) + (e / NP) * PL] = ((const T *)a.Qf)[b * nn + e];
+        Qim[(e % NP) + (e / NP) * PL] = Qb[e];
+    }
+    for (int e = tid; e < NP * MP; e += 256) Bim[(e % NP) + (e / NP) * PL] = Bb[e];
+    T *Pall = a.p_all ? (T *)a.P + (size_t)b * nn * N : nullptr;
+    T *Kb = (T *)a.K + (size_t)b * (size_t)(N - 1) * nm;
+    int info = 0;
+    acc Xi[MT][MT], Xp[MT][MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < MT; ++j) Xi[i][j] = Xp[i][j] = acc{0, 0, 0, 0};
+    __syncthreads();
+    if (Pall)
+        for (int e = tid; e < NP * NP; e += 256) Pall[(size_t)(N - 1) * nn + e] = Pim[(e % NP) + (e / NP) * PL];
+
+    for (int k = N - 1; k >= 1; --k) {           // :61
+        // :38, :40 — one pass over the P image: PA[:, w] and PB[w][:]
+        acc PA[NT], PB[MT];
+#pragma unroll
+        for (int i = 0; i < NT; ++i) PA[i] = acc{0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < MT; ++j) PB[j] = acc{0, 0, 0, 0};
+#pragma unroll
+        for (int kk = 0; kk < NT; ++kk) {
+            acc Pt[NT];
+#pragma unroll
+            for (int i = 0; i < NT; ++i) Pt[i] = wg4_tload(Pim + 16 * kk + 16 * i * PL, PL, lane);   // P[kk][i]
+#pragma unroll
+            for (int i = 0; i < NT; ++i) wg4_mtn<T>(PA[i], Pt[i], Ar[0][kk]);
+            const acc Pw = wg4_tload(Pim + 16 * kk + 16 * w * PL, PL, lane);                     // P[kk][w]
+#pragma unroll
+            for (int j = 0; j < MT; ++j) wg4_mtn<T>(PB[j], Pw, Bt(kk, j));
+        }
+#pragma unroll
+        for (int j = 0; j < MT; ++j) wg4_tstore(PBim + 16 * w + 16 * j * NP, NP, PB[j], lane);
+        __syncthreads();                                   // B1: PB image complete, P image read
+        // :39 E tile, :41 G[:, w]
+        if (w < MT * MT) {
+            acc Et = Rw;
+#pragma unroll
+            for (int kk = 0; kk < NT; ++kk) {
+                const acc Y = wg4_tload(PBim + 16 * kk + 16 * ej * NP, NP, lane);               // PB[kk][ej]
+                wg4_mtn<T>(Et, Bt(kk, ei), Y);
+            }
+            wg4_tstore(Eim + 16 * ei + 16 * ej * CS, CS, Et, lane);
+        }
+        acc G[MT];
+#pragma unroll
+        for (int c = 0; c < MT; ++c) {
+            G[c] = acc{0, 0, 0, 0};
+#pragma unroll
+            for (int kk = 0; kk < NT; ++kk) wg4_mtn<T>(G[c], Bt(kk, c), PA[kk]);
+            wg4_tstore(Gim + 16 * c + 16 * w * CS, CS, G[c], lane);
+        }
+        __syncthreads();                                   // B2: E and G images complete
+        // :42 X ≈ E⁻¹ (warm-started Newton–Schulz; the exact sweep on wave 0 otherwise)
+        acc E[MT][MT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < MT; ++j) E[i][j] = wg4_tload(Eim + 16 * i + 16 * j * CS, CS, lane);
+        bool have = false;
+        if (k < N - 1) {
+            // warm start 2X_{k+1} − X_{k+2}; Xp takes X_{k+1} before the refinement
+            acc Id[MT][MT];
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < MT; ++j) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) Id[i][j][r] = (i == j && Tile<T>::row(lane, r) == tcol(lane)) ? (T)1 : (T)0;
+                    const acc x1 = Xi[i][j];
+                    Xi[i][j] = (T)2 * x1 - Xp[i][j];
+                    Xp[i][j] = x1;
+                }
+            have = ns_refine<T, MT>(Xi, E, Id, lane);
+        }
+        if (!have) {                                       // uniform: every wave computed alike
+            if (w == 0) {
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < MT; ++j) wg4_tstore(aug + 16 * i + 16 * j * CS, CS, E[i][j], lane);
+                wsync_w();
+                const bool ok = aug_ldl_forward<T, MP, 0, CS, 0>(aug, lane);
+                if (lane == 0) *flag = ok ? 1 : 0;
+            }
+            __syncthreads();
+            if (!*flag && info == 0) info = k;
+            acc Wt[MT][MT], DW[MT][MT];
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < MT; ++j) Wt[i][j] = wg4_tload(aug + MP * CS + 16 * i + 16 * j * CS, CS, lane);
+            const T *rinv = aug + 2 * MP * CS + 64;
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const T sc = rinv[i * 16 + Tile<T>::row(lane, r)];
+#pragma unroll
+                    for (int j = 0; j < MT; ++j) DW[i][j][r] = Wt[i][j][r] * sc;
+                }
+            tiles_zero<T, MT, MT>(Xi);
+            mma_tn<T, MT, MT, MT>(Xi, Wt, DW);             // X = Wᵀ D⁻¹ W = E⁻¹
+            if (k == N - 1) {
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < MT; ++j) Xp[i][j] = Xi[i][j];
+            }
+        }
+        // K[:, w] = XᵀG[:, w]  → sol.K[k−1] columns 16w…16w+15
+        acc Kt[MT];
+#pragma unroll
+        for (int c = 0; c < MT; ++c) {
+            Kt[c] = acc{0, 0, 0, 0};
+#pragma unroll
+            for (int i = 0; i < MT; ++i) wg4_mtn<T>(Kt[c], Xi[i][c], G[i]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                Kb[(size_t)(k - 1) * nm + 16 * c + Tile<T>::row(lane, r) + (size_t)(16 * w + tcol(lane)) * MP] = Kt[c][r];
+        }
+        // :51 P_ tiles (i, w) = Q + A[:, i]ᵀPA[:, w] − G[:, i]ᵀK[:, w] → the P image, mirrored
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int i = wg4_pn_row(w, t);
+            if (i < 0) continue;
+            acc Pn = wg4_tload(Qim + 16 * i + 16 * w * PL, PL, lane);                        // Q[i][w]
+#pragma unroll
+            for (int kk = 0; kk < NT; ++kk) wg4_mtn<T>(Pn, Ar[t][kk], PA[kk]);
+#pragma unroll
+            for (int c = 0; c < MT; ++c)
+                wg4_mtn<T, true>(Pn, wg4_tload(Gim + 16 * c + 16 * i * CS, CS, lane), Kt[c]);
+            T *at = Pim + 16 * i + 16 * w * PL, *mr = Pim + 16 * w + 16 * i * PL;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int rr = Tile<T>::row(lane, r), cc = tcol(lane);
+                if (i != w) {
+                    at[rr + cc * PL] = Pn[r];
+                    mr[cc + rr * PL] = Pn[r];
+                } else if (rr >= cc) {                     // diagonal tile: its lower triangle
+                    at[rr + cc * PL] = Pn[r];
+                    at[cc + rr * PL] = Pn[r];
+                }
+            }
+        }
+        __syncthreads();                                   // B3: P_ image complete
+        if (Pall)
+            for (int e = tid; e < NP * NP; e += 256) Pall[(size_t)(k - 1) * nn + e] = Pim[(e % NP) + (e / NP) * PL];
+    }
+    if (!a.p_all)
+        for (int e = tid; e < NP * NP; e += 256) ((T *)a.P)[b * nn + e] = Pim[(e % NP) + (e / NP) * PL];
+    if (a.info && tid == 0) a.info[b] = info;
+    // rollout on wave 0 once every wave's K stores are visible to it
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (w == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        dp_rollout_full<T, NT, MT, LQRX_DP_KD, false>(a, b, lds, lane);
+    }
+}
+
 // ------------------------------------------------------------------ launcher
 template <typename T, int NT, int MT, int WAVES = 2, int VAR = 0>
 static hipError_t launch_dp(const DpArgs &a, hipStream_t s);
@@ -933,6 +1195,15 @@ hipError_t dp_launch(const DpArgs &a, hipStream_t s)
         if (nt <= 1 && mt <= 1) return launch_dp_tv<double, 1, 1>(a, s);
         if (nt <= 2 && mt <= 1) return launch_dp_tv<double, 2, 1, LQRX_DP_WAVES, LQRX_DP_VAR>(a, s);
         if (nt <= 2 && mt <= 2) return launch_dp_tv<double, 2, 2>(a, s);
+        // n = 64, m ∈ {16, 32}, time-invariant, no linear terms: four waves per trajectory
+        // (LQRX_DP_WG4=0 in the environment: the one-wave kernel, for A/B runs and tests)
+        static const bool wg4 = [] { const char *e = std::getenv("LQRX_DP_WG4"); return LQRX_DP_WG4 && !(e && *e == '0'); }();
+        if (wg4 && a.n == 64 && (a.m == 16 || a.m == 32) && !a.lin && !a.tv_AB && !a.tv_QR) {
+            dim3 grid((unsigned)a.batch), block(256);
+            if (a.m == 16) hipLaunchKernelGGL((dp_wg4_kernel<double, 1>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((dp_wg4_kernel<double, 2>), grid, block, 0, s, a);
+            return hipGetLastError();
+        }
         if (nt <= 4 && mt <= 2) return launch_dp_tv<double, 4, 2, 1>(a, s);   // n ≤ 64: 1 wave/SIMD
     } else {
         if (nt <= 1 && mt <= 1) return launch_dp_tv<float, 1, 1>(a, s);

@@ -61,6 +61,58 @@ def test_dp_parity_f64(lqrx, oracle, gpu_ok, n, m, N, batch):
     assert np.abs(got["U"] - ref["U"]).max() <= TOL64 * max(1.0, np.abs(ref["U"]).max())
 
 
+@pytest.mark.parametrize("n,m,N,batch,all_P", [
+    (64, 32, 40, 5, True),     # dp_wg4_kernel<double, 2>: four waves per trajectory
+    (64, 16, 30, 3, True),     # dp_wg4_kernel<double, 1>
+    (64, 32, 150, 2, False),   # long horizon (warm-started inverse), P_1 only
+])
+def test_dp_wg4_parity_f64(lqrx, oracle, gpu_ok, n, m, N, batch, all_P):
+    """fp64 n = 64 runs on the four-wave kernel (lqrx_dp.hip dp_wg4_kernel)."""
+    got, ref = run_pair(lqrx, oracle, n, m, N, batch, seed=4000 + N, all_P=all_P)
+    assert got["rc"] == 0 and (got["info"] == 0).all()
+    assert relerr_per_knot(got["K"], ref["K"]) <= TOL64
+    P = got["P"] if all_P else got["P"][:, None]
+    assert relerr_per_knot(P, ref["P"] if all_P else ref["P"][:, None]) <= TOL64
+    assert np.abs(got["X"] - ref["X"]).max() <= TOL64 * max(1.0, np.abs(ref["X"]).max())
+    assert np.abs(got["U"] - ref["U"]).max() <= TOL64 * max(1.0, np.abs(ref["U"]).max())
+
+
+def test_dp_wg4_matches_one_wave(lqrx, gpu_ok):
+    """The four-wave and the one-wave kernel (LQRX_DP_WG4=0) agree to rounding on n=64."""
+    import subprocess
+    import sys
+    import os
+    code = ("import numpy as np, lqrx; from lqrx.dp import abi_to_batch; "
+            "d = lqrx.random_batch(64, 32, 24, 3, seed=9); "
+            "g = lqrx.solve_batch(abi_to_batch(d), all_P=True); "
+            "np.save(__import__('sys').argv[1], np.concatenate([g['K'].ravel(), g['P'].ravel()]))")
+    outs = []
+    for flag in ("1", "0"):
+        f = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"wg4_{flag}_{os.getpid()}.npy")
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        env = dict(os.environ, LQRX_DP_WG4=flag,
+                   PYTHONPATH=os.pathsep.join([os.path.join(root, "lqr.jl_amd"), os.environ.get("PYTHONPATH", "")]))
+        subprocess.run([sys.executable, "-c", code, f], env=env, check=True, timeout=120)
+        outs.append(np.load(f))
+        os.remove(f)
+    a, b = outs
+    assert np.abs(a - b).max() <= 1e-11 * np.abs(b).max()
+
+
+def test_dp_wg4_non_spd_sets_info(lqrx, gpu_ok):
+    from lqrx.dp import abi_to_batch
+
+    n, m, N, bt = 64, 32, 8, 3
+    d = lqrx.random_batch(n, m, N, bt, seed=13)
+    b = abi_to_batch(d)
+    b.R[1] = -100.0 * np.eye(m)
+    b.B[1] *= 1e-3
+    got = lqrx.solve_batch(b)
+    assert got["rc"] == 1
+    assert got["info"][1] == N - 1
+    assert got["info"][0] == 0 and got["info"][2] == 0
+
+
 def test_dp_p1_only(lqrx, oracle, gpu_ok):
     """p_mode 0 returns P_1 = solver.P after solve! (dynamic_programming.jl:63)."""
     got, ref = run_pair(lqrx, oracle, 32, 16, 40, 6, seed=5, all_P=False)
