@@ -1265,6 +1265,12 @@ constexpr int KF_LDS = 64 * KF_LU + 64 + KF_SCR;      // per wave: U image, vect
 #ifndef KF_INV_SWEEP
 #define KF_INV_SWEEP 0                                // 1: the round-4 leaf inverse sweep (A/B builds)
 #endif
+#ifndef KF_LEAF_UNSCALED
+#define KF_LEAF_UNSCALED 0   // 1 (A/B builds): unscaled rows, 1/d and 1/√d formed during the LDS
+                             // round trip — measured slower (fp32 157.4 vs 155.3 ms, fp64 169.1
+                             // vs 167.7 ms configs[4] KKT, profiles r05p): the extra fp64 VALU
+                             // costs more than the rsqrt latency it takes off the chain
+#endif
 
 // image of one knot (elements of T from the knot's base): tiles D, F, B, E, C (256 elements
 // each, lane-major C layout: element 4·lane + r = register r of lane `lane`), then
@@ -1740,6 +1746,25 @@ __device__ __forceinline__ int leaf_chol_inv_e(acc_t<T> &X, T *scr, T *Dg, int q
         const int gi = F64 ? (i & 3) : (i >> 2), rgi = F64 ? (i >> 2) : (i & 3);
         const T d = readlane(X[rgi], 16 * gi + i);
         if (!(d > (T)0) && i < q && !bad) bad = i + 1;
+#if KF_LEAF_UNSCALED
+        // the UNSCALED rows go out at once and 1/d, 1/√d are formed while they cross the LDS:
+        // U[i][r]·U[i][c] = x_r·(x_c/d), the E rows below take (e_i/d), row i itself e_i/√d
+        wsync();
+        ub[16 * g + c] = c > i ? X[rgi] : (T)0;
+        eb[16 * g + c] = E[rgi];
+        wsync();
+        const T id = rcp_full(d), sc = rsqrt_nr(d);
+        const T uc = ub[16 * gi + c], ec = eb[16 * gi + c];
+        T ur[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ur[r] = ub[16 * gi + Tile<T>::row(lane, r)];
+        const T tu = uc * id, te = ec * id, es = ec * sc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            X[r] = fma(-ur[r], tu, X[r]);
+            E[r] = Tile<T>::row(lane, r) == i ? es : fma(-ur[r], te, E[r]);
+        }
+#else
         const T sc = rsqrt_nr(d);
         wsync();
         ub[16 * g + c] = c > i ? X[rgi] * sc : (T)0;
@@ -1754,6 +1779,7 @@ __device__ __forceinline__ int leaf_chol_inv_e(acc_t<T> &X, T *scr, T *Dg, int q
             X[r] = fma(-ur[r], uc, X[r]);
             E[r] = Tile<T>::row(lane, r) == i ? ec : fma(-ur[r], ec, E[r]);
         }
+#endif
     }
     wsync();
 #pragma unroll
