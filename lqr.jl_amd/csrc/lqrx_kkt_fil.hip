@@ -1950,6 +1950,8 @@ LQRX_FILD_INST(6, 3, 6, 1, 6)
 LQRX_FILD_INST(4, 2, 4, 1, 4)
 LQRX_FILD_INST(5, 2, 5, 0, 5)
 LQRX_FILD_INST(7, 3, 7, 0, 7)
+LQRX_FILD_INST(6, 2, 6, 0, 6)
+LQRX_FILD_INST(8, 4, 8, 0, 8)
 // padded direct variants (layout 0, diagonal H and SOC): every smaller trajectory structure
 #define LQRX_FILP_INST(NX, M, A0, AK, AN)                                                                 \
     template __global__ void kkt_fild_kernel<Shape<NX, M, A0, AK, AN, true, true, false, true>>(const KktArgs, double *__restrict__); \
@@ -2146,6 +2148,8 @@ static bool fil_dispatch(const KktArgs &a, const int32_t *n1, const int32_t *p, 
     LQRX_FILD(4, 2, 4, 1, 4)       // DoubleIntegrator(2)
     LQRX_FILD(5, 2, 5, 0, 5)       // trajectory_structure(5, 2, N), diagonal H (the SQP problems' shape)
     LQRX_FILD(7, 3, 7, 0, 7)       // trajectory_structure(7, 3, N), diagonal H
+    LQRX_FILD(6, 2, 6, 0, 6)       // trajectory_structure(6, 2, N) (round 5)
+    LQRX_FILD(8, 4, 8, 0, 8)       // trajectory_structure(8, 4, N) (round 5)
     // any other trajectory structure up to a padded bin (layout 0; layout 1 is staged): the
     // smallest bin that holds it, its own sizes at run time (Shape PAD, Rt).  LQRX_KKT_PAD=0
     // sends them to the large-block kernels instead (A/B)

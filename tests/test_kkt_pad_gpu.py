@@ -1,6 +1,7 @@
 """GPU parity: trajectory-form KKT structures outside the compile-time shapes, on the padded
 direct kernel (kkt_fild_kernel<Shape<…, PAD>>, lqrx_kkt_fil.hip) — blocks zero-padded in
-registers up to a bin (4,2,4,1,4) / (6,3,6,1,6) / (8,4,8,1,8), the structure's own sizes at run time.
+registers up to a bin (4,2,4,1,4) / (6,3,6,1,6) / (8,4,8,1,8), the structure's own sizes at run time
+— and round 5's exact direct shapes for trajectory_structure(6, 2, N) and (8, 4, N).
 
 Reference: the block structure ConstraintBlocks builds (conblocks.jl:403-425) for any (n, m)
 and stage constraints; the solve is cholesky_solver.jl:166-236 on it.  Oracle: oracle/
@@ -49,11 +50,12 @@ CASES = [
     (4, 2, 6, "stage", 33),
     (3, 2, 9, "nogoal", 70),
     (5, 1, 31, "traj", 65),
-    (6, 2, 101, "traj", 96),
+    (6, 2, 101, "traj", 96),             # exact direct shape (6,2,6,0,6) since round 5
     (6, 3, 40, "traj", 17),
     (5, 3, 12, "stage", 40),
     (6, 1, 4, "nogoal", 9),
-    (8, 4, 21, "traj", 66),              # bin (8,4,8,1,8)
+    (8, 4, 21, "traj", 66),              # exact direct shape (8,4,8,0,8) since round 5
+    (8, 4, 13, "stage", 33),             # bin (8,4,8,1,8)
     (7, 2, 12, "stage", 31),
     (8, 3, 5, "nogoal", 5),
 ]
@@ -78,12 +80,29 @@ def test_kkt_padded_layout1_staged(lqrx, gpu_ok):
     """Layout 1 (SoA) of a padded structure: staged to layout 0, bit-identical results."""
     import lqrx.kkt as K
 
-    st = K.trajectory_structure(6, 2, 33)
+    st = K.trajectory_structure(5, 1, 33)          # padded bin (6,3,6,1,6)
     pb = K.random_kkt(st, 70, seed=5, h_mode=2)
     a = K.kkt_solve(pb, layout=0)
     b = K.kkt_solve(pb, layout=1)
     assert a["rc"] == 0 and b["rc"] == 0
     assert np.array_equal(a["dz"], b["dz"]) and np.array_equal(a["lam"], b["lam"])
+
+
+@pytest.mark.parametrize("n,m,N,batch", [(6, 2, 37, 70), (8, 4, 29, 65)])
+@pytest.mark.parametrize("ginv", [1, 0])
+def test_kkt_exact_traj_shapes_layouts(lqrx, gpu_ok, n, m, N, batch, ginv):
+    """Round 5's exact direct shapes (6,2,6,0,6) and (8,4,8,0,8) — trajectory_structure(6, 2, N)
+    and (8, 4, N) — in both ABI layouts (layout 1 native, SoA) against the oracle."""
+    import lqrx.kkt as K
+
+    st = K.trajectory_structure(n, m, N)
+    pb = K.random_kkt(st, batch, seed=70 + n + N + ginv, h_mode=2)
+    ref = _ref(st, pb, ginv)
+    for layout in (0, 1):
+        got = K.kkt_solve(pb, ginv=ginv, layout=layout)
+        assert got["rc"] == 0 and (got["info"] == 0).all()
+        assert rel(got["dz"], ref["dz"].reshape(batch, -1)) <= TOL
+        assert rel(got["lam"], ref["lam"].reshape(batch, -1)) <= TOL
 
 
 def test_kkt_padded_matches_large_block_path(lqrx, gpu_ok, tmp_path):
@@ -116,7 +135,8 @@ def test_kkt_padded_matches_large_block_path(lqrx, gpu_ok, tmp_path):
 DENSE = [
     ("di3", None, None, 101, 50),        # DoubleIntegrator(3): exact direct shape (6,3,6,1,6)
     ("di2", None, None, 12, 37),         # DoubleIntegrator(2): exact (4,2,4,1,4)
-    ("traj", 6, 2, 101, 40),             # padded bin (6,3,6,1,6)
+    ("traj", 6, 2, 101, 40),             # exact (6,2,6,0,6)
+    ("traj", 5, 1, 41, 40),              # padded bin (6,3,6,1,6)
     ("traj", 5, 2, 31, 65),              # exact (5,2,5,0,5)
     ("traj", 4, 1, 21, 70),              # cartpole's shape: the LDS-staged FIL kernel (diagonal only)
     ("stage", 3, 2, 9, 20),              # padded bin (4,2,4,1,4)
