@@ -60,6 +60,9 @@ struct KktArgs {
     // runtime (n̄, m, P0, PK, PN) of a trajectory-form structure solved on a padded compile-time
     // shape (lqrx_kkt_fil.hip, Shape<…, PAD>); unused otherwise
     int32_t rt[5];
+    // live trajectories per 64-lane wave of the direct FIL kernel (lqrx_kkt_fil.hip kkt_fild_kernel,
+    // layout 0; set by its launcher): 64, or 32 on small batches so that twice the waves run
+    int32_t lpw;
 };
 
 hipError_t kkt_launch(const KktArgs &a, hipStream_t s);

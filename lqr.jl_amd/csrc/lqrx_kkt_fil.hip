@@ -1791,10 +1791,13 @@ __global__ __launch_bounds__(64) void kkt_fild_kernel(const KktArgs a, double *_
     using L = typename S::L;
     __shared__ __attribute__((aligned(16))) double ost[S::SOA ? 1 : 64 * (S::WOUT + S::LOUT)];
     const int N = a.N;                                          // ≥ 4 (host-checked)
-    const int64_t t0 = (int64_t)blockIdx.x * 64;
+    // LPW live trajectories per wave (fild_lpw: 32 on small layout-0 batches, the other lanes
+    // shadow the last live one); layout 1 keeps 64 (gld's row base)
+    const int LPW = S::SOA ? 64 : a.lpw;
+    const int64_t t0 = (int64_t)blockIdx.x * LPW;
     Ctx<S> c;
     c.lane = threadIdx.x;
-    c.nlive = (int)(a.batch - t0 < 64 ? a.batch - t0 : 64);
+    c.nlive = (int)(a.batch - t0 < LPW ? a.batch - t0 : LPW);
     c.live = c.lane < c.nlive;
     const int64_t t = t0 + (c.live ? c.lane : c.nlive - 1);     // dead lanes re-read a live one
     c.bS = scratch + (int64_t)blockIdx.x * N * S::SLOT * 64;
@@ -1904,9 +1907,21 @@ __global__ __launch_bounds__(64) void kkt_fild_kernel(const KktArgs a, double *_
     if (a.info && c.live) a.info[t0 + c.lane] = info;
 }
 
+// live trajectories per wave of the direct kernel.  A/B (LQRX_FILD_LPW=32: a layout-0 batch
+// ≤ 32768 runs 32 per wave, twice the waves) measured slower at B = 16384 — (6,2,101) 2.24 →
+// 2.60 ms, (8,4,101) 6.24 → 7.75, (5,2,101) 1.38 → 1.54, DoubleIntegrator(3) 2.64 → 2.91
+// (profiles/r05/r): the kernel is bound by its waves' instruction issue, not by loads in flight
+#ifndef LQRX_FILD_LPW
+#define LQRX_FILD_LPW 64
+#endif
+template <class S> int fild_lpw(const KktArgs &a)
+{
+    return (!S::SOA && a.batch <= 32768) ? LQRX_FILD_LPW : 64;
+}
 template <class S> size_t slab_bytes(const KktArgs &a)
 {
-    const size_t Bp = ((size_t)a.batch + 63) & ~(size_t)63;   // wave-major slab, 64 lanes/wave
+    const int lpw = fild_lpw<S>(a);   // (also the LDS-ring kernel's bound at 64: ≥ its need)
+    const size_t Bp = (((size_t)a.batch + lpw - 1) / lpw) * 64;   // wave-major slab, 64 lanes/wave
     // (+1 KiB: the backward slab DMA of the last knot may read up to 512 B past its chunk)
     return Bp * (size_t)a.N * S::SLOT * sizeof(double) + 1024;
 }
@@ -1917,11 +1932,15 @@ hipError_t launch(const KktArgs &a, hipStream_t s)
     Scratch sc;
     hipError_t e = sc.get(a, slab_bytes<S>(a), s);
     if (e != hipSuccess) return e;
-    dim3 grid((unsigned)((a.batch + 63) / 64)), block(64);
-    if constexpr (DIRECT)
-        hipLaunchKernelGGL((kkt_fild_kernel<S>), grid, block, 0, s, a, (double *)sc.p);
-    else
+    if constexpr (DIRECT) {
+        KktArgs b = a;
+        b.lpw = fild_lpw<S>(a);
+        dim3 grid((unsigned)((a.batch + b.lpw - 1) / b.lpw)), block(64);
+        hipLaunchKernelGGL((kkt_fild_kernel<S>), grid, block, 0, s, b, (double *)sc.p);
+    } else {
+        dim3 grid((unsigned)((a.batch + 63) / 64)), block(64);
         hipLaunchKernelGGL((kkt_fil_kernel<S>), grid, block, 0, s, a, (double *)sc.p);
+    }
     e = hipGetLastError();
     hipError_t ef = sc.release(s);
     return e != hipSuccess ? e : ef;
