@@ -112,6 +112,18 @@ recipe_kkt() {   # the large-block KKT path (configs[4]'s KKT half): its tests, 
     sub t pytest tests/test_kkt_big_gpu.py tests/test_full_size_gpu.py tests/test_kkt_pad_gpu.py &&
     sub kkt32 kt $CFG4KKT && sub kkt64 kt $CFG4KKT64
 }
+recipe_r5a() {   # round-5 closing set, part 1: suite + smoke, the DP lines and cfg2/cfg3 with traffic
+    sub t tests && sub cfg4 prof && sub cfg5 prof --n 64 --m 32 --N 512 --batch 8192 --dtype f32 &&
+    sub dp64 prof --n 64 --m 32 --N 512 --batch 8192 --dtype f64 && sub cfg2 prof --workload cartpole &&
+    KREGEX=dp_quad PMC="$SQ1;$SQ2" sub cfg2sq pmc --workload cartpole &&
+    sub cfg3 prof --workload kkt && sub cfg3soa prof --workload kkt --kkt-layout 1
+}
+recipe_r5b() {   # part 2: the large-block / workgroup / small-structure KKT lines with traffic + SQ
+    sub kkt32 prof $CFG4KKT && KREGEX=kb_ PMC="$SQ1;$SQ2" sub kkt32sq pmc $CFG4KKT &&
+    sub kkt64 prof $CFG4KKT64 && sub wg96 prof $WG96 &&
+    sub t62 prof --workload kkt --kkt-structure dense --n 6 --m 2 --N 101 --batch 16384 --dtype f64 &&
+    sub t84 prof --workload kkt --kkt-structure dense --n 8 --m 4 --N 101 --batch 16384 --dtype f64
+}
 recipe_list() { declare -F | sed -n 's/^declare -f recipe_//p'; }
 
 case "$MODE" in
