@@ -124,6 +124,14 @@ recipe_r5b() {   # part 2: the large-block / workgroup / small-structure KKT lin
     sub t62 prof --workload kkt --kkt-structure dense --n 6 --m 2 --N 101 --batch 16384 --dtype f64 &&
     sub t84 prof --workload kkt --kkt-structure dense --n 8 --m 4 --N 101 --batch 16384 --dtype f64
 }
+recipe_r5lines() {   # the closing lines again, now that traffic_r05.json holds their HEAD entries
+    sub cfg4 bench && sub cfg5 bench --n 64 --m 32 --N 512 --batch 8192 --dtype f32 &&
+    sub dp64 bench --n 64 --m 32 --N 512 --batch 8192 --dtype f64 && sub cfg2 bench --workload cartpole &&
+    sub cfg3 bench --workload kkt && sub cfg3soa bench --workload kkt --kkt-layout 1 &&
+    sub kkt32 bench $CFG4KKT && sub kkt64 bench $CFG4KKT64 && sub wg96 bench $WG96 &&
+    sub t62 bench --workload kkt --kkt-structure dense --n 6 --m 2 --N 101 --batch 16384 --dtype f64 &&
+    sub t84 bench --workload kkt --kkt-structure dense --n 8 --m 4 --N 101 --batch 16384 --dtype f64
+}
 recipe_list() { declare -F | sed -n 's/^declare -f recipe_//p'; }
 
 case "$MODE" in
