@@ -50,7 +50,7 @@ def dp_bytes_per_traj(n, m, N, s=8, tv=False):
     return rd * s + ((N - 1) * m * n + N * n + (N - 1) * m + n * n) * s
 
 
-def _dp_kernel_name(n, m, bt, tv, lin=False):
+def _dp_kernel_name(n, m, bt, tv, lin=False, f64=False):
     """Which DP kernel lqrx_dp_solve dispatches to (mirrors dp_launch / dp_lane_launch)."""
     if n <= 4 and m <= 4:
         small = os.environ.get("LQRX_DP_SMALL", "")
@@ -61,6 +61,8 @@ def _dp_kernel_name(n, m, bt, tv, lin=False):
         return "dp_quad_kernel" if quad else "dp_lane_kernel"
     if n > 64 or m > 32:
         return "dp_big_kernel"      # workgroup per trajectory, past the register tiles
+    if f64 and n == 64 and m in (16, 32) and not tv and not lin and os.environ.get("LQRX_DP_WG4", "") != "0":
+        return "dp_wg4_kernel"      # four waves per trajectory (lqrx_dp.hip, round 5)
     return "dp_riccati_kernel"
 
 
@@ -837,7 +839,7 @@ def main(argv=None):
                                            + ("_lin" if args.linear else ""), args.traffic_json)
             roof = {"bound": "mfma", "achieved": achieved, "peak": peak,
                     "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
-                    "kernel": _dp_kernel_name(n, m, bt, args.tv or args.linear),
+                    "kernel": _dp_kernel_name(n, m, bt, args.tv or args.linear, f64=f64),
                     "kernel_ms": kern_ms,
                     "flops_per_traj": dp_flops_per_traj(n, m, N),
                     "alg_bytes_per_launch": dp_bytes_per_traj(n, m, N, 8 if f64 else 4, args.tv) * bt}
@@ -870,7 +872,7 @@ def main(argv=None):
                 # each running a serial N-knot chain; report that beside the HBM fraction
                 ab = dp_bytes_per_traj(n, m, N, 8 if f64 else 4, False) * bt
                 hbm = ab / (kern_ms * 1e-3) / 1e9
-                kname = _dp_kernel_name(n, m, bt, False, args.linear)
+                kname = _dp_kernel_name(n, m, bt, False, args.linear, f64=f64)
                 lanes = {"dp_hex_kernel": 16, "dp_quad_kernel": 4}.get(kname, 1)
                 waves = -(-bt * lanes // 64)
                 roof = {"bound": "hbm", "achieved": hbm, "peak": PEAK_HBM_GBS, "unit": "GB/s",
