@@ -2339,11 +2339,7 @@ __device__ __forceinline__ void fu_schur2(const Kn &q1, const T *Y1, const T *hg
     constexpr int KU_PF = ku_pf<T>();
     T f1[KU_PF][NB], f2[KU_PF][NT], h1[KU_PF], c1[KU_PF], h2[KU_PF], c2[KU_PF];
     auto load = [&](int s, T (&a1)[NB], T (&a2)[NT], T &hh1, T &gg1, T &hh2, T &gg2) __attribute__((always_inline)) {
-#ifdef KU_ABL_CACHED
-        const int o1 = (s & 1) * so1, o2 = (s & 1) * so2;    // timing ablation only: two slices re-read (cache-resident)
-#else
         const int o1 = s * so1, o2 = s * so2;
-#endif
         const __amdgpu_buffer_rsrc_t r1 =
             __builtin_amdgcn_make_buffer_rsrc((void *)(yb1 + o1), (short)0, max(yn1 - o1, 0), 0x00020000);
         const __amdgpu_buffer_rsrc_t r2 =
