@@ -910,11 +910,14 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
 template <typename T, int MT>
 struct Wg4Cfg {
     static constexpr int NT = 4, NP = 64, MP = 16 * MT;
-    static constexpr int PL = NP + 2;                    // P image column stride (bank spread)
-    static constexpr int CS = MP + 2;                    // PB / E / G images, aug sweep
+    // odd column strides: the compiler pairs a tile's rows into ds_read2_b64 / ds_write_b64, whose
+    // 16-lane groups bank by (a/4) mod 32 — at an even stride (NP + 2) columns c and c + 8 of a tile
+    // shared banks (2-way; SQ_LDS_BANK_CONFLICT ≈ a quarter of the kernel's cycles)
+    static constexpr int PL = NP + 1;                    // P, Q, B images
+    static constexpr int CS = MP + 1;                    // PB / E / G images, aug sweep
     static constexpr int P_EL = NP * PL;
     static constexpr int AUG = 2 * MP * CS + 64 + MP;   // [E | I] sweep image + row/rinv
-    static constexpr int PB_EL = (MP * CS > AUG ? MP * CS : AUG) > NP * CS ? (MP * CS > AUG ? MP * CS : AUG) : NP * CS;
+    static constexpr int PB_EL = (MP * PL > AUG ? MP * PL : AUG);   // PB (NP × MP, stride PL) | the sweep image
     static constexpr int E_EL = MP * CS, G_EL = NP * CS;
     static constexpr int B_EL = MP * PL;                                 // B image (NP × MP)
     static constexpr int LDS = 2 * P_EL + B_EL + PB_EL + E_EL + G_EL + 8;   // P, Q, B images
@@ -1018,14 +1021,14 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
             for (int j = 0; j < MT; ++j) wg4_mtn<T>(PB[j], Pw, Bt(kk, j));
         }
 #pragma unroll
-        for (int j = 0; j < MT; ++j) wg4_tstore(PBim + 16 * w + 16 * j * NP, NP, PB[j], lane);
+        for (int j = 0; j < MT; ++j) wg4_tstore(PBim + 16 * w + 16 * j * PL, PL, PB[j], lane);
         __syncthreads();                                   // B1: PB image complete, P image read
         // :39 E tile, :41 G[:, w]
         if (w < MT * MT) {
             acc Et = Rw;
 #pragma unroll
             for (int kk = 0; kk < NT; ++kk) {
-                const acc Y = wg4_tload(PBim + 16 * kk + 16 * ej * NP, NP, lane);               // PB[kk][ej]
+                const acc Y = wg4_tload(PBim + 16 * kk + 16 * ej * PL, PL, lane);               // PB[kk][ej]
                 wg4_mtn<T>(Et, Bt(kk, ei), Y);
             }
             wg4_tstore(Eim + 16 * ei + 16 * ej * CS, CS, Et, lane);
