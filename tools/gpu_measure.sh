@@ -132,6 +132,12 @@ recipe_r5lines() {   # the closing lines again, now that traffic_r05.json holds 
     sub t62 bench --workload kkt --kkt-structure dense --n 6 --m 2 --N 101 --batch 16384 --dtype f64 &&
     sub t84 bench --workload kkt --kkt-structure dense --n 8 --m 4 --N 101 --batch 16384 --dtype f64
 }
+recipe_r5dp() {   # after a change in lqrx_dp.hip: its suite files, then the three DP lines with traffic
+    sub t pytest tests/test_dp_gpu.py tests/test_dp_linear_gpu.py tests/test_layout_gpu.py &&
+    sub cfg4 prof && sub cfg5 prof --n 64 --m 32 --N 512 --batch 8192 --dtype f32 &&
+    sub dp64 prof --n 64 --m 32 --N 512 --batch 8192 --dtype f64 &&
+    KREGEX=dp_wg4 PMC="$SQ1;$SQ2" sub dp64sq pmc --n 64 --m 32 --N 512 --batch 8192 --dtype f64
+}
 recipe_list() { declare -F | sed -n 's/^declare -f recipe_//p'; }
 
 case "$MODE" in
