@@ -59,6 +59,9 @@
 #ifndef LQRX_DP_WG4
 #define LQRX_DP_WG4 1         // fp64 n = 64: the four-wave kernel (A/B builds: 0 = one wave)
 #endif
+#ifndef LQRX_WG4_AIMG
+#define LQRX_WG4_AIMG 1       // four-wave kernel: A in an LDS image, only A[:, w] in registers (0: A/B)
+#endif
 #ifndef LQRX_DP_ROLL_FULL
 #define LQRX_DP_ROLL_FULL 1   // exact tile grids: the register-streamed rollout (A/B builds: 0)
 #endif
@@ -920,7 +923,11 @@ struct Wg4Cfg {
     static constexpr int PB_EL = (MP * PL > AUG ? MP * PL : AUG);   // PB (NP × MP, stride PL) | the sweep image
     static constexpr int E_EL = MP * CS, G_EL = NP * CS;
     static constexpr int B_EL = MP * PL;                                 // B image (NP × MP)
+#if LQRX_WG4_AIMG
+    static constexpr int LDS = 3 * P_EL + B_EL + PB_EL + E_EL + G_EL + 8;   // P, Q, A, B images
+#else
     static constexpr int LDS = 2 * P_EL + B_EL + PB_EL + E_EL + G_EL + 8;   // P, Q, B images
+#endif
 };
 // row tile of wave w's t-th P_ tile (column tile w), −1: none
 __host__ __device__ constexpr int wg4_pn_row(int w, int t)
@@ -961,7 +968,12 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
     __shared__ T lds[C::LDS];
     T *Pim = lds, *Qim = Pim + C::P_EL, *Bim = Qim + C::P_EL, *PBim = Bim + C::B_EL, *Eim = PBim + C::PB_EL;
     T *Gim = Eim + C::E_EL;
+#if LQRX_WG4_AIMG
+    T *Aim = Gim + C::G_EL;              // A (the P_ rows' A columns are read from here)
+    int *flag = (int *)(Aim + C::P_EL);
+#else
     int *flag = (int *)(Gim + C::G_EL);
+#endif
     T *aug = PBim;                       // the exact sweep reuses the PB image (read before it)
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -974,9 +986,14 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
     const T *Qb = (const T *)a.Q + b * nn, *Rb = (const T *)a.R + b * mm;
 
     // time-invariant register operands
-    acc Ar[3][NT], Rw = acc{0, 0, 0, 0};
+#if LQRX_WG4_AIMG
+    constexpr int NAR = 1;               // A[:, w] in registers, the other P_ rows' columns from LDS
+#else
+    constexpr int NAR = 3;
+#endif
+    acc Ar[NAR][NT], Rw = acc{0, 0, 0, 0};
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
+    for (int t = 0; t < NAR; ++t) {
         const int i = wg4_pn_row(w, t) < 0 ? 0 : wg4_pn_row(w, t);
 #pragma unroll
         for (int k = 0; k < NT; ++k) Ar[t][k] = wg4_tload(Ab + 16 * k + (size_t)16 * i * NP, NP, lane);  // A[k][i]
@@ -990,6 +1007,9 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
         Qim[(e % NP) + (e / NP) * PL] = Qb[e];
     }
     for (int e = tid; e < NP * MP; e += 256) Bim[(e % NP) + (e / NP) * PL] = Bb[e];
+#if LQRX_WG4_AIMG
+    for (int e = tid; e < NP * NP; e += 256) Aim[(e % NP) + (e / NP) * PL] = Ab[e];
+#endif
     T *Pall = a.p_all ? (T *)a.P + (size_t)b * nn * N : nullptr;
     T *Kb = (T *)a.K + (size_t)b * (size_t)(N - 1) * nm;
     int info = 0;
@@ -1117,7 +1137,14 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
             if (i < 0) continue;
             acc Pn = wg4_tload(Qim + 16 * i + 16 * w * PL, PL, lane);                        // Q[i][w]
 #pragma unroll
-            for (int kk = 0; kk < NT; ++kk) wg4_mtn<T>(Pn, Ar[t][kk], PA[kk]);
+            for (int kk = 0; kk < NT; ++kk) {
+#if LQRX_WG4_AIMG
+                const acc At = t == 0 ? Ar[0][kk] : wg4_tload(Aim + 16 * kk + 16 * i * PL, PL, lane);  // A[kk][i]
+                wg4_mtn<T>(Pn, At, PA[kk]);
+#else
+                wg4_mtn<T>(Pn, Ar[t][kk], PA[kk]);
+#endif
+            }
 #pragma unroll
             for (int c = 0; c < MT; ++c)
                 wg4_mtn<T, true>(Pn, wg4_tload(Gim + 16 * c + 16 * i * CS, CS, lane), Kt[c]);
