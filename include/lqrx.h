@@ -38,13 +38,14 @@
 extern "C" {
 #endif
 
-#define LQRX_ABI_VERSION 4   /* 2: layout 1 (DP, KKT), lqrx_sqp_* (models, stage constraints);
+#define LQRX_ABI_VERSION 5   /* 2: layout 1 (DP, KKT), lqrx_sqp_* (models, stage constraints);
                                 3: lqrx_dp_solve_linear[_host] (linear cost terms), and
                                    dtype LQRX_F32 on the KKT path (large-block kernels);
                                 4: lqrx_scratch_trim (release the library's pooled scratch);
                                    KKT blocks past 64 rows (up to 512, w up to 1024);
                                    KKT layout 1 for every structure (staged);
-                                   lqrx_dp_compute_ctg[_host] (per-knot surface) */
+                                   lqrx_dp_compute_ctg[_host] (per-knot surface);
+                                5: lqrx_*_host_devices (one call sharded over GPUs) */
 
 #define LQRX_F64 0
 #define LQRX_F32 1
@@ -118,8 +119,8 @@ int lqrx_dp_solve_host(const lqrx_dp_desc *desc, const void *A, const void *B, c
  * The n ≥ 5 and n ≤ 4 kernel families use the symmetric fast form (P_ = Q + AᵀPA − GᵀK on the
  * lower triangle, mirrored), the n > 64 workgroup kernel the reference's operation order, so
  * for a non-symmetric P or Q the result depends on the family.  The host wrappers (Python
- * lqrx.compute_ctg*, Julia compute_ctg!) reject P or Q whose asymmetry exceeds 1e-10 of the
- * matrix's largest entry. */
+ * lqrx.compute_ctg*, Julia compute_ctg!) reject P or Q whose asymmetry exceeds
+ * max(1e-10, 100 ulp of the dtype) of the matrix's largest entry (Q only when P_ is asked). */
 int lqrx_dp_compute_ctg(const lqrx_dp_desc *desc, const void *A, const void *B, const void *Q,
                         const void *R, const void *P, void *K, void *P_, int32_t *info, void *stream);
 int lqrx_dp_compute_ctg_host(const lqrx_dp_desc *desc, const void *A, const void *B, const void *Q,
@@ -240,6 +241,34 @@ int lqrx_kkt_solve_ws(const lqrx_kkt_desc *desc, const void *Y, const void *y, c
 /* sizes (elements per trajectory) of the packed KKT buffers, for allocation */
 int lqrx_kkt_sizes(const lqrx_kkt_desc *desc, int64_t *nY, int64_t *ny, int64_t *nH,
                    int64_t *ng, int64_t *nlam);
+
+/* ------------------------------------------------------------------------------------
+ * Multi-device host entries — SURVEY.md §8(e): "the batch of independent problems shards
+ * embarrassingly across the 8 GPUs of one node".  Same arguments and results as the *_host
+ * call they extend (lqrx_dp_solve_host, lqrx_dp_solve_linear_host, lqrx_kkt_solve_host; the
+ * reference's solve! per shard, dynamic_programming.jl:54-72 / cholesky_solver.jl:166-182),
+ * plus devices[ndev]: HIP device ordinals, repeats allowed (two shards on one GPU).  The batch
+ * is split into ndev contiguous shards (trajectories [b0, b0 + nb), the first batch mod ndev
+ * shards one longer); each runs concurrently on its own thread and non-blocking stream on its
+ * device: its slice of every input is copied in (layout 1: the strided slice of every element
+ * row), solved by the single-device path, and K/P/X/U (δz/λ) and info land in the caller's
+ * host arrays at the shard's offset.  No collective and no peer traffic: the gather IS the
+ * D2H into the caller's arrays.  Every trajectory is solved exactly as by the single-device
+ * call, so results are bit-identical (n ≤ 4 DP: when the shard batches pick the same quad /
+ * lane kernel as the whole batch, ≤ 16384 trajectories per shard or > 16384 in both).
+ * Returns -13 / -14 (dp), -14 / -15 (dp linear), -9 / -10 (kkt) for a NULL devices / an
+ * entry that is not a device, and ndev < 1; a failing shard's status, with its device and
+ * trajectory range in lqrx_last_error; 1 if any trajectory has info != 0. */
+int lqrx_dp_solve_host_devices(const lqrx_dp_desc *desc, const void *A, const void *B, const void *Q,
+                               const void *R, const void *Qf, const void *x0, void *K, void *P,
+                               void *X, void *U, int32_t *info, const int32_t *devices, int32_t ndev);
+int lqrx_dp_solve_linear_host_devices(const lqrx_dp_desc *desc, const void *A, const void *B,
+                                      const void *Q, const void *R, const void *Qf, const void *x0,
+                                      const lqrx_dp_linear *lin, void *K, void *P, void *X, void *U,
+                                      int32_t *info, const int32_t *devices, int32_t ndev);
+int lqrx_kkt_solve_host_devices(const lqrx_kkt_desc *desc, const void *Y, const void *y,
+                                const void *H, const void *g, void *dz, void *lam, int32_t *info,
+                                const int32_t *devices, int32_t ndev);
 
 /* ------------------------------------------------------------------------------------
  * Batched trajectory-optimisation SQP around the KKT path: per

@@ -89,23 +89,37 @@ DPSolver{T}(n::Integer, m::Integer, N::Integer) where T = DPSolver{T}(n, m, N, z
 DPSolver(b::LQRBatch{T}) where T = DPSolver{T}(size(b.B, 1), size(b.B, 2), b.N)
 
 """
-    solve!(sol, solver, prob::LQRBatch)
+    solve!(sol, solver, prob::LQRBatch; devices=nothing)
 
 Batched Riccati backward pass + forward rollout on the GPU (host arrays in, host arrays
 out; lqrx_dp_solve_host).  Same outputs as src/dynamic_programming.jl:54-72 for every
 problem in the batch; returns 1 if some trajectory had a non-SPD R + BᵀPB (see sol.info).
+`devices = 0:7` shards the batch over those GPUs in the same call (lqrx_dp_solve_host_devices:
+contiguous shards, one thread + stream per device, results bit-identical to one device).
 """
-function solve!(sol::LQRSolution{T}, solver::DPSolver{T}, prob::LQRBatch{T}) where T
+function solve!(sol::LQRSolution{T}, solver::DPSolver{T}, prob::LQRBatch{T};
+                devices::Union{Nothing,AbstractVector{<:Integer}}=nothing) where T
     n, m, N = solver.n, solver.m, solver.N
     batch = size(prob.A, 3)
     all_P = ndims(sol.P) == 4
     d = Ref(DpDesc(n, m, N, dtypecode(T), batch, 0, all_P ? 1 : 0, 0, 0))
-    GC.@preserve prob sol begin
-        rc = ccall((:lqrx_dp_solve_host, liblqrx), Cint,
-                   (Ref{DpDesc}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T},
-                    Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{Int32}),
-                   d, prob.A, prob.B, prob.Q, prob.R, prob.Qf, prob.x0,
-                   sol.Kdata, sol.P, sol.Xdata, sol.Udata, sol.info)
+    if devices === nothing
+        GC.@preserve prob sol begin
+            rc = ccall((:lqrx_dp_solve_host, liblqrx), Cint,
+                       (Ref{DpDesc}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T},
+                        Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{Int32}),
+                       d, prob.A, prob.B, prob.Q, prob.R, prob.Qf, prob.x0,
+                       sol.Kdata, sol.P, sol.Xdata, sol.Udata, sol.info)
+        end
+    else
+        dv = Vector{Int32}(devices)
+        GC.@preserve prob sol dv begin
+            rc = ccall((:lqrx_dp_solve_host_devices, liblqrx), Cint,
+                       (Ref{DpDesc}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T},
+                        Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{Int32}, Ptr{Int32}, Int32),
+                       d, prob.A, prob.B, prob.Q, prob.R, prob.Qf, prob.x0,
+                       sol.Kdata, sol.P, sol.Xdata, sol.Udata, sol.info, dv, Int32(length(dv)))
+        end
     end
     return check(rc)
 end
@@ -158,14 +172,16 @@ The reference's per-knot surface (src/dynamic_programming.jl:34-52, called by te
 on `sol.K[1]`): K = (R + BᵀPB)⁻¹BᵀPA from P = solver.P, and for compute_ctg! also
 solver.P_ = Q + AᵀPA − AᵀPB·K — lqrx_dp_compute_ctg_host (the same kernels as solve!, on a
 2-knot problem with Qf = P).  P = solver.P and Q must be symmetric (the kernels' symmetric
-fast form, include/lqrx.h): an asymmetry above 1e-10 of the largest entry throws.
+fast form, include/lqrx.h): an asymmetry above max(1e-10, 100 eps(T)) of the largest entry
+throws (Q is not checked by compute_gain!, where it never enters K).
 """
 function compute_ctg!(K::AbstractMatrix{T}, solver::DPSolver{T}, prob::LQRProblem{n,m,T};
                       gain_only::Bool=false) where {n,m,T}
     dense(M, r, c) = reshape(Matrix{T}(M), r, c)
     A, B, Q, R = dense(prob.A, n, n), dense(prob.B, n, m), dense(prob.Q, n, n), dense(prob.R, m, m)
-    for (nm, M) in (("P", solver.P), ("Q", Q))
-        maximum(abs, M - transpose(M); init=zero(T)) > 1e-10 * max(maximum(abs, M; init=zero(T)), floatmin(T)) &&
+    rtol = max(1e-10, 100 * eps(T))            # never tighter than 100 ulp of T (fp32 AᵀPA)
+    for (nm, M) in (gain_only ? (("P", solver.P),) : (("P", solver.P), ("Q", Q)))
+        maximum(abs, M - transpose(M); init=zero(T)) > rtol * max(maximum(abs, M; init=zero(T)), floatmin(T)) &&
             throw(ArgumentError("compute_ctg!: $nm must be symmetric (lqrx_dp_compute_ctg precondition)"))
     end
     Kd = Matrix{T}(undef, m, n)
@@ -228,12 +244,14 @@ end
 One CholeskySolver._solve! (src/cholesky_solver.jl:166-182) per trajectory: Y, y, H, g are
 the per-knot ConstraintBlock.Y / .y, cost Hessian and gradient, packed (column-major
 blocks, concatenated over knots) with the batch as the last dimension.  ginv=0 is the
-second_order_correction! variant (:254-273).
+second_order_correction! variant (:254-273).  `devices = 0:7` shards the batch over those GPUs
+in the same call (lqrx_kkt_solve_host_devices).
 """
 function kkt_solve!(dz::Matrix{T}, lam::Matrix{T}, info::Vector{Int32},
                     n1::Vector{Int32}, p::Vector{Int32}, n2::Vector{Int32}, w::Vector{Int32},
                     Y::Matrix{T}, y::Matrix{T}, H::Matrix{T}, g::Matrix{T};
-                    h_mode::Integer=2, ginv::Integer=1) where {T<:Union{Float64,Float32}}
+                    h_mode::Integer=2, ginv::Integer=1,
+                    devices::Union{Nothing,AbstractVector{<:Integer}}=nothing) where {T<:Union{Float64,Float32}}
     # Float32 runs the large-block MFMA kernels (blocks up to 64 rows, w up to 128 —
     # BASELINE configs[4]'s banded KKT) and the workgroup-per-trajectory kernel past them;
     # every H mode and ginv, blocks up to 512 rows and w up to 1024 in either precision
@@ -241,9 +259,16 @@ function kkt_solve!(dz::Matrix{T}, lam::Matrix{T}, info::Vector{Int32},
     GC.@preserve n1 p n2 w Y y H g dz lam info begin
         d = Ref(KktDesc(length(n1), dtypecode(T), batch, pointer(n1), pointer(p), pointer(n2), pointer(w),
                         h_mode, ginv, 0, 0))
-        rc = ccall((:lqrx_kkt_solve_host, liblqrx), Cint,
-                   (Ref{KktDesc}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{Int32}),
-                   d, Y, y, H, g, dz, lam, info)
+        if devices === nothing
+            rc = ccall((:lqrx_kkt_solve_host, liblqrx), Cint,
+                       (Ref{KktDesc}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{Int32}),
+                       d, Y, y, H, g, dz, lam, info)
+        else
+            dv = Vector{Int32}(devices)
+            rc = GC.@preserve dv ccall((:lqrx_kkt_solve_host_devices, liblqrx), Cint,
+                       (Ref{KktDesc}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{T}, Ptr{Int32}, Ptr{Int32}, Int32),
+                       d, Y, y, H, g, dz, lam, info, dv, Int32(length(dv)))
+        end
     end
     return check(rc)
 end

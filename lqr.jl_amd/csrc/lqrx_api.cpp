@@ -939,6 +939,234 @@ int lqrx_make_random_dp(int32_t n, int32_t m, int64_t batch, int64_t traj0, uint
 
 } // extern "C"
 
+// ------------------------------------------------------------------ multi-device host entries
+// SURVEY §8(e) through the drop-in boundary: the batch split into contiguous shards, one per
+// entry of devices[] (repeats allowed: two shards on one GPU), each shard on its own thread with
+// its own non-blocking stream on its device — H2D of its slice, the single-device solve, D2H into
+// the caller's arrays at the shard's offset.  Every trajectory is solved exactly as by the
+// single-device call (one wave / lane / workgroup per trajectory, no cross-trajectory
+// arithmetic), so the outputs are bit-identical whenever the shards select the same kernel as
+// the whole batch (the n ≤ 4 quad/lane choice depends on the batch, see dp_lane.hip use_quad).
+namespace {
+struct Shard {
+    int64_t b0 = 0, nb = 0;
+    int dev = 0;
+    int st = 0;
+    std::string err;
+};
+
+// shard boundaries: contiguous, the first (B mod ndev) shards one trajectory longer
+std::vector<Shard> make_shards(int64_t B, const int32_t *devices, int32_t ndev)
+{
+    std::vector<Shard> sh((size_t)ndev);
+    const int64_t q = B / ndev, r = B % ndev;
+    int64_t b0 = 0;
+    for (int i = 0; i < ndev; ++i) {
+        sh[i].b0 = b0;
+        sh[i].nb = q + (i < r ? 1 : 0);
+        sh[i].dev = devices[i];
+        b0 += sh[i].nb;
+    }
+    return sh;
+}
+
+int check_devices(const int32_t *devices, int32_t ndev, int ai_dev, int ai_ndev)
+{
+    if (ndev < 1) return set_err(-ai_ndev, "ndev must be >= 1 (got %d)", ndev);
+    if (!devices) return set_err(-ai_dev, "devices is NULL");
+    int cnt = 0;
+    const hipError_t e = hipGetDeviceCount(&cnt);
+    if (e != hipSuccess) return set_err(LQRX_ERR_NODEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    for (int i = 0; i < ndev; ++i)
+        if (devices[i] < 0 || devices[i] >= cnt)
+            return set_err(-ai_dev, "devices[%d] = %d is not a device (0..%d)", i, devices[i], cnt - 1);
+    return 0;
+}
+
+// one host array of S elements per trajectory: the shard's slice ↔ a packed device buffer of
+// nb trajectories in the same layout (layout 0: one contiguous run; layout 1: S rows of nb
+// elements at pitch B)
+hipError_t shard_h2d(void *dst, const void *src, size_t S, size_t es, const Shard &sh, int64_t B, int layout,
+                     hipStream_t s)
+{
+    if (layout == 0)
+        return hipMemcpyAsync(dst, (const char *)src + (size_t)sh.b0 * S * es, (size_t)sh.nb * S * es,
+                              hipMemcpyHostToDevice, s);
+    return hipMemcpy2DAsync(dst, (size_t)sh.nb * es, (const char *)src + (size_t)sh.b0 * es, (size_t)B * es,
+                            (size_t)sh.nb * es, S, hipMemcpyHostToDevice, s);
+}
+hipError_t shard_d2h(void *dst, const void *src, size_t S, size_t es, const Shard &sh, int64_t B, int layout,
+                     hipStream_t s)
+{
+    if (layout == 0)
+        return hipMemcpyAsync((char *)dst + (size_t)sh.b0 * S * es, src, (size_t)sh.nb * S * es,
+                              hipMemcpyDeviceToHost, s);
+    return hipMemcpy2DAsync((char *)dst + (size_t)sh.b0 * es, (size_t)B * es, src, (size_t)sh.nb * es,
+                            (size_t)sh.nb * es, S, hipMemcpyDeviceToHost, s);
+}
+
+// a shard's device buffers and stream, released on its own device
+struct ShardCtx {
+    hipStream_t s = nullptr;
+    std::vector<void *> bufs;
+    ~ShardCtx()
+    {
+        if (s) (void)hipStreamSynchronize(s);
+        for (void *p : bufs) (void)hipFree(p);
+        if (s) (void)hipStreamDestroy(s);
+    }
+    int alloc(void **p, size_t bytes)
+    {
+        hipError_t e = hipMalloc(p, bytes ? bytes : 16);
+        if (e != hipSuccess) return hip_err(e, "hipMalloc shard");
+        bufs.push_back(*p);
+        return 0;
+    }
+};
+
+// run fn(shard) for every non-empty shard concurrently, each on its device; the first failing
+// shard's status and message become the call's; else 1 if any trajectory has info != 0
+template <typename F> int run_shards(std::vector<Shard> &sh, const int32_t *info, int64_t B, F fn)
+{
+    std::vector<std::thread> th;
+    for (auto &x : sh) {
+        if (x.nb == 0) continue;
+        th.emplace_back([&x, &fn] {
+            hipError_t e = hipSetDevice(x.dev);
+            x.st = e != hipSuccess ? hip_err(e, "hipSetDevice") : fn(x);
+            if (x.st < 0) x.err = g_err;
+        });
+    }
+    for (auto &t : th) t.join();
+    for (auto &x : sh)
+        if (x.st < 0) return set_err(x.st, "shard on device %d (trajectories %lld..%lld): %s", x.dev,
+                                     (long long)x.b0, (long long)(x.b0 + x.nb - 1), x.err.c_str());
+    if (info)
+        for (int64_t b = 0; b < B; ++b)
+            if (info[b]) return 1;
+    return 0;
+}
+
+int dp_solve_host_devices_impl(const lqrx_dp_desc *d, const void *A, const void *B, const void *Q,
+                               const void *R, const void *Qf, const void *x0, const lqrx_dp_linear *lin,
+                               void *K, void *P, void *X, void *U, int32_t *info, const int32_t *devices,
+                               int32_t ndev)
+{
+    int st = validate_dp(d);
+    if (st) return st;
+    const int o = lin ? 1 : 0;
+    if ((st = check_devices(devices, ndev, 13 + o, 14 + o))) return st;
+    if (d->batch == 0) return 0;
+    const size_t es = dsize(d->dtype), n = d->n, m = d->m, N = d->N;
+    const size_t kAB = d->knot_stride_AB ? N - 1 : 1, kQR = d->knot_stride_QR ? N - 1 : 1;
+    const int nin = lin ? 9 : 6, nout = lin ? 6 : 4;
+    const size_t szin[9] = {n * n * kAB, n * m * kAB, n * n * kQR, m * m * kQR, n * n, n, n * kQR, m * kQR, n};
+    const void *hin[9] = {A, B, Q, R, Qf, x0, lin ? lin->q : nullptr, lin ? lin->r : nullptr,
+                          lin ? lin->qf : nullptr};
+    const size_t szout[6] = {m * n * (N - 1), d->p_mode ? n * n * N : n * n, n * N, m * (N - 1),
+                             m * (N - 1), d->p_mode ? n * N : n};
+    void *hout[6] = {K, P, X, U, lin ? lin->d : nullptr, lin ? lin->p : nullptr};
+    for (int i = 0; i < nin; ++i)
+        if (!hin[i]) return set_err(i < 6 ? -(i + 2) : -8, "input pointer %d is NULL", i < 6 ? i + 2 : 8);
+    for (int i = 0; i < nout; ++i)
+        if (!hout[i]) return set_err(i < 4 ? -(i + 8 + o) : -8, "output pointer %d is NULL", i < 4 ? i + 8 + o : 8);
+    std::vector<Shard> sh = make_shards(d->batch, devices, ndev);
+    const int64_t Bt = d->batch;
+    const int lay = d->layout;
+    return run_shards(sh, info, Bt, [&](Shard &x) -> int {
+        ShardCtx c;
+        hipError_t e = hipStreamCreateWithFlags(&c.s, hipStreamNonBlocking);
+        if (e != hipSuccess) return hip_err(e, "hipStreamCreate");
+        void *din[9] = {}, *dout[6] = {}, *dinfo = nullptr;
+        int r;
+        for (int i = 0; i < nin; ++i) {
+            if ((r = c.alloc(&din[i], szin[i] * es * x.nb))) return r;
+            if ((e = shard_h2d(din[i], hin[i], szin[i], es, x, Bt, lay, c.s)) != hipSuccess) return hip_err(e, "H2D");
+        }
+        for (int i = 0; i < nout; ++i)
+            if ((r = c.alloc(&dout[i], szout[i] * es * x.nb))) return r;
+        if ((r = c.alloc(&dinfo, 4 * x.nb))) return r;
+        lqrx_dp_desc ds = *d;
+        ds.batch = x.nb;
+        lqrx_dp_linear dl{};
+        if (lin) {
+            dl.q = din[6]; dl.r = din[7]; dl.qf = din[8]; dl.d = dout[4]; dl.p = dout[5];
+        }
+        if ((r = dp_solve_impl(&ds, din[0], din[1], din[2], din[3], din[4], din[5], lin ? &dl : nullptr, dout[0],
+                               dout[1], dout[2], dout[3], (int32_t *)dinfo, c.s)) < 0)
+            return r;
+        for (int i = 0; i < nout; ++i)
+            if ((e = shard_d2h(hout[i], dout[i], szout[i], es, x, Bt, lay, c.s)) != hipSuccess) return hip_err(e, "D2H");
+        if (info && (e = hipMemcpyAsync(info + x.b0, dinfo, 4 * x.nb, hipMemcpyDeviceToHost, c.s)) != hipSuccess)
+            return hip_err(e, "D2H info");
+        if ((e = hipStreamSynchronize(c.s)) != hipSuccess) return hip_err(e, "dp shard");
+        return 0;
+    });
+}
+} // namespace
+
+extern "C" int lqrx_dp_solve_host_devices(const lqrx_dp_desc *d, const void *A, const void *B, const void *Q,
+                                          const void *R, const void *Qf, const void *x0, void *K, void *P, void *X,
+                                          void *U, int32_t *info, const int32_t *devices, int32_t ndev)
+{
+    return dp_solve_host_devices_impl(d, A, B, Q, R, Qf, x0, nullptr, K, P, X, U, info, devices, ndev);
+}
+
+extern "C" int lqrx_dp_solve_linear_host_devices(const lqrx_dp_desc *d, const void *A, const void *B,
+                                                 const void *Q, const void *R, const void *Qf, const void *x0,
+                                                 const lqrx_dp_linear *lin, void *K, void *P, void *X, void *U,
+                                                 int32_t *info, const int32_t *devices, int32_t ndev)
+{
+    if (!lin) return set_err(-8, "lin is NULL");
+    return dp_solve_host_devices_impl(d, A, B, Q, R, Qf, x0, lin, K, P, X, U, info, devices, ndev);
+}
+
+extern "C" int lqrx_kkt_solve_host_devices(const lqrx_kkt_desc *d, const void *Y, const void *y, const void *H,
+                                           const void *g, void *dz, void *lam, int32_t *info,
+                                           const int32_t *devices, int32_t ndev)
+{
+    KktLayout L;
+    int st = kkt_layout(d, L);
+    if (st) return st;
+    if ((st = check_devices(devices, ndev, 9, 10))) return st;
+    if (d->batch == 0) return 0;
+    const void *hin[4] = {Y, y, H, g};
+    for (int i = 0; i < 4; ++i)
+        if (!hin[i]) return set_err(-(i + 2), "input pointer %d is NULL", i + 2);
+    if (!dz) return set_err(-6, "dz is NULL");
+    if (!lam) return set_err(-7, "lam is NULL");
+    const size_t es = d->dtype == LQRX_F32 ? 4 : 8;
+    const size_t szin[4] = {(size_t)L.sY, (size_t)L.sy, (size_t)L.sH, (size_t)L.sg};
+    std::vector<Shard> sh = make_shards(d->batch, devices, ndev);
+    const int64_t Bt = d->batch;
+    const int lay = d->layout;
+    return run_shards(sh, info, Bt, [&](Shard &x) -> int {
+        ShardCtx c;
+        hipError_t e = hipStreamCreateWithFlags(&c.s, hipStreamNonBlocking);
+        if (e != hipSuccess) return hip_err(e, "hipStreamCreate");
+        void *din[4] = {}, *ddz = nullptr, *dlam = nullptr, *dinfo = nullptr;
+        int r;
+        for (int i = 0; i < 4; ++i) {
+            if ((r = c.alloc(&din[i], szin[i] * es * x.nb))) return r;
+            if ((e = shard_h2d(din[i], hin[i], szin[i], es, x, Bt, lay, c.s)) != hipSuccess) return hip_err(e, "H2D");
+        }
+        if ((r = c.alloc(&ddz, (size_t)L.sg * es * x.nb)) || (r = c.alloc(&dlam, (size_t)L.sy * es * x.nb)) ||
+            (r = c.alloc(&dinfo, 4 * x.nb)))
+            return r;
+        lqrx_kkt_desc ds = *d;
+        ds.batch = x.nb;
+        if ((r = kkt_solve_impl(&ds, din[0], din[1], din[2], din[3], ddz, dlam, (int32_t *)dinfo, nullptr, 0, c.s)) < 0)
+            return r;
+        if ((e = shard_d2h(dz, ddz, (size_t)L.sg, es, x, Bt, lay, c.s)) != hipSuccess ||
+            (e = shard_d2h(lam, dlam, (size_t)L.sy, es, x, Bt, lay, c.s)) != hipSuccess)
+            return hip_err(e, "D2H");
+        if (info && (e = hipMemcpyAsync(info + x.b0, dinfo, 4 * x.nb, hipMemcpyDeviceToHost, c.s)) != hipSuccess)
+            return hip_err(e, "D2H info");
+        if ((e = hipStreamSynchronize(c.s)) != hipSuccess) return hip_err(e, "kkt shard");
+        return 0;
+    });
+}
+
 // ------------------------------------------------------------------ batched trajectory SQP
 namespace {
 int validate_sqp(const lqrx_sqp_desc *d, int *nx, int *nu)

@@ -907,7 +907,8 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
 //        as 3, 3, 2, 2 per wave: Q + A[:, i]ᵀPA[:, w] − G[:, i]ᵀK[:, w], written to the P image
 //        at (i, w) and mirrored to (w, i) (diagonal tiles from their lower triangle), so the
 //        image stays exactly symmetric as tiles_symmetrize_lower keeps the one-wave P.
-// Three workgroup barriers per knot (after PB/PA, after E/G, after P_).  Registers per wave:
+// Four workgroup barriers per knot (after PB/PA, after E/G, the inverse's verdict vote, after
+// P_).  Registers per wave:
 // the A columns its P_ rows need (3 × 4 tiles, the first is A[:, w]), B, Q's P_ tiles, R's E
 // tile — time-invariant, loaded once.  The rollout (:66-70) is dp_rollout_full on wave 0.
 template <typename T, int MT>
@@ -975,6 +976,7 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
     int *flag = (int *)(Gim + C::G_EL);
 #endif
     T *aug = PBim;                       // the exact sweep reuses the PB image (read before it)
+    int *vote = flag + 4;                // per-wave Newton–Schulz verdicts (flag[0]: the sweep's)
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1083,8 +1085,15 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
                     Xp[i][j] = x1;
                 }
             have = ns_refine<T, MT>(Xi, E, Id, lane);
+            // workgroup-uniform verdict by construction (the branch below holds a barrier): each
+            // wave posts its own Newton–Schulz verdict, every wave takes the AND of all four — no
+            // reliance on the four refinements agreeing bitwise.  (The slots are rewritten only
+            // after this knot's B3, which every wave reaches after reading them.)
+            if (lane == 0) vote[w] = have ? 1 : 0;
+            __syncthreads();
+            have = (vote[0] & vote[1] & vote[2] & vote[3]) != 0;
         }
-        if (!have) {                                       // uniform: every wave computed alike
+        if (!have) {                                       // uniform (k == N − 1, or the vote above)
             if (w == 0) {
 #pragma unroll
                 for (int i = 0; i < MT; ++i)

@@ -146,7 +146,9 @@ __device__ __forceinline__ void kw_gram_st(const Knot<T> &K, const Knot<T> *Kp, 
                 wg::tile_ld<T>(D[i][j], Kp->C + bI[i].off + (size_t)bJ[j].off * K.p1, bI[i].nv, bJ[j].nv, 1, K.p1, lane);
         }
     const char *yb = (const char *)Yk;
-    const int yn = rows * w * (int)TS, nks = (w + 3) >> 2;
+    // fp64: one slice = 4 consecutive columns (kq = 4); fp32: kq = 1, so a 16-column k-tile takes
+    // all 4 of its slices even when only part of it lies below w (the rest read 0)
+    const int yn = rows * w * (int)TS, nks = kq == 1 ? 4 * ((w + 15) >> 4) : (w + 3) >> 2;
     // slice s: columns 16(s/4) + row(lane, s mod 4) — descriptor base at the slice's first column
     auto base = [&](int s) { return 16 * (s >> 2) + kq * (s & 3); };
     constexpr int PF = 2;
@@ -433,11 +435,16 @@ size_t kw_elems(const KktArgs &a, const int32_t *n1, const int32_t *p, const int
     return e;
 }
 
-int64_t kw_chunk(const KktArgs &a, size_t per_bytes)
+// per-launch scratch caps: the library's own pool takes up to 24 GiB (n = 96: ~10 MB per
+// trajectory — the B = 2048 batch in one launch instead of five under-filled ones) and halves
+// on an out-of-memory; lqrx_kkt_workspace_size quotes the round-4 4 GiB, so a caller-owned
+// workspace stays modest (the launch then runs the batch in more chunks)
+constexpr int64_t KW_POOL_CAP = (int64_t)24 << 30, KW_WS_CAP = (int64_t)4 << 30;
+
+int64_t kw_chunk(const KktArgs &a, size_t per_bytes, int64_t cap_bytes)
 {
-    // up to 24 GiB of per-trajectory scratch per launch (n = 96: ~10 MB per trajectory — the
-    // B = 2048 batch in one launch instead of five under-filled ones), chunks evened out
-    const int64_t cap = std::max<int64_t>(1, ((int64_t)24 << 30) / (int64_t)per_bytes);
+    // chunks of at most cap_bytes of per-trajectory scratch, evened out over the launches
+    const int64_t cap = std::max<int64_t>(1, cap_bytes / (int64_t)per_bytes);
     const int64_t nl = (a.batch + cap - 1) / cap;
     int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(a.batch, (a.batch + nl - 1) / nl));
     if (const char *ev = std::getenv("LQRX_KKT_WG_CHUNK"))   // tests: force the multi-chunk path
@@ -460,7 +467,7 @@ size_t kkt_wg_scratch_bytes(const KktArgs &a, const int32_t *n1, const int32_t *
 {
     if (a.batch == 0 || !kkt_wg_supported(a, n1, p, n2, w)) return 0;
     const size_t per = kw_elems(a, n1, p, n2, w) * (a.dtype == 0 ? 8 : 4);
-    return per * (size_t)kw_chunk(a, per);
+    return per * (size_t)kw_chunk(a, per, KW_WS_CAP);
 }
 
 hipError_t kkt_wg_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2, const int32_t *w,
@@ -468,11 +475,18 @@ hipError_t kkt_wg_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, 
 {
     if (!kkt_wg_supported(a, n1, p, n2, w)) return hipErrorNotSupported;
     const size_t elems = kw_elems(a, n1, p, n2, w), per = elems * (a.dtype == 0 ? 8 : 4);
-    int64_t chunk = kw_chunk(a, per);
+    int64_t chunk = kw_chunk(a, per, a.ws ? (int64_t)std::min<size_t>(a.ws_bytes, (size_t)KW_POOL_CAP) : KW_POOL_CAP);
     if (a.ws) chunk = std::min<int64_t>(chunk, (int64_t)(a.ws_bytes / per));
     if (chunk < 1) return hipErrorInvalidValue;
     Scratch sc;
     hipError_t e = sc.get(a, per * (size_t)chunk, s);
+    // library scratch: when the pool cannot hold the chunk (the device partly in use by torch or
+    // another rank), halve until it fits or one trajectory fails — as kb_launch_t does
+    while (e == hipErrorOutOfMemory && !a.ws && chunk > 1) {
+        (void)hipGetLastError();
+        chunk = kw_chunk(a, per, (int64_t)per * ((chunk + 1) / 2));
+        e = sc.get(a, per * (size_t)chunk, s);
+    }
     if (e != hipSuccess) return e;
     for (int64_t b0 = 0; b0 < a.batch && e == hipSuccess; b0 += chunk) {
         dim3 grid((unsigned)std::min<int64_t>(chunk, a.batch - b0)), block(BT);

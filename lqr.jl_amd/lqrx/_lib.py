@@ -90,6 +90,10 @@ _SIGS = {
                              + [_VP] * 4 + [_VP, _VP]),
     "lqrx_dp_solve_linear_host": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 6
                                   + [C.POINTER(DpLinear)] + [_VP] * 5),
+    "lqrx_dp_solve_host_devices": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 10 + [_VP, _VP, C.c_int32]),
+    "lqrx_dp_solve_linear_host_devices": (C.c_int, [C.POINTER(DpDesc)] + [_VP] * 6 + [C.POINTER(DpLinear)]
+                                          + [_VP] * 5 + [_VP, C.c_int32]),
+    "lqrx_kkt_solve_host_devices": (C.c_int, [C.POINTER(KktDesc)] + [_VP] * 7 + [_VP, C.c_int32]),
     "lqrx_kkt_solve": (C.c_int, [C.POINTER(KktDesc)] + [_VP] * 7 + [_VP]),
     "lqrx_kkt_solve_host": (C.c_int, [C.POINTER(KktDesc)] + [_VP] * 7),
     "lqrx_kkt_sizes": (C.c_int, [C.POINTER(KktDesc)] + [C.POINTER(C.c_int64)] * 5),

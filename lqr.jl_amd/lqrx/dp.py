@@ -176,12 +176,20 @@ def _ptr(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p)
 
 
-def solve_batch(b: LQRBatch, dtype: int = _lib.F64, all_P: bool = False, layout: int = 0):
+def _devices(devices):
+    """(int32 array, ctypes pointer, count) for a devices= argument."""
+    dv = np.ascontiguousarray(np.asarray(list(devices), dtype=np.int32))
+    return dv, dv.ctypes.data_as(C.c_void_p), C.c_int32(len(dv))
+
+
+def solve_batch(b: LQRBatch, dtype: int = _lib.F64, all_P: bool = False, layout: int = 0,
+                devices=None):
     """Batched solve! through lqrx_dp_solve_host.  Returns dict of logical arrays
     K (batch, N-1, m, n), P (batch, n, n) or (batch, N, n, n), X (batch, N, n),
     U (batch, N-1, m), info (batch,), and the ABI return code.  layout = 1 hands the
     library batch-fastest (SoA) buffers (the conversion here is host-side bookkeeping; the
-    result is the same logical arrays)."""
+    result is the same logical arrays).  devices = [d0, d1, …] shards the batch over those
+    GPUs in one call (lqrx_dp_solve[_linear]_host_devices; repeats allowed)."""
     lib = _lib.load()
     n, m, N = b.size()
     bt = b.batch
@@ -212,12 +220,21 @@ def solve_batch(b: LQRBatch, dtype: int = _lib.F64, all_P: bool = False, layout:
         pv = np.zeros(bt * n * (N if all_P else 1), npdt)
         ln = _lib.DpLinear(_ptr(q).value, _ptr(r).value, _ptr(qf).value, _ptr(dff).value,
                            _ptr(pv).value)
-        rc = _lib.check(lib.lqrx_dp_solve_linear_host(
-            C.byref(d), *[_ptr(a) for a in ins], _ptr(x0), C.byref(ln), _ptr(K), _ptr(P),
-            _ptr(X), _ptr(U), _ptr(info)))
+        args = (C.byref(d), *[_ptr(a) for a in ins], _ptr(x0), C.byref(ln), _ptr(K), _ptr(P),
+                _ptr(X), _ptr(U), _ptr(info))
+        if devices is None:
+            rc = _lib.check(lib.lqrx_dp_solve_linear_host(*args))
+        else:
+            dv, dp_, nd = _devices(devices)
+            rc = _lib.check(lib.lqrx_dp_solve_linear_host_devices(*args, dp_, nd))
     else:
-        rc = _lib.check(lib.lqrx_dp_solve_host(C.byref(d), *[_ptr(a) for a in ins], _ptr(x0),
-                                               _ptr(K), _ptr(P), _ptr(X), _ptr(U), _ptr(info)))
+        args = (C.byref(d), *[_ptr(a) for a in ins], _ptr(x0), _ptr(K), _ptr(P), _ptr(X), _ptr(U),
+                _ptr(info))
+        if devices is None:
+            rc = _lib.check(lib.lqrx_dp_solve_host(*args))
+        else:
+            dv, dp_, nd = _devices(devices)
+            rc = _lib.check(lib.lqrx_dp_solve_host_devices(*args, dp_, nd))
     if layout == 1:
         K, P, X, U = (from_soa(a, bt) for a in (K, P, X, U))
         if lin:
@@ -254,10 +271,14 @@ def compute_ctg_batch(A, B, Q, R, P, dtype: int = _lib.F64, gain_only: bool = Fa
     lib = _lib.load()
     A = np.asarray(A)
     bt, n, m = A.shape[0], A.shape[-1], np.asarray(B).shape[-1]
-    # the kernels' symmetric fast form needs symmetric P and Q (include/lqrx.h precondition)
-    for name, M in (("P", P), ("Q", Q)):
+    # the kernels' symmetric fast form needs symmetric P and Q (include/lqrx.h precondition);
+    # the tolerance is relative to the largest entry and never tighter than 100 ulp of the
+    # working dtype (an fp32 AᵀPA is symmetric only to fp32 rounding); Q never enters K, so a
+    # gain-only call does not check it
+    rtol = max(1e-10, 100.0 * float(np.finfo(np.float64 if dtype == _lib.F64 else np.float32).eps))
+    for name, M in (("P", P),) + (() if gain_only else (("Q", Q),)):
         M = np.asarray(M, dtype=np.float64)
-        if np.abs(M - np.swapaxes(M, -1, -2)).max(initial=0.0) > 1e-10 * max(np.abs(M).max(initial=0.0), 1e-300):
+        if np.abs(M - np.swapaxes(M, -1, -2)).max(initial=0.0) > rtol * max(np.abs(M).max(initial=0.0), 1e-300):
             raise ValueError(f"compute_ctg: {name} must be symmetric (the Riccati cost-to-go / cost "
                              "Hessian; lqrx_dp_compute_ctg precondition)")
     npdt = np.float64 if dtype == _lib.F64 else np.float32

@@ -202,11 +202,14 @@ def _ptr(a):
     return a.ctypes.data_as(C.c_void_p)
 
 
-def kkt_solve(pb: KktProblem, ginv: int = 1, layout: int = 0, dtype: int | None = None):
+def kkt_solve(pb: KktProblem, ginv: int = 1, layout: int = 0, dtype: int | None = None,
+              devices=None):
     """Batched _solve! via lqrx_kkt_solve_host.  Returns dict dz (batch, NN), lam
     (batch, P), info (batch,), rc.  layout=1 hands the library batch-fastest (SoA) copies
     ([element][batch]) and transposes the outputs back — same results.  dtype=F32 rounds the
-    inputs to float32 and runs the fp32 (large-block) kernels; outputs come back as float32."""
+    inputs to float32 and runs the fp32 (large-block) kernels; outputs come back as float32.
+    devices = [d0, d1, …] shards the batch over those GPUs in one call
+    (lqrx_kkt_solve_host_devices; repeats allowed)."""
     lib = _lib.load()
     st, bt = pb.st, pb.batch
     sY, sy, sH, sg = st.sizes(pb.h_mode)
@@ -219,8 +222,13 @@ def kkt_solve(pb: KktProblem, ginv: int = 1, layout: int = 0, dtype: int | None 
     dz = np.zeros((sg, bt) if layout == 1 else (bt, sg), npdt)
     lam = np.zeros((sy, bt) if layout == 1 else (bt, sy), npdt)
     info = np.zeros(bt, np.int32)
-    rc = _lib.check(lib.lqrx_kkt_solve_host(C.byref(d), _ptr(Y), _ptr(y), _ptr(H), _ptr(g),
-                                            _ptr(dz), _ptr(lam), _ptr(info)))
+    args = (C.byref(d), _ptr(Y), _ptr(y), _ptr(H), _ptr(g), _ptr(dz), _ptr(lam), _ptr(info))
+    if devices is None:
+        rc = _lib.check(lib.lqrx_kkt_solve_host(*args))
+    else:
+        dv = np.ascontiguousarray(np.asarray(list(devices), dtype=np.int32))
+        rc = _lib.check(lib.lqrx_kkt_solve_host_devices(*args, dv.ctypes.data_as(C.c_void_p),
+                                                        C.c_int32(len(dv))))
     if layout == 1:
         dz, lam = np.ascontiguousarray(dz.T), np.ascontiguousarray(lam.T)
     return dict(dz=dz, lam=lam, info=info, rc=rc)

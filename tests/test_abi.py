@@ -18,7 +18,7 @@ def test_exports_every_header_symbol(lqrx):
 
 
 def test_abi_version(lqrx):
-    assert lqrx.load().lqrx_abi_version() == 4
+    assert lqrx.load().lqrx_abi_version() == 5
 
 
 def test_scratch_trim_without_pools(lqrx):
@@ -283,3 +283,66 @@ def test_compute_ctg_rejects_asymmetric_cost():
     Q2[0, 4, 1] = 1e-3
     with pytest.raises(ValueError, match="Q must be symmetric"):
         compute_ctg_batch(A, B, Q2, R, np.tile(np.eye(5), (2, 1, 1)))
+
+
+def test_compute_ctg_symmetry_tolerance_follows_dtype():
+    """an fp32 P symmetric only to fp32 rounding (~1e-7 relative) passes the
+    wrapper's check (tolerance max(1e-10, 100 ulp of the dtype)), the same P in fp64 does not;
+    Q is not checked on a gain-only call.  The accepted calls reach the library (here, with no
+    GPU, a device error rather than the symmetry ValueError)."""
+    import numpy as np
+    import lqrx
+    from lqrx.dp import compute_ctg_batch
+
+    rng = np.random.default_rng(1)
+    A, B = rng.standard_normal((2, 5, 5)), rng.standard_normal((2, 5, 2))
+    Q, R = np.tile(np.eye(5), (2, 1, 1)), np.tile(np.eye(2), (2, 1, 1))
+    P = np.tile(np.eye(5), (2, 1, 1))
+    P[1, 0, 3] += 3e-7
+
+    def reached_library(**kw):
+        try:
+            compute_ctg_batch(A, B, kw.pop("Q", Q), R, P, **kw)
+        except ValueError as e:
+            assert "symmetric" not in str(e), e
+        except lqrx.LqrxError:
+            pass
+        return True
+
+    assert reached_library(dtype=lqrx.F32)
+    with pytest.raises(ValueError, match="P must be symmetric"):
+        compute_ctg_batch(A, B, Q, R, P, dtype=lqrx.F64)
+    P[1, 0, 3] = 0.0
+    Q2 = Q.copy()
+    Q2[0, 4, 1] = 1e-3
+    assert reached_library(Q=Q2, gain_only=True)
+
+
+def test_host_devices_argument_codes(lqrx):
+    """the multi-device host entries (ABI 5) validate devices / ndev before
+    any device call — NULL devices and ndev < 1 give the negative argument index (dp: 13 / 14,
+    dp linear: 14 / 15, kkt: 9 / 10); the descriptor is still argument 1.  (An ordinal that is
+    not a device is checked against hipGetDeviceCount: the -m gpu test covers it.)"""
+    from lqrx import _lib
+    import lqrx.kkt as K
+
+    lib = lqrx.load()
+    d = _lib.DpDesc(8, 4, 10, 0, 4, 0, 0, 0, 0)
+    buf = np.zeros(16)
+    p = buf.ctypes.data_as(C.c_void_p)
+    dv = np.zeros(2, np.int32)
+    dp_ = dv.ctypes.data_as(C.c_void_p)
+    assert lib.lqrx_dp_solve_host_devices(C.byref(d), p, p, p, p, p, p, p, p, p, p, None, None, 2) == -13
+    assert lib.lqrx_dp_solve_host_devices(C.byref(d), p, p, p, p, p, p, p, p, p, p, None, dp_, 0) == -14
+    ln = _lib.DpLinear(p.value, p.value, p.value, p.value, p.value)
+    assert lib.lqrx_dp_solve_linear_host_devices(C.byref(d), p, p, p, p, p, p, C.byref(ln), p, p, p, p, None,
+                                                 None, 2) == -14
+    assert lib.lqrx_dp_solve_linear_host_devices(C.byref(d), p, p, p, p, p, p, C.byref(ln), p, p, p, p, None,
+                                                 dp_, -1) == -15
+    assert lib.lqrx_dp_solve_linear_host_devices(C.byref(d), p, p, p, p, p, p, None, p, p, p, p, None,
+                                                 dp_, 2) == -8
+    kd = K.dubins_structure(5).desc(4, 2, 1)
+    assert lib.lqrx_kkt_solve_host_devices(C.byref(kd), p, p, p, p, p, p, None, None, 1) == -9
+    assert lib.lqrx_kkt_solve_host_devices(C.byref(kd), p, p, p, p, p, p, None, dp_, 0) == -10
+    d.n = 0
+    assert lib.lqrx_dp_solve_host_devices(C.byref(d), p, p, p, p, p, p, p, p, p, p, None, dp_, 2) == -1

@@ -68,6 +68,26 @@ def test_wg_kkt_f32(lqrx, gpu_ok, n, m, N):
     assert e <= F32_TOL
 
 
+@pytest.mark.parametrize("n,m,N", [(70, 30, 9), (72, 40, 7), (67, 20, 5)])
+@pytest.mark.parametrize("ginv", [1, 0])
+def test_wg_kkt_f32_ragged_w(lqrx, gpu_ok, n, m, N, ginv):
+    """the fp32 diagonal-H Gram path with w mod 16 in 3..8 — w = 100 for
+    (70, 30), the last knot's w = 72 for (72, 40), w = 87 for (67, 20).  In fp32 one lane's
+    k index steps by 1 per slice, so a partial 16-column k-tile still needs all 4 slices; the
+    round-5 slice count ceil(w/4) dropped columns 16t+2, 16t+3 (…) of the last tile."""
+    import lqrx.kkt as K
+
+    st = K.trajectory_structure(n, m, N)
+    assert any(int(w) % 16 in range(3, 9) for w in st.w)
+    pb = _round32(K.random_kkt(st, 3, seed=11 * n + m, h_mode=K.H_DIAG, dyn="dense"))
+    got = K.kkt_solve(pb, dtype=lqrx.F32, ginv=ginv)
+    ref = _ref(st, pb, ginv=ginv)
+    assert got["rc"] == 0 and (got["info"] == 0).all()
+    e = max(traj_rel(got["dz"], ref["dz"]), traj_rel(got["lam"], ref["lam"]))
+    print(f"fp32 n={n} m={m} N={N} ginv={ginv}: max rel err {e:.3e}")
+    assert e <= F32_TOL
+
+
 @pytest.mark.parametrize("n,m,N,h_mode", [(80, 40, 9, 0), (66, 20, 7, 1), (40, 100, 6, 0)])
 def test_wg_kkt_dense_h(lqrx, gpu_ok, n, m, N, h_mode):
     """Dense / block-diagonal H_k (potrf per knot, H⁻¹ by potrs) with blocks past 64 rows or
