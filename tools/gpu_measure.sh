@@ -138,6 +138,17 @@ recipe_r5dp() {   # after a change in lqrx_dp.hip: its suite files, then the thr
     sub dp64 prof --n 64 --m 32 --N 512 --batch 8192 --dtype f64 &&
     KREGEX=dp_wg4 PMC="$SQ1;$SQ2" sub dp64sq pmc --n 64 --m 32 --N 512 --batch 8192 --dtype f64
 }
+DP64="--n 64 --m 32 --N 512 --batch 8192 --dtype f64"
+DP64TV="--n 64 --m 32 --N 512 --batch 2048 --dtype f64 --tv"
+recipe_r6lines() {   # the lines whose kernels changed in round 5 (TV / LIN rollout,
+                     # DoubleIntegrator(3) KKT) with traffic, and the fp64 n = 64 TV / LIN lines
+    sub tv prof --tv && sub lin prof --linear && sub di prof --workload kkt --kkt-structure di &&
+    sub tv64 kt $DP64TV && sub lin64 kt $DP64 --linear
+}
+recipe_r6dp64() {   # the fp64 n = 64 DP surface: its tests, then plain / TV / LIN lines with traffic
+    sub t pytest tests/test_dp_gpu.py tests/test_dp_linear_gpu.py tests/test_dp_lane_gpu.py &&
+    sub dp64 prof $DP64 && sub tv64 prof $DP64TV && sub lin64 prof $DP64 --linear
+}
 recipe_list() { declare -F | sed -n 's/^declare -f recipe_//p'; }
 
 case "$MODE" in
