@@ -197,7 +197,7 @@ def cpu_baseline_kkt(N, target_s=12.0, threads=None, structure="dubins", h_mode=
                        f"of _solve!), OpenMP {threads} threads, {dt:.1f} s")
 
 
-TRAFFIC_FILES = ("traffic_r05.json", "traffic_r04.json", "traffic_r03.json", "traffic_r02.json")
+TRAFFIC_FILES = ("traffic_r06.json", "traffic_r05.json", "traffic_r04.json", "traffic_r03.json", "traffic_r02.json")
 
 
 def traffic_lookup(key, path=None):
@@ -431,7 +431,7 @@ def main(argv=None):
     ap.add_argument("--no-gather", action="store_true",
                     help="skip the final info + P_1 gather to rank 0 (N > 1)")
     ap.add_argument("--traffic-json", default=None,
-                    help="PMC traffic table (default: profiles/traffic_r05.json, then the older rounds'; a "
+                    help="PMC traffic table (default: profiles/traffic_r06.json, then the older rounds'; a "
                          "figure is reported only while its kernel's code is unchanged, see traffic_validate)")
     ap.add_argument("--kkt-structure", choices=["dubins", "di", "dense"], default="dubins",
                     help="kkt workload: Dubins (configs[2]), DoubleIntegrator(3,N) (test/problems.jl), or "

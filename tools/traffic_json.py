@@ -1,5 +1,5 @@
 """HBM traffic per solve from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes →
-profiles/traffic_r05.json (the `roofline.traffic` field of bench.py), stamped with what it was
+profiles/traffic_r06.json (the `roofline.traffic` field of bench.py), stamped with what it was
 measured on.
 
     python tools/traffic_json.py KEY RUN_DIR [--kernels SUBSTR] [--solves N] [--out JSON]
@@ -37,7 +37,7 @@ ap.add_argument("key")
 ap.add_argument("run_dir")
 ap.add_argument("--kernels", default="")
 ap.add_argument("--solves", type=int, default=2)
-ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "traffic_r05.json"))
+ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "traffic_r06.json"))
 a = ap.parse_args()
 
 
