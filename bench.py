@@ -61,8 +61,8 @@ def _dp_kernel_name(n, m, bt, tv, lin=False, f64=False):
         return "dp_quad_kernel" if quad else "dp_lane_kernel"
     if n > 64 or m > 32:
         return "dp_big_kernel"      # workgroup per trajectory, past the register tiles
-    if f64 and n == 64 and m in (16, 32) and not tv and not lin and os.environ.get("LQRX_DP_WG4", "") != "0":
-        return "dp_wg4_kernel"      # four waves per trajectory (lqrx_dp.hip, round 5)
+    if f64 and n == 64 and m in (16, 32) and os.environ.get("LQRX_DP_WG4", "") != "0":
+        return "dp_wg4_kernel"      # four waves per trajectory (lqrx_dp.hip; TV / LIN variants: round 6)
     return "dp_riccati_kernel"
 
 
@@ -861,7 +861,7 @@ def main(argv=None):
                 hbm = ab / (kern_ms * 1e-3) / 1e9
                 roof = {"bound": "hbm", "achieved": hbm, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": hbm / PEAK_HBM_GBS, "traffic": traffic,
-                        "kernel": _dp_kernel_name(n, m, bt, True), "kernel_ms": kern_ms,
+                        "kernel": _dp_kernel_name(n, m, bt, True, f64=f64), "kernel_ms": kern_ms,
                         "alg_bytes_per_launch": ab, "min_traffic_bytes_per_launch": min_traffic,
                         "min_traffic_frac": min_traffic / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                         "fp64_tflops": achieved, "fp64_frac": achieved / peak}

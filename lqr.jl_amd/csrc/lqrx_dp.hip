@@ -59,9 +59,6 @@
 #ifndef LQRX_DP_WG4
 #define LQRX_DP_WG4 1         // fp64 n = 64: the four-wave kernel (A/B builds: 0 = one wave)
 #endif
-#ifndef LQRX_WG4_AIMG
-#define LQRX_WG4_AIMG 1       // four-wave kernel: A in an LDS image, only A[:, w] in registers (0: A/B)
-#endif
 #ifndef LQRX_DP_ROLL_FULL
 #define LQRX_DP_ROLL_FULL 1   // exact tile grids: the register-streamed rollout (A/B builds: 0)
 #endif
@@ -893,42 +890,57 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
 }
 
 // ------------------------------------------------------------------ four waves per trajectory
-// dp_wg4_kernel<T, MT> — fp64 n = 64, m = 16·MT (time-invariant, no linear terms): the shape
-// whose tile grid does not fit one wave (A alone is 128 fp64 registers; the one-wave kernel
-// spills ~2–3 KB per lane there).  One 256-thread workgroup per trajectory, one wave per SIMD,
-// the same fast form and the same Newton–Schulz / exact-sweep inverse as dp_riccati_kernel,
-// with the knot's products split by the n-dimension's 16-column tiles (wave w ↔ tile column w):
-//   :38  PB[w][:] = P[:, w]ᵀ·B            (P tiles from the LDS image, B in registers)
+// dp_wg4_kernel<T, MT, VAR> — fp64 n = 64, m = 16·MT: the shape whose tile grid does not fit one
+// wave (A alone is 128 fp64 registers; the one-wave kernel spills ~2–3 KB per lane there).  One
+// 256-thread workgroup per trajectory, one wave per SIMD, the same fast form and the same
+// Newton–Schulz / exact-sweep inverse as dp_riccati_kernel, with the knot's products split by the
+// n-dimension's 16-column tiles (wave w ↔ tile column w):
+//   :38  PB[w][:] = P[:, w]ᵀ·B            (P tiles from the LDS image, B from its image)
 //   :40  PA[:, w] = Pᵀ·A[:, w]             (all of P from LDS, A[:, w] in registers)
 //   :39  E tile (w mod MT, w / MT) = R + BᵀPB   (PB from its LDS image; one tile per wave)
 //   :41  G[:, w] = Bᵀ·PA[:, w]             (registers only; also to an LDS image)
-//   :42  X ≈ E⁻¹ (every wave, bitwise alike), K[:, w] = XᵀG[:, w], stored to sol.K
+//   :42  X ≈ E⁻¹ (every wave; the four verdicts are AND-ed), K[:, w] = XᵀG[:, w], stored to sol.K
 //   :51  P_ tiles (i, w), i from wave w's row list — the ten tiles of the symmetric 4×4 grid
 //        as 3, 3, 2, 2 per wave: Q + A[:, i]ᵀPA[:, w] − G[:, i]ᵀK[:, w], written to the P image
 //        at (i, w) and mirrored to (w, i) (diagonal tiles from their lower triangle), so the
 //        image stays exactly symmetric as tiles_symmetrize_lower keeps the one-wave P.
 // Four workgroup barriers per knot (after PB/PA, after E/G, the inverse's verdict vote, after
-// P_).  Registers per wave:
-// the A columns its P_ rows need (3 × 4 tiles, the first is A[:, w]), B, Q's P_ tiles, R's E
-// tile — time-invariant, loaded once.  The rollout (:66-70) is dp_rollout_full on wave 0.
-template <typename T, int MT>
+// P_).  A lives in an LDS image (the P_ rows' A columns are read from it), A[:, w] also in
+// registers; B, Q in images; R's E tile in registers.
+// VAR_TV (constrained_problem.jl:3-4: per-knot A_k, B_k, Q_k, R_k): A is double-buffered in LDS
+// (the time-invariant Q image's space — Q_k's P_ tiles come straight from HBM into the P_
+// accumulators); knot k−1's A, B and R are requested at the top of knot k and land in LDS after
+// the last reader of their buffer (A: the other buffer, after PB/PA; B: after B2; R: registers).
+// VAR_LIN (lqrx_dp_solve_linear): w = r + Bᵀp (every wave, beside PB), d = Xᵀw (every wave, its
+// own X), p ← q + Aᵀp − Gᵀd for rows 16w…16w+15 (A[:, w], G[:, w] are the wave's own tiles);
+// p is double-buffered in LDS, w and d pass from column to row layout through per-wave slots.
+// The rollout (:66-70): dp_rollout_wg4 on all four waves (an LQRX_WG4_ROLL4=0 build runs the
+// time-invariant one as dp_rollout_full on wave 0: 234.1 vs 224.4 ms at n=64 m=32 N=512 B=8192).
+// The Newton–Schulz step split over the waves (wg4_ns_split, LQRX_WG4_NS_SPLIT=1) measured
+// slower (247.5 vs 234.1 ms: one more barrier per step and 224 B of spills) and is off.
+#ifndef LQRX_WG4_NS_SPLIT
+#define LQRX_WG4_NS_SPLIT 0   // 1: the Newton–Schulz step split over the four waves (m = 32; A/B — measured slower)
+#endif
+#ifndef LQRX_WG4_ROLL4
+#define LQRX_WG4_ROLL4 1      // time-invariant four-wave kernel: the four-wave rollout (0: wave 0 alone, A/B)
+#endif
+template <typename T, int MT, int VAR>
 struct Wg4Cfg {
+    static constexpr bool TV = (VAR & VAR_TV) != 0, LIN = (VAR & VAR_LIN) != 0;
     static constexpr int NT = 4, NP = 64, MP = 16 * MT;
     // odd column strides: the compiler pairs a tile's rows into ds_read2_b64 / ds_write_b64, whose
     // 16-lane groups bank by (a/4) mod 32 — at an even stride (NP + 2) columns c and c + 8 of a tile
     // shared banks (2-way; SQ_LDS_BANK_CONFLICT ≈ a quarter of the kernel's cycles)
-    static constexpr int PL = NP + 1;                    // P, Q, B images
+    static constexpr int PL = NP + 1;                    // P, Q, A, B images
     static constexpr int CS = MP + 1;                    // PB / E / G images, aug sweep
     static constexpr int P_EL = NP * PL;
     static constexpr int AUG = 2 * MP * CS + 64 + MP;   // [E | I] sweep image + row/rinv
     static constexpr int PB_EL = (MP * PL > AUG ? MP * PL : AUG);   // PB (NP × MP, stride PL) | the sweep image
     static constexpr int E_EL = MP * CS, G_EL = NP * CS;
     static constexpr int B_EL = MP * PL;                                 // B image (NP × MP)
-#if LQRX_WG4_AIMG
-    static constexpr int LDS = 3 * P_EL + B_EL + PB_EL + E_EL + G_EL + 8;   // P, Q, A, B images
-#else
-    static constexpr int LDS = 2 * P_EL + B_EL + PB_EL + E_EL + G_EL + 8;   // P, Q, B images
-#endif
+    static constexpr int V_EL = LIN ? 2 * NP + 8 * MP : 0;               // p (×2), per-wave w, d
+    static constexpr int LDS = 3 * P_EL + B_EL + PB_EL + E_EL + G_EL + V_EL + 8;   // P, Q | A₂, A, B images
+    static_assert(LDS * sizeof(T) <= 160 * 1024, "dp_wg4_kernel LDS");
 };
 // row tile of wave w's t-th P_ tile (column tile w), −1: none
 __host__ __device__ constexpr int wg4_pn_row(int w, int t)
@@ -959,24 +971,178 @@ __device__ __forceinline__ void wg4_mtn(typename Tile<T>::acc &D, const typename
 #pragma unroll
     for (int r = 0; r < 4; ++r) D = NEG ? Tile<T>::mma_nega(M[r], Y[r], D) : Tile<T>::mma(M[r], Y[r], D);
 }
+// y += Mᵀv for one tile M (rows 16i…, this lane's column) and v in row layout (lin_rows)
+template <typename T>
+__device__ __forceinline__ T wg4_vtn(T y, const typename Tile<T>::acc &M, const T (&v)[4])
+{
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y = fma(M[r], v[r], y);
+    return y;
+}
 
+// Forward rollout (dynamic_programming.jl:66-70) on the four waves of dp_wg4_kernel: wave w owns
+// rows 16w…16w+15 of x_{k+1} = A_k x_k + B_k u_k (lane l: row 16w + (l & 15), column quarter l >> 4
+// of A's and B's columns, summed by two xor-shuffles); every wave forms the whole
+// u_k = −K_k x_k (− d_k) itself (lane l: row l mod MP of K_k, a contiguous run of its columns), so
+// the only workgroup barrier per knot publishes x_{k+1} (a double-buffered LDS vector).  K_k, d_k
+// and — time-varying — the wave's rows of A_k, B_k are requested one knot ahead.
+template <typename T, int MT, bool TV, bool LIN>
+__device__ __forceinline__ void dp_rollout_wg4(const DpArgs &a, int64_t b, T *lds, int w, int lane)
+{
+    constexpr int NP = 64, MP = 16 * MT;
+    constexpr int SU = 64 / MP, CU = NP / SU;        // lanes per K row, K columns per lane
+    constexpr int CA = NP / 4, CB = MP / 4;          // A, B columns per lane
+    const int N = a.N;
+    constexpr size_t mn = (size_t)MP * NP;
+    const bool tvab = TV && a.tv_AB;
+    const int64_t sA = tvab ? (int64_t)NP * NP : 0, sB = tvab ? (int64_t)NP * MP : 0;
+    const T *__restrict__ Kg = (const T *)a.K + (size_t)b * (size_t)(N - 1) * mn;
+    const T *__restrict__ Ag = (const T *)a.A + (size_t)b * NP * NP * (tvab ? (size_t)(N - 1) : 1);
+    const T *__restrict__ Bg = (const T *)a.B + (size_t)b * NP * MP * (tvab ? (size_t)(N - 1) : 1);
+    T *__restrict__ Xg = (T *)a.X + (size_t)b * (size_t)N * NP;
+    T *__restrict__ Ug = (T *)a.U + (size_t)b * (size_t)(N - 1) * MP;
+    const T *Dg = LIN ? (const T *)a.d + (size_t)b * (size_t)(N - 1) * MP : nullptr;
+    T *xs = lds, *us = lds + 2 * NP + w * MP;        // x_k double-buffered; this wave's u_k
+    const int iu = lane % MP, hu = lane / MP;
+    const int ix = 16 * w + (lane & 15), hx = lane >> 4;
+    T ar[CA], br[CB], arn[TV ? CA : 1], brn[TV ? CB : 1];
+    auto load_ab = [&](int kk, T *ra, T *rb) __attribute__((always_inline)) {
+        const T *Ak = Ag + (int64_t)(kk - 1) * sA + ix + (size_t)hx * CA * NP;
+        const T *Bk = Bg + (int64_t)(kk - 1) * sB + ix + (size_t)hx * CB * NP;
+#pragma unroll
+        for (int c = 0; c < CA; ++c) ra[c] = Ak[(size_t)c * NP];
+#pragma unroll
+        for (int c = 0; c < CB; ++c) rb[c] = Bk[(size_t)c * NP];
+    };
+    T kr[CU], krn[CU], dr = (T)0, drn = (T)0;
+    auto load_k = [&](int kk, T *rk, T &dd) __attribute__((always_inline)) {
+        const T *Kk = Kg + (size_t)(kk - 1) * mn + iu + (size_t)hu * CU * MP;
+#pragma unroll
+        for (int c = 0; c < CU; ++c) rk[c] = Kk[(size_t)c * MP];
+        if constexpr (LIN) dd = Dg[(size_t)(kk - 1) * MP + iu];
+    };
+    load_ab(1, ar, br);
+    load_k(1, kr, dr);
+    if (N - 1 >= 2) {
+        load_k(2, krn, drn);
+        if constexpr (TV) load_ab(2, arn, brn);
+    }
+    const T *x0 = (const T *)a.x0 + (size_t)b * NP;
+    if (w == 0) {
+        const T v = x0[lane];
+        xs[NP + lane] = v;                           // x_1 in buffer 1 (knot k reads buffer k & 1)
+        Xg[lane] = v;
+    }
+    __syncthreads();
+    for (int k = 1; k <= N - 1; ++k) {
+        const T *xc = xs + (k & 1) * NP;
+        // u = −K_k x_k (− d_k)   (dynamic_programming.jl:68)
+        T s0 = (T)0, s1 = (T)0;
+#pragma unroll
+        for (int c = 0; c < CU; c += 2) {
+            s0 = fma(kr[c], xc[hu * CU + c], s0);
+            s1 = fma(kr[c + 1], xc[hu * CU + c + 1], s1);
+        }
+        T su = s0 + s1;
+#pragma unroll
+        for (int o = MP; o < 64; o <<= 1) su += xor_shfl(su, (lane ^ o) << 2);
+        const T u = LIN ? -(su + dr) : -su;
+#pragma unroll
+        for (int c = 0; c < CU; ++c) kr[c] = krn[c];
+        dr = drn;
+        if (k + 2 <= N - 1) load_k(k + 2, krn, drn);
+        if (hu == 0) {
+            us[iu] = u;
+            if (w == 0) Ug[(size_t)(k - 1) * MP + iu] = u;
+        }
+        wsync_w();
+        // x_{k+1} = A_k x_k + B_k u_k   (:69), rows 16w…16w+15
+        T t0 = (T)0, t1 = (T)0;
+#pragma unroll
+        for (int c = 0; c < CA; c += 2) {
+            t0 = fma(ar[c], xc[hx * CA + c], t0);
+            t1 = fma(ar[c + 1], xc[hx * CA + c + 1], t1);
+        }
+#pragma unroll
+        for (int c = 0; c < CB; ++c) t1 = fma(br[c], us[hx * CB + c], t1);
+        T xn = t0 + t1;
+        xn += xor_shfl(xn, (lane ^ 16) << 2);
+        xn += xor_shfl(xn, (lane ^ 32) << 2);
+        if constexpr (TV) {
+#pragma unroll
+            for (int c = 0; c < CA; ++c) ar[c] = arn[c];
+#pragma unroll
+            for (int c = 0; c < CB; ++c) br[c] = brn[c];
+            if (k + 2 <= N - 1) load_ab(k + 2, arn, brn);
+        }
+        if (lane < 16) {
+            xs[((k + 1) & 1) * NP + ix] = xn;
+            Xg[(size_t)k * NP + ix] = xn;
+        }
+        __syncthreads();
+    }
+}
+
+// Newton–Schulz on the four waves (MT = 2, ns_refine's step split by output tile): wave w owns
+// tile (w & 1, w >> 1) of R = I − EᵀX and of X + XᵀR; the residual tiles and their magnitude keys
+// meet in LDS (rimg, keys), the new X in ximg — every wave reads the same four keys, so the
+// verdict is workgroup-uniform by construction, and each wave issues a quarter of the refinement
+// (16 instead of 64 MFMAs per step).  X: the full inverse in every wave, in and out.
 template <typename T, int MT>
+__device__ __forceinline__ bool wg4_ns_split(typename Tile<T>::acc (&X)[MT][MT], const T *eimg,
+                                             T *rimg, T *ximg, int *keys, int ld, int w, int lane)
+{
+    static_assert(MT == 2, "one output tile per wave");
+    using acc = typename Tile<T>::acc;
+    const int ti = w & 1, tj = w >> 1;
+    for (int it = 0; it < NsTol<T>::it; ++it) {
+        acc R;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) R[r] = (ti == tj && Tile<T>::row(lane, r) == tcol(lane)) ? (T)1 : (T)0;
+#pragma unroll
+        for (int l = 0; l < MT; ++l)                                               // R = I − EᵀX
+            wg4_mtn<T, true>(R, wg4_tload(eimg + 16 * l + 16 * ti * ld, ld, lane), X[l][tj]);
+        int key = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) key = max(key, mag_key(R[r]));
+        key = wave_max_uniform_i(key);
+        wg4_tstore(rimg + 16 * ti + 16 * tj * ld, ld, R, lane);
+        if (lane == 0) keys[w] = key;
+        __syncthreads();
+        key = max(max(keys[0], keys[1]), max(keys[2], keys[3]));
+        const T rho = (T)(16 * MT) * key_bound(key, (T)0);
+        if (rho <= NsTol<T>::v) return true;                    // X already at working precision
+        if (!(rho < (T)1)) return false;                        // no contraction (or NaN): exact sweep
+        acc Xn = X[ti][tj];
+#pragma unroll
+        for (int l = 0; l < MT; ++l) wg4_mtn<T>(Xn, X[l][ti], wg4_tload(rimg + 16 * l + 16 * tj * ld, ld, lane));
+        wg4_tstore(ximg + 16 * ti + 16 * tj * ld, ld, Xn, lane);   // X + XᵀR
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < MT; ++j) X[i][j] = wg4_tload(ximg + 16 * i + 16 * j * ld, ld, lane);
+        if (rho <= NsTol<T>::one_step) return true;             // new residual ≤ cond·ρ² ≪ eps
+    }
+    return false;
+}
+
+template <typename T, int MT, int VAR>
 __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
 {
-    using C = Wg4Cfg<T, MT>;
+    using C = Wg4Cfg<T, MT, VAR>;
     using acc = typename Tile<T>::acc;
+    constexpr bool TV = C::TV, LIN = C::LIN;
     constexpr int NT = C::NT, NP = C::NP, MP = C::MP, PL = C::PL, CS = C::CS;
+    constexpr int BPT = NP * MP / 256;           // B elements per thread (TV staging)
     __shared__ T lds[C::LDS];
-    T *Pim = lds, *Qim = Pim + C::P_EL, *Bim = Qim + C::P_EL, *PBim = Bim + C::B_EL, *Eim = PBim + C::PB_EL;
-    T *Gim = Eim + C::E_EL;
-#if LQRX_WG4_AIMG
-    T *Aim = Gim + C::G_EL;              // A (the P_ rows' A columns are read from here)
-    int *flag = (int *)(Aim + C::P_EL);
-#else
-    int *flag = (int *)(Gim + C::G_EL);
-#endif
+    T *Pim = lds, *Q2 = Pim + C::P_EL, *Bim = Q2 + C::P_EL, *PBim = Bim + C::B_EL, *Eim = PBim + C::PB_EL;
+    T *Gim = Eim + C::E_EL, *Aim = Gim + C::G_EL, *vec = Aim + C::P_EL;
+    int *flag = (int *)(vec + C::V_EL);
+    T *Qim = Q2;                         // time-invariant Q; time-varying: A's second buffer
     T *aug = PBim;                       // the exact sweep reuses the PB image (read before it)
     int *vote = flag + 4;                // per-wave Newton–Schulz verdicts (flag[0]: the sweep's)
+    T *pimg = vec, *wslot = vec + 2 * NP, *dslot = wslot + 4 * MP;   // VAR_LIN vectors
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -984,34 +1150,45 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
     if (b >= a.batch) return;            // whole workgroup
     const int N = a.N;
     constexpr size_t nn = (size_t)NP * NP, nm = (size_t)NP * MP, mm = (size_t)MP * MP;
-    const T *Ab = (const T *)a.A + b * nn, *Bb = (const T *)a.B + b * nm;
-    const T *Qb = (const T *)a.Q + b * nn, *Rb = (const T *)a.R + b * mm;
+    // per-trajectory bases; time-varying fields hold N−1 knots (knot k at index k−1)
+    const size_t kAB = (TV && a.tv_AB) ? (size_t)(N - 1) : 1, kQR = (TV && a.tv_QR) ? (size_t)(N - 1) : 1;
+    const size_t sA = kAB > 1 ? nn : 0, sB = kAB > 1 ? nm : 0, sQ = kQR > 1 ? nn : 0, sR = kQR > 1 ? mm : 0;
+    const T *Ab = (const T *)a.A + b * nn * kAB, *Bb = (const T *)a.B + b * nm * kAB;
+    const T *Qb = (const T *)a.Q + b * nn * kQR, *Rb = (const T *)a.R + b * mm * kQR;
+    auto abuf = [&](int k) { return (TV && (k & 1)) ? Q2 : Aim; };   // knot k's A image
+    const size_t k0 = TV ? (size_t)(N - 2) : 0;                     // first backward knot k = N − 1
+    // linear terms: q_k, r_k (knot stride with Q, R), outputs d_k and p (p_1 or every p_k)
+    const size_t sq = (LIN && kQR > 1) ? (size_t)NP : 0, sr = (LIN && kQR > 1) ? (size_t)MP : 0;
+    const T *qg = LIN ? (const T *)a.q + (size_t)b * NP * kQR : nullptr;
+    const T *rg = LIN ? (const T *)a.r + (size_t)b * MP * kQR : nullptr;
+    T *dg = LIN ? (T *)a.d + (size_t)b * (size_t)(N - 1) * MP : nullptr;
+    T *pallv = (LIN && a.p_all) ? (T *)a.p + (size_t)b * (size_t)N * NP : nullptr;
 
-    // time-invariant register operands
-#if LQRX_WG4_AIMG
-    constexpr int NAR = 1;               // A[:, w] in registers, the other P_ rows' columns from LDS
-#else
-    constexpr int NAR = 3;
-#endif
-    acc Ar[NAR][NT], Rw = acc{0, 0, 0, 0};
-#pragma unroll
-    for (int t = 0; t < NAR; ++t) {
-        const int i = wg4_pn_row(w, t) < 0 ? 0 : wg4_pn_row(w, t);
-#pragma unroll
-        for (int k = 0; k < NT; ++k) Ar[t][k] = wg4_tload(Ab + 16 * k + (size_t)16 * i * NP, NP, lane);  // A[k][i]
-    }
+    acc Ar[NT], Rw = acc{0, 0, 0, 0};
     auto Bt = [&](int kk, int j) { return wg4_tload(Bim + 16 * kk + 16 * j * PL, PL, lane); };   // B[kk][j]
     const int ei = w % MT, ej = w / MT;          // this wave's E tile (w < MT²)
-    if (w < MT * MT) Rw = wg4_tload(Rb + 16 * ei + (size_t)16 * ej * MP, MP, lane);
-    // P = Qf (:58) into the image; Q (the P_ accumulators' start) into its own
-    for (int e = tid; e < NP * NP; e += 256) {
-        Pim[(e % NP) + (e / NP) * PL] = ((const T *)a.Qf)[b * nn + e];
-        Qim[(e % NP) + (e / NP) * PL] = Qb[e];
+    if (w < MT * MT) Rw = wg4_tload(Rb + k0 * sR + 16 * ei + (size_t)16 * ej * MP, MP, lane);
+    if constexpr (!TV) {
+#pragma unroll
+        for (int kk = 0; kk < NT; ++kk) Ar[kk] = wg4_tload(Ab + 16 * kk + (size_t)16 * w * NP, NP, lane);  // A[kk][w]
     }
-    for (int e = tid; e < NP * MP; e += 256) Bim[(e % NP) + (e / NP) * PL] = Bb[e];
-#if LQRX_WG4_AIMG
-    for (int e = tid; e < NP * NP; e += 256) Aim[(e % NP) + (e / NP) * PL] = Ab[e];
-#endif
+    // P = Qf (:58) into the image; Q (the P_ accumulators' start) into its own; A, B of knot N−1
+    {
+        T *A0 = abuf(N - 1);
+        for (int e = tid; e < NP * NP; e += 256) {
+            Pim[(e % NP) + (e / NP) * PL] = ((const T *)a.Qf)[b * nn + e];
+            if constexpr (!TV) Qim[(e % NP) + (e / NP) * PL] = Qb[e];
+            A0[(e % NP) + (e / NP) * PL] = Ab[k0 * sA + e];
+        }
+    }
+    for (int e = tid; e < NP * MP; e += 256) Bim[(e % NP) + (e / NP) * PL] = Bb[k0 * sB + e];
+    if constexpr (LIN) {
+        if (tid < NP) {
+            const T v = ((const T *)a.qf)[(size_t)b * NP + tid];          // p = qf
+            pimg[(N & 1) * NP + tid] = v;                                // p_k in buffer k & 1
+            if (pallv) pallv[(size_t)(N - 1) * NP + tid] = v;
+        }
+    }
     T *Pall = a.p_all ? (T *)a.P + (size_t)b * nn * N : nullptr;
     T *Kb = (T *)a.K + (size_t)b * (size_t)(N - 1) * nm;
     int info = 0;
@@ -1025,6 +1202,29 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
         for (int e = tid; e < NP * NP; e += 256) Pall[(size_t)(N - 1) * nn + e] = Pim[(e % NP) + (e / NP) * PL];
 
     for (int k = N - 1; k >= 1; --k) {           // :61
+        T *Acur = abuf(k);
+        // time-varying: knot k−1's A, B (this thread's elements) and R tile, requested now
+        T An[TV ? 16 : 1], Bn[TV ? BPT : 1];
+        acc Rn = Rw;
+        if constexpr (TV) {
+#pragma unroll
+            for (int kk = 0; kk < NT; ++kk) Ar[kk] = wg4_tload(Acur + 16 * kk + 16 * w * PL, PL, lane);
+            if (k > 1) {
+                const T *Ak = Ab + (size_t)(k - 2) * sA, *Bk = Bb + (size_t)(k - 2) * sB;
+#pragma unroll
+                for (int s = 0; s < 16; ++s) An[s] = Ak[tid + 256 * s];
+#pragma unroll
+                for (int s = 0; s < BPT; ++s) Bn[s] = Bk[tid + 256 * s];
+                if (w < MT * MT) Rn = wg4_tload(Rb + (size_t)(k - 2) * sR + 16 * ei + (size_t)16 * ej * MP, MP, lane);
+            }
+        }
+        // linear terms: w = Bᵀp_{k+1} partials (p_{k+1} read per row tile, in row layout)
+        const T *pk1 = pimg + ((k + 1) & 1) * NP;
+        T wv[LIN ? MT : 1];
+        if constexpr (LIN) {
+#pragma unroll
+            for (int j = 0; j < MT; ++j) wv[j] = (T)0;
+        }
         // :38, :40 — one pass over the P image: PA[:, w] and PB[w][:]
         acc PA[NT], PB[MT];
 #pragma unroll
@@ -1037,13 +1237,32 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
 #pragma unroll
             for (int i = 0; i < NT; ++i) Pt[i] = wg4_tload(Pim + 16 * kk + 16 * i * PL, PL, lane);   // P[kk][i]
 #pragma unroll
-            for (int i = 0; i < NT; ++i) wg4_mtn<T>(PA[i], Pt[i], Ar[0][kk]);
+            for (int i = 0; i < NT; ++i) wg4_mtn<T>(PA[i], Pt[i], Ar[kk]);
             const acc Pw = wg4_tload(Pim + 16 * kk + 16 * w * PL, PL, lane);                     // P[kk][w]
+            T prow[4];
+            if constexpr (LIN) {
 #pragma unroll
-            for (int j = 0; j < MT; ++j) wg4_mtn<T>(PB[j], Pw, Bt(kk, j));
+                for (int r = 0; r < 4; ++r) prow[r] = pk1[16 * kk + Tile<T>::row(lane, r)];
+            }
+#pragma unroll
+            for (int j = 0; j < MT; ++j) {
+                const acc Bkj = Bt(kk, j);
+                wg4_mtn<T>(PB[j], Pw, Bkj);
+                if constexpr (LIN) wv[j] = wg4_vtn<T>(wv[j], Bkj, prow);                          // Bᵀp
+            }
         }
 #pragma unroll
         for (int j = 0; j < MT; ++j) wg4_tstore(PBim + 16 * w + 16 * j * PL, PL, PB[j], lane);
+        if constexpr (TV) {
+            if (k > 1) {                                   // knot k−1's A into the other buffer
+                T *An_img = abuf(k - 1);
+#pragma unroll
+                for (int s = 0; s < 16; ++s) {
+                    const int e = tid + 256 * s;
+                    An_img[(e % NP) + (e / NP) * PL] = An[s];
+                }
+            }
+        }
         __syncthreads();                                   // B1: PB image complete, P image read
         // :39 E tile, :41 G[:, w]
         if (w < MT * MT) {
@@ -1063,13 +1282,23 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
             for (int kk = 0; kk < NT; ++kk) wg4_mtn<T>(G[c], Bt(kk, c), PA[kk]);
             wg4_tstore(Gim + 16 * c + 16 * w * CS, CS, G[c], lane);
         }
-        __syncthreads();                                   // B2: E and G images complete
+        __syncthreads();                                   // B2: E and G images complete, B read
+        acc Qt[TV ? 3 : 1];
+        if constexpr (TV) {
+            if (k > 1) {                                   // knot k−1's B (B's last reader was G)
+#pragma unroll
+                for (int s = 0; s < BPT; ++s) {
+                    const int e = tid + 256 * s;
+                    Bim[(e % NP) + (e / NP) * PL] = Bn[s];
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {                  // Q_k's P_ tiles straight from HBM
+                const int i = wg4_pn_row(w, t) < 0 ? w : wg4_pn_row(w, t);
+                Qt[t] = wg4_tload(Qb + (size_t)(k - 1) * sQ + 16 * i + (size_t)16 * w * NP, NP, lane);
+            }
+        }
         // :42 X ≈ E⁻¹ (warm-started Newton–Schulz; the exact sweep on wave 0 otherwise)
-        acc E[MT][MT];
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-            for (int j = 0; j < MT; ++j) E[i][j] = wg4_tload(Eim + 16 * i + 16 * j * CS, CS, lane);
         bool have = false;
         if (k < N - 1) {
             // warm start 2X_{k+1} − X_{k+2}; Xp takes X_{k+1} before the refinement
@@ -1084,21 +1313,33 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
                     Xi[i][j] = (T)2 * x1 - Xp[i][j];
                     Xp[i][j] = x1;
                 }
-            have = ns_refine<T, MT>(Xi, E, Id, lane);
-            // workgroup-uniform verdict by construction (the branch below holds a barrier): each
-            // wave posts its own Newton–Schulz verdict, every wave takes the AND of all four — no
-            // reliance on the four refinements agreeing bitwise.  (The slots are rewritten only
-            // after this knot's B3, which every wave reaches after reading them.)
-            if (lane == 0) vote[w] = have ? 1 : 0;
-            __syncthreads();
-            have = (vote[0] & vote[1] & vote[2] & vote[3]) != 0;
+            if constexpr (MT == 2 && LQRX_WG4_NS_SPLIT) {
+                // split over the waves; the PB image is free after B2 (the exact sweep below, which
+                // reuses it, starts only once every wave has left the refinement)
+                have = wg4_ns_split<T, MT>(Xi, Eim, PBim, PBim + MP * CS, vote, CS, w, lane);
+            } else {
+                acc E[MT][MT];
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < MT; ++j) E[i][j] = wg4_tload(Eim + 16 * i + 16 * j * CS, CS, lane);
+                have = ns_refine<T, MT>(Xi, E, Id, lane);
+                // workgroup-uniform verdict by construction (the branch below holds a barrier): each
+                // wave posts its own Newton–Schulz verdict, every wave takes the AND of all four — no
+                // reliance on the four refinements agreeing bitwise.  (The slots are rewritten only
+                // after this knot's B3, which every wave reaches after reading them.)
+                if (lane == 0) vote[w] = have ? 1 : 0;
+                __syncthreads();
+                have = (vote[0] & vote[1] & vote[2] & vote[3]) != 0;
+            }
         }
         if (!have) {                                       // uniform (k == N − 1, or the vote above)
             if (w == 0) {
 #pragma unroll
                 for (int i = 0; i < MT; ++i)
 #pragma unroll
-                    for (int j = 0; j < MT; ++j) wg4_tstore(aug + 16 * i + 16 * j * CS, CS, E[i][j], lane);
+                    for (int j = 0; j < MT; ++j)
+                        wg4_tstore(aug + 16 * i + 16 * j * CS, CS, wg4_tload(Eim + 16 * i + 16 * j * CS, CS, lane), lane);
                 wsync_w();
                 const bool ok = aug_ldl_forward<T, MP, 0, CS, 0>(aug, lane);
                 if (lane == 0) *flag = ok ? 1 : 0;
@@ -1139,20 +1380,55 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
             for (int r = 0; r < 4; ++r)
                 Kb[(size_t)(k - 1) * nm + 16 * c + Tile<T>::row(lane, r) + (size_t)(16 * w + tcol(lane)) * MP] = Kt[c][r];
         }
+        if constexpr (LIN) {
+            // d = Xᵀw (w = r + Bᵀp, the companion of K = XᵀG); p_k rows 16w… = q + Aᵀp − Gᵀd
+            T *ws_ = wslot + w * MP, *ds_ = dslot + w * MP;
+#pragma unroll
+            for (int j = 0; j < MT; ++j) {
+                const T wj = rg[(size_t)(k - 1) * sr + 16 * j + tcol(lane)] + lin_rowsum(wv[j]);   // r + Bᵀp
+                if (lane < 16) ws_[16 * j + lane] = wj;
+            }
+            wsync_w();
+            T wrow[MT][4], dv[MT];
+            lin_rows<T, MT>(wrow, ws_, lane);
+#pragma unroll
+            for (int j = 0; j < MT; ++j) {
+                dv[j] = (T)0;
+#pragma unroll
+                for (int i = 0; i < MT; ++i) dv[j] = wg4_vtn<T>(dv[j], Xi[i][j], wrow[i]);
+                dv[j] = lin_rowsum(dv[j]);
+                if (lane < 16) {
+                    ds_[16 * j + lane] = dv[j];
+                    if (w == 0) dg[(size_t)(k - 1) * MP + 16 * j + lane] = dv[j];
+                }
+            }
+            wsync_w();
+            T drow[MT][4];
+            lin_rows<T, MT>(drow, ds_, lane);
+            T ap = (T)0, gd = (T)0, prow[NT][4];
+            lin_rows<T, NT>(prow, pk1, lane);
+#pragma unroll
+            for (int kk = 0; kk < NT; ++kk) ap = wg4_vtn<T>(ap, Ar[kk], prow[kk]);
+#pragma unroll
+            for (int c = 0; c < MT; ++c) gd = wg4_vtn<T>(gd, G[c], drow[c]);
+            const T pn = qg[(size_t)(k - 1) * sq + 16 * w + tcol(lane)] + lin_rowsum(ap) - lin_rowsum(gd);
+            if (lane < 16) {
+                pimg[(k & 1) * NP + 16 * w + lane] = pn;
+                if (pallv) pallv[(size_t)(k - 1) * NP + 16 * w + lane] = pn;
+            }
+        }
         // :51 P_ tiles (i, w) = Q + A[:, i]ᵀPA[:, w] − G[:, i]ᵀK[:, w] → the P image, mirrored
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
             const int i = wg4_pn_row(w, t);
             if (i < 0) continue;
-            acc Pn = wg4_tload(Qim + 16 * i + 16 * w * PL, PL, lane);                        // Q[i][w]
+            acc Pn;
+            if constexpr (TV) Pn = Qt[t];
+            else Pn = wg4_tload(Qim + 16 * i + 16 * w * PL, PL, lane);                           // Q[i][w]
 #pragma unroll
             for (int kk = 0; kk < NT; ++kk) {
-#if LQRX_WG4_AIMG
-                const acc At = t == 0 ? Ar[0][kk] : wg4_tload(Aim + 16 * kk + 16 * i * PL, PL, lane);  // A[kk][i]
+                const acc At = t == 0 ? Ar[kk] : wg4_tload(Acur + 16 * kk + 16 * i * PL, PL, lane);  // A[kk][i]
                 wg4_mtn<T>(Pn, At, PA[kk]);
-#else
-                wg4_mtn<T>(Pn, Ar[t][kk], PA[kk]);
-#endif
             }
 #pragma unroll
             for (int c = 0; c < MT; ++c)
@@ -1170,21 +1446,40 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
                 }
             }
         }
+        if constexpr (TV) Rw = Rn;
         __syncthreads();                                   // B3: P_ image complete
         if (Pall)
             for (int e = tid; e < NP * NP; e += 256) Pall[(size_t)(k - 1) * nn + e] = Pim[(e % NP) + (e / NP) * PL];
     }
     if (!a.p_all)
         for (int e = tid; e < NP * NP; e += 256) ((T *)a.P)[b * nn + e] = Pim[(e % NP) + (e / NP) * PL];
+    if constexpr (LIN) {
+        if (!a.p_all && tid < NP) ((T *)a.p)[(size_t)b * NP + tid] = pimg[NP + tid];   // p_1 (buffer 1)
+    }
     if (a.info && tid == 0) a.info[b] = info;
-    // rollout on wave 0 once every wave's K stores are visible to it
+    // rollout once every wave's K (and d) stores are visible to the waves that read them
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (w == 0) {
+    if constexpr (TV || LQRX_WG4_ROLL4) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        dp_rollout_full<T, NT, MT, LQRX_DP_KD, false>(a, b, lds, lane);
+        dp_rollout_wg4<T, MT, TV, LIN>(a, b, lds, w, lane);
+    } else if (w == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        dp_rollout_full<T, NT, MT, LQRX_DP_KD, LIN>(a, b, lds, lane);
     }
+}
+
+template <int MT>
+static hipError_t launch_wg4(const DpArgs &a, hipStream_t s)
+{
+    dim3 grid((unsigned)a.batch), block(256);
+    const bool tv = a.tv_AB || a.tv_QR;
+    if (a.lin && tv) hipLaunchKernelGGL((dp_wg4_kernel<double, MT, VAR_TV | VAR_LIN>), grid, block, 0, s, a);
+    else if (a.lin) hipLaunchKernelGGL((dp_wg4_kernel<double, MT, VAR_LIN>), grid, block, 0, s, a);
+    else if (tv) hipLaunchKernelGGL((dp_wg4_kernel<double, MT, VAR_TV>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((dp_wg4_kernel<double, MT, 0>), grid, block, 0, s, a);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ launcher
@@ -1233,16 +1528,18 @@ hipError_t dp_launch(const DpArgs &a, hipStream_t s)
     if (a.dtype == 0) {
         if (nt <= 1 && mt <= 1) return launch_dp_tv<double, 1, 1>(a, s);
         if (nt <= 2 && mt <= 1) return launch_dp_tv<double, 2, 1, LQRX_DP_WAVES, LQRX_DP_VAR>(a, s);
+        // 2×2 fp64 tiles do not fit 256 registers (≈ 450 live): the 2-wave launch bound compiles
+        // to occupancy 1 (hipcc: "desired occupancy 2, final occupancy 1"; 44–60 B of spills).
+        // Declaring one wave per SIMD instead (launch_dp_tv<double, 2, 2, 1>) gave an allocation
+        // with 124 B of spills whose launch ended the process with SIGABRT on the box (round 6,
+        // profiles/r06/d) — kept at the launch bound that passes, see DESIGN §3.1
         if (nt <= 2 && mt <= 2) return launch_dp_tv<double, 2, 2>(a, s);
-        // n = 64, m ∈ {16, 32}, time-invariant, no linear terms: four waves per trajectory
-        // (LQRX_DP_WG4=0 in the environment: the one-wave kernel, for A/B runs and tests)
+        // n = 64, m ∈ {16, 32}: four waves per trajectory — time-invariant or time-varying, with
+        // or without linear terms (LQRX_DP_WG4=0 in the environment: the one-wave kernel, for A/B
+        // runs and tests)
         static const bool wg4 = [] { const char *e = std::getenv("LQRX_DP_WG4"); return LQRX_DP_WG4 && !(e && *e == '0'); }();
-        if (wg4 && a.n == 64 && (a.m == 16 || a.m == 32) && !a.lin && !a.tv_AB && !a.tv_QR) {
-            dim3 grid((unsigned)a.batch), block(256);
-            if (a.m == 16) hipLaunchKernelGGL((dp_wg4_kernel<double, 1>), grid, block, 0, s, a);
-            else hipLaunchKernelGGL((dp_wg4_kernel<double, 2>), grid, block, 0, s, a);
-            return hipGetLastError();
-        }
+        if (wg4 && a.n == 64 && (a.m == 16 || a.m == 32))
+            return a.m == 16 ? launch_wg4<1>(a, s) : launch_wg4<2>(a, s);
         if (nt <= 4 && mt <= 2) return launch_dp_tv<double, 4, 2, 1>(a, s);   // n ≤ 64: 1 wave/SIMD
     } else {
         if (nt <= 1 && mt <= 1) return launch_dp_tv<float, 1, 1>(a, s);

@@ -100,6 +100,14 @@ def test_cfg5_full_batch_parity_f32(lqrx, oracle, gpu_ok):
     assert max(errs.values()) <= TOL32_N512
 
 
+def test_dp64_wg4_full_batch_parity(lqrx, oracle, gpu_ok):
+    """fp64 n=64 m=32 N=512 at the bench batch B=8192 on the four-wave kernel
+    (dp_wg4_kernel<double, 2>): whole-batch device scan, 24 strided
+    trajectories (0 and 8191 included) against the fp64 oracle."""
+    errs = full_size_case(lqrx, oracle, 64, 32, 512, 8192, True, 24, seed=20260106)
+    assert max(errs.values()) <= TOL64, errs
+
+
 def kkt_full_size_case(lqrx, oracle, f64, B, nsample, seed):
     """configs[4]'s KKT half at its full batch: the trajectory structure n=64 m=32 N=512
     generated in HBM (206 GB of Y at B=8192 fp32 / B=4096 fp64 — past host memory), solved

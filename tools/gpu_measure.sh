@@ -146,7 +146,8 @@ recipe_r6lines() {   # the lines whose kernels changed in rou
     sub tv64 kt $DP64TV && sub lin64 kt $DP64 --linear
 }
 recipe_r6dp64() {   # the fp64 n = 64 DP surface: its tests, then plain / TV / LIN lines with traffic
-    sub t pytest tests/test_dp_gpu.py tests/test_dp_linear_gpu.py tests/test_dp_lane_gpu.py &&
+    sub t pytest tests/test_dp_gpu.py tests/test_dp_wg4_gpu.py tests/test_dp_linear_gpu.py tests/test_dp_lane_gpu.py \
+        tests/test_full_size_gpu.py::test_dp64_wg4_full_batch_parity &&
     sub dp64 prof $DP64 && sub tv64 prof $DP64TV && sub lin64 prof $DP64 --linear
 }
 recipe_list() { declare -F | sed -n 's/^declare -f recipe_//p'; }
