@@ -434,6 +434,9 @@ __device__ __forceinline__ float qbcast(float v)
 template <int R, typename T>
 __device__ __forceinline__ T qfrom(T v) { return qbcast<R | (R << 2) | (R << 4) | (R << 6)>(v); }
 
+#ifndef LQRX_QUAD_RCP
+#define LQRX_QUAD_RCP 1         // m = 1: K = G·rcp(E) instead of the two potrs scalings by rsq(E) (0: A/B)
+#endif
 #ifndef LQRX_QUAD_PB_REPL
 #define LQRX_QUAD_PB_REPL 0     // A/B: 1 = PB = P·B replicated in every lane of the quad (round 4)
 #endif
@@ -590,6 +593,16 @@ __global__ __launch_bounds__(64) void dp_quad_kernel(const DpArgs a)
 #pragma unroll
             for (int p = i + 1; p < MP; ++p) s = fma(-L[p][i], Kq[p], s);
             Kq[i] = s * Linv[i];
+        }
+        if constexpr (MP == 1 && sizeof(T) == 8 && LQRX_QUAD_RCP) {
+            // m = 1: potrs is K = G/E.  1/E as v_rcp + one Newton step (≈ 2e-15 relative, rcp_nr)
+            // is 3 fp64 instructions where 1/√E (v_rsq + two Newton steps) and the two scalings
+            // by it took 9: the backward knot is VALU-issue-bound (≈ 80 VALU per knot on one wave
+            // per SIMD, tools/chain_len.py), so the 6 instructions are what it saves.  The pivot
+            // test and the L used by the linear terms are unchanged.  fp64 only: in fp32 the
+            // random-problem parity bound of test_lane_parity_f32 is conditioning-tight and the
+            // float rcp step moved it past its limit.
+            Kq[0] = Gq[0] * rcp_nr(E[0][0]);
         }
         if (q < n) {
             T *Kk = Kb + ((int64_t)(k - 1) * nm + q * m) * es;    // sol.K[k] column q
