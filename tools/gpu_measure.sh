@@ -150,6 +150,12 @@ recipe_r6dp64() {   # the fp64 n = 64 DP surface: its tests, then plain / TV / L
         tests/test_full_size_gpu.py::test_dp64_wg4_full_batch_parity &&
     sub dp64 prof $DP64 && sub tv64 prof $DP64TV && sub lin64 prof $DP64 --linear
 }
+recipe_r6close() {   # round-6 closing set: suite + smoke, every line whose kernel source changed this
+                     # round (lqrx_dp.hip, lqrx_dp_lane.hip, lqrx_kkt_wg.hip) with traffic, cfg3 for the record
+    sub t tests && sub cfg4 prof && sub cfg5 prof --n 64 --m 32 --N 512 --batch 8192 --dtype f32 &&
+    sub dp64 prof $DP64 && sub cfg2 prof --workload cartpole && sub tv prof --tv && sub lin prof --linear &&
+    sub wg96 prof $WG96 && sub cfg3 kt --workload kkt && sub kkt32 kt $CFG4KKT
+}
 recipe_list() { declare -F | sed -n 's/^declare -f recipe_//p'; }
 
 case "$MODE" in
