@@ -438,13 +438,28 @@ size_t kw_elems(const KktArgs &a, const int32_t *n1, const int32_t *p, const int
 // per-launch scratch caps: the library's own pool takes up to 24 GiB (n = 96: ~10 MB per
 // trajectory — the B = 2048 batch in one launch instead of five under-filled ones) and halves
 // on an out-of-memory; lqrx_kkt_workspace_size quotes the round-4 4 GiB, so a caller-owned
-// workspace stays modest (the launch then runs the batch in more chunks)
+// workspace stays modest (the launch then runs the batch in more chunks) — but never less than
+// one full residency of the device (kw_resident: 2 workgroups per CU): a chunk below that leaves
+// CUs idle in every launch (round 6: 4 GiB = 410 trajectories of n = 96 per launch on 512 slots
+// took the B = 2048 line 131 → 162 ms, profiles/r06/m)
 constexpr int64_t KW_POOL_CAP = (int64_t)24 << 30, KW_WS_CAP = (int64_t)4 << 30;
 
-int64_t kw_chunk(const KktArgs &a, size_t per_bytes, int64_t cap_bytes)
+// workgroups of kkt_wg_kernel the current device holds at once (launch bounds: 2 per CU)
+int64_t kw_resident()
 {
-    // chunks of at most cap_bytes of per-trajectory scratch, evened out over the launches
-    const int64_t cap = std::max<int64_t>(1, cap_bytes / (int64_t)per_bytes);
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    (void)hipGetLastError();
+    return 2 * (int64_t)std::max(cus, 1);
+}
+
+int64_t kw_chunk(const KktArgs &a, size_t per_bytes, int64_t cap_bytes, bool full = false)
+{
+    // chunks of at most cap_bytes of per-trajectory scratch (full: at least one device residency),
+    // evened out over the launches
+    int64_t cap = std::max<int64_t>(1, cap_bytes / (int64_t)per_bytes);
+    if (full) cap = std::max(cap, kw_resident());
     const int64_t nl = (a.batch + cap - 1) / cap;
     int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(a.batch, (a.batch + nl - 1) / nl));
     if (const char *ev = std::getenv("LQRX_KKT_WG_CHUNK"))   // tests: force the multi-chunk path
@@ -467,7 +482,7 @@ size_t kkt_wg_scratch_bytes(const KktArgs &a, const int32_t *n1, const int32_t *
 {
     if (a.batch == 0 || !kkt_wg_supported(a, n1, p, n2, w)) return 0;
     const size_t per = kw_elems(a, n1, p, n2, w) * (a.dtype == 0 ? 8 : 4);
-    return per * (size_t)kw_chunk(a, per, KW_WS_CAP);
+    return per * (size_t)kw_chunk(a, per, KW_WS_CAP, true);
 }
 
 hipError_t kkt_wg_launch(const KktArgs &a, const int32_t *n1, const int32_t *p, const int32_t *n2, const int32_t *w,
