@@ -921,6 +921,9 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
 #ifndef LQRX_WG4_NS_SPLIT
 #define LQRX_WG4_NS_SPLIT 0   // 1: the Newton–Schulz step split over the four waves (m = 32; A/B — measured slower)
 #endif
+#ifndef LQRX_WG4_NS_ONE
+#define LQRX_WG4_NS_ONE 1     // m = 32, time-invariant: the inverse on wave 3, the others' P_ A-parts meanwhile (0: A/B)
+#endif
 #ifndef LQRX_WG4_ROLL4
 #define LQRX_WG4_ROLL4 1      // time-invariant four-wave kernel: the four-wave rollout (0: wave 0 alone, A/B)
 #endif
@@ -946,6 +949,13 @@ struct Wg4Cfg {
 __host__ __device__ constexpr int wg4_pn_row(int w, int t)
 {
     constexpr int tab[4][3] = {{0, 1, 2}, {1, 2, 3}, {2, 3, -1}, {3, 0, -1}};
+    return tab[w][t];
+}
+// the same ten tiles when wave 3 runs the knot's Newton–Schulz inverse alone (wg4 "NS on one
+// wave", m = 32): 3, 3, 3, 1 — each pair {i, j} is formed by one of its two column waves
+__host__ __device__ constexpr int wg4_pn_row1(int w, int t)
+{
+    constexpr int tab[4][3] = {{0, 1, 3}, {1, 2, 3}, {2, 0, 3}, {3, -1, -1}};
     return tab[w][t];
 }
 
@@ -1298,9 +1308,61 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
                 Qt[t] = wg4_tload(Qb + (size_t)(k - 1) * sQ + 16 * i + (size_t)16 * w * NP, NP, lane);
             }
         }
+        // m = 32, time-invariant (NS1): wave 3 alone refines X ≈ E⁻¹ and publishes it through the free
+        // PB image while waves 0–2 form the K-independent part Q + A[:, i]ᵀPA[:, w] of their three
+        // P_ tiles — the knot's critical path drops from 16 + 4 + 18 tile products (inverse in every
+        // wave, 3/3/2/2 P_ tiles) to 16 + 4 + 6 (3/3/3/1 tiles, wg4_pn_row1)
+        constexpr bool NS1 = MT == 2 && !TV && LQRX_WG4_NS_ONE;
+        acc PnA[NS1 ? 3 : 1];
+        if constexpr (NS1) {
+            if (w != 3) {
+#pragma unroll
+                for (int t = 0; t < 3; ++t) {
+                    const int i = wg4_pn_row1(w, t);
+                    PnA[t] = wg4_tload(Qim + 16 * i + 16 * w * PL, PL, lane);                     // Q[i][w]
+#pragma unroll
+                    for (int kk = 0; kk < NT; ++kk) {
+                        const acc At = t == 0 ? Ar[kk] : wg4_tload(Acur + 16 * kk + 16 * i * PL, PL, lane);
+                        wg4_mtn<T>(PnA[t], At, PA[kk]);
+                    }
+                }
+            }
+        }
         // :42 X ≈ E⁻¹ (warm-started Newton–Schulz; the exact sweep on wave 0 otherwise)
         bool have = false;
-        if (k < N - 1) {
+        if (NS1 && k < N - 1) {
+            T *Ximg = PBim;                              // free after B2 (the sweep reuses it only when !have)
+            if (w == 3) {
+                acc Id[MT][MT], E[MT][MT];
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < MT; ++j) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) Id[i][j][r] = (i == j && Tile<T>::row(lane, r) == tcol(lane)) ? (T)1 : (T)0;
+                        E[i][j] = wg4_tload(Eim + 16 * i + 16 * j * CS, CS, lane);
+                        const acc x1 = Xi[i][j];
+                        Xi[i][j] = (T)2 * x1 - Xp[i][j];
+                        Xp[i][j] = x1;
+                    }
+                have = ns_refine<T, MT>(Xi, E, Id, lane);
+                if (have) {
+#pragma unroll
+                    for (int i = 0; i < MT; ++i)
+#pragma unroll
+                        for (int j = 0; j < MT; ++j) wg4_tstore(Ximg + 16 * i + 16 * j * CS, CS, Xi[i][j], lane);
+                }
+                if (lane == 0) vote[0] = have ? 1 : 0;
+            }
+            __syncthreads();                             // wave 3's verdict (uniform by construction) and X
+            have = vote[0] != 0;
+            if (have && w != 3) {
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < MT; ++j) Xi[i][j] = wg4_tload(Ximg + 16 * i + 16 * j * CS, CS, lane);
+            }
+        } else if (k < N - 1) {
             // warm start 2X_{k+1} − X_{k+2}; Xp takes X_{k+1} before the refinement
             acc Id[MT][MT];
 #pragma unroll
@@ -1420,15 +1482,19 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
         // :51 P_ tiles (i, w) = Q + A[:, i]ᵀPA[:, w] − G[:, i]ᵀK[:, w] → the P image, mirrored
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
-            const int i = wg4_pn_row(w, t);
+            const int i = NS1 ? wg4_pn_row1(w, t) : wg4_pn_row(w, t);
             if (i < 0) continue;
             acc Pn;
-            if constexpr (TV) Pn = Qt[t];
-            else Pn = wg4_tload(Qim + 16 * i + 16 * w * PL, PL, lane);                           // Q[i][w]
+            if (NS1 && w != 3) {
+                Pn = PnA[NS1 ? t : 0];                   // Q + A[:, i]ᵀPA[:, w] formed beside the inverse
+            } else {
+                if constexpr (TV) Pn = Qt[t];
+                else Pn = wg4_tload(Qim + 16 * i + 16 * w * PL, PL, lane);                       // Q[i][w]
 #pragma unroll
-            for (int kk = 0; kk < NT; ++kk) {
-                const acc At = t == 0 ? Ar[kk] : wg4_tload(Acur + 16 * kk + 16 * i * PL, PL, lane);  // A[kk][i]
-                wg4_mtn<T>(Pn, At, PA[kk]);
+                for (int kk = 0; kk < NT; ++kk) {
+                    const acc At = t == 0 ? Ar[kk] : wg4_tload(Acur + 16 * kk + 16 * i * PL, PL, lane);  // A[kk][i]
+                    wg4_mtn<T>(Pn, At, PA[kk]);
+                }
             }
 #pragma unroll
             for (int c = 0; c < MT; ++c)
