@@ -899,12 +899,15 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
 //   :40  PA[:, w] = Pᵀ·A[:, w]             (all of P from LDS, A[:, w] in registers)
 //   :39  E tile (w mod MT, w / MT) = R + BᵀPB   (PB from its LDS image; one tile per wave)
 //   :41  G[:, w] = Bᵀ·PA[:, w]             (registers only; also to an LDS image)
-//   :42  X ≈ E⁻¹ (every wave; the four verdicts are AND-ed), K[:, w] = XᵀG[:, w], stored to sol.K
+//   :42  X ≈ E⁻¹ — m = 32, time-invariant: on wave 3 alone, published with its verdict through
+//        the PB image while waves 0–2 form the K-independent half Q + A[:, i]ᵀPA[:, w] of their P_
+//        tiles; otherwise in every wave, the four verdicts AND-ed — then K[:, w] = XᵀG[:, w] to sol.K
 //   :51  P_ tiles (i, w), i from wave w's row list — the ten tiles of the symmetric 4×4 grid
-//        as 3, 3, 2, 2 per wave: Q + A[:, i]ᵀPA[:, w] − G[:, i]ᵀK[:, w], written to the P image
-//        at (i, w) and mirrored to (w, i) (diagonal tiles from their lower triangle), so the
-//        image stays exactly symmetric as tiles_symmetrize_lower keeps the one-wave P.
-// Four workgroup barriers per knot (after PB/PA, after E/G, the inverse's verdict vote, after
+//        as 3, 3, 3, 1 (inverse on wave 3) or 3, 3, 2, 2 per wave: Q + A[:, i]ᵀPA[:, w] −
+//        G[:, i]ᵀK[:, w], written to the P image at (i, w) and mirrored to (w, i) (diagonal tiles
+//        from their lower triangle), so the image stays exactly symmetric as
+//        tiles_symmetrize_lower keeps the one-wave P.
+// Four workgroup barriers per knot (after PB/PA, after E/G, the inverse's verdict (and X), after
 // P_).  A lives in an LDS image (the P_ rows' A columns are read from it), A[:, w] also in
 // registers; B, Q in images; R's E tile in registers.
 // VAR_TV (constrained_problem.jl:3-4: per-knot A_k, B_k, Q_k, R_k): A is double-buffered in LDS
@@ -1312,6 +1315,9 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
         // PB image while waves 0–2 form the K-independent part Q + A[:, i]ᵀPA[:, w] of their three
         // P_ tiles — the knot's critical path drops from 16 + 4 + 18 tile products (inverse in every
         // wave, 3/3/2/2 P_ tiles) to 16 + 4 + 6 (3/3/3/1 tiles, wg4_pn_row1)
+        // (time-varying problems keep the inverse in every wave: with Q_k's tiles from HBM added
+        // after the barrier the TV / TV+LIN variants measured 73.2 vs 72.7 and 159.5 vs 121.1 ms,
+        // profiles/r06/u)
         constexpr bool NS1 = MT == 2 && !TV && LQRX_WG4_NS_ONE;
         acc PnA[NS1 ? 3 : 1];
         if constexpr (NS1) {

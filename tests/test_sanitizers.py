@@ -14,7 +14,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _run(make_dir, exe):
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, make_dir), "asan"], check=True, timeout=600)
+    jobs = str(min(8, os.cpu_count() or 1))
+    subprocess.run(["make", "-s", "-j", jobs, "-C", os.path.join(ROOT, make_dir), "asan"], check=True, timeout=900)
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_error=1",
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
     r = subprocess.run([os.path.join(ROOT, exe)], env=env, capture_output=True, text=True, timeout=300)
