@@ -778,7 +778,7 @@ __global__ __launch_bounds__(64, WAVES) void dp_riccati_kernel(const DpArgs a)
                             X0[i][j] = Xi[i][j];
                             Xi[i][j] = (T)2 * Xi[i][j] - Xp[i][j];   // = X_{k+1} at k = N−2 (Xp = Xi there)
                         }
-                    have = ns_refine<T, MT>(Xi, E, Id, lane);
+                    have = !a.ns_off && ns_refine<T, MT>(Xi, E, Id, lane);
 #pragma unroll
                     for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -1351,7 +1351,7 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
                         Xi[i][j] = (T)2 * x1 - Xp[i][j];
                         Xp[i][j] = x1;
                     }
-                have = ns_refine<T, MT>(Xi, E, Id, lane);
+                have = !a.ns_off && ns_refine<T, MT>(Xi, E, Id, lane);
                 if (have) {
 #pragma unroll
                     for (int i = 0; i < MT; ++i)
@@ -1391,7 +1391,7 @@ __global__ __launch_bounds__(256, 1) void dp_wg4_kernel(const DpArgs a)
                 for (int i = 0; i < MT; ++i)
 #pragma unroll
                     for (int j = 0; j < MT; ++j) E[i][j] = wg4_tload(Eim + 16 * i + 16 * j * CS, CS, lane);
-                have = ns_refine<T, MT>(Xi, E, Id, lane);
+                have = !a.ns_off && ns_refine<T, MT>(Xi, E, Id, lane);
                 // workgroup-uniform verdict by construction (the branch below holds a barrier): each
                 // wave posts its own Newton–Schulz verdict, every wave takes the AND of all four — no
                 // reliance on the four refinements agreeing bitwise.  (The slots are rewritten only
@@ -1587,8 +1587,11 @@ static hipError_t launch_dp(const DpArgs &a, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t dp_launch(const DpArgs &a, hipStream_t s)
+hipError_t dp_launch(const DpArgs &a_in, hipStream_t s)
 {
+    static const int ns_off = [] { const char *e = std::getenv("LQRX_DP_NS_OFF"); return e && *e == '1' ? 1 : 0; }();
+    DpArgs a = a_in;
+    a.ns_off = ns_off;
     // n ≤ 4: one lane per trajectory (a 16×16 MFMA tile would be mostly padding)
     if (dp_lane_supported(a.n, a.m)) return dp_lane_launch(a, s);
     // smallest instantiated tile grid that covers (n, m); padding is exact (zero rows /

@@ -24,6 +24,9 @@ struct DpArgs {
     int lin;
     const void *q, *r, *qf;
     void *d, *p;
+    // tests only (LQRX_DP_NS_OFF=1, read by dp_launch): no Newton–Schulz step, every knot takes the
+    // exact LDLᵀ sweep — exercises the sweep / verdict paths of the MFMA kernels at every knot
+    int ns_off;
 };
 
 hipError_t dp_launch(const DpArgs &a, hipStream_t s);

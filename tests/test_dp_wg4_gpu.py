@@ -124,3 +124,33 @@ def test_wg4_variants_match_one_wave(lqrx, gpu_ok):
         os.remove(f)
     a, b = outs
     assert np.abs(a - b).max() <= 1e-11 * np.abs(b).max()
+
+
+_SWEEP = """
+import sys, numpy as np, lqrx
+sys.path.insert(0, sys.argv[1])
+from oracle import oracle as orc
+from lqrx.dp import abi_to_batch, from_abi
+n, m, N, bt = (int(v) for v in sys.argv[2:6])
+d = lqrx.random_batch(n, m, N, bt, seed=n + 7 * m)
+got = lqrx.solve_batch(abi_to_batch(d), all_P=True)
+ref = orc.dp_solve_abi(d, N, all_P=True)
+K = from_abi(ref["K"], (bt, N - 1, m, n)); P = from_abi(ref["P"], (bt, N, n, n))
+ek = np.abs(got["K"] - K).max() / np.abs(K).max(); ep = np.abs(got["P"] - P).max() / np.abs(P).max()
+ex = np.abs(got["X"] - ref["X"].reshape(bt, N, n)).max() / max(1.0, np.abs(ref["X"]).max())
+print(n, m, ek, ep, ex)
+sys.exit(0 if (got["rc"] == 0 and (got["info"] == 0).all() and max(ek, ep, ex) <= 1e-10) else 1)
+"""
+
+
+@pytest.mark.parametrize("n,m,N,bt", [(64, 32, 20, 3), (64, 16, 17, 2), (32, 16, 30, 4), (17, 5, 12, 3)])
+def test_exact_sweep_every_knot(lqrx, gpu_ok, n, m, N, bt):
+    """LQRX_DP_NS_OFF=1 (tests only): no Newton–Schulz step, every knot takes the exact LDLᵀ sweep
+    and its verdict path — in the four-wave kernel (m = 32: the wave-3 verdict barrier, then the
+    sweep on wave 0 at every knot) and the one-wave kernel — still equal to the oracle at 1e-10."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LQRX_DP_NS_OFF="1",
+               PYTHONPATH=os.pathsep.join([os.path.join(root, "lqr.jl_amd"), root, os.environ.get("PYTHONPATH", "")]))
+    r = subprocess.run([sys.executable, "-c", _SWEEP, root, str(n), str(m), str(N), str(bt)], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
