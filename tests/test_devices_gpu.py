@@ -35,6 +35,7 @@ def _same(a, b):
     (32, 16, 64, 301, 0, [0, 0]),          # cfg4 shape, ragged shards (151 + 150)
     (32, 16, 64, 301, 1, [0, 0, 0]),       # layout 1: strided element rows per shard
     (64, 16, 12, 37, 0, [0, 0]),           # fp64 n = 64: the four-wave kernel per shard
+    (64, 32, 10, 9, 0, [0, 0, 0]),         # m = 32: the four-wave kernel with the inverse on wave 3
     (6, 3, 40, 129, 0, [0, 0]),
     (4, 1, 101, 4096, 0, [0, 0]),          # cfg2 shape: both shards and the whole batch on the quad kernel
     (4, 1, 101, 1000, 1, [0, 0]),          # n ≤ 4 layout 1 (native SoA lane kernels)

@@ -111,7 +111,7 @@ def test_dp_linear_parity_f64(lqrx, oracle, gpu_ok, n, m, N, bt, tvq, tvab, all_
     check(got, ref, n, m, N, bt, all_P, TOL64)
 
 
-@pytest.mark.parametrize("n,m,N,bt", [(4, 2, 50, 70), (32, 16, 40, 3)])
+@pytest.mark.parametrize("n,m,N,bt", [(4, 2, 50, 70), (32, 16, 40, 3), (64, 32, 14, 2)])   # 64: four-wave TV + LIN
 def test_dp_linear_layout1(lqrx, oracle, gpu_ok, n, m, N, bt):
     """Layout 1 (SoA) for the linear arrays too: bit-identical to layout 0."""
     d = lin_problem(lqrx, n, m, N, bt, 77 + n, tv_QR=True)

@@ -44,7 +44,7 @@ def test_soa_mfma_staged(lqrx, gpu_ok, n, m, N, bt, dtype):
     _pair(lqrx, abi_to_batch(d), dtype=dtype, all_P=(n < 64))
 
 
-@pytest.mark.parametrize("n,m", [(4, 2), (6, 3)])
+@pytest.mark.parametrize("n,m", [(4, 2), (6, 3), (64, 32), (64, 16)])   # n = 64: the four-wave TV kernel
 def test_soa_time_varying(lqrx, gpu_ok, n, m):
     from test_dp_lane_gpu import _tv_batch
 
