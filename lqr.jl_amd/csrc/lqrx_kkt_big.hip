@@ -43,6 +43,7 @@
 // straddle block boundaries; the arithmetic on padding adds exact zeros.
 #include "lqrx_internal.h"
 #include "lqrx_tile.h"
+#include <type_traits>
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -1265,6 +1266,13 @@ constexpr int KF_LDS = 64 * KF_LU + 64 + KF_SCR;      // per wave: U image, vect
 #ifndef KF_INV_SWEEP
 #define KF_INV_SWEEP 0                                // 1: the round-4 leaf inverse sweep (A/B builds)
 #endif
+#ifndef KF_RSQ_RAW
+#define KF_RSQ_RAW 1         // fp32 leaf pivots: v_rsq_f32 without its Newton step (0: A/B)
+#endif
+#ifndef KU_ZERO_PEEL
+#define KU_ZERO_PEEL 1       // the fused stream's first slice starts its accumulators from a zero C
+                             // operand instead of zeroing 26 tiles by v_mov (0: A/B)
+#endif
 #ifndef KF_LEAF_UNSCALED
 #define KF_LEAF_UNSCALED 0   // 1 (A/B builds): unscaled rows, 1/d and 1/√d formed during the LDS
                              // round trip — measured slower (fp32 157.4 vs 155.3 ms, fp64 169.1
@@ -1672,6 +1680,9 @@ __device__ __forceinline__ void kf_info(int32_t *info, int64_t t, int v, int kb,
 // broadcast the same way and B_R −= U[R][k]·T_k with U's strictly-upper columns from an LDS
 // image.  Only the upper triangle of X is read.  q = real pivots (pivots ≥ q are identity
 // padding); returns 1 + the first non-positive pivot, else 0.  scr: KF_SCR elements of LDS.
+__device__ __forceinline__ float leaf_rsq(float d) { return __builtin_amdgcn_rsqf(d); }
+__device__ __forceinline__ double leaf_rsq(double d) { return rsqrt_nr(d); }
+
 template <typename T>
 __device__ __forceinline__ int leaf_chol_inv_t(acc_t<T> &X, T *scr, int q, int lane)
 {
@@ -1765,7 +1776,9 @@ __device__ __forceinline__ int leaf_chol_inv_e(acc_t<T> &X, T *scr, T *Dg, int q
             E[r] = Tile<T>::row(lane, r) == i ? es : fma(-ur[r], te, E[r]);
         }
 #else
-        const T sc = rsqrt_nr(d);
+        // fp32 (KF_RSQ_RAW): v_rsq_f32 alone — the Newton step (4 VALU per pivot, 256 per knot of
+        // the fused kernel) buys nothing at the fp32 solve's 1e-4 tolerance; fp64 keeps two steps
+        const T sc = (!F64 && KF_RSQ_RAW) ? leaf_rsq(d) : rsqrt_nr(d);
         wsync();
         ub[16 * g + c] = c > i ? X[rgi] * sc : (T)0;
         eb[16 * g + c] = E[rgi] * sc;
@@ -2323,12 +2336,14 @@ __device__ __forceinline__ void fu_schur2(const Kn &q1, const T *Y1, const T *hg
         for (int v = 0; v < NT; ++v)
             vo2[v] = i16 < q2.p1 - 16 * v ? (uint32_t)((g4 * q2.rows + 16 * v + i16) * (int)TS) : OOB;
     }
+    if constexpr (!KU_ZERO_PEEL) {
 #pragma unroll
-    for (int u = 0; u < NT * NT; ++u) G[u] = tzero<T>();
+        for (int u = 0; u < NT * NT; ++u) G[u] = tzero<T>();
 #pragma unroll
-    for (int i = 0; i < NT; ++i)
+        for (int i = 0; i < NT; ++i)
 #pragma unroll
-        for (int j = i; j < NT; ++j) P[up4(i, j)] = tzero<T>();
+            for (int j = i; j < NT; ++j) P[up4(i, j)] = tzero<T>();
+    }
     T rp[NB];
 #pragma unroll
     for (int v = 0; v < NB; ++v) rp[v] = (T)0;
@@ -2357,7 +2372,11 @@ __device__ __forceinline__ void fu_schur2(const Kn &q1, const T *Y1, const T *hg
             gg2 = hg2[KS_HG + 4 * s + g4];
         }
     };
-    auto step = [&](const T (&a1)[NB], const T (&a2)[NT], T hh1, T gg1, T hh2, T gg2, int s) __attribute__((always_inline)) {
+    // FIRST (std::true_type, KU_ZERO_PEEL): the stream's first slice — the accumulators start from
+    // a zero C operand (an MFMA inline constant) instead of 26 zeroed tiles
+    auto step = [&](auto first, const T (&a1)[NB], const T (&a2)[NT], T hh1, T gg1, T hh2, T gg2, int s)
+        __attribute__((always_inline)) {
+        constexpr bool F0 = decltype(first)::value;
         if constexpr (KU_LEAN) {      // H⁻¹, g of the slice straight from LDS (no ring registers)
             hh1 = hg1[4 * s + g4];
             gg1 = hg1[KS_HG + 4 * s + g4];
@@ -2372,11 +2391,13 @@ __device__ __forceinline__ void fu_schur2(const Kn &q1, const T *Y1, const T *hg
 #pragma unroll
         for (int i = 0; i < NT; ++i)
 #pragma unroll
-            for (int j = 0; j < NT; ++j) G[i * NT + j] = Tile<T>::mma(a1[i], fh1[NT + j], G[i * NT + j]);
+            for (int j = 0; j < NT; ++j)
+                G[i * NT + j] = Tile<T>::mma(a1[i], fh1[NT + j], F0 ? tzero<T>() : G[i * NT + j]);
 #pragma unroll
         for (int i = 0; i < NT; ++i)
 #pragma unroll
-            for (int j = i; j < NT; ++j) P[up4(i, j)] = Tile<T>::mma(a1[NT + i], fh1[NT + j], P[up4(i, j)]);
+            for (int j = i; j < NT; ++j)
+                P[up4(i, j)] = Tile<T>::mma(a1[NT + i], fh1[NT + j], F0 ? tzero<T>() : P[up4(i, j)]);
 #pragma unroll
         for (int i = 0; i < NT; ++i)
 #pragma unroll
@@ -2390,10 +2411,23 @@ __device__ __forceinline__ void fu_schur2(const Kn &q1, const T *Y1, const T *hg
     for (int u = 0; u < KU_PF; ++u) load(u, f1[u], f2[u], h1[u], c1[u], h2[u], c2[u]);
     // branch-free ring (slices past a block's last read 0 and carry h = 0): each step waits
     // only for its own slice, requested KU_PF steps earlier
-    for (int s0 = 0; s0 < nks; s0 += KU_PF) {
+    int s00 = 0;
+    if constexpr (KU_ZERO_PEEL) {            // the first group of KU_PF slices, peeled
+        step(std::true_type{}, f1[0], f2[0], h1[0], c1[0], h2[0], c2[0], 0);
+        load(KU_PF, f1[0], f2[0], h1[0], c1[0], h2[0], c2[0]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 1; u < KU_PF; ++u) {
+            step(std::false_type{}, f1[u], f2[u], h1[u], c1[u], h2[u], c2[u], u);
+            load(u + KU_PF, f1[u], f2[u], h1[u], c1[u], h2[u], c2[u]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        s00 = KU_PF;
+    }
+    for (int s0 = s00; s0 < nks; s0 += KU_PF) {
 #pragma unroll
         for (int u = 0; u < KU_PF; ++u) {
-            step(f1[u], f2[u], h1[u], c1[u], h2[u], c2[u], s0 + u);
+            step(std::false_type{}, f1[u], f2[u], h1[u], c1[u], h2[u], c2[u], s0 + u);
             load(s0 + u + KU_PF, f1[u], f2[u], h1[u], c1[u], h2[u], c2[u]);
             __builtin_amdgcn_sched_barrier(0);
         }
