@@ -1269,6 +1269,9 @@ constexpr int KF_LDS = 64 * KF_LU + 64 + KF_SCR;      // per wave: U image, vect
 #ifndef KF_RSQ_RAW
 #define KF_RSQ_RAW 1         // fp32 leaf pivots: v_rsq_f32 without its Newton step (0: A/B)
 #endif
+#ifndef KF_RSQ1_F64
+#define KF_RSQ1_F64 1        // fp64 leaf pivots: v_rsq_f64 + one Newton step instead of two (0: A/B)
+#endif
 #ifndef KU_ZERO_PEEL
 #define KU_ZERO_PEEL 1       // the fused stream's first slice starts its accumulators from a zero C
                              // operand instead of zeroing 26 tiles by v_mov (0: A/B)
@@ -1681,7 +1684,15 @@ __device__ __forceinline__ void kf_info(int32_t *info, int64_t t, int v, int kb,
 // image.  Only the upper triangle of X is read.  q = real pivots (pivots ≥ q are identity
 // padding); returns 1 + the first non-positive pivot, else 0.  scr: KF_SCR elements of LDS.
 __device__ __forceinline__ float leaf_rsq(float d) { return __builtin_amdgcn_rsqf(d); }
-__device__ __forceinline__ double leaf_rsq(double d) { return rsqrt_nr(d); }
+// fp64: v_rsq_f64 (≈ 1e-8 relative, as v_rcp_f64's 4.6e-8) and ONE Newton step — quadratic, so
+// ≈ 1e-16 — where rsqrt_nr takes two (KF_RSQ1_F64 = 0: A/B)
+__device__ __forceinline__ double leaf_rsq(double a)
+{
+    if constexpr (!KF_RSQ1_F64) return rsqrt_nr(a);
+    const double y = __builtin_amdgcn_rsq(a);
+    const double h = 0.5 * a * y;
+    return fma(y, fma(-h, y, 0.5), y);
+}
 
 template <typename T>
 __device__ __forceinline__ int leaf_chol_inv_t(acc_t<T> &X, T *scr, int q, int lane)
@@ -1777,8 +1788,8 @@ __device__ __forceinline__ int leaf_chol_inv_e(acc_t<T> &X, T *scr, T *Dg, int q
         }
 #else
         // fp32 (KF_RSQ_RAW): v_rsq_f32 alone — the Newton step (4 VALU per pivot, 256 per knot of
-        // the fused kernel) buys nothing at the fp32 solve's 1e-4 tolerance; fp64 keeps two steps
-        const T sc = (!F64 && KF_RSQ_RAW) ? leaf_rsq(d) : rsqrt_nr(d);
+        // the fused kernel) buys nothing at the fp32 solve's 1e-4 tolerance; fp64: one step (leaf_rsq)
+        const T sc = (F64 || KF_RSQ_RAW) ? leaf_rsq(d) : rsqrt_nr(d);
         wsync();
         ub[16 * g + c] = c > i ? X[rgi] * sc : (T)0;
         eb[16 * g + c] = E[rgi] * sc;
