@@ -156,6 +156,11 @@ recipe_r6close() {   # round-6 closing set: suite + smoke, every line whose kern
     sub dp64 prof $DP64 && sub cfg2 prof --workload cartpole && sub tv prof --tv && sub lin prof --linear &&
     sub wg96 prof $WG96 && sub cfg3 kt --workload kkt && sub kkt32 kt $CFG4KKT
 }
+recipe_r6kkt() {   # configs[4] KKT half after the round-6 fused-kernel changes (leaf rsqrt, zero-C peel):
+                   # its tests, fp32 with traffic + SQ counters, fp64 with traffic
+    sub t pytest tests/test_kkt_big_gpu.py tests/test_full_size_gpu.py && sub kkt32 prof $CFG4KKT &&
+    KREGEX=kb_ PMC="$SQ1;$SQ2" sub kkt32sq pmc $CFG4KKT && sub kkt64 prof $CFG4KKT64
+}
 recipe_list() { declare -F | sed -n 's/^declare -f recipe_//p'; }
 
 case "$MODE" in
