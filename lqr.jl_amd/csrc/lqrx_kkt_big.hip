@@ -2284,6 +2284,10 @@ struct KuArgs {
 #ifndef KU_STAGGER
 #define KU_STAGGER 0         // > 0 (with KU_WAVES 8): waves 4–7 start this many s_sleep units late
 #endif
+#ifndef KU_HG_AHEAD
+#define KU_HG_AHEAD 1        // (KU_LEAN) a slice's H⁻¹/g LDS reads issued one stream step ahead:
+                             // 1 fp64 only, 2 fp32 as well, 0 off (A/B)
+#endif
 #ifndef KU_PRIO
 #define KU_PRIO 1            // the factor phase (latency-bound chain) runs at raised issue priority
 #endif
@@ -2364,6 +2368,17 @@ __device__ __forceinline__ void fu_schur2(const Kn &q1, const T *Y1, const T *hg
     const int nks = max(q1.w + 3, q2.w + 3) >> 2;
     constexpr int KU_PF = ku_pf<T>();
     T f1[KU_PF][NB], f2[KU_PF][NT], h1[KU_PF], c1[KU_PF], h2[KU_PF], c2[KU_PF];
+    // AHEAD: the step of slice s uses the H⁻¹/g values the previous step read and reads those of
+    // slice s + 1, so the LDS round trip is not between a step's start and its first MFMA (rows
+    // are KS_HG = KB_WMAX + 4 long; the read index is clamped to the row)
+    constexpr bool AHEAD = KU_LEAN && (KU_HG_AHEAD == 2 || (KU_HG_AHEAD == 1 && sizeof(T) == 8));
+    T nh1 = (T)0, ng1 = (T)0, nh2 = (T)0, ng2 = (T)0;
+    if constexpr (AHEAD) {
+        nh1 = hg1[g4];
+        ng1 = hg1[KS_HG + g4];
+        nh2 = hg2[g4];
+        ng2 = hg2[KS_HG + g4];
+    }
     auto load = [&](int s, T (&a1)[NB], T (&a2)[NT], T &hh1, T &gg1, T &hh2, T &gg2) __attribute__((always_inline)) {
         const int o1 = s * so1, o2 = s * so2;
         const __amdgpu_buffer_rsrc_t r1 =
@@ -2388,7 +2403,17 @@ __device__ __forceinline__ void fu_schur2(const Kn &q1, const T *Y1, const T *hg
     auto step = [&](auto first, const T (&a1)[NB], const T (&a2)[NT], T hh1, T gg1, T hh2, T gg2, int s)
         __attribute__((always_inline)) {
         constexpr bool F0 = decltype(first)::value;
-        if constexpr (KU_LEAN) {      // H⁻¹, g of the slice straight from LDS (no ring registers)
+        if constexpr (AHEAD) {
+            hh1 = nh1;
+            gg1 = ng1;
+            hh2 = nh2;
+            gg2 = ng2;
+            const int sn = min(s + 1, KS_HG / 4 - 1);      // (a slice past the last step: unused)
+            nh1 = hg1[4 * sn + g4];
+            ng1 = hg1[KS_HG + 4 * sn + g4];
+            nh2 = hg2[4 * sn + g4];
+            ng2 = hg2[KS_HG + 4 * sn + g4];
+        } else if constexpr (KU_LEAN) {      // H⁻¹, g of the slice straight from LDS (no ring registers)
             hh1 = hg1[4 * s + g4];
             gg1 = hg1[KS_HG + 4 * s + g4];
             hh2 = hg2[4 * s + g4];
