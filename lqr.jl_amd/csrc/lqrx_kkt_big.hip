@@ -2424,11 +2424,17 @@ __device__ __forceinline__ void fu_schur2(const Kn &q1, const T *Y1, const T *hg
         for (int v = NT; v < NB; ++v) fh1[v] = a1[v] * hh1;
 #pragma unroll
         for (int v = 0; v < NT; ++v) fh2[v] = a2[v] * hh2;
+#ifndef KU_ABL_MM
+#define KU_ABL_MM 0          // timing ablations only (wrong results): 1 no F (G) products, 2 no C / A
+#endif
+        if constexpr (KU_ABL_MM != 1) {
 #pragma unroll
         for (int i = 0; i < NT; ++i)
 #pragma unroll
             for (int j = 0; j < NT; ++j)
                 G[i * NT + j] = Tile<T>::mma(a1[i], fh1[NT + j], F0 ? tzero<T>() : G[i * NT + j]);
+        }
+        if constexpr (KU_ABL_MM != 2) {
 #pragma unroll
         for (int i = 0; i < NT; ++i)
 #pragma unroll
@@ -2438,6 +2444,7 @@ __device__ __forceinline__ void fu_schur2(const Kn &q1, const T *Y1, const T *hg
         for (int i = 0; i < NT; ++i)
 #pragma unroll
             for (int j = i; j < NT; ++j) P[up4(i, j)] = Tile<T>::mma(a2[i], fh2[j], P[up4(i, j)]);
+        }
 #pragma unroll
         for (int v = NT; v < NB; ++v) rp[v] = fma(fh1[v], gg1, rp[v]);
 #pragma unroll
