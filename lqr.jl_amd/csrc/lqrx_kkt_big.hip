@@ -1753,17 +1753,8 @@ __device__ __forceinline__ int leaf_chol_inv_t(acc_t<T> &X, T *scr, int q, int l
 // 16-step back-substitution chain of leaf_chol_inv_t disappears.  T = U⁻¹ = Eᵀ goes through the
 // caller's image Dg (column-major, KF_LU; where leaf_chol_inv_t's caller stored T): E is written
 // transposed and read back as X.  Returns 1 + the first non-positive pivot (< q), else 0.
-#ifndef KU_TICK_AT
-#define KU_TICK_AT 1         // where a pivot step's tick goes: 0 after its LDS writes, 1 after its reads
-#endif
-// no-op factor tick (chol_inv_reg alone)
-struct NoTick {
-    __device__ __forceinline__ void operator()(int) const {}
-};
-// tick(t0 + i) is called once per pivot step i, after the step's rows went out to LDS: the fused
-// fp64 kernel issues independent MFMA work there (GPass below) while the round trip is in flight
-template <typename T, class TK = NoTick>
-__device__ __forceinline__ int leaf_chol_inv_e(acc_t<T> &X, T *scr, T *Dg, int q, int lane, TK &&tick = TK{}, int t0 = 0)
+template <typename T>
+__device__ __forceinline__ int leaf_chol_inv_e(acc_t<T> &X, T *scr, T *Dg, int q, int lane)
 {
     T *ub = scr, *eb = scr + 64;                        // pivot row of U, scaled row of E
     const int c = lane & 15, g = lane >> 4;
@@ -1783,14 +1774,12 @@ __device__ __forceinline__ int leaf_chol_inv_e(acc_t<T> &X, T *scr, T *Dg, int q
         wsync();
         ub[16 * g + c] = c > i ? X[rgi] : (T)0;
         eb[16 * g + c] = E[rgi];
-        if constexpr (KU_TICK_AT == 0) tick(t0 + i);
         wsync();
         const T id = rcp_full(d), sc = rsqrt_nr(d);
         const T uc = ub[16 * gi + c], ec = eb[16 * gi + c];
         T ur[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) ur[r] = ub[16 * gi + Tile<T>::row(lane, r)];
-        if constexpr (KU_TICK_AT == 1) tick(t0 + i);
         const T tu = uc * id, te = ec * id, es = ec * sc;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1804,13 +1793,11 @@ __device__ __forceinline__ int leaf_chol_inv_e(acc_t<T> &X, T *scr, T *Dg, int q
         wsync();
         ub[16 * g + c] = c > i ? X[rgi] * sc : (T)0;
         eb[16 * g + c] = E[rgi] * sc;
-        if constexpr (KU_TICK_AT == 0) tick(t0 + i);
         wsync();
         const T uc = ub[16 * gi + c], ec = eb[16 * gi + c];
         T ur[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) ur[r] = ub[16 * gi + Tile<T>::row(lane, r)];
-        if constexpr (KU_TICK_AT == 1) tick(t0 + i);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             X[r] = fma(-ur[r], uc, X[r]);
@@ -1834,9 +1821,8 @@ __device__ __forceinline__ int leaf_chol_inv_e(acc_t<T> &X, T *scr, T *Dg, int q
 // first non-positive pivot.
 // kbc (KB_PROF timing builds only, else null): cycles of the leaves, the panel / trailing
 // updates and the inverse assembly added to kbc[0..2]
-template <typename T, class TK = NoTick>
-__device__ __forceinline__ int chol_inv_reg(acc_t<T> (&X)[10], int nb, int p, T *U, T *scr, int lane, int64_t *kbc = nullptr,
-                                            TK &&tick = TK{})
+template <typename T>
+__device__ int chol_inv_reg(acc_t<T> (&X)[10], int nb, int p, T *U, T *scr, int lane, int64_t *kbc = nullptr)
 {
     int64_t kc0 = kbc ? clock64() : 0;
     auto kct = [&](int i) {
@@ -1871,15 +1857,13 @@ __device__ __forceinline__ int chol_inv_reg(acc_t<T> (&X)[10], int nb, int p, T 
 #elif defined(KF_NOLEAF)
             const int b = 0;       // timing ablation only: no leaf factor (wrong results)
             (void)scr;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) tick(16 * jb + i);
 #elif KF_INV_SWEEP
             // A/B: the round-4 leaf (inverse by a second 16-step back-substitution sweep)
             const int b = leaf_chol_inv_t<T>(X[up4(jb, jb)], scr, min(16, p - 16 * jb), lane);
             if (b && !bad) bad = 16 * jb + b;
             tstore(Dg, KF_LU, X[up4(jb, jb)], lane);     // T_jj for the inverse assembly's reads
 #else
-            const int b = leaf_chol_inv_e<T>(X[up4(jb, jb)], scr, Dg, min(16, p - 16 * jb), lane, tick, 16 * jb);
+            const int b = leaf_chol_inv_e<T>(X[up4(jb, jb)], scr, Dg, min(16, p - 16 * jb), lane);
             if (b && !bad) bad = 16 * jb + b;            // (T_jj is in Dg for the inverse assembly)
 #endif
             kct(0);
@@ -2561,232 +2545,6 @@ __device__ __forceinline__ void fu_stream(const int32_t *meta, int kn, const T *
     }
 }
 
-// ---- fp64: knot k+1's F tiles during knot k's factor (round 6)
-// In fp64 the fused kernel runs one wave per SIMD, so the factor's latency-bound leaf chain (64
-// pivot steps, each an LDS round trip) leaves the matrix pipe idle for ~20 % of a knot, while the
-// F products of the next knot (G = D2 H⁻¹ D1ᵀ, 16 of the stream's 36 MFMAs per slice at NT = 4)
-// depend on nothing the factor produces and G is dead until the reduction.  GPass streams them
-// through the factor: every pivot step issues one half slice (TPS = 2 ticks per slice for NT ≥ 3,
-// a whole slice for NT ≤ 2) from its own KG-deep ring of Y loads (D2 and D1 rows of knot k+1),
-// with r2 = D1 H⁻¹ g accumulated beside it; slices past the 16·NT / TPS the ticks cover are
-// drained after the factor.  The C / A stream then reads only D1 of k+1 and D2 of k+2
-// (fu_schur_ca).  H⁻¹/g rows of k+1 are the ones the previous step staged as its q2, so the
-// kernel ping-pongs the two row areas of the wave's LDS (the leaf scratch takes the other one).
-#ifndef KU_GPASS
-#define KU_GPASS 0           // 1: fp64 forms the F products during the factor (A/B: slower, profiles/r06/ac_64, ad_64)
-#endif
-#ifndef KU_GP_KG
-#define KU_GP_KG 2           // GPass Y slices in flight
-#endif
-template <typename T> constexpr bool ku_gpass()
-{
-    return sizeof(T) == 8 && KU_GPASS && !KF_OLD_LEAF && !KF_INV_SWEEP;
-}
-template <typename T, int NT, bool FULL>
-struct GPass {
-    static constexpr int NB = 2 * NT, KG = KU_GP_KG, TPS = NT >= 3 ? 2 : 1, S_T = 16 * NT / TPS, I0 = (NT + 1) / 2;
-    static constexpr uint32_t TS = sizeof(T), OOB = 0x80000000u;
-    acc_t<T> (&G)[16];
-    const char *yb;
-    const T *hg;
-    int yn, so, nks, g4;
-    bool on;
-    uint32_t vo[FULL ? 1 : NB];
-    T f[KG][NB], fh[NT], rp[NT], nh, ng;
-
-    __device__ __forceinline__ void load(int s, T (&a)[NB])
-    {
-        const int o = s * so;
-        const __amdgpu_buffer_rsrc_t r =
-            __builtin_amdgcn_make_buffer_rsrc((void *)(yb + o), (short)0, max(yn - o, 0), 0x00020000);
-#pragma unroll
-        for (int v = 0; v < NB; ++v) a[v] = bload<T>(r, FULL ? vo[0] + (uint32_t)(16 * v * (int)TS) : vo[FULL ? 0 : v], 0u);
-    }
-    // q: knot k+1 (any valid knot when !on: nothing is read then), Yk: its Y block, hgq: its
-    // staged H⁻¹ / g rows
-    __device__ __forceinline__ GPass(const Kn &q, const T *Yk, const T *hgq, bool on_, acc_t<T> (&G_)[16], int lane)
-        : G(G_), yb((const char *)Yk), hg(hgq), on(on_)
-    {
-        const int i16 = lane & 15;
-        g4 = lane >> 4;
-        yn = on ? q.rows * q.w * (int)TS : 0;               // !on: every load out of range (reads 0)
-        so = 4 * q.rows * (int)TS;
-        nks = (q.w + 3) >> 2;
-        if constexpr (FULL) {
-            vo[0] = (uint32_t)((g4 * q.rows + i16) * (int)TS);
-        } else {
-#pragma unroll
-            for (int v = 0; v < NB; ++v) {
-                const int rb = v < NT ? 16 * v : q.p1 + q.ps + 16 * (v - NT);
-                const int lim = v < NT ? q.p1 - 16 * v : q.p2 - 16 * (v - NT);
-                vo[FULL ? 0 : v] = i16 < lim ? (uint32_t)((g4 * q.rows + rb + i16) * (int)TS) : OOB;
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < NT; ++j) rp[j] = (T)0;
-        nh = hg[g4];
-        ng = hg[KS_HG + g4];
-#pragma unroll
-        for (int u = 0; u < KG; ++u) load(u, f[u]);
-    }
-    // half h of slice s from ring slot f[sl] (static after unrolling): the D1 products of the
-    // slice (and the next slice's H⁻¹ / g reads) on its first half, its G rows [i0, i1)
-    __device__ __forceinline__ void part(int s, int h, T (&a)[NB])
-    {
-        if (h == 0) {
-            const T hh = nh, gg = ng;
-            const int sn = min(s + 1, KS_HG / 4 - 1);
-            nh = hg[4 * sn + g4];
-            ng = hg[KS_HG + 4 * sn + g4];
-#pragma unroll
-            for (int j = 0; j < NT; ++j) {
-                fh[j] = a[NT + j] * hh;
-                rp[j] = fma(fh[j], gg, rp[j]);
-            }
-        }
-        const int i0 = (TPS == 1 || h == 0) ? 0 : I0, i1 = (TPS == 1 || h == 1) ? NT : I0;
-#pragma unroll
-        for (int i = 0; i < NT; ++i)
-            if (i >= i0 && i < i1) {
-#pragma unroll
-                for (int j = 0; j < NT; ++j) G[i * NT + j] = Tile<T>::mma(a[i], fh[j], s == 0 ? tzero<T>() : G[i * NT + j]);
-            }
-    }
-    // pivot step t of the factor (t static after unrolling)
-    __device__ __forceinline__ void operator()(int t)
-    {
-        const int s = t / TPS, h = t % TPS, sl = s % KG;
-        if (on && s < nks) part(s, h, f[sl]);
-        if (h == TPS - 1) load(s + KG, f[sl]);      // unconditional: out-of-range slices read 0
-    }
-    // the slices the factor's ticks did not reach (NT < 4 with wide knots)
-    __device__ __forceinline__ void drain()
-    {
-        if constexpr (S_T < (KB_WMAX + 3) / 4) {
-            if (on) {
-                for (int s0 = S_T; s0 < nks; s0 += KG) {
-#pragma unroll
-                    for (int u = 0; u < KG; ++u) {
-                        constexpr int base = S_T % KG;
-                        const int sl = (base + u) % KG;
-                        if (s0 + u < nks) {
-#pragma unroll
-                            for (int h = 0; h < TPS; ++h) part(s0 + u, h, f[sl]);
-                        }
-                        load(s0 + u + KG, f[sl]);
-                    }
-                }
-            }
-        }
-    }
-    // r2 (column layout) into rv[NT + j]
-    __device__ __forceinline__ void finish(T (&rv)[2 * NT])
-    {
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-            T x = rp[j];
-            x += __shfl_xor(x, 16);
-            x += __shfl_xor(x, 32);
-            rv[NT + j] = x;
-        }
-    }
-};
-
-// fu_schur2 without the F products (GPass made them): of knot q1 the C tiles (D1 H⁻¹ D1ᵀ) from
-// its D1 rows, of q2 the A tiles (D2 H⁻¹ D2ᵀ) into the same P tiles and r1 into rv[v < NT]
-template <typename T, int NT, bool FULL>
-__device__ __forceinline__ void fu_schur_ca(const Kn &q1, const T *Y1, const T *hg1, const Kn &q2, const T *Y2, const T *hg2,
-                                            acc_t<T> (&P)[10], T (&rv)[2 * NT], int lane)
-{
-    const int i16 = lane & 15, g4 = lane >> 4;
-    constexpr uint32_t TS = sizeof(T), OOB = 0x80000000u;
-    constexpr int NV = FULL ? 1 : NT;
-    uint32_t vo1[NV], vo2[NV];
-    if constexpr (FULL) {
-        vo1[0] = (uint32_t)((g4 * q1.rows + 16 * NT + i16) * (int)TS);
-        vo2[0] = (uint32_t)((g4 * q2.rows + i16) * (int)TS);
-    } else {
-#pragma unroll
-        for (int v = 0; v < NT; ++v) {
-            vo1[FULL ? 0 : v] = i16 < q1.p2 - 16 * v ? (uint32_t)((g4 * q1.rows + q1.p1 + q1.ps + 16 * v + i16) * (int)TS) : OOB;
-            vo2[FULL ? 0 : v] = i16 < q2.p1 - 16 * v ? (uint32_t)((g4 * q2.rows + 16 * v + i16) * (int)TS) : OOB;
-        }
-    }
-    T rp[NT];
-#pragma unroll
-    for (int v = 0; v < NT; ++v) rp[v] = (T)0;
-    const char *yb1 = (const char *)Y1, *yb2 = (const char *)Y2;
-    const int yn1 = q1.rows * q1.w * (int)TS, so1 = 4 * q1.rows * (int)TS;
-    const int yn2 = q2.rows * q2.w * (int)TS, so2 = 4 * q2.rows * (int)TS;
-    const int nks = max(q1.w + 3, q2.w + 3) >> 2;
-    constexpr int PF = ku_pf<T>();
-    T f1[PF][NT], f2[PF][NT];
-    auto load = [&](int s, T (&a1)[NT], T (&a2)[NT]) __attribute__((always_inline)) {
-        const int o1 = s * so1, o2 = s * so2;
-        const __amdgpu_buffer_rsrc_t r1 =
-            __builtin_amdgcn_make_buffer_rsrc((void *)(yb1 + o1), (short)0, max(yn1 - o1, 0), 0x00020000);
-        const __amdgpu_buffer_rsrc_t r2 =
-            __builtin_amdgcn_make_buffer_rsrc((void *)(yb2 + o2), (short)0, max(yn2 - o2, 0), 0x00020000);
-#pragma unroll
-        for (int v = 0; v < NT; ++v)
-            a1[v] = bload<T>(r1, FULL ? vo1[0] + (uint32_t)(16 * v * (int)TS) : vo1[FULL ? 0 : v], 0u);
-#pragma unroll
-        for (int v = 0; v < NT; ++v)
-            a2[v] = bload<T>(r2, FULL ? vo2[0] + (uint32_t)(16 * v * (int)TS) : vo2[FULL ? 0 : v], 0u);
-    };
-    T nh1 = hg1[g4], nh2 = hg2[g4], ng2 = hg2[KS_HG + g4];
-    auto step = [&](auto first, const T (&a1)[NT], const T (&a2)[NT], int s) __attribute__((always_inline)) {
-        constexpr bool F0 = decltype(first)::value;
-        const T hh1 = nh1, hh2 = nh2, gg2 = ng2;
-        const int sn = min(s + 1, KS_HG / 4 - 1);
-        nh1 = hg1[4 * sn + g4];
-        nh2 = hg2[4 * sn + g4];
-        ng2 = hg2[KS_HG + 4 * sn + g4];
-        T fh1[NT], fh2[NT];
-#pragma unroll
-        for (int v = 0; v < NT; ++v) {
-            fh1[v] = a1[v] * hh1;
-            fh2[v] = a2[v] * hh2;
-        }
-#pragma unroll
-        for (int i = 0; i < NT; ++i)
-#pragma unroll
-            for (int j = i; j < NT; ++j) P[up4(i, j)] = Tile<T>::mma(a1[i], fh1[j], F0 ? tzero<T>() : P[up4(i, j)]);
-#pragma unroll
-        for (int i = 0; i < NT; ++i)
-#pragma unroll
-            for (int j = i; j < NT; ++j) P[up4(i, j)] = Tile<T>::mma(a2[i], fh2[j], P[up4(i, j)]);
-#pragma unroll
-        for (int v = 0; v < NT; ++v) rp[v] = fma(fh2[v], gg2, rp[v]);
-    };
-#pragma unroll
-    for (int u = 0; u < PF; ++u) load(u, f1[u], f2[u]);
-    step(std::true_type{}, f1[0], f2[0], 0);
-    load(PF, f1[0], f2[0]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 1; u < PF; ++u) {
-        step(std::false_type{}, f1[u], f2[u], u);
-        load(u + PF, f1[u], f2[u]);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    for (int s0 = PF; s0 < nks; s0 += PF) {
-#pragma unroll
-        for (int u = 0; u < PF; ++u) {
-            step(std::false_type{}, f1[u], f2[u], s0 + u);
-            load(s0 + u + PF, f1[u], f2[u]);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-#pragma unroll
-    for (int v = 0; v < NT; ++v) {
-        T x = rp[v];
-        x += __shfl_xor(x, 16);
-        x += __shfl_xor(x, 32);
-        rv[v] = x;
-    }
-}
-
 template <typename T, int NT, bool FULL>
 __global__ void __launch_bounds__(64 * ku_w<T>(), sizeof(T) == 4 ? 8 / ku_w<T>() : 1) kb_fuse_mid_kernel(KuArgs<T> a)
 {
@@ -2838,43 +2596,21 @@ __global__ void __launch_bounds__(64 * ku_w<T>(), sizeof(T) == 4 ? 8 / ku_w<T>()
 #ifdef KB_PROF
     int64_t kb_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     KB_T0();
-    int64_t *kbc = kb_acc + 4;
-#else
-    int64_t *kbc = nullptr;
 #endif
-    constexpr bool GP = ku_gpass<T>();
-    // GP: the LDS H⁻¹/g row areas ping-pong — hcur holds knot k+1's rows (staged as the previous
-    // stream's q2, or the prologue's), the leaf scratch and then knot k+2's rows take hoth
-    T *hcur = hgl + 2 * KS_HG, *hoth = hgl;
     for (int k = a.kb; k < a.ke; ++k) {
         const int p2 = a.meta[8 * k + 2];
-        const bool more = k + 1 < a.ke;
         // C̃_k = chol(P) → P = W_k (:61-62)
         if constexpr (KU_PRIO) __builtin_amdgcn_s_setprio(2);
-        int bad = 0;
-        T rv1[2 * NT];
-        if constexpr (GP) {
-            const Kn qn = kn_load(a.meta, more ? k + 1 : k);
-            GPass<T, NT, FULL> gp(qn, Yt + qn.oY, hcur, more, G, lane);
 #ifdef KU_NOCHOL
-            (void)p2;
-            (void)kbc;
-#pragma unroll
-            for (int t = 0; t < 16 * NT; ++t) gp(t);
+        const int bad = 0;         // timing ablation only: no factorisation (wrong results)
+        (void)p2;
 #else
-            bad = chol_inv_reg<T>(P, NT, p2, U, hoth, lane, kbc, gp);
-#endif
-            gp.drain();
-            gp.finish(rv1);
-        } else {
-            (void)rv1;
-#ifdef KU_NOCHOL
-            (void)p2;              // timing ablation only: no factorisation (wrong results)
-            (void)kbc;
+#ifdef KB_PROF
+        const int bad = chol_inv_reg<T>(P, NT, p2, U, hgl, lane, kb_acc + 4);
 #else
-            bad = chol_inv_reg<T>(P, NT, p2, U, hgl, lane, kbc);
+        const int bad = chol_inv_reg<T>(P, NT, p2, U, hgl, lane);
 #endif
-        }
+#endif
         KB_T(0);
         // λ_k = W_kᵀ x_k (:108-116)
         T xr[4][4], lc[4];
@@ -2924,7 +2660,7 @@ __global__ void __launch_bounds__(64 * ku_w<T>(), sizeof(T) == 4 ? 8 / ku_w<T>()
         if (bad && !info) info = k + 1;
         if constexpr (KU_PRIO) __builtin_amdgcn_s_setprio(0);
         KB_T(1);
-        if (more) {
+        if (k + 1 < a.ke) {
             // W_k to the LDS image (chol_inv_reg's scratch is free again): no tile is live
             // across the streaming but G and P (zeroed there)
             wsync();
@@ -2932,22 +2668,7 @@ __global__ void __launch_bounds__(64 * ku_w<T>(), sizeof(T) == 4 ? 8 / ku_w<T>()
             for (int i = 0; i < NT; ++i)
 #pragma unroll
                 for (int j = i; j < NT; ++j) tstore(U + 16 * i + 16 * j * KF_LU, KF_LU, P[up4(i, j)], lane);
-            if constexpr (GP) {
-                // C of knot k+1 and A / r1 of knot k+2 (F and r2 of k+1 came from the factor)
-                const Kn q1 = kn_load(a.meta, k + 1), q2 = kn_load(a.meta, k + 2);
-                fu_stage_hg<T>(hoth, q2, Ht, gt, a.hinv, a.useg, lane);
-                fu_schur_ca<T, NT, FULL>(q1, Yt + q1.oY, hcur, q2, Yt + q2.oY, hoth, P, rv1, lane);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int e = 16 * j + (lane & 15);
-                    xn[j] = (j < NT && e < q1.p2) ? (rv1[NT + j] - yt[q1.oy + e]) + rv1[j] : (T)0;
-                }
-                T *const h2 = hcur;
-                hcur = hoth;
-                hoth = h2;
-            } else {
-                fu_stream<T, NT, FULL>(a.meta, k + 1, Yt, yt, Ht, gt, a.hinv, a.useg, hgl, G, P, xn, lane);
-            }
+            fu_stream<T, NT, FULL>(a.meta, k + 1, Yt, yt, Ht, gt, a.hinv, a.useg, hgl, G, P, xn, lane);
             wsync();
             KB_T(2);
             if constexpr (KU_LEAN) col2row<T>(lam, lcol, vb, lane);
