@@ -161,6 +161,17 @@ recipe_r6kkt() {   # configs[4] KKT half after the round-6 fused-kernel changes 
     sub t pytest tests/test_kkt_big_gpu.py tests/test_full_size_gpu.py && sub kkt32 prof $CFG4KKT &&
     KREGEX=kb_ PMC="$SQ1;$SQ2" sub kkt32sq pmc $CFG4KKT && sub kkt64 prof $CFG4KKT64
 }
+recipe_r6final() {   # round-6 final closing set at HEAD: suite + smoke, every bench line with traffic
+                     # (lqrx_internal.h's DpArgs changed, so every traffic_r06.json entry is re-measured)
+    sub t tests && sub cfg4 prof && sub cfg5 prof --n 64 --m 32 --N 512 --batch 8192 --dtype f32 &&
+    sub dp64 prof $DP64 && sub lin64 prof $DP64 --linear && sub tv64 prof $DP64TV &&
+    sub kkt32 prof $CFG4KKT && sub kkt64 prof $CFG4KKT64 && sub cfg2 prof --workload cartpole &&
+    sub tv prof --tv && sub lin prof --linear && sub wg96 prof $WG96 &&
+    sub cfg3 prof --workload kkt && sub cfg3soa kt --workload kkt --kkt-layout 1 &&
+    sub di prof --workload kkt --kkt-structure di &&
+    sub t62 prof --workload kkt --kkt-structure dense --n 6 --m 2 --N 101 --batch 16384 --dtype f64 &&
+    sub t84 prof --workload kkt --kkt-structure dense --n 8 --m 4 --N 101 --batch 16384 --dtype f64
+}
 recipe_list() { declare -F | sed -n 's/^declare -f recipe_//p'; }
 
 case "$MODE" in
