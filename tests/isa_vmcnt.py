@@ -38,6 +38,7 @@ Findings:
   * `untagged`: a hand wait with N > 0 inside inline asm that names no target group, in a
     function that issues DMA (an unchecked bound).
 """
+import functools
 import re
 
 INF = 1 << 30
@@ -51,14 +52,16 @@ LABEL = re.compile(r"^([.\w$]+):")
 TAG = re.compile(r"lqrx\.wait\s+g=(\d+)")
 
 
+@functools.lru_cache(maxsize=None)
 def regs(text):
-    """VGPR numbers named in an operand string (v7, v[4:7])."""
+    """VGPR numbers named in an operand string (v7, v[4:7]) (memoised: the dataflow revisits the
+    same instruction text many times)."""
     out = set()
     for a, b in re.findall(r"\bv\[(\d+):(\d+)\]", text):
         out.update(range(int(a), int(b) + 1))
     for a in re.findall(r"\bv(\d+)\b", re.sub(r"\bv\[\d+:\d+\]", "", text)):
         out.add(int(a))
-    return out
+    return frozenset(out)
 
 
 def vmcnt_of(wait_operands):
@@ -175,6 +178,7 @@ def _join(a, b):
     return out
 
 
+@functools.lru_cache(maxsize=None)
 def sregs(text):
     """SGPR numbers named in an operand string (s7, s[4:5])."""
     out = set()
@@ -182,7 +186,7 @@ def sregs(text):
         out.update(range(int(a), int(b) + 1))
     for a in re.findall(r"\bs(\d+)\b", re.sub(r"\bs\[\d+:\d+\]", "", text)):
         out.add(int(a))
-    return out
+    return frozenset(out)
 
 
 VCCDEF = re.compile(r"^s_(and|andn2)_b64\s+vcc,\s*exec,\s*(s\[\d+:\d+\])\s*$")
@@ -201,6 +205,7 @@ def _flag_regs(body):
     return out
 
 
+@functools.lru_cache(maxsize=None)
 def _sig_update(sig, s, flags):
     """New flag signature after instruction s (sig: tuple of (flag, value) incl. ('vcc', bool))."""
     d = dict(sig)
@@ -336,7 +341,11 @@ def analyse(asm, name_re):
                 st["hand_waits"] += 1
                 st["tagged_waits"] += bool(TAG.search(s))
         stats[sym] = st
-        flags = _flag_regs(body)
+        if not st["asm_loads"] and not st["dma"]:
+            # nothing for the model to find: no inline-asm load can be pending (no hazard), and
+            # bound / untagged findings need DMA groups — skip the dataflow (most functions)
+            continue
+        flags = frozenset(_flag_regs(body))
         bl = blocks(body)
         idx = {b[0]: i for i, b in enumerate(bl)}
         ins = [None] * len(bl)
