@@ -2288,6 +2288,9 @@ struct KuArgs {
 #define KU_HG_AHEAD 1        // (KU_LEAN) a slice's H⁻¹/g LDS reads issued one stream step ahead:
                              // 1 fp64 only, 2 fp32 as well, 0 off (A/B)
 #endif
+#ifndef KU_PP
+#define KU_PP 1              // H⁻¹/g row areas ping-pong: each step stages only knot k+2's rows (0: A/B)
+#endif
 #ifndef KU_PRIO
 #define KU_PRIO 1            // the factor phase (latency-bound chain) runs at raised issue priority
 #endif
@@ -2530,14 +2533,14 @@ __device__ __forceinline__ void fu_reduce(acc_t<T> (&P)[10], acc_t<T> (&G)[16], 
 // to xn: d_kn = r2 − y + r1 of the next knot, as the image's v)
 template <typename T, int NT, bool FULL>
 __device__ __forceinline__ void fu_stream(const int32_t *meta, int kn, const T *Yt, const T *yt, const T *Ht, const T *gt,
-                                          int hinv, int useg, T *hgl, acc_t<T> (&G)[16], acc_t<T> (&P)[10], T (&xn)[4],
-                                          int lane)
+                                          int hinv, int useg, T *h1, T *h2, bool stage1, acc_t<T> (&G)[16],
+                                          acc_t<T> (&P)[10], T (&xn)[4], int lane)
 {
     const Kn q1 = kn_load(meta, kn), q2 = kn_load(meta, kn + 1);
     T rv[2 * NT];
-    fu_stage_hg<T>(hgl, q1, Ht, gt, hinv, useg, lane);
-    fu_stage_hg<T>(hgl + 2 * KS_HG, q2, Ht, gt, hinv, useg, lane);
-    fu_schur2<T, NT, FULL>(q1, Yt + q1.oY, hgl, q2, Yt + q2.oY, hgl + 2 * KS_HG, G, P, rv, lane);
+    if (stage1) fu_stage_hg<T>(h1, q1, Ht, gt, hinv, useg, lane);
+    fu_stage_hg<T>(h2, q2, Ht, gt, hinv, useg, lane);
+    fu_schur2<T, NT, FULL>(q1, Yt + q1.oY, h1, q2, Yt + q2.oY, h2, G, P, rv, lane);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int e = 16 * j + (lane & 15);
@@ -2588,7 +2591,11 @@ __global__ void __launch_bounds__(64 * ku_w<T>(), sizeof(T) == 4 ? 8 / ku_w<T>()
             for (int j = i; j < NT; ++j) tstore(U + 16 * i + 16 * j * KF_LU, KF_LU, P[up4(i, j)], lane);
     }
     // prologue: knot kb's F, C, d and knot kb+1's A; then F̃_kb, x_kb, P = C_kb + A_{kb+1} − F̃ᵀF̃
-    fu_stream<T, NT, FULL>(a.meta, a.kb, Yt, yt, Ht, gt, a.hinv, a.useg, hgl, G, P, xn, lane);
+    // H⁻¹/g rows: knot k+1's were staged by the previous stream (as its q2) — KU_PP: the two row
+    // areas ping-pong (hcur: knot k+1's rows, kept through the factor; hoth: the leaf scratch, then
+    // knot k+2's rows) instead of re-staging both knots every step
+    T *hcur = hgl + 2 * KS_HG, *hoth = hgl;
+    fu_stream<T, NT, FULL>(a.meta, a.kb, Yt, yt, Ht, gt, a.hinv, a.useg, hgl, hgl + 2 * KS_HG, true, G, P, xn, lane);
     wsync();
     if constexpr (KU_LEAN) col2row<T>(lam, lcol, vb, lane);
     fu_reduce<T, NT>(P, G, U, lam, xn, x, lane);
@@ -2606,9 +2613,9 @@ __global__ void __launch_bounds__(64 * ku_w<T>(), sizeof(T) == 4 ? 8 / ku_w<T>()
         (void)p2;
 #else
 #ifdef KB_PROF
-        const int bad = chol_inv_reg<T>(P, NT, p2, U, hgl, lane, kb_acc + 4);
+        const int bad = chol_inv_reg<T>(P, NT, p2, U, KU_PP ? hoth : hgl, lane, kb_acc + 4);
 #else
-        const int bad = chol_inv_reg<T>(P, NT, p2, U, hgl, lane);
+        const int bad = chol_inv_reg<T>(P, NT, p2, U, KU_PP ? hoth : hgl, lane);
 #endif
 #endif
         KB_T(0);
@@ -2668,7 +2675,15 @@ __global__ void __launch_bounds__(64 * ku_w<T>(), sizeof(T) == 4 ? 8 / ku_w<T>()
             for (int i = 0; i < NT; ++i)
 #pragma unroll
                 for (int j = i; j < NT; ++j) tstore(U + 16 * i + 16 * j * KF_LU, KF_LU, P[up4(i, j)], lane);
-            fu_stream<T, NT, FULL>(a.meta, k + 1, Yt, yt, Ht, gt, a.hinv, a.useg, hgl, G, P, xn, lane);
+            if constexpr (KU_PP) {
+                fu_stream<T, NT, FULL>(a.meta, k + 1, Yt, yt, Ht, gt, a.hinv, a.useg, hcur, hoth, false, G, P, xn, lane);
+                T *const h = hcur;
+                hcur = hoth;
+                hoth = h;
+            } else {
+                fu_stream<T, NT, FULL>(a.meta, k + 1, Yt, yt, Ht, gt, a.hinv, a.useg, hgl, hgl + 2 * KS_HG, true, G, P,
+                                       xn, lane);
+            }
             wsync();
             KB_T(2);
             if constexpr (KU_LEAN) col2row<T>(lam, lcol, vb, lane);
