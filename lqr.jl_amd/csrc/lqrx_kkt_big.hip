@@ -2291,6 +2291,9 @@ struct KuArgs {
 #ifndef KU_PP
 #define KU_PP 1              // H⁻¹/g row areas ping-pong: each step stages only knot k+2's rows (0: A/B)
 #endif
+#ifndef KU_HGPF
+#define KU_HGPF 1            // (KU_PP) knot k+2's H / g loads issued before knot k's factor (0: A/B)
+#endif
 #ifndef KU_PRIO
 #define KU_PRIO 1            // the factor phase (latency-bound chain) runs at raised issue priority
 #endif
@@ -2315,6 +2318,24 @@ __device__ __forceinline__ void fu_stage_hg(T *hgl, const Kn &q, const T *Ht, co
             const bool in = c < q.w;
             hgl[c] = in ? (hinv ? (T)1 / Ht[q.oH + c] : (T)1) : (T)0;
             hgl[KS_HG + c] = (in && useg) ? gt[q.og + c] : (T)0;
+        }
+    }
+    wsync();
+}
+
+// the same rows from values the caller loaded earlier (hv / gv: columns lane + 64u of H and g)
+template <typename T>
+__device__ __forceinline__ void fu_put_hg(T *hgl, const Kn &q, const T (&hv)[(KS_HG + 63) / 64], const T (&gv)[(KS_HG + 63) / 64],
+                                          int hinv, int useg, int lane)
+{
+    wsync();
+#pragma unroll
+    for (int u = 0; u < (KS_HG + 63) / 64; ++u) {
+        const int c = lane + 64 * u;
+        if (c < KS_HG) {
+            const bool in = c < q.w;
+            hgl[c] = in ? (hinv ? (T)1 / hv[u] : (T)1) : (T)0;
+            hgl[KS_HG + c] = (in && useg) ? gv[u] : (T)0;
         }
     }
     wsync();
@@ -2534,12 +2555,14 @@ __device__ __forceinline__ void fu_reduce(acc_t<T> (&P)[10], acc_t<T> (&G)[16], 
 template <typename T, int NT, bool FULL>
 __device__ __forceinline__ void fu_stream(const int32_t *meta, int kn, const T *Yt, const T *yt, const T *Ht, const T *gt,
                                           int hinv, int useg, T *h1, T *h2, bool stage1, acc_t<T> (&G)[16],
-                                          acc_t<T> (&P)[10], T (&xn)[4], int lane)
+                                          acc_t<T> (&P)[10], T (&xn)[4], int lane,
+                                          const T (*hv)[(KS_HG + 63) / 64] = nullptr, const T (*gv)[(KS_HG + 63) / 64] = nullptr)
 {
     const Kn q1 = kn_load(meta, kn), q2 = kn_load(meta, kn + 1);
     T rv[2 * NT];
     if (stage1) fu_stage_hg<T>(h1, q1, Ht, gt, hinv, useg, lane);
-    fu_stage_hg<T>(h2, q2, Ht, gt, hinv, useg, lane);
+    if (hv) fu_put_hg<T>(h2, q2, *hv, *gv, hinv, useg, lane);      // q2's H / g loaded before the factor
+    else fu_stage_hg<T>(h2, q2, Ht, gt, hinv, useg, lane);
     fu_schur2<T, NT, FULL>(q1, Yt + q1.oY, h1, q2, Yt + q2.oY, h2, G, P, rv, lane);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -2604,8 +2627,25 @@ __global__ void __launch_bounds__(64 * ku_w<T>(), sizeof(T) == 4 ? 8 / ku_w<T>()
     int64_t kb_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     KB_T0();
 #endif
+    constexpr bool HGPF = KU_PP && KU_HGPF;
+    constexpr int NHG = (KS_HG + 63) / 64;
     for (int k = a.kb; k < a.ke; ++k) {
         const int p2 = a.meta[8 * k + 2];
+        // HGPF: knot k+2's H and g requested before the factor (they land under it; the stream
+        // after it only forms H⁻¹ and writes the LDS rows)
+        T hv[NHG], gv[NHG];
+        if constexpr (HGPF) {
+            if (k + 1 < a.ke) {
+                const Kn q2 = kn_load(a.meta, k + 2);
+#pragma unroll
+                for (int u = 0; u < NHG; ++u) {
+                    const int c = lane + 64 * u;
+                    const bool in = c < q2.w;
+                    hv[u] = (in && a.hinv) ? Ht[q2.oH + c] : (T)1;
+                    gv[u] = (in && a.useg) ? gt[q2.og + c] : (T)0;
+                }
+            }
+        }
         // C̃_k = chol(P) → P = W_k (:61-62)
         if constexpr (KU_PRIO) __builtin_amdgcn_s_setprio(2);
 #ifdef KU_NOCHOL
@@ -2676,7 +2716,8 @@ __global__ void __launch_bounds__(64 * ku_w<T>(), sizeof(T) == 4 ? 8 / ku_w<T>()
 #pragma unroll
                 for (int j = i; j < NT; ++j) tstore(U + 16 * i + 16 * j * KF_LU, KF_LU, P[up4(i, j)], lane);
             if constexpr (KU_PP) {
-                fu_stream<T, NT, FULL>(a.meta, k + 1, Yt, yt, Ht, gt, a.hinv, a.useg, hcur, hoth, false, G, P, xn, lane);
+                fu_stream<T, NT, FULL>(a.meta, k + 1, Yt, yt, Ht, gt, a.hinv, a.useg, hcur, hoth, false, G, P, xn, lane,
+                                       HGPF ? &hv : nullptr, HGPF ? &gv : nullptr);
                 T *const h = hcur;
                 hcur = hoth;
                 hoth = h;
