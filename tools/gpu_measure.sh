@@ -172,6 +172,11 @@ recipe_r6final() {   # round-6 final closing set at HEAD: suite + smoke, every b
     sub t62 prof --workload kkt --kkt-structure dense --n 6 --m 2 --N 101 --batch 16384 --dtype f64 &&
     sub t84 prof --workload kkt --kkt-structure dense --n 8 --m 4 --N 101 --batch 16384 --dtype f64
 }
+recipe_r6kkt2() {   # after the fused kernel's H/g ping-pong + prefetch: suite + smoke, the configs[4] KKT
+                    # lines with traffic and SQ counters, the headline for the record
+    sub t tests && sub kkt32 prof $CFG4KKT && KREGEX=kb_ PMC="$SQ1;$SQ2" sub kkt32sq pmc $CFG4KKT &&
+    sub kkt64 prof $CFG4KKT64 && sub cfg4 bench
+}
 recipe_list() { declare -F | sed -n 's/^declare -f recipe_//p'; }
 
 case "$MODE" in
